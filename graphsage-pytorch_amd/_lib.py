@@ -1,0 +1,150 @@
+"""ctypes binding of libgraphsage_amd.so (declared in include/graphsage_amd.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C graphsage-pytorch_amd/csrc``).  There is no fallback: if the library
+is missing every entry point raises, so a GPU run can never silently execute
+something other than the HIP kernels.
+
+torch is imported before the library is loaded so that the HIP runtime torch
+ships (SONAME libamdhip64.so.7) is the one the kernels bind to — one runtime,
+one device context, torch's streams usable as ``hipStream_t``.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load first: shares its HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgraphsage_amd.so")
+
+GS_OK, GS_EINVAL, GS_ENOMEM, GS_EHIP, GS_ERANGE, GS_EEMPTY = range(6)
+GS_F32, GS_BF16 = 0, 1
+GS_AGG_MEAN, GS_AGG_MAX = 0, 1
+GS_SAMPLE_GCN, GS_SAMPLE_FULL = 1, 2
+GS_MAX_HOPS = 8
+(GS_PK_POS_PTR, GS_PK_POS, GS_PK_DST_IDS, GS_PK_NBR_PTR, GS_PK_NBR, GS_PK_SELF,
+ GS_PK_TPTR, GS_PK_TIDX, GS_PK_NFIELDS) = range(9)
+
+_i32, _i64, _u32, _u64, _f32, _f64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                      ctypes.c_uint64, ctypes.c_float, ctypes.c_double)
+_vp = ctypes.c_void_p
+_p = ctypes.POINTER
+
+
+class HopView(ctypes.Structure):
+    _fields_ = [
+        ("n_dst", _i64), ("n_pos", _i64), ("n_src", _i64), ("n_nbr", _i64),
+        ("dst_ids", _p(_i64)), ("pos_ptr", _p(_i32)), ("pos", _p(_i32)),
+        ("src_ids", _p(_i64)), ("nbr_ptr", _p(_i32)), ("nbr", _p(_i32)),
+        ("self_local", _p(_i32)), ("set_ptr", _p(_i32)), ("set_items", _p(_i64)),
+    ]
+
+
+class PackLayout(ctypes.Structure):
+    _fields_ = [("total", _i64), ("off", (_i64 * GS_PK_NFIELDS) * GS_MAX_HOPS)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "gs_last_error": (ctypes.c_char_p, []),
+    "gs_version": (ctypes.c_char_p, []),
+    "gs_rng_create": (_i32, [_p(_vp)]),
+    "gs_rng_destroy": (None, [_vp]),
+    "gs_rng_seed_words": (_i32, [_vp, _vp, _i64]),
+    "gs_rng_set_state": (_i32, [_vp, _vp, _i64]),
+    "gs_rng_get_state": (_i32, [_vp, _vp, _p(_i64)]),
+    "gs_rng_getrandbits": (_i32, [_vp, _i32, _i64, _vp]),
+    "gs_rng_randbelow": (_i32, [_vp, _u32, _i64, _vp]),
+    "gs_rng_sample_positions": (_i32, [_vp, _i64, _i64, _vp]),
+    "gs_rng_choice_position": (_i32, [_vp, _i64, _p(_i64)]),
+    "gs_pyset_union_of_lists": (_i32, [_vp, _vp, _i64, _vp, _p(_i64)]),
+    "gs_graph_build": (_i32, [_vp, _vp, _i64, _i64, _i32, _p(_vp)]),
+    "gs_graph_from_tables": (_i32, [_i64, _vp, _vp, _vp, _vp, _vp, _p(_vp)]),
+    "gs_graph_destroy": (None, [_vp]),
+    "gs_graph_dims": (_i32, [_vp, _p(_i64), _p(_i64), _p(_i64)]),
+    "gs_graph_row_ptr": (_vp, [_vp]),
+    "gs_graph_col": (_vp, [_vp]),
+    "gs_rmat_pairs": (_i32, [_i32, _i64, _f64, _f64, _f64, _u64, _i32, _i32, _vp, _vp, _p(_i64)]),
+    "gs_sample_run": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _p(_vp)]),
+    "gs_sample_destroy": (None, [_vp]),
+    "gs_sample_n_hops": (_i32, [_vp, _p(_i32)]),
+    "gs_sample_hop": (_i32, [_vp, _i32, _p(HopView)]),
+    "gs_sample_pack_layout": (_i32, [_vp, _p(PackLayout)]),
+    "gs_sample_pack": (_i32, [_vp, _vp, _i64]),
+    "gs_fill_uniform": (_i32, [_vp, _i32, _i64, _i64, _i64, _u64, _vp]),
+    "gs_uniform_host": (_i32, [_u64, _i64, _i64, _i64, _vp]),
+    "gs_agg_fwd": (_i32, [_i32, _i32, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32,
+                          _vp, _i32, _i64, _vp, _vp]),
+    "gs_sage_linear_fwd": (_i32, [_i32, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
+                                  _i64, _i32, _vp]),
+    "gs_sage_linear_bwd_weight_ws": (_i64, [_i64, _i64, _i64]),
+    "gs_sage_linear_bwd_weight": (_i32, [_i32, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp,
+                                         _vp, _i64, _i32, _vp, _vp, _i64, _vp]),
+    "gs_sage_linear_bwd_input": (_i32, [_i64, _i64, _i64, _vp, _vp, _i64, _i32, _vp, _vp, _vp,
+                                        _i64, _vp]),
+    "gs_agg_bwd": (_i32, [_i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp,
+                          _vp]),
+    "gs_cls_nll_ws_floats": (_i64, [_i64, _i64, _i64]),
+    "gs_cls_nll_fwd_bwd": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp]),
+    "gs_clip_sgd": (_i32, [_i32, _vp, _vp, _vp, _f32, _f32, _f32, _vp, _vp]),
+    "gs_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
+}
+
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the configured ctypes library."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(
+                f"{LIB_PATH} is not built; run __graft_entry__.build() or "
+                "`make -C graphsage-pytorch_amd/csrc` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)  # CDLL releases the GIL around every call
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, what=""):
+    """Raise the reference's exception type for a non-zero status."""
+    if rc == GS_OK:
+        return
+    msg = lib().gs_last_error().decode(errors="replace") or what
+    if rc in (GS_EINVAL,):
+        raise ValueError(msg)
+    if rc == GS_ERANGE:
+        # random.sample: ValueError; unknown node ids: IndexError (features[node])
+        raise (ValueError if "Sample larger" in msg else IndexError)(msg)
+    if rc == GS_EEMPTY:
+        raise IndexError(msg)
+    if rc == GS_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def ptr(t):
+    """Raw address of a torch tensor / numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_ptr(device=None):
+    """hipStream_t of torch's current stream on `device`."""
+    return torch.cuda.current_stream(device).cuda_stream

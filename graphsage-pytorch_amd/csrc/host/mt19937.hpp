@@ -1,0 +1,162 @@
+// CPython 3.10 random.Random restated for the sampler: the MT19937 core of
+// Modules/_randommodule.c (genrand_uint32, init_genrand, init_by_array) plus
+// the Lib/random.py pieces the reference calls — _randbelow_with_getrandbits,
+// sample() (both branches) and choice().  The reference's sampling semantics
+// are *defined* by these (models.py:281-282 random.sample, :178 random.choice),
+// so the state here is word-for-word interchangeable with random.getstate().
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+namespace gs {
+
+struct MT19937 {
+    static constexpr int N = 624;
+    static constexpr int M = 397;
+    uint32_t mt[N];
+    int index = N + 1;
+
+    void init_genrand(uint32_t s) {
+        mt[0] = s;
+        for (int i = 1; i < N; ++i)
+            mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + static_cast<uint32_t>(i);
+        index = N;
+    }
+
+    // random.seed(int): init_by_array over the 32-bit words of abs(seed).
+    void init_by_array(const uint32_t* key, size_t len) {
+        init_genrand(19650218u);
+        size_t i = 1, j = 0;
+        size_t k = (N > len ? N : len);
+        for (; k; --k) {
+            mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1664525u)) + key[j] +
+                    static_cast<uint32_t>(j);
+            ++i;
+            ++j;
+            if (i >= static_cast<size_t>(N)) {
+                mt[0] = mt[N - 1];
+                i = 1;
+            }
+            if (j >= len) j = 0;
+        }
+        for (k = N - 1; k; --k) {
+            mt[i] = (mt[i] ^ ((mt[i - 1] ^ (mt[i - 1] >> 30)) * 1566083941u)) -
+                    static_cast<uint32_t>(i);
+            ++i;
+            if (i >= static_cast<size_t>(N)) {
+                mt[0] = mt[N - 1];
+                i = 1;
+            }
+        }
+        mt[0] = 0x80000000u;
+        index = N;
+    }
+
+    void twist() {
+        static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+        int kk = 0;
+        uint32_t y;
+        for (; kk < N - M; ++kk) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + M] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        for (; kk < N - 1; ++kk) {
+            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ mag01[y & 1u];
+        }
+        y = (mt[N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+        mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+        index = 0;
+    }
+
+    inline uint32_t next() {
+        if (index >= N) twist();
+        uint32_t y = mt[index++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+
+    // getrandbits(k) for 1 <= k <= 32 (the fast path of _random_Random_getrandbits).
+    inline uint32_t getrandbits(int k) { return next() >> (32 - k); }
+
+    // Random._randbelow_with_getrandbits(n): k = n.bit_length(); reject r >= n.
+    // n == 1 still consumes words (k = 1) — the randbelow(1) quirk.
+    inline uint32_t randbelow(uint64_t n) {
+        if (n == 0) return 0;
+        const int k = 64 - __builtin_clzll(n);
+        uint32_t r = getrandbits(k);
+        while (r >= n) r = getrandbits(k);
+        return r;
+    }
+};
+
+// random.sample(): `setsize` decides between the list-pool and the
+// selected-set branch (Lib/random.py, 3.10).
+inline int64_t sample_setsize(int64_t k) {
+    int64_t setsize = 21;
+    if (k > 5) {
+        const double e = std::ceil(std::log(static_cast<double>(k * 3)) / std::log(4.0));
+        int64_t p = 1;
+        for (int64_t t = 0; t < static_cast<int64_t>(e); ++t) p *= 4;
+        setsize += p;
+    }
+    return setsize;
+}
+
+// random.sample(population, k) expressed on positions 0..n-1 of the
+// population: writes the k chosen positions in result order.  `scratch` must
+// hold 2*k entries.  Requires 0 <= k <= n.
+inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize,
+                             int64_t* out, int64_t* scratch) {
+    if (n <= setsize) {
+        // pool branch: pool = list(population); j = randbelow(n-i);
+        // result[i] = pool[j]; pool[j] = pool[n-i-1].  The pool is tracked as
+        // a sparse overlay on the identity permutation (<= k entries moved).
+        int64_t* mkey = scratch;      // overridden pool slots
+        int64_t* mval = scratch + k;  // their contents
+        int64_t nm = 0;
+        auto pool_get = [&](int64_t idx) -> int64_t {
+            for (int64_t t = 0; t < nm; ++t)
+                if (mkey[t] == idx) return mval[t];
+            return idx;
+        };
+        auto pool_set = [&](int64_t idx, int64_t v) {
+            for (int64_t t = 0; t < nm; ++t)
+                if (mkey[t] == idx) {
+                    mval[t] = v;
+                    return;
+                }
+            mkey[nm] = idx;
+            mval[nm] = v;
+            ++nm;
+        };
+        for (int64_t i = 0; i < k; ++i) {
+            const int64_t j = rng.randbelow(static_cast<uint64_t>(n - i));
+            out[i] = pool_get(j);
+            pool_set(j, pool_get(n - i - 1));
+        }
+    } else {
+        // selected-set branch: redraw while j already selected.
+        for (int64_t i = 0; i < k; ++i) {
+            int64_t j;
+            bool dup;
+            do {
+                j = rng.randbelow(static_cast<uint64_t>(n));
+                dup = false;
+                for (int64_t t = 0; t < i; ++t)
+                    if (out[t] == j) {
+                        dup = true;
+                        break;
+                    }
+            } while (dup);
+            out[i] = j;
+        }
+    }
+}
+
+}  // namespace gs

@@ -1,0 +1,386 @@
+// Host neighbour sampler: GraphSage._get_unique_neighs_list (models.py:277-289)
+// applied hop by hop as GraphSage.forward does (models.py:246-251), bit-exact
+// with the reference's CPython `random` stream and set iteration order.
+//
+// Per hop j (frontier F(j-1) -> union Fj), for every frontier node v in order:
+//   deg(v) >= k : positions = random.sample(range(deg), k)   (consumes rng)
+//   otherwise   : the whole row                               (no rng)
+// Only the hops whose union feeds a later hop need the CPython-set replay
+// (set(sample) | {v}, then set.union over the frontier).  The last hop's union
+// only orders the rows of a gather, so by default it is skipped and the
+// device expands the sampled positions through the CSR itself.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "common.hpp"
+#include "graph.hpp"
+#include "mt19937.hpp"
+#include "pyset.hpp"
+
+struct gs_rng {
+    gs::MT19937 mt;
+};
+
+namespace gs {
+
+struct Hop {
+    int64_t k = 0;
+    bool materialised = false;
+    std::vector<int64_t> dst_ids;
+    std::vector<int32_t> pos_ptr, pos;
+    std::vector<int64_t> src_ids;
+    std::vector<int32_t> nbr_ptr, nbr, self_local;
+    std::vector<int32_t> set_ptr;
+    std::vector<int64_t> set_items;
+    std::vector<int32_t> tptr, tidx;  // transposed (src -> dst) incl. self edges as -(r+1)
+};
+
+struct Sample {
+    int32_t n_hops = 0;
+    int32_t flags = 0;
+    Hop hops[GS_MAX_HOPS];
+};
+
+// Draw the sampled row positions of every frontier node, in frontier order.
+static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    h.pos_ptr.assign(n + 1, 0);
+    int64_t total = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t d = g.degree(h.dst_ids[r]);
+        total += (h.k > 0 && d >= h.k) ? h.k : d;
+        GS_REQUIRE(total < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
+        h.pos_ptr[r + 1] = static_cast<int32_t>(total);
+    }
+    h.pos.resize(total);
+    const int64_t setsize = sample_setsize(h.k);
+    std::vector<int64_t> out(std::max<int64_t>(h.k, 1)), scratch(2 * std::max<int64_t>(h.k, 1));
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t v = h.dst_ids[r];
+        const int64_t d = g.degree(v);
+        int32_t* dstp = h.pos.data() + h.pos_ptr[r];
+        if (h.k > 0 && d >= h.k) {
+            sample_positions(rng, d, h.k, setsize, out.data(), scratch.data());
+            for (int64_t t = 0; t < h.k; ++t) dstp[t] = static_cast<int32_t>(out[t]);
+        } else {
+            for (int64_t t = 0; t < d; ++t) dstp[t] = static_cast<int32_t>(t);
+        }
+    }
+}
+
+// CPython-set replay of :282-288 for one hop: per-node sets, their union
+// (the next frontier, in iteration order), local neighbour lists, and the
+// transposed lists the backward pass gathers over.
+static void materialise(const Graph& g, Hop& h, bool gcn) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    std::vector<PySet> sets(n);
+    PySet s;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t v = h.dst_ids[r];
+        const int64_t rs = g.row_ptr[v], d = g.degree(v);
+        const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
+        if (h.k > 0 && d >= h.k) {
+            // set(random.sample(adj, k)) : adds in result order
+            s.reset();
+            for (int64_t t = 0; t < cnt; ++t) s.add(g.col[rs + h.pos[h.pos_ptr[r] + t]]);
+        } else {
+            // the adjacency set object itself, with its own table layout
+            std::vector<int64_t> keys(d);
+            for (int64_t t = 0; t < d; ++t) keys[t] = g.col[rs + t];
+            s.assign_layout((size_t(1) << g.log2size[v]) - 1, keys.data(), g.slot.data() + rs, d);
+            if (!g.dirty.empty() && g.dirty[v]) s.fill = s.used + 1;  // dummies: no slot-copy fast path
+        }
+        sets[r] = copy_of(s);      // samp_neigh | set([v])  (:285)
+        sets[r].merge_single(v);
+    }
+    // samp_neighs as the reference holds them (API / parity views).
+    h.set_ptr.assign(n + 1, 0);
+    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] = h.set_ptr[r] + static_cast<int32_t>(sets[r].used);
+    h.set_items.resize(h.set_ptr[n]);
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t w = h.set_ptr[r];
+        sets[r].for_each([&](int64_t key) { h.set_items[w++] = key; });
+    }
+    // list(set.union(*samp_neighs))  (:286)
+    PySet u;
+    if (n > 0) {
+        u = copy_of(sets[0]);
+        for (int64_t r = 1; r < n; ++r) u.merge(sets[r]);
+    }
+    std::vector<int32_t> slot_pos(u.mask + 1, -1);
+    h.src_ids.clear();
+    h.src_ids.reserve(u.used);
+    for (size_t sl = 0; sl <= u.mask; ++sl) {
+        if (u.tab[sl] == PySet::EMPTY) continue;
+        slot_pos[sl] = static_cast<int32_t>(h.src_ids.size());
+        h.src_ids.push_back(u.tab[sl]);
+    }
+    auto local_of = [&](int64_t key) -> int32_t {
+        const int64_t sl = u.find_slot(key);
+        GS_REQUIRE(sl >= 0, GS_EINVAL, "internal: key missing from union");
+        return slot_pos[sl];
+    };
+    // Neighbourhoods in union-local ids, ascending (= the dense mask's column
+    // order, :305-308); non-gcn removes self (:297-298).
+    h.nbr_ptr.assign(n + 1, 0);
+    h.nbr.clear();
+    h.self_local.resize(n);
+    std::vector<int32_t> tmp;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t v = h.dst_ids[r];
+        tmp.clear();
+        sets[r].for_each([&](int64_t key) {
+            if (!gcn && key == v) return;
+            tmp.push_back(local_of(key));
+        });
+        std::sort(tmp.begin(), tmp.end());
+        h.nbr.insert(h.nbr.end(), tmp.begin(), tmp.end());
+        h.nbr_ptr[r + 1] = static_cast<int32_t>(h.nbr.size());
+        h.self_local[r] = local_of(v);
+    }
+    // Transposed lists over Fj: for source c, the destinations reading it
+    // (r >= 0) and the destinations whose self row it is (-(r+1)), r ascending.
+    const int64_t ns = static_cast<int64_t>(h.src_ids.size());
+    h.tptr.assign(ns + 1, 0);
+    for (int32_t c : h.nbr) ++h.tptr[c + 1];
+    for (int32_t c : h.self_local) ++h.tptr[c + 1];
+    for (int64_t c = 0; c < ns; ++c) h.tptr[c + 1] += h.tptr[c];
+    h.tidx.resize(h.tptr[ns]);
+    std::vector<int32_t> cur(h.tptr.begin(), h.tptr.end() - 1);
+    for (int64_t r = 0; r < n; ++r) {
+        h.tidx[cur[h.self_local[r]]++] = static_cast<int32_t>(-(r + 1));
+        for (int32_t e = h.nbr_ptr[r]; e < h.nbr_ptr[r + 1]; ++e)
+            h.tidx[cur[h.nbr[e]]++] = static_cast<int32_t>(r);
+    }
+    h.materialised = true;
+}
+
+static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
+                          const int32_t* fanouts, int32_t n_hops, int32_t flags) {
+    GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
+    GS_REQUIRE(n_roots >= 1 && roots, GS_EINVAL, "empty nodes_batch");
+    for (int64_t i = 0; i < n_roots; ++i)
+        GS_REQUIRE(roots[i] >= 0 && roots[i] < g.n_nodes, GS_ERANGE, "node id out of range");
+    std::unique_ptr<Sample> s(new Sample());
+    s->n_hops = n_hops;
+    s->flags = flags;
+    const bool gcn = flags & GS_SAMPLE_GCN;
+    std::vector<int64_t> frontier(roots, roots + n_roots);
+    for (int32_t j = 0; j < n_hops; ++j) {
+        Hop& h = s->hops[j];
+        h.k = fanouts ? fanouts[j] : 10;
+        h.dst_ids = frontier;
+        draw_positions(g, rng, h);
+        const bool last = (j == n_hops - 1);
+        if (!last || (flags & GS_SAMPLE_FULL)) {
+            materialise(g, h, gcn);
+            frontier = h.src_ids;
+        }
+    }
+    return s.release();
+}
+
+}  // namespace gs
+
+using gs::Hop;
+using gs::Sample;
+
+extern "C" {
+
+int gs_rng_create(gs_rng** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(out, GS_EINVAL, "out is NULL");
+    *out = new gs_rng();
+    const uint32_t zero = 0;
+    (*out)->mt.init_by_array(&zero, 1);
+    GS_API_END
+}
+
+void gs_rng_destroy(gs_rng* rng) { delete rng; }
+
+int gs_rng_seed_words(gs_rng* rng, const uint32_t* key, int64_t key_len) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && key && key_len >= 1, GS_EINVAL, "bad seed key");
+    rng->mt.init_by_array(key, static_cast<size_t>(key_len));
+    GS_API_END
+}
+
+int gs_rng_set_state(gs_rng* rng, const uint32_t* mt624, int64_t pos) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && mt624, GS_EINVAL, "bad state");
+    GS_REQUIRE(pos >= 0 && pos <= gs::MT19937::N, GS_EINVAL, "state index out of range");
+    std::memcpy(rng->mt.mt, mt624, sizeof(rng->mt.mt));
+    rng->mt.index = static_cast<int>(pos);
+    GS_API_END
+}
+
+int gs_rng_get_state(const gs_rng* rng, uint32_t* mt624, int64_t* pos) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && mt624 && pos, GS_EINVAL, "bad state buffers");
+    std::memcpy(mt624, rng->mt.mt, sizeof(rng->mt.mt));
+    *pos = rng->mt.index;
+    GS_API_END
+}
+
+int gs_rng_getrandbits(gs_rng* rng, int32_t k, int64_t count, uint32_t* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && out && count >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(k >= 1 && k <= 32, GS_EINVAL, "k must be in [1, 32]");
+    for (int64_t i = 0; i < count; ++i) out[i] = rng->mt.getrandbits(k);
+    GS_API_END
+}
+
+int gs_rng_randbelow(gs_rng* rng, uint32_t n, int64_t count, uint32_t* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && out && count >= 0, GS_EINVAL, "bad arguments");
+    for (int64_t i = 0; i < count; ++i) out[i] = rng->mt.randbelow(n);
+    GS_API_END
+}
+
+int gs_rng_sample_positions(gs_rng* rng, int64_t n, int64_t k, int64_t* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && (out || k == 0), GS_EINVAL, "bad arguments");
+    GS_REQUIRE(n >= 0 && n < (int64_t(1) << 32), GS_EINVAL, "population size out of range");
+    GS_REQUIRE(k >= 0 && k <= n, GS_ERANGE, "Sample larger than population or is negative");
+    std::vector<int64_t> scratch(2 * std::max<int64_t>(k, 1));
+    gs::sample_positions(rng->mt, n, k, gs::sample_setsize(k), out, scratch.data());
+    GS_API_END
+}
+
+int gs_rng_choice_position(gs_rng* rng, int64_t n, int64_t* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(rng && out, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(n >= 1 && n < (int64_t(1) << 32), GS_EINVAL, "choice from an empty sequence");
+    *out = rng->mt.randbelow(static_cast<uint64_t>(n));
+    GS_API_END
+}
+
+int gs_pyset_union_of_lists(const int64_t* items, const int64_t* ptr, int64_t n_lists, int64_t* out,
+                            int64_t* out_len) {
+    GS_API_BEGIN
+    GS_REQUIRE(ptr && out && out_len && n_lists >= 1, GS_EINVAL, "bad arguments");
+    std::vector<gs::PySet> sets(n_lists);
+    for (int64_t l = 0; l < n_lists; ++l)
+        for (int64_t t = ptr[l]; t < ptr[l + 1]; ++t) {
+            GS_REQUIRE(items[t] >= 0, GS_EINVAL, "keys must be non-negative");
+            sets[l].add(items[t]);
+        }
+    gs::PySet u = gs::copy_of(sets[0]);
+    for (int64_t l = 1; l < n_lists; ++l) u.merge(sets[l]);
+    int64_t w = 0;
+    u.for_each([&](int64_t key) { out[w++] = key; });
+    *out_len = w;
+    GS_API_END
+}
+
+int gs_sample_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots,
+                  const int32_t* fanouts, int32_t n_hops, int32_t flags, gs_sample** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(gp && rng && out, GS_EINVAL, "NULL graph/rng/out");
+    const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
+    *out = reinterpret_cast<gs_sample*>(
+        gs::run_sample(g, rng->mt, roots, n_roots, fanouts, n_hops, flags));
+    GS_API_END
+}
+
+void gs_sample_destroy(gs_sample* s) { delete reinterpret_cast<Sample*>(s); }
+
+int gs_sample_n_hops(const gs_sample* sp, int32_t* n_hops) {
+    GS_API_BEGIN
+    GS_REQUIRE(sp && n_hops, GS_EINVAL, "NULL argument");
+    *n_hops = reinterpret_cast<const Sample*>(sp)->n_hops;
+    GS_API_END
+}
+
+int gs_sample_hop(const gs_sample* sp, int32_t hop, gs_hop_view* v) {
+    GS_API_BEGIN
+    GS_REQUIRE(sp && v, GS_EINVAL, "NULL argument");
+    const Sample& s = *reinterpret_cast<const Sample*>(sp);
+    GS_REQUIRE(hop >= 1 && hop <= s.n_hops, GS_EINVAL, "hop out of range");
+    const Hop& h = s.hops[hop - 1];
+    std::memset(v, 0, sizeof(*v));
+    v->n_dst = static_cast<int64_t>(h.dst_ids.size());
+    v->n_pos = static_cast<int64_t>(h.pos.size());
+    v->dst_ids = h.dst_ids.data();
+    v->pos_ptr = h.pos_ptr.data();
+    v->pos = h.pos.data();
+    if (h.materialised) {
+        v->n_src = static_cast<int64_t>(h.src_ids.size());
+        v->n_nbr = static_cast<int64_t>(h.nbr.size());
+        v->src_ids = h.src_ids.data();
+        v->nbr_ptr = h.nbr_ptr.data();
+        v->nbr = h.nbr.data();
+        v->self_local = h.self_local.data();
+        v->set_ptr = h.set_ptr.data();
+        v->set_items = h.set_items.data();
+    } else {
+        v->n_src = -1;
+        v->n_nbr = -1;
+    }
+    GS_API_END
+}
+
+static void layout_of(const Sample& s, gs_pack_layout* L) {
+    for (auto& row : L->off)
+        for (auto& o : row) o = -1;
+    int64_t at = 0;
+    auto put = [&](int32_t hop, int field, int64_t n) {
+        L->off[hop][field] = at;
+        at += (n + 3) & ~int64_t(3);  // keep every array 16-byte aligned
+    };
+    for (int32_t j = 0; j < s.n_hops; ++j) {
+        const Hop& h = s.hops[j];
+        const int64_t nd = static_cast<int64_t>(h.dst_ids.size());
+        if (j == s.n_hops - 1) {
+            put(j, GS_PK_POS_PTR, nd + 1);
+            put(j, GS_PK_POS, static_cast<int64_t>(h.pos.size()));
+            put(j, GS_PK_DST_IDS, nd);
+        } else {
+            put(j, GS_PK_NBR_PTR, nd + 1);
+            put(j, GS_PK_NBR, static_cast<int64_t>(h.nbr.size()));
+            put(j, GS_PK_SELF, nd);
+            put(j, GS_PK_TPTR, static_cast<int64_t>(h.tptr.size()));
+            put(j, GS_PK_TIDX, static_cast<int64_t>(h.tidx.size()));
+        }
+    }
+    L->total = at;
+}
+
+int gs_sample_pack_layout(const gs_sample* sp, gs_pack_layout* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(sp && out, GS_EINVAL, "NULL argument");
+    layout_of(*reinterpret_cast<const Sample*>(sp), out);
+    GS_API_END
+}
+
+int gs_sample_pack(const gs_sample* sp, int32_t* buf, int64_t cap) {
+    GS_API_BEGIN
+    GS_REQUIRE(sp && buf, GS_EINVAL, "NULL argument");
+    const Sample& s = *reinterpret_cast<const Sample*>(sp);
+    gs_pack_layout L;
+    layout_of(s, &L);
+    GS_REQUIRE(cap >= L.total, GS_EINVAL, "pack buffer too small");
+    auto cpy = [&](int32_t j, int f, const int32_t* p, size_t n) {
+        if (n) std::memcpy(buf + L.off[j][f], p, n * sizeof(int32_t));
+    };
+    for (int32_t j = 0; j < s.n_hops; ++j) {
+        const Hop& h = s.hops[j];
+        if (j == s.n_hops - 1) {
+            cpy(j, GS_PK_POS_PTR, h.pos_ptr.data(), h.pos_ptr.size());
+            cpy(j, GS_PK_POS, h.pos.data(), h.pos.size());
+            int32_t* d = buf + L.off[j][GS_PK_DST_IDS];
+            for (size_t r = 0; r < h.dst_ids.size(); ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
+        } else {
+            cpy(j, GS_PK_NBR_PTR, h.nbr_ptr.data(), h.nbr_ptr.size());
+            cpy(j, GS_PK_NBR, h.nbr.data(), h.nbr.size());
+            cpy(j, GS_PK_SELF, h.self_local.data(), h.self_local.size());
+            cpy(j, GS_PK_TPTR, h.tptr.data(), h.tptr.size());
+            cpy(j, GS_PK_TIDX, h.tidx.data(), h.tidx.size());
+        }
+    }
+    GS_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,286 @@
+// Segmented gather-aggregate for GraphSage.aggregate (models.py:291-330) and
+// its backward.  The reference builds a dense [n_dst, n_src] 0/1 mask and
+// multiplies (MEAN, :305-314) or loops rows in Python (MAX, :316-326); here
+// each destination is owned by a group of G lanes of one wavefront that
+// streams its neighbours' feature rows straight from HBM (16 B per lane, so a
+// 1 KiB fp32 F=256 row is one coalesced wave load) and reduces in registers.
+// Nothing of size n_dst x n_src is ever formed.
+#include "kcommon.hpp"
+
+namespace gs {
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;  // neighbour rows in flight per lane group
+
+// One group of G lanes per destination r.  EXPAND: the neighbourhood is the
+// sampled positions idx[ptr[r]..ptr[r+1]) of node dst_ids[r]'s CSR row,
+// expanded on the fly (col[row_ptr[node] + pos]); self is skipped unless gcn,
+// and gcn adds it once (models.py:285, :297-298).  Otherwise idx holds the
+// source rows of X directly (already self-filtered and ascending).
+template <int OP, typename T, int VEC, int G, bool EXPAND>
+__global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
+    const T* __restrict__ X, int64_t ldx, int F, int n_dst, const int* __restrict__ ptr,
+    const int* __restrict__ idx, const int64_t* __restrict__ row_ptr, const int* __restrict__ col,
+    const int* __restrict__ dst_ids, int gcn, T* __restrict__ out, int64_t ldo,
+    int* __restrict__ argmax) {
+    const int gl = threadIdx.x % G;
+    const int r = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    if (r >= n_dst) return;  // whole lane groups leave together
+    const int beg = ptr[r], end = ptr[r + 1];
+    int node = 0;
+    int64_t rs = 0;
+    if (EXPAND) {
+        node = dst_ids[r];
+        rs = row_ptr[node];
+    }
+    const bool want_am = (OP == GS_AGG_MAX) && (argmax != nullptr);
+    for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
+        const bool act = f0 < F;
+        float acc[VEC];
+        int am[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+            acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
+            am[v] = -1;
+        }
+        int cnt = 0;
+        for (int base = beg; base < end; base += G) {
+            const int m = min(G, end - base);
+            int my = -1;
+            if (gl < m) {
+                const int e = idx[base + gl];
+                if (EXPAND) {
+                    const int nb = col[rs + e];
+                    my = (gcn || nb != node) ? nb : -1;
+                } else {
+                    my = e;
+                }
+            }
+            for (int j = 0; j < m; j += kUnroll) {
+                int rows[kUnroll];
+                float x[kUnroll][VEC];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    rows[u] = __shfl(my, j + u < m ? j + u : 0, G);
+                    if (j + u >= m) rows[u] = -1;
+                }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    if (rows[u] >= 0 && act) RowIO<T, VEC>::load(X + static_cast<int64_t>(rows[u]) * ldx + f0, x[u]);
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    if (rows[u] < 0) continue;
+                    ++cnt;
+                    if (!act) continue;
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) {
+                        if (OP == GS_AGG_MEAN) {
+                            acc[v] += x[u][v];
+                        } else if (x[u][v] > acc[v]) {  // strict: first index wins ties
+                            acc[v] = x[u][v];
+                            am[v] = rows[u];
+                        }
+                    }
+                }
+            }
+        }
+        if (EXPAND && gcn) {
+            bool self_seen = false;  // gcn keeps self exactly once (set semantics)
+            for (int e = beg; e < end; ++e) self_seen |= (col[rs + idx[e]] == node);
+            if (!self_seen) {
+                ++cnt;
+                if (act) {
+                    float x[VEC];
+                    RowIO<T, VEC>::load(X + static_cast<int64_t>(node) * ldx + f0, x);
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) {
+                        if (OP == GS_AGG_MEAN) acc[v] += x[v];
+                        else if (x[v] > acc[v]) { acc[v] = x[v]; am[v] = node; }
+                    }
+                }
+            }
+        }
+        if (!act) continue;
+        if (OP == GS_AGG_MEAN) {
+            const float inv = 1.0f / static_cast<float>(cnt);  // cnt == 0 -> NaN row, as 0/0 in :313
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v] *= inv;
+        }
+        RowIO<T, VEC>::store(out + static_cast<int64_t>(r) * ldo + f0, acc);
+        if (want_am) {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) argmax[static_cast<int64_t>(r) * F + f0 + v] = am[v];
+        }
+    }
+}
+
+// Backward over source rows c (transposed neighbourhood lists, GS_PK_TIDX
+// encoding): self-row gradient + mean/max routing, then the relu mask of the
+// layer that produced these rows.  Fixed order, no atomics.
+template <int OP, int VEC, int G>
+__global__ __launch_bounds__(kBlock) void agg_bwd_kernel(
+    int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,
+    const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
+    int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
+    float* __restrict__ dH) {
+    const int gl = threadIdx.x % G;
+    const int c = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    if (c >= n_src) return;
+    const int beg = tptr[c], end = tptr[c + 1];
+    for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
+        const bool act = f0 < F;
+        float g[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) g[v] = 0.f;
+        for (int t = beg; t < end; ++t) {
+            const int e = tidx[t];
+            if (!act) continue;
+            float x[VEC];
+            if (e < 0) {
+                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0, x);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += x[v];
+            } else if (OP == GS_AGG_MEAN) {
+                const float w = 1.0f / static_cast<float>(ptr[e + 1] - ptr[e]);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += x[v] * w;
+            } else {
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v)
+                    if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += x[v];
+            }
+        }
+        if (!act) continue;
+        if (Hprev) {
+            float h[VEC];
+            RowIO<float, VEC>::load(Hprev + static_cast<int64_t>(c) * ldh + f0, h);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) g[v] = h[v] > 0.f ? g[v] : 0.f;
+        }
+        RowIO<float, VEC>::store(dH + static_cast<int64_t>(c) * ldh + f0, g);
+    }
+}
+
+static int pick_group(int F, int vec) {
+    const int lanes = (F + vec - 1) / vec;
+    int g = 16;
+    while (g < lanes && g < 64) g <<= 1;
+    return g;
+}
+
+template <int OP, typename T, bool EXPAND>
+static void launch_fwd(int vec, const T* X, int64_t ldx, int F, int n_dst, const int* ptr,
+                       const int* idx, const int64_t* row_ptr, const int* col, const int* dst_ids,
+                       int gcn, T* out, int64_t ldo, int* am, hipStream_t st) {
+    constexpr int V = sizeof(T) == 4 ? 4 : 8;
+    if (vec == 1) {
+        const dim3 grid((n_dst + (kBlock / 64) - 1) / (kBlock / 64));
+        agg_fwd_kernel<OP, T, 1, 64, EXPAND><<<grid, kBlock, 0, st>>>(X, ldx, F, n_dst, ptr, idx, row_ptr,
+                                                                       col, dst_ids, gcn, out, ldo, am);
+        return;
+    }
+    const int G = pick_group(F, V);
+    const dim3 grid((n_dst + (kBlock / G) - 1) / (kBlock / G));
+#define GS_AGG_FWD(GG)                                                                              \
+    agg_fwd_kernel<OP, T, V, GG, EXPAND><<<grid, kBlock, 0, st>>>(X, ldx, F, n_dst, ptr, idx, row_ptr, \
+                                                                   col, dst_ids, gcn, out, ldo, am)
+    if (G == 16) GS_AGG_FWD(16);
+    else if (G == 32) GS_AGG_FWD(32);
+    else GS_AGG_FWD(64);
+#undef GS_AGG_FWD
+}
+
+template <int OP>
+static void launch_bwd(int vec, int n_src, int F, const int* tptr, const int* tidx, const int* ptr,
+                       const float* dA, const float* dSelf, int64_t ldd, const int* am,
+                       const float* Hprev, int64_t ldh, float* dH, hipStream_t st) {
+    if (vec == 1) {
+        const dim3 grid((n_src + 3) / 4);
+        agg_bwd_kernel<OP, 1, 64><<<grid, kBlock, 0, st>>>(n_src, F, tptr, tidx, ptr, dA, dSelf, ldd, am,
+                                                           Hprev, ldh, dH);
+        return;
+    }
+    const int G = pick_group(F, 4);
+    const dim3 grid((n_src + (kBlock / G) - 1) / (kBlock / G));
+#define GS_AGG_BWD(GG)                                                                          \
+    agg_bwd_kernel<OP, 4, GG><<<grid, kBlock, 0, st>>>(n_src, F, tptr, tidx, ptr, dA, dSelf, ldd, am, \
+                                                       Hprev, ldh, dH)
+    if (G == 16) GS_AGG_BWD(16);
+    else if (G == 32) GS_AGG_BWD(32);
+    else GS_AGG_BWD(64);
+#undef GS_AGG_BWD
+}
+
+}  // namespace gs
+
+extern "C" {
+
+int gs_agg_fwd(gs_agg op, gs_dtype xdt, const void* X, int64_t ldx, int64_t F, int64_t n_dst,
+               const int32_t* ptr, const int32_t* idx, const int64_t* row_ptr, const int32_t* col,
+               const int32_t* dst_ids, int32_t gcn, void* out, gs_dtype odt, int64_t ldo,
+               int32_t* argmax, void* stream) {
+    GS_API_BEGIN
+    using namespace gs;
+    GS_REQUIRE(op == GS_AGG_MEAN || op == GS_AGG_MAX, GS_EINVAL, "agg_func must be MEAN or MAX");
+    GS_REQUIRE(xdt == odt, GS_EINVAL, "output dtype must equal feature dtype");
+    GS_REQUIRE(F >= 1 && F < (1 << 30) && n_dst >= 0 && n_dst < (int64_t(1) << 31), GS_EINVAL, "bad sizes");
+    GS_REQUIRE(ldx >= F && ldo >= F, GS_EINVAL, "leading dimension smaller than F");
+    if (n_dst == 0) return GS_OK;
+    GS_REQUIRE(X && ptr && idx && out, GS_EINVAL, "NULL device pointer");
+    const bool expand = row_ptr != nullptr;
+    GS_REQUIRE(!expand || (col && dst_ids), GS_EINVAL, "expand mode needs col and dst_ids");
+    GS_REQUIRE(!(argmax && expand), GS_EINVAL, "argmax is only produced in explicit mode");
+    const int V = xdt == GS_F32 ? 4 : 8;
+    const int vec = (F % V == 0 && ldx % V == 0 && ldo % V == 0 && aligned16(X) && aligned16(out)) ? V : 1;
+    hipStream_t st = as_stream(stream);
+    const int f = static_cast<int>(F), n = static_cast<int>(n_dst);
+#define GS_DISPATCH(OPV, TT)                                                                              \
+    do {                                                                                                  \
+        if (expand)                                                                                       \
+            launch_fwd<OPV, TT, true>(vec, static_cast<const TT*>(X), ldx, f, n, ptr, idx, row_ptr, col,  \
+                                      dst_ids, gcn, static_cast<TT*>(out), ldo, nullptr, st);             \
+        else                                                                                              \
+            launch_fwd<OPV, TT, false>(vec, static_cast<const TT*>(X), ldx, f, n, ptr, idx, nullptr,      \
+                                       nullptr, nullptr, 0, static_cast<TT*>(out), ldo, argmax, st);      \
+    } while (0)
+    if (op == GS_AGG_MEAN) {
+        if (xdt == GS_F32) GS_DISPATCH(GS_AGG_MEAN, float);
+        else GS_DISPATCH(GS_AGG_MEAN, bf16_t);
+    } else {
+        if (xdt == GS_F32) GS_DISPATCH(GS_AGG_MAX, float);
+        else GS_DISPATCH(GS_AGG_MAX, bf16_t);
+    }
+#undef GS_DISPATCH
+    check_launch("gs_agg_fwd");
+    GS_API_END
+}
+
+int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr, const int32_t* tidx,
+               const int32_t* ptr, const float* dA, const float* dSelf, int64_t ldd,
+               const int32_t* argmax, const float* Hprev, int64_t ldh, float* dH, void* stream) {
+    GS_API_BEGIN
+    using namespace gs;
+    GS_REQUIRE(op == GS_AGG_MEAN || op == GS_AGG_MAX, GS_EINVAL, "agg_func must be MEAN or MAX");
+    GS_REQUIRE(F >= 1 && n_src >= 0 && n_src < (int64_t(1) << 31), GS_EINVAL, "bad sizes");
+    GS_REQUIRE(ldd >= F && ldh >= F, GS_EINVAL, "leading dimension smaller than F");
+    if (n_src == 0) return GS_OK;
+    GS_REQUIRE(tptr && tidx && ptr && dA && dSelf && dH, GS_EINVAL, "NULL device pointer");
+    GS_REQUIRE(op != GS_AGG_MAX || argmax, GS_EINVAL, "MAX backward needs argmax");
+    const int vec = (F % 4 == 0 && ldd % 4 == 0 && ldh % 4 == 0 && aligned16(dA) && aligned16(dSelf) &&
+                     aligned16(dH) && (!Hprev || aligned16(Hprev)))
+                        ? 4
+                        : 1;
+    hipStream_t st = as_stream(stream);
+    if (op == GS_AGG_MEAN)
+        launch_bwd<GS_AGG_MEAN>(vec, static_cast<int>(n_src), static_cast<int>(F), tptr, tidx, ptr, dA, dSelf,
+                                ldd, argmax, Hprev, ldh, dH, st);
+    else
+        launch_bwd<GS_AGG_MAX>(vec, static_cast<int>(n_src), static_cast<int>(F), tptr, tidx, ptr, dA, dSelf,
+                               ldd, argmax, Hprev, ldh, dH, st);
+    check_launch("gs_agg_bwd");
+    GS_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+/*
+ * graphsage_amd.h — C-ABI of libgraphsage_amd.so, the MI355X-native GraphSAGE
+ * sample-and-aggregate path.
+ *
+ * Plain C types only: pointers, sizes, enums.  No torch types cross this line.
+ * Every function returns an int status (GS_OK == 0); on failure the calling
+ * thread's message is available from gs_last_error().  Device entry points are
+ * asynchronous on the caller's hipStream_t (passed as void*) and never allocate
+ * or synchronise: the caller owns every buffer (the Python host allocates them
+ * through the torch caching allocator).
+ *
+ * Each entry point names the reference code it stands in for
+ * (paths relative to Lolash/graphSAGE-pytorch).
+ */
+#ifndef GRAPHSAGE_AMD_H
+#define GRAPHSAGE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+#define GS_OK 0
+#define GS_EINVAL 1  /* bad argument (ValueError in the Python host)              */
+#define GS_ENOMEM 2  /* host allocation failed                                    */
+#define GS_EHIP 3    /* HIP runtime error (launch/config)                         */
+#define GS_ERANGE 4  /* "Sample larger than population" / id out of range          */
+#define GS_EEMPTY 5  /* MAX over an empty neighbourhood (reference: IndexError,
+                        models.py:321-325)                                       */
+
+const char* gs_last_error(void);
+const char* gs_version(void);
+
+/* ------------------------------------------------------------------- RNG
+ * CPython 3.10 `random.Random` (MT19937) stream.  The reference draws every
+ * neighbour sample from the module-global `random` (models.py:281-282) and
+ * shares that stream with UnsupervisedLoss (models.py:164,178); the handle
+ * below is interchangeable with random.getstate()/setstate() (version 3). */
+typedef struct gs_rng gs_rng;
+
+int gs_rng_create(gs_rng** out);
+void gs_rng_destroy(gs_rng* rng);
+/* random.seed(n) for an int n: key = little-endian 32-bit words of abs(n)
+ * (main.py:40 seeds with 824). */
+int gs_rng_seed_words(gs_rng* rng, const uint32_t* key, int64_t key_len);
+/* random.setstate((3, mt[0..623] + (pos,), gauss)) / getstate(). */
+int gs_rng_set_state(gs_rng* rng, const uint32_t* mt624, int64_t pos);
+int gs_rng_get_state(const gs_rng* rng, uint32_t* mt624, int64_t* pos);
+/* Known-answer helpers: getrandbits(k) (k<=32) and _randbelow(n), `count` times. */
+int gs_rng_getrandbits(gs_rng* rng, int32_t k, int64_t count, uint32_t* out);
+int gs_rng_randbelow(gs_rng* rng, uint32_t n, int64_t count, uint32_t* out);
+/* random.sample(range(n), k) as positions (both CPython branches, random.py
+ * sample(); what models.py:282 calls on tuple(adj_set)). */
+int gs_rng_sample_positions(gs_rng* rng, int64_t n, int64_t k, int64_t* out);
+/* random.choice(seq) position for len(seq)==n (models.py:178). */
+int gs_rng_choice_position(gs_rng* rng, int64_t n, int64_t* out);
+
+/* ------------------------------------------------- CPython set known answers
+ * list(set.union(*[set(l) for l in lists])) — the set(list) + union that
+ * produce the frontier order at models.py:282-286.  out must hold Σ len. */
+int gs_pyset_union_of_lists(const int64_t* items, const int64_t* ptr,
+                            int64_t n_lists, int64_t* out, int64_t* out_len);
+
+/* ------------------------------------------------------------------ graph
+ * Adjacency in CPython-set iteration order.  Replaces the dict-of-sets built
+ * by DataCenter (dataCenter.py:33-41 cora, :77-86 pubmed):
+ *   for (a, b) in pairs: adj[a].add(b); adj[b].add(a)
+ * Row v of the CSR lists tuple(adj[v]) — the population random.sample sees.
+ * The slot layout of each row's set is kept (host side) because a row with
+ * fewer than k neighbours enters the frontier union as that very set
+ * (models.py:282, :285). */
+typedef struct gs_graph gs_graph;
+
+int gs_graph_build(const int64_t* src, const int64_t* dst, int64_t n_pairs,
+                   int64_t n_nodes, int32_t n_threads, gs_graph** out);
+/* Adopt rows whose set layout the caller read from live CPython set objects
+ * (the drop-in path: GraphSage(adj_lists=...) with a caller-built dict of
+ * sets).  Per row v: entries row_ptr[v]..row_ptr[v+1] in slot order, slot[e]
+ * their table slots (strictly increasing), table size 1 << log2size[v];
+ * dirty[v] != 0 when the set holds dummy entries (fill != used).  dirty may
+ * be NULL. */
+int gs_graph_from_tables(int64_t n_nodes, const int64_t* row_ptr,
+                         const int32_t* col, const uint32_t* slot,
+                         const uint8_t* log2size, const uint8_t* dirty,
+                         gs_graph** out);
+void gs_graph_destroy(gs_graph* g);
+int gs_graph_dims(const gs_graph* g, int64_t* n_nodes, int64_t* n_entries,
+                  int64_t* max_degree);
+/* Borrowed views, valid until gs_graph_destroy: row_ptr[n_nodes+1], col[n_entries]. */
+const int64_t* gs_graph_row_ptr(const gs_graph* g);
+const int32_t* gs_graph_col(const gs_graph* g);
+
+/* Synthetic R-MAT(a,b,c,1-a-b-c) pair list: `scale` id bits,
+ * n_pairs draws, self pairs dropped, optional seeded id permutation.
+ * src/dst must hold n_pairs; *n_kept receives the pairs written. */
+int gs_rmat_pairs(int32_t scale, int64_t n_pairs, double a, double b, double c,
+                  uint64_t seed, int32_t permute, int32_t n_threads,
+                  int64_t* src, int64_t* dst, int64_t* n_kept);
+
+/* ---------------------------------------------------------------- sampler
+ * GraphSage._get_unique_neighs_list (models.py:277-289) for every hop of a
+ * forward (models.py:246-251), consuming the rng exactly as the reference.
+ *
+ * Hops are numbered from the roots: hop 1 samples the roots (frontier F0 =
+ * nodes_batch) and its union is F1; hop j samples F(j-1) and unions into Fj.
+ * fanouts[j-1] = num_sample of hop j (the reference hard-codes 10); <=0 means
+ * "no sampling" (num_sample=None, models.py:283-284).
+ *
+ * The last hop's union (the deepest frontier, L0 of the reference) only feeds
+ * a row gather, so unless GS_SAMPLE_FULL is set it is not materialised: its
+ * sampled *positions* go to the device, which expands them through the CSR. */
+#define GS_SAMPLE_GCN 1  /* gcn=True: self stays in its own neighbourhood      */
+#define GS_SAMPLE_FULL 2 /* materialise the last hop's sets + union (API/parity) */
+#define GS_MAX_HOPS 8
+
+typedef struct gs_sample gs_sample;
+
+typedef struct {
+    int64_t n_dst;            /* |F(j-1)|                                       */
+    int64_t n_pos;            /* sampled row positions = Σ min(deg, k)           */
+    int64_t n_src;            /* |Fj|, -1 when not materialised                  */
+    int64_t n_nbr;            /* neighbourhood entries after the self rule, -1   */
+    const int64_t* dst_ids;   /* [n_dst] F(j-1) in order                         */
+    const int32_t* pos_ptr;   /* [n_dst+1]                                       */
+    const int32_t* pos;       /* [n_pos] positions into CSR row of dst, in
+                                 random.sample result order (or row order)       */
+    const int64_t* src_ids;   /* [n_src] Fj in CPython set order (models.py:286) */
+    const int32_t* nbr_ptr;   /* [n_dst+1]                                       */
+    const int32_t* nbr;       /* [n_nbr] index into src_ids, ascending per dst
+                                 (the dense mask's column order, models.py:306)  */
+    const int32_t* self_local;/* [n_dst] index of dst in Fj (_nodes_map :271)    */
+    const int32_t* set_ptr;   /* [n_dst+1] samp_neighs[i] incl. self, iteration */
+    const int64_t* set_items; /*   order of the reference's set object           */
+} gs_hop_view;
+
+/* Device pack: everything the kernels read for one batch, one int32 buffer. */
+enum {
+    GS_PK_POS_PTR = 0, /* last hop: [n_dst+1]                                 */
+    GS_PK_POS,         /* last hop: [n_pos]                                   */
+    GS_PK_DST_IDS,     /* last hop: [n_dst] global ids of F(L-1)              */
+    GS_PK_NBR_PTR,     /* hops < L: [n_dst+1]                                 */
+    GS_PK_NBR,         /* hops < L: [n_nbr]                                   */
+    GS_PK_SELF,        /* hops < L: [n_dst]                                   */
+    GS_PK_TPTR,        /* hops < L: transposed CSR over Fj, [n_src+1]         */
+    GS_PK_TIDX,        /* hops < L: [n_nbr + n_dst] per source c, ascending r:
+                          r >= 0 → c is in dst r's neighbourhood,
+                          -(r+1) → c is dst r's own (self) row               */
+    GS_PK_NFIELDS
+};
+
+typedef struct {
+    int64_t total;                               /* int32 elements            */
+    int64_t off[GS_MAX_HOPS][GS_PK_NFIELDS];     /* element offsets, -1 absent */
+} gs_pack_layout;
+
+int gs_sample_run(const gs_graph* g, gs_rng* rng, const int64_t* roots,
+                  int64_t n_roots, const int32_t* fanouts, int32_t n_hops,
+                  int32_t flags, gs_sample** out);
+void gs_sample_destroy(gs_sample* s);
+int gs_sample_n_hops(const gs_sample* s, int32_t* n_hops);
+int gs_sample_hop(const gs_sample* s, int32_t hop, gs_hop_view* out);
+int gs_sample_pack_layout(const gs_sample* s, gs_pack_layout* out);
+/* Writes the layout's int32 image into buf (cap elements, typically pinned). */
+int gs_sample_pack(const gs_sample* s, int32_t* buf, int64_t cap);
+
+/* --------------------------------------------------------- device kernels */
+typedef enum { GS_F32 = 0, GS_BF16 = 1 } gs_dtype;
+typedef enum { GS_AGG_MEAN = 0, GS_AGG_MAX = 1 } gs_agg;
+
+/* Fill X[N, F] (row stride ld) with U(-1,1) from a counter hash of
+ * (seed, row, col) — the synthetic feature table. */
+int gs_fill_uniform(void* X, gs_dtype dt, int64_t N, int64_t F, int64_t ld,
+                    uint64_t seed, void* stream);
+/* Mirror of the host feature hash for checks (fp32, n values). */
+int gs_uniform_host(uint64_t seed, int64_t row0, int64_t F, int64_t n_rows,
+                    float* out);
+
+/* GraphSage.aggregate (models.py:291-330): mean (mask/rowsum @ X, :311-314)
+ * or element-wise max (:316-326) of source rows per destination.
+ *   explicit mode (row_ptr == NULL): sources of dst r are rows idx[ptr[r]..ptr[r+1]).
+ *   expand mode (row_ptr != NULL): node = dst_ids[r]; sources are
+ *     col[row_ptr[node] + idx[e]], minus node itself unless gcn; gcn adds node
+ *     once (models.py:285, :297-298).
+ * MEAN of an empty neighbourhood is NaN like the reference (0/0); MAX of one
+ * is reported as GS_EEMPTY by the host before launch.  argmax (MAX, optional)
+ * receives the winning source row per element, first index on ties. */
+int gs_agg_fwd(gs_agg op, gs_dtype xdt, const void* X, int64_t ldx, int64_t F,
+               int64_t n_dst, const int32_t* ptr, const int32_t* idx,
+               const int64_t* row_ptr, const int32_t* col,
+               const int32_t* dst_ids, int32_t gcn,
+               void* out, gs_dtype odt, int64_t ldo, int32_t* argmax,
+               void* stream);
+
+/* SageLayer.forward (models.py:209-220):
+ *   out[n, H] = relu( [Xs[sidx[i]] | A[i]] · Wᵀ )   (cat order self first, :216)
+ * Xs == NULL → gcn form out = relu(A · Wᵀ) with W [H, F] (:218).
+ * sidx == NULL → identity.  W is [H, K] with K = 2F (or F); Wd is W in the
+ * compute dtype (== W for GS_F32).  Inputs of dtype dt, fp32 accumulate. */
+int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H,
+                       const void* Xs, int64_t ldxs, const int32_t* sidx,
+                       const void* A, int64_t lda, const void* Wd,
+                       float* out, int64_t ldo, int32_t relu, void* stream);
+
+/* Autograd of SageLayer (utils.py:184 through models.py:219):
+ *   dZ = dOut ⊙ (out > 0)        (relu backward; relu=0 → dZ = dOut)
+ *   dW[H, K] = dZᵀ · [Xs[sidx] | A]      (overwritten)
+ * ws: fp32 workspace of gs_sage_linear_bwd_weight_ws(n, K, H) bytes. */
+int64_t gs_sage_linear_bwd_weight_ws(int64_t n, int64_t K, int64_t H);
+int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H,
+                              const void* Xs, int64_t ldxs, const int32_t* sidx,
+                              const void* A, int64_t lda,
+                              const float* dout, const float* out, int64_t ldo,
+                              int32_t relu, float* dW, void* ws, int64_t ws_bytes,
+                              void* stream);
+/*   dIn[n, K] = dZ · W, written as dSelf[n, F] | dA[n, F] (dSelf NULL in gcn). */
+int gs_sage_linear_bwd_input(int64_t n, int64_t F, int64_t H,
+                             const float* dout, const float* out, int64_t ldo,
+                             int32_t relu, const float* W,
+                             float* dSelf, float* dA, int64_t ldd, void* stream);
+
+/* Backward of aggregate + the self-row gather of the next layer
+ * (models.py:265 `pre_hidden_embs[nb]`, :314 mask.mm), over source rows c of
+ * the previous hidden state, with the transposed CSR of one hop
+ * (GS_PK_TPTR / GS_PK_TIDX encoding):
+ *   g[c] = Σ_{t ∈ tptr[c]..tptr[c+1]}  tidx[t] = -(r+1) : dSelf[r]
+ *                                       tidx[t] = r      : MEAN dA[r] / deg(r)
+ *                                                          MAX  dA[r] where argmax[r] == c
+ *   dH[c] = g[c] ⊙ (Hprev[c] > 0)   (the relu of the layer below; Hprev NULL → g)
+ * deg(r) = ptr[r+1] - ptr[r] of the forward neighbourhood.  Deterministic:
+ * no atomics, fixed summation order. */
+int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr,
+               const int32_t* tidx, const int32_t* ptr,
+               const float* dA, const float* dSelf, int64_t ldd,
+               const int32_t* argmax, const float* Hprev, int64_t ldh,
+               float* dH, void* stream);
+
+/* Classification (models.py:8-27) + NLL mean (utils.py:159-164), fused
+ * forward + backward: logits = E·Wcᵀ + bc, logp = log_softmax (max-shifted),
+ * loss = -Σ_i logp[i, y_i] / B; writes loss[0], dE[B,D], dWc[C,D], dbc[C]
+ * (all overwritten).  ws: gs_cls_nll_ws_floats(B, D, C) floats.
+ * Deterministic (fixed-order partial sums, no atomics). */
+int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C);
+int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E,
+                       const float* Wc, const float* bc, const int32_t* labels,
+                       float* loss, float* dE, float* dWc, float* dbc, float* ws,
+                       void* stream);
+
+/* clip_grad_norm_(params, max_norm) per group (utils.py:185-186) then SGD
+ * (utils.py:136,187): p -= lr * g * min(1, max_norm / (||g_group|| + 1e-6)).
+ * grads scaled by `grad_scale` first (1/world_size after an RCCL sum).
+ * Groups are contiguous ranges [goff[i], goff[i+1]) of the flat buffers.
+ * ws: fp32 workspace of >= 65 * n_groups floats.  Up to 8 groups. */
+int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params,
+                float* grads, float grad_scale, float max_norm, float lr,
+                float* ws, void* stream);
+
+/* f32 → bf16 (RNE) cast, n elements. */
+int gs_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRAPHSAGE_AMD_H */
