@@ -1,0 +1,261 @@
+"""Headline benchmark: GraphSAGE supervised training throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config rmat2m]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (data parallel, RCCL)
+
+A step = one pass of the hot path over one batch of B roots per GPU: sample
+both hops (bit-exact host sampler, prefetched on a thread) -> one H2D copy ->
+layer-1 gather-aggregate + MFMA SageLayer -> layer 2 -> classifier + NLL ->
+full backward -> RCCL all-reduce of the flat gradient -> clip + SGD.
+Throughput = roots processed by all ranks / max-over-ranks wall time of the
+timed steps (weak scaling: B roots per GPU per step).
+
+Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel (the
+layer-1 gather-aggregate, K-agg) from its algorithmic bytes and its HIP-event
+duration inside the timed region; `cpu_baseline` times the oracle (the CPU
+restatement of the reference's algorithm) on a bounded sample of the same
+workload on this host.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import importlib  # noqa: E402
+
+gs = importlib.import_module("graphsage-pytorch_amd")
+from importlib import import_module  # noqa: E402
+
+train = import_module("graphsage-pytorch_amd.train")
+ops = import_module("graphsage-pytorch_amd.hip_ops")
+models = import_module("graphsage-pytorch_amd.models")
+
+CONFIGS = {
+    # BASELINE.json configs[2]: the headline metric's workload
+    "rmat2m": dict(scale=21, pairs=20_000_000, feat=256, fanouts=(25, 10), agg="MEAN", dtype="fp32",
+                   batch=512, classes=16),
+    # configs[3]
+    "rmat2m-max-bf16": dict(scale=21, pairs=20_000_000, feat=256, fanouts=(25, 10), agg="MAX",
+                            dtype="bf16", batch=512, classes=16),
+    # configs[4] (per-GPU share of the 8-GPU job)
+    "rmat16m": dict(scale=24, pairs=160_000_000, feat=128, fanouts=(25, 10), agg="MEAN", dtype="fp32",
+                    batch=512, classes=16),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def host_threads():
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def build_workload(cfg, device, seed=824):
+    t0 = time.perf_counter()
+    src, dst = gs.rmat_pairs(cfg["scale"], cfg["pairs"], seed=seed, n_threads=host_threads())
+    n = 1 << cfg["scale"]
+    graph = gs.CSRGraph.from_pairs(src, dst, n, n_threads=host_threads())
+    t_graph = time.perf_counter() - t0
+    dt = torch.bfloat16 if cfg["dtype"] == "bf16" else torch.float32
+    X = torch.empty(n, cfg["feat"], dtype=dt, device=device)
+    ops.fill_uniform(X, seed)
+    labels = torch.from_numpy((np.arange(n, dtype=np.int64) % cfg["classes"]).astype(np.int32)).to(device)
+    deg = graph.degrees()
+    candidates = np.nonzero(deg > 0)[0]
+    return dict(src=src, dst=dst, n=n, graph=graph, X=X, labels=labels, candidates=candidates,
+                t_graph=t_graph, deg=deg)
+
+
+class Agg1Timer:
+    """HIP events around the layer-1 gather-aggregate launch, on its stream."""
+
+    def __init__(self):
+        self.pairs = []
+        self.bytes = []
+        self.active = False
+        self._orig = None
+
+    def install(self, elem_bytes):
+        orig = ops.agg_fwd
+        timer = self
+
+        def timed(agg_func, X, ptr_, idx, out, **kw):
+            if not (timer.active and kw.get("row_ptr") is not None):
+                return orig(agg_func, X, ptr_, idx, out, **kw)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            r = orig(agg_func, X, ptr_, idx, out, **kw)
+            b.record()
+            timer.pairs.append((a, b))
+            return r
+
+        self._orig = orig
+        models.ops.agg_fwd = timed
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+
+
+def agg1_bytes(s, F, elem):
+    """Algorithmic HBM bytes of one layer-1 K-agg launch:
+    neighbour feature rows once per sampled edge + sampled positions and CSR
+    column entries (4 B each) + one output row per destination + per-destination
+    metadata (dst id 4 B, row_ptr 8 B, pos_ptr 4 B)."""
+    L = s.n_hops
+    n_dst, n_pos, _, _ = s.sizes(L)
+    return n_pos * (F * elem + 8) + n_dst * (F * elem + 16)
+
+
+def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
+    """Oracle train step (CPU restatement of the reference) on this host."""
+    import random as pyrandom
+    import oracle
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    adj = oracle.Adjacency(wl["src"], wl["dst"], wl["n"])
+    t_adj = time.perf_counter() - t0
+    sage_w, cls_w, cls_b = train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, seed)
+    W = [w.clone().requires_grad_(True) for w in sage_w]
+    cw, cb = cls_w.clone().requires_grad_(True), cls_b.clone().requires_grad_(True)
+    X = wl["X"].float().cpu()  # same feature table, fetched once (not timed)
+    labels_all = wl["labels"].cpu().long()
+    batches = train.rank_batches(wl["candidates"], cfg["batch"], 0, 1, seed + 1000)
+    pyrandom.seed(seed)
+    times = []
+    t_start = time.perf_counter()
+    for i, roots in enumerate(batches):
+        t = time.perf_counter()
+        oracle.train_step_dense(adj, roots.tolist(), list(cfg["fanouts"]), X, W, cw, cb,
+                                labels_all[torch.from_numpy(roots)], agg=cfg["agg"])
+        times.append(time.perf_counter() - t)
+        if time.perf_counter() - t_start > seconds_budget and len(times) >= 3:
+            break
+    med = float(np.median(times[1:] if len(times) > 1 else times))
+    return {"value": cfg["batch"] / med, "unit": "root nodes/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle train steps of B={cfg['batch']} roots (first untimed), "
+                      f"median {med * 1e3:.1f} ms/step; lazy dict-of-sets adjacency (built "
+                      f"per touched node), dense-mask mean, torch CPU {threads} threads; "
+                      f"pair-list indexing {t_adj:.1f} s excluded"}
+
+
+def load_traffic(config_name):
+    """Per-launch HBM bytes of K-agg from a committed rocprofv3 --pmc summary."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("config") == config_name and "agg1_hbm_bytes_per_launch" in d:
+            best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="rmat2m", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=824)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0)
+    args = ap.parse_args()
+
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["batch"] = args.batch
+    rank, world = train.init_distributed()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    wl = build_workload(cfg, device, args.seed)
+    trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2,
+                                  hidden=128, fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=args.seed)
+    rng = train.make_rng(args.seed, rank)
+    total_steps = args.warmup + args.steps
+    batches = []
+    epoch = 0
+    while len(batches) < total_steps:
+        batches.extend(train.rank_batches(wl["candidates"], cfg["batch"], rank, world, args.seed + 1000, epoch))
+        epoch += 1
+    batches = batches[:total_steps]
+    pf = train.Prefetcher(wl["graph"], rng, batches, cfg["fanouts"], False, device)
+    timer = Agg1Timer()
+    timer.install(2 if cfg["dtype"] == "bf16" else 4)
+    elem = 2 if cfg["dtype"] == "bf16" else 4
+
+    for _ in range(args.warmup):
+        ds, roots_dev, s = pf.next()
+        trainer.step(ds, roots_dev, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.active = True
+    agg_bytes, n_edges = [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ds, roots_dev, s = pf.next()
+        trainer.step(ds, roots_dev, world)
+        agg_bytes.append(agg1_bytes(s, cfg["feat"], elem))
+        n_edges += s.sizes(1)[1] + s.sizes(2)[1]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.active = False
+    loss = float(trainer.loss.item())
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    agg_ms = timer.mean_ms()
+    value = cfg["batch"] * args.steps * world / elapsed
+
+    if rank == 0:
+        achieved = float(np.mean(agg_bytes)) / (agg_ms * 1e-3) / 1e9
+        tr = load_traffic(args.config)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": (tr["agg1_hbm_bytes_per_launch"] if tr else None),
+                "kernel": "agg_fwd_kernel (layer-1 expand gather-mean)", "avg_launch_us": round(agg_ms * 1e3, 2),
+                "algo_bytes_per_launch": int(np.mean(agg_bytes))}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(wl, cfg, args.cpu_budget, args.seed)
+        out = {
+            "metric": "sampled nodes/sec (2-layer, fanout 25,10) at 1/2/4/8 MI355X",
+            "value": round(value, 1), "unit": "root nodes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
+            "data": "synthetic (R-MAT graph, hashed U(-1,1) features, labels id%16)",
+            "config": {"workload": f"{args.config}: R-MAT scale {cfg['scale']} "
+                                   f"({wl['n']} ids), {cfg['pairs']} pairs, feat {cfg['feat']}, "
+                                   f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
+                       "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
+                       "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
+                       "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    pf.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

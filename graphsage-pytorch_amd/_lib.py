@@ -37,6 +37,7 @@ class HopView(ctypes.Structure):
         ("dst_ids", _p(_i64)), ("pos_ptr", _p(_i32)), ("pos", _p(_i32)),
         ("src_ids", _p(_i64)), ("nbr_ptr", _p(_i32)), ("nbr", _p(_i32)),
         ("self_local", _p(_i32)), ("set_ptr", _p(_i32)), ("set_items", _p(_i64)),
+        ("n_empty", _i64),
     ]
 
 

@@ -35,6 +35,7 @@ struct Hop {
     std::vector<int32_t> set_ptr;
     std::vector<int64_t> set_items;
     std::vector<int32_t> tptr, tidx;  // transposed (src -> dst) incl. self edges as -(r+1)
+    int64_t n_empty = 0;              // empty neighbourhoods after the self rule
 };
 
 struct Sample {
@@ -68,6 +69,19 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
             for (int64_t t = 0; t < d; ++t) dstp[t] = static_cast<int32_t>(t);
         }
     }
+}
+
+// Destinations left without neighbours once self is removed (non-gcn): the
+// sampled entries are distinct, so only 0 entries or a lone self qualify.
+static int64_t count_empty(const Graph& g, const Hop& h, bool gcn) {
+    int64_t e = 0;
+    for (size_t r = 0; r < h.dst_ids.size(); ++r) {
+        const int64_t c = h.pos_ptr[r + 1] - h.pos_ptr[r];
+        if (gcn) continue;  // self is always present
+        if (c == 0) ++e;
+        else if (c == 1 && g.col[g.row_ptr[h.dst_ids[r]] + h.pos[h.pos_ptr[r]]] == h.dst_ids[r]) ++e;
+    }
+    return e;
 }
 
 // CPython-set replay of :282-288 for one hop: per-node sets, their union
@@ -173,6 +187,7 @@ static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, in
         h.k = fanouts ? fanouts[j] : 10;
         h.dst_ids = frontier;
         draw_positions(g, rng, h);
+        h.n_empty = count_empty(g, h, gcn);
         const bool last = (j == n_hops - 1);
         if (!last || (flags & GS_SAMPLE_FULL)) {
             materialise(g, h, gcn);
@@ -306,6 +321,7 @@ int gs_sample_hop(const gs_sample* sp, int32_t hop, gs_hop_view* v) {
     v->dst_ids = h.dst_ids.data();
     v->pos_ptr = h.pos_ptr.data();
     v->pos = h.pos.data();
+    v->n_empty = h.n_empty;
     if (h.materialised) {
         v->n_src = static_cast<int64_t>(h.src_ids.size());
         v->n_nbr = static_cast<int64_t>(h.nbr.size());

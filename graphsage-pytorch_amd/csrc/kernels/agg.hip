@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kBlock) void agg_bwd_kernel(
             if (!act) continue;
             float x[VEC];
             if (e < 0) {
+                if (!dSelf) continue;  // gcn: self rows feed no linear input
                 RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0, x);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) g[v] += x[v];
@@ -266,9 +267,9 @@ int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr, const i
     GS_REQUIRE(F >= 1 && n_src >= 0 && n_src < (int64_t(1) << 31), GS_EINVAL, "bad sizes");
     GS_REQUIRE(ldd >= F && ldh >= F, GS_EINVAL, "leading dimension smaller than F");
     if (n_src == 0) return GS_OK;
-    GS_REQUIRE(tptr && tidx && ptr && dA && dSelf && dH, GS_EINVAL, "NULL device pointer");
+    GS_REQUIRE(tptr && tidx && ptr && dA && dH, GS_EINVAL, "NULL device pointer");
     GS_REQUIRE(op != GS_AGG_MAX || argmax, GS_EINVAL, "MAX backward needs argmax");
-    const int vec = (F % 4 == 0 && ldd % 4 == 0 && ldh % 4 == 0 && aligned16(dA) && aligned16(dSelf) &&
+    const int vec = (F % 4 == 0 && ldd % 4 == 0 && ldh % 4 == 0 && aligned16(dA) && (!dSelf || aligned16(dSelf)) &&
                      aligned16(dH) && (!Hprev || aligned16(Hprev)))
                         ? 4
                         : 1;

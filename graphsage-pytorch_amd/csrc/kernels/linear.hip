@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
             const int row = m0 + 4 * (lane >> 4) + j;
             if (row < n) {
                 const float v = acc[t][j];
-                out[static_cast<int64_t>(row) * ldo + col] = RELU ? fmaxf(v, 0.f) : v;
+                out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;  // NaN kept, as torch.relu
             }
         }
     }

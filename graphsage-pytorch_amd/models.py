@@ -1,0 +1,352 @@
+"""Drop-in replacements for the reference's src/models.py modules.
+
+Same constructor signatures, attributes, state_dict keys and forward contracts
+as ``SageLayer`` (models.py:189-220), ``GraphSage`` (models.py:222-330) and
+``Classification`` (models.py:8-27); the work runs through the native sampler
+and the gfx950 kernels:
+
+  GraphSage.forward(nodes_batch)
+    host : sample all hops (bit-exact with the reference's `random` stream and
+           set order; the module-global `random` state is consumed exactly as
+           the reference consumes it), pack one int32 image, one H2D copy
+    HIP  : per layer, segmented gather-aggregate (K-agg) + MFMA SageLayer
+           (K-sage-linear); backward through the transposed neighbourhoods.
+
+There is no CPU execution path: raw_features must live on a HIP device.
+"""
+import random as _pyrandom
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import hip_ops as ops
+from .graph import CSRGraph
+from .sampler import RNG, sample
+
+PK = {  # field ids of the device pack
+    "pos_ptr": _lib.GS_PK_POS_PTR, "pos": _lib.GS_PK_POS, "dst_ids": _lib.GS_PK_DST_IDS,
+    "nbr_ptr": _lib.GS_PK_NBR_PTR, "nbr": _lib.GS_PK_NBR, "self": _lib.GS_PK_SELF,
+    "tptr": _lib.GS_PK_TPTR, "tidx": _lib.GS_PK_TIDX,
+}
+
+
+class DeviceSample:
+    """One batch's sampled computation graph resident on the device."""
+
+    def __init__(self, s, device, buf=None):
+        self.n_hops = s.n_hops
+        self.sizes = [s.sizes(j) for j in range(1, s.n_hops + 1)]
+        self.offsets = s.offsets
+        if buf is None:
+            host = s.pack(pin=torch.device(device).type == "cuda")
+            buf = host.to(device, non_blocking=True)
+        self.buf = buf
+
+    def field(self, hop, name):
+        """int32 view of `name` for hop (1-based)."""
+        n_dst, n_pos, n_src, n_nbr = self.sizes[hop - 1]
+        n = {"pos_ptr": n_dst + 1, "pos": n_pos, "dst_ids": n_dst, "nbr_ptr": n_dst + 1,
+             "nbr": n_nbr, "self": n_dst, "tptr": n_src + 1, "tidx": n_nbr + n_dst}[name]
+        off = self.offsets[hop - 1][PK[name]]
+        if off < 0:
+            raise KeyError(f"hop {hop} has no '{name}' on the device")
+        return self.buf[off:off + n]
+
+
+# ------------------------------------------------------------ shared compute
+def sage_forward(ds, X, weights, agg_func, gcn, row_ptr, col, weights_lowp=None):
+    """Bottom-up forward (models.py:255-267) over a DeviceSample.
+
+    Returns (h_list, agg_list, argmax_list); h_list[-1] is [len(roots), H]."""
+    L = ds.n_hops
+    hs, aggs, ams = [], [], []
+    # layer 1 reads the raw features through the last hop, expanded on device
+    n_dst = ds.sizes[L - 1][0]
+    dst = ds.field(L, "dst_ids")
+    a1 = torch.empty(n_dst, X.shape[1], dtype=X.dtype, device=X.device)
+    ops.agg_fwd(agg_func, X, ds.field(L, "pos_ptr"), ds.field(L, "pos"), a1,
+                row_ptr=row_ptr, col=col, dst_ids=dst, gcn=gcn)
+    W1 = weights_lowp[0] if weights_lowp is not None else weights[0]
+    h = torch.empty(n_dst, weights[0].shape[0], dtype=torch.float32, device=X.device)
+    ops.sage_linear_fwd(a1, W1, h, Xs=None if gcn else X, sidx=dst)
+    hs.append(h)
+    aggs.append(a1)
+    ams.append(None)
+    for layer in range(2, L + 1):
+        j = L - layer + 1
+        n_dst = ds.sizes[j - 1][0]
+        prev = hs[-1]
+        a = torch.empty(n_dst, prev.shape[1], dtype=torch.float32, device=X.device)
+        am = (torch.empty(n_dst, prev.shape[1], dtype=torch.int32, device=X.device)
+              if agg_func == "MAX" else None)
+        ops.agg_fwd(agg_func, prev, ds.field(j, "nbr_ptr"), ds.field(j, "nbr"), a, argmax=am)
+        h = torch.empty(n_dst, weights[layer - 1].shape[0], dtype=torch.float32, device=X.device)
+        ops.sage_linear_fwd(a, weights[layer - 1], h, Xs=None if gcn else prev, sidx=ds.field(j, "self"))
+        hs.append(h)
+        aggs.append(a)
+        ams.append(am)
+    return hs, aggs, ams
+
+
+def sage_backward(ds, X, weights, agg_func, gcn, hs, aggs, ams, dout, dWs):
+    """Autograd of sage_forward for the weights (raw features get no grad,
+    models.py:234).  dWs[l] receives layer l+1's weight gradient."""
+    L = ds.n_hops
+    dH = dout
+    relu = True
+    for layer in range(L, 0, -1):
+        j = L - layer + 1
+        if layer == 1:
+            x_in, sidx = X, ds.field(L, "dst_ids")
+        else:
+            x_in, sidx = hs[layer - 2], ds.field(j, "self")
+        ops.sage_linear_bwd_weight(aggs[layer - 1], dH, hs[layer - 1], dWs[layer - 1],
+                                   Xs=None if gcn else x_in, sidx=sidx, relu=relu)
+        if layer == 1:
+            break
+        n_dst = ds.sizes[j - 1][0]
+        H_in = hs[layer - 2].shape[1]
+        dIn = torch.empty(n_dst, H_in if gcn else 2 * H_in, dtype=torch.float32, device=X.device)
+        dSelf = None if gcn else dIn[:, :H_in]
+        dA = dIn if gcn else dIn[:, H_in:]
+        ops.sage_linear_bwd_input(dH, hs[layer - 1], weights[layer - 1], dA, dSelf=dSelf, relu=relu)
+        dprev = torch.empty_like(hs[layer - 2])
+        ops.agg_bwd(agg_func, ds.field(j, "tptr"), ds.field(j, "tidx"), ds.field(j, "nbr_ptr"), dA,
+                    dprev, dSelf=dSelf, argmax=ams[layer - 1], Hprev=hs[layer - 2])
+        dH = dprev
+        relu = False  # dprev is already masked by relu'(h_{layer-1})
+
+
+class _GraphSageFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ds, row_ptr, col, agg_func, gcn, X, *weights):
+        lowp = None
+        if X.dtype == torch.bfloat16:
+            lowp = [ops.cast_bf16(weights[0].detach().contiguous(),
+                                  torch.empty(weights[0].shape, dtype=torch.bfloat16, device=X.device))]
+        ws = [w.detach().contiguous() for w in weights]
+        hs, aggs, ams = sage_forward(ds, X, ws, agg_func, gcn, row_ptr, col, lowp)
+        ctx.ds, ctx.agg, ctx.gcn = ds, agg_func, gcn
+        ctx.save_for_backward(X, *ws)
+        ctx.acts = (hs, aggs, ams)
+        return hs[-1]
+
+    @staticmethod
+    def backward(ctx, dout):
+        X, *ws = ctx.saved_tensors
+        hs, aggs, ams = ctx.acts
+        dWs = [torch.empty_like(w) for w in ws]
+        sage_backward(ctx.ds, X, ws, ctx.agg, ctx.gcn, hs, aggs, ams, dout.contiguous().float(), dWs)
+        ctx.acts = None
+        return (None, None, None, None, None, None, *dWs)
+
+
+class _SageLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, self_feats, agg_feats, weight, gcn):
+        A = agg_feats.contiguous()
+        Xs = None if gcn else self_feats.contiguous()
+        W = weight.detach().contiguous()
+        Wd = W if A.dtype == torch.float32 else W.to(A.dtype)
+        out = torch.empty(A.shape[0], W.shape[0], dtype=torch.float32, device=A.device)
+        ops.sage_linear_fwd(A, Wd, out, Xs=Xs)
+        ctx.gcn = gcn
+        ctx.save_for_backward(Xs if Xs is not None else A, A, W, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        Xs, A, W, out = ctx.saved_tensors
+        gcn = ctx.gcn
+        dout = dout.contiguous().float()
+        dW = torch.empty_like(W)
+        ops.sage_linear_bwd_weight(A, dout, out, dW, Xs=None if gcn else Xs)
+        d_self = d_agg = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            F = A.shape[1]
+            dIn = torch.empty(A.shape[0], F if gcn else 2 * F, dtype=torch.float32, device=A.device)
+            dS = None if gcn else dIn[:, :F]
+            dA = dIn if gcn else dIn[:, F:]
+            ops.sage_linear_bwd_input(dout, out, W, dA, dSelf=dS)
+            d_agg = dA.to(A.dtype)
+            d_self = None if gcn else dS.to(Xs.dtype)
+        return d_self, d_agg, dW, None
+
+
+class _AggregateFn(torch.autograd.Function):
+    """GraphSage.aggregate on explicit neighbourhoods (API path)."""
+
+    @staticmethod
+    def forward(ctx, agg_func, X, nptr, nidx, tptr, tidx):
+        n = nptr.numel() - 1
+        out = torch.empty(n, X.shape[1], dtype=X.dtype, device=X.device)
+        am = (torch.empty(n, X.shape[1], dtype=torch.int32, device=X.device)
+              if agg_func == "MAX" and X.dtype == torch.float32 else None)
+        ops.agg_fwd(agg_func, X, nptr, nidx, out, argmax=am)
+        ctx.agg, ctx.n_src = agg_func, X.shape[0]
+        ctx.save_for_backward(nptr, tptr, tidx)
+        ctx.am = am
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nptr, tptr, tidx = ctx.saved_tensors
+        if ctx.agg == "MAX" and ctx.am is None:
+            raise RuntimeError("MAX aggregate backward is implemented for float32 inputs")
+        dX = torch.empty(ctx.n_src, dout.shape[1], dtype=torch.float32, device=dout.device)
+        ops.agg_bwd(ctx.agg, tptr, tidx, nptr, dout.contiguous().float(), dX, argmax=ctx.am)
+        return None, dX, None, None, None, None
+
+
+# ------------------------------------------------------------------ modules
+class SageLayer(nn.Module):
+    """Encodes a node's features the 'convolutional' GraphSage way (models.py:189-220)."""
+
+    def __init__(self, input_size, out_size, gcn=False):
+        super().__init__()
+        self.input_size = input_size
+        self.out_size = out_size
+        self.gcn = gcn
+        self.weight = nn.Parameter(torch.FloatTensor(out_size, self.input_size if self.gcn else 2 * self.input_size))
+        self.init_params()
+
+    def init_params(self):
+        for param in self.parameters():
+            nn.init.xavier_uniform_(param)
+
+    def forward(self, self_feats, aggregate_feats, neighs=None):
+        return _SageLinearFn.apply(self_feats, aggregate_feats, self.weight, self.gcn)
+
+
+class GraphSage(nn.Module):
+    """GraphSage encoder (models.py:222-330) on the native sampler + HIP kernels.
+
+    Extra keyword arguments (all optional, defaults reproduce the reference):
+      fanouts : num_sample per hop, roots first (reference: 10 at every hop,
+                models.py:277); None entries mean "all neighbours".
+      rng     : a sampler.RNG to draw from instead of the module-global
+                `random` (the reference always uses the global stream).
+    """
+
+    def __init__(self, num_layers, input_size, out_size, raw_features, adj_lists, device, gcn=False,
+                 agg_func='MEAN', *, fanouts=None, rng=None):
+        super().__init__()
+        self.input_size = input_size
+        self.out_size = out_size
+        self.num_layers = num_layers
+        self.gcn = gcn
+        self.device = device
+        self.agg_func = agg_func
+        self.raw_features = raw_features
+        self.adj_lists = adj_lists
+        self.fanouts = list(fanouts) if fanouts is not None else [10] * num_layers
+        if len(self.fanouts) != num_layers:
+            raise ValueError("need one fanout per layer")
+        self.rng = rng
+        self._graph = adj_lists if isinstance(adj_lists, CSRGraph) else None
+        for index in range(1, num_layers + 1):
+            layer_size = out_size if index != 1 else input_size
+            setattr(self, 'sage_layer' + str(index), SageLayer(layer_size, out_size, gcn=self.gcn))
+
+    # -------------------------------------------------------------- helpers
+    @property
+    def graph(self):
+        if self._graph is None:
+            self._graph = CSRGraph.from_adj_lists(self.adj_lists, n_nodes=len(self.raw_features))
+        return self._graph
+
+    def _draw(self, roots, fanouts, full=False):
+        rng = self.rng if self.rng is not None else RNG.from_python(_pyrandom)
+        s = sample(self.graph, rng, roots, fanouts, gcn=self.gcn, full=full)
+        if self.rng is None:
+            rng.to_python(_pyrandom)
+        return s
+
+    @staticmethod
+    def _roots(nodes_batch):
+        if isinstance(nodes_batch, torch.Tensor):
+            return nodes_batch.detach().cpu().numpy().astype(np.int64).reshape(-1)
+        return np.asarray(list(nodes_batch), dtype=np.int64).reshape(-1)
+
+    # -------------------------------------------------------------- forward
+    def forward(self, nodes_batch):
+        """Embeddings [len(nodes_batch), out_size]; row i is nodes_batch[i]."""
+        roots = self._roots(nodes_batch)
+        X = self.raw_features
+        if not isinstance(X, torch.Tensor) or not X.is_cuda:
+            raise RuntimeError("graphsage_amd.GraphSage runs on a HIP device: raw_features must be a "
+                               "cuda tensor (the reference's --cuda path, main.py:52)")
+        if self.agg_func not in ("MEAN", "MAX"):
+            raise ValueError(f"agg_func must be 'MEAN' or 'MAX', got {self.agg_func!r}")
+        s = self._draw(roots, self.fanouts)
+        if self.agg_func == "MAX":
+            for j in range(1, s.n_hops + 1):
+                if s.n_empty(j):
+                    raise IndexError("MAX aggregation over an empty neighbourhood "
+                                     "(reference: models.py:321-325)")
+        ds = DeviceSample(s, X.device)
+        row_ptr, col = self.graph.device_csr(X.device)
+        weights = [getattr(self, 'sage_layer' + str(i)).weight for i in range(1, self.num_layers + 1)]
+        Xc = X if X.is_contiguous() else X.contiguous()
+        return _GraphSageFn.apply(ds, row_ptr, col, self.agg_func, self.gcn, Xc, *weights)
+
+    # ------------------------------------------------ reference helper API
+    def _nodes_map(self, nodes, hidden_embs, neighs):
+        layer_nodes, samp_neighs, layer_nodes_dict = neighs
+        assert len(samp_neighs) == len(nodes)
+        return [layer_nodes_dict[x] for x in nodes]
+
+    def _get_unique_neighs_list(self, nodes, num_sample=10):
+        """(samp_neighs list of sets, {id: pos}, unique list) — models.py:277-289."""
+        s = self._draw(self._roots(nodes), [num_sample], full=True)
+        h = s.hop(1)
+        samp = [set(x) for x in h.sets()]
+        uniq = h.src_ids.tolist()
+        return samp, dict(zip(uniq, range(len(uniq)))), uniq
+
+    def aggregate(self, nodes, pre_hidden_embs, pre_neighs, num_sample=10):
+        """models.py:291-330 on explicit neighbourhoods (API path)."""
+        unique_nodes_list, samp_neighs, unique_nodes = pre_neighs
+        assert len(nodes) == len(samp_neighs)
+        assert all(nodes[i] in samp_neighs[i] for i in range(len(samp_neighs)))
+        if not self.gcn:
+            samp_neighs = [samp_neighs[i] - {nodes[i]} for i in range(len(samp_neighs))]
+        direct = len(pre_hidden_embs) == len(unique_nodes)  # :300-303
+        cols = [sorted(unique_nodes[n] for n in sn) for sn in samp_neighs]
+        if self.agg_func == "MAX" and any(len(c) == 0 for c in cols):
+            raise IndexError("MAX aggregation over an empty neighbourhood")
+        rows = [c if direct else [unique_nodes_list[x] for x in c] for c in cols]
+        nptr = np.zeros(len(rows) + 1, np.int32)
+        nptr[1:] = np.cumsum([len(r) for r in rows])
+        nidx = np.array([x for r in rows for x in r], np.int32)
+        n_src = len(pre_hidden_embs)
+        tcnt = np.zeros(n_src + 1, np.int64)
+        np.add.at(tcnt, nidx.astype(np.int64) + 1, 1)
+        tptr = np.cumsum(tcnt).astype(np.int32)
+        order = np.argsort(nidx, kind="stable")
+        dsts = np.repeat(np.arange(len(rows), dtype=np.int32), np.diff(nptr))
+        tidx = dsts[order].astype(np.int32)
+        dev = pre_hidden_embs.device
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        X = pre_hidden_embs if pre_hidden_embs.is_contiguous() else pre_hidden_embs.contiguous()
+        return _AggregateFn.apply(self.agg_func, X, t(nptr), t(nidx if len(nidx) else np.zeros(1, np.int32)),
+                                  t(tptr), t(tidx if len(tidx) else np.zeros(1, np.int32)))
+
+
+class Classification(nn.Module):
+    """log_softmax(Linear(emb)) head (models.py:8-27); plain torch ops."""
+
+    def __init__(self, emb_size, num_classes):
+        super().__init__()
+        self.layer = nn.Sequential(nn.Linear(emb_size, num_classes))
+        self.init_params()
+
+    def init_params(self):
+        for param in self.parameters():
+            if len(param.size()) == 2:
+                nn.init.xavier_uniform_(param)
+
+    def forward(self, embeds):
+        return torch.log_softmax(self.layer(embeds), 1)

@@ -121,6 +121,7 @@ class Hop:
     def __init__(self, v):
         self.n_dst, self.n_pos = int(v.n_dst), int(v.n_pos)
         self.n_src, self.n_nbr = int(v.n_src), int(v.n_nbr)
+        self.n_empty = int(v.n_empty)
         self.dst_ids = _arr(v.dst_ids, self.n_dst, ctypes.c_int64)
         self.pos_ptr = _arr(v.pos_ptr, self.n_dst + 1, ctypes.c_int32)
         self.pos = _arr(v.pos, self.n_pos, ctypes.c_int32)
@@ -154,10 +155,12 @@ class Sample:
         self.offsets = [[int(lay.off[j][f]) for f in range(_lib.GS_PK_NFIELDS)]
                         for j in range(self.n_hops)]
         self._sizes = []
+        self._empty = []
         for j in range(1, self.n_hops + 1):
             v = _lib.HopView()
             check(lib().gs_sample_hop(self._h, j, ctypes.byref(v)))
             self._sizes.append((int(v.n_dst), int(v.n_pos), int(v.n_src), int(v.n_nbr)))
+            self._empty.append(int(v.n_empty))
 
     def hop(self, j):
         """Host view of hop j (1 = the roots' hop)."""
@@ -170,6 +173,10 @@ class Sample:
     def sizes(self, j):
         """(n_dst, n_pos, n_src, n_nbr) of hop j."""
         return self._sizes[j - 1]
+
+    def n_empty(self, j):
+        """Destinations of hop j with an empty neighbourhood after the self rule."""
+        return self._empty[j - 1]
 
     def pack_into(self, buf):
         """Write the device image into `buf` (int32 tensor / array, >= pack_total)."""

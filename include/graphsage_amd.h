@@ -134,6 +134,8 @@ typedef struct {
     const int32_t* self_local;/* [n_dst] index of dst in Fj (_nodes_map :271)    */
     const int32_t* set_ptr;   /* [n_dst+1] samp_neighs[i] incl. self, iteration */
     const int64_t* set_items; /*   order of the reference's set object           */
+    int64_t n_empty;          /* destinations with no neighbour after the self
+                                 rule (MEAN gives NaN, MAX raises IndexError)    */
 } gs_hop_view;
 
 /* Device pack: everything the kernels read for one batch, one int32 buffer. */
@@ -226,6 +228,7 @@ int gs_sage_linear_bwd_input(int64_t n, int64_t F, int64_t H,
  * the previous hidden state, with the transposed CSR of one hop
  * (GS_PK_TPTR / GS_PK_TIDX encoding):
  *   g[c] = Σ_{t ∈ tptr[c]..tptr[c+1]}  tidx[t] = -(r+1) : dSelf[r]
+ *                          (skipped when dSelf == NULL: gcn mode)
  *                                       tidx[t] = r      : MEAN dA[r] / deg(r)
  *                                                          MAX  dA[r] where argmax[r] == c
  *   dH[c] = g[c] ⊙ (Hprev[c] > 0)   (the relu of the layer below; Hprev NULL → g)

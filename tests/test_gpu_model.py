@@ -1,0 +1,196 @@
+"""Model-level parity on the MI355X: the drop-in GraphSage / SageLayer against
+the reference's golden vectors (embeddings within 1e-5 fp32, weight gradients,
+RNG stream position) and against the oracle on the benchmark's fanouts; the
+native fused training step against the oracle's training step."""
+import importlib
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from tests.golden.synth import hashed_binary_features, uniform_features
+
+pytestmark = pytest.mark.gpu
+
+models = importlib.import_module("graphsage-pytorch_amd.models")
+train = importlib.import_module("graphsage-pytorch_amd.train")
+DEV = torch.device("cuda", 0)
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _graph(gs, name):
+    g = np.load(os.path.join(G, "graphs.npz"))
+    n = int(g[f"{name}_n"][0])
+    return gs.CSRGraph.from_pairs(g[f"{name}_src"], g[f"{name}_dst"], n), g, n
+
+
+def _features(name, n):
+    if name == "cora":
+        return hashed_binary_features(n, 1433)
+    if name == "rmat":
+        return uniform_features(77, n, 100)
+    return uniform_features(11, n, 64)
+
+
+FORWARDS = [("cora", "MEAN", "sage", 824), ("cora", "MAX", "sage", 824), ("cora", "MEAN", "gcn", 824),
+            ("cora", "MAX", "gcn", 824), ("rmat", "MEAN", "sage", 5), ("rmat", "MAX", "sage", 5),
+            ("pubmed", "MEAN", "sage", 824)]
+
+
+@pytest.mark.parametrize("name,agg,mode,seed", FORWARDS)
+@pytest.mark.parametrize("adj_kind", ["pairs", "adj_lists"])
+def test_graphsage_matches_reference_vectors(gs, name, agg, mode, seed, adj_kind):
+    R = np.load(os.path.join(G, f"forward_{name}_{agg}_{mode}.npz"))
+    graph, g, n = _graph(gs, name)
+    if adj_kind == "adj_lists":
+        from collections import defaultdict
+        adj = defaultdict(set)
+        for a, b in zip(g[f"{name}_src"].tolist(), g[f"{name}_dst"].tolist()):
+            adj[a].add(b)
+            adj[b].add(a)
+        graph = adj
+    X = torch.from_numpy(_features(name, n)).to(DEV)
+    torch.manual_seed(seed)  # the reference's init path reproduces the captured weights
+    model = models.GraphSage(2, X.shape[1], 128, X, graph, DEV, gcn=(mode == "gcn"), agg_func=agg).to(DEV)
+    for i in (1, 2):
+        w = getattr(model, f"sage_layer{i}").weight
+        assert torch.equal(w.detach().cpu(), torch.from_numpy(R[f"w__sage_layer{i}.weight"]))
+    random.seed(seed)
+    emb = model(R["roots"].tolist())
+    assert list(random.getstate()[1]) == R["state"].tolist()  # same rng words consumed
+    torch.testing.assert_close(emb.detach().cpu(), torch.from_numpy(R["emb"]), atol=1e-5, rtol=1e-5)
+    (emb * torch.from_numpy(uniform_features(31, len(R["roots"]), 128)).to(DEV)).sum().backward()
+    for i in (1, 2):
+        torch.testing.assert_close(getattr(model, f"sage_layer{i}").weight.grad.cpu(),
+                                   torch.from_numpy(R[f"grad__sage_layer{i}.weight"]), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+@pytest.mark.parametrize("fanouts", [[25, 10], [5, 3, 2]])
+def test_graphsage_vs_oracle_bench_fanouts(gs, agg, fanouts):
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(3, n, 256))
+    torch.manual_seed(1)
+    model = models.GraphSage(len(fanouts), 256, 128, X.to(DEV), graph, DEV, agg_func=agg, fanouts=fanouts).to(DEV)
+    roots = np.nonzero(graph.degrees())[0][::3][:100].tolist()
+    random.seed(11)
+    emb = model(roots)
+    W = [getattr(model, f"sage_layer{i}").weight.detach().cpu().clone().requires_grad_(True)
+         for i in range(1, len(fanouts) + 1)]
+    random.seed(11)
+    hops = oracle.sample_layers(oracle.Adjacency(g["rmat_src"], g["rmat_dst"], n), roots, fanouts)
+    ref = oracle.forward_dense(hops, X, W, agg, False)
+    torch.testing.assert_close(emb.detach().cpu(), ref.detach(), atol=1e-5, rtol=1e-5)
+    up = torch.from_numpy(uniform_features(9, len(roots), 128))
+    (emb * up.to(DEV)).sum().backward()
+    (ref * up).sum().backward()
+    for i in range(1, len(fanouts) + 1):
+        torch.testing.assert_close(getattr(model, f"sage_layer{i}").weight.grad.cpu(), W[i - 1].grad,
+                                   atol=1e-4, rtol=1e-4)
+
+
+def test_graphsage_bf16_max_vs_oracle(gs):
+    """configs[3] numerics: bf16 feature table, fp32 accumulate; oracle on the
+    same bf16-rounded features, bf16-rounded W1 (tolerance stated: 2e-2)."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(3, n, 256)).to(torch.bfloat16)
+    torch.manual_seed(1)
+    model = models.GraphSage(2, 256, 128, X.to(DEV), graph, DEV, agg_func="MAX", fanouts=[25, 10]).to(DEV)
+    roots = np.nonzero(graph.degrees())[0][:64].tolist()
+    random.seed(2)
+    emb = model(roots).detach().cpu()
+    W = [getattr(model, "sage_layer1").weight.detach().cpu().to(torch.bfloat16).float(),
+         getattr(model, "sage_layer2").weight.detach().cpu()]
+    random.seed(2)
+    hops = oracle.sample_layers(oracle.Adjacency(g["rmat_src"], g["rmat_dst"], n), roots, [25, 10])
+    ref = oracle.forward_dense(hops, X.float(), W, "MAX", False)
+    torch.testing.assert_close(emb, ref, atol=2e-2, rtol=2e-2)
+
+
+def test_sagelayer_api_and_aggregate_api(gs):
+    graph, g, n = _graph(gs, "cora")
+    X = torch.from_numpy(hashed_binary_features(n, 1433)).to(DEV)
+    torch.manual_seed(824)
+    model = models.GraphSage(2, 1433, 128, X, graph, DEV).to(DEV)
+    nodes = list(range(0, 60, 3))
+    random.seed(5)
+    samp, d, uniq = model._get_unique_neighs_list(nodes)
+    random.seed(5)
+    ref = oracle.sample_hop(oracle.Adjacency(g["cora_src"], g["cora_dst"], n), nodes, 10)
+    assert uniq == ref[2] and d == ref[1] and samp == ref[0]
+    agg = model.aggregate(nodes, X, (uniq, samp, d))
+    ref_s = [s - {nodes[i]} for i, s in enumerate(samp)]
+    want = torch.stack([X[torch.tensor(sorted(s), device=DEV)].mean(0) for s in ref_s])
+    torch.testing.assert_close(agg, want, atol=1e-6, rtol=1e-5)
+    layer = model.sage_layer1
+    sf = X[torch.tensor(nodes, device=DEV)].requires_grad_(True)
+    af = agg.detach().requires_grad_(True)
+    out = layer(sf, af)
+    ref_out = torch.relu(layer.weight.mm(torch.cat([sf, af], 1).t())).t()
+    torch.testing.assert_close(out, ref_out, atol=1e-5, rtol=1e-5)
+    out.sum().backward()
+    g1 = layer.weight.grad.clone()
+    layer.weight.grad = None
+    sf2, af2 = sf.detach().requires_grad_(True), af.detach().requires_grad_(True)
+    torch.relu(layer.weight.mm(torch.cat([sf2, af2], 1).t())).t().sum().backward()
+    torch.testing.assert_close(g1, layer.weight.grad, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(sf.grad, sf2.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(af.grad, af2.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_max_empty_neighbourhood_raises(gs):
+    # node 0 only links to itself: after self removal MAX has nothing to reduce
+    src = np.array([0, 1, 2, 3], np.int64)
+    dst = np.array([0, 2, 3, 1], np.int64)
+    graph = gs.CSRGraph.from_pairs(src, dst, 4)
+    X = torch.randn(4, 16, device=DEV)
+    model = models.GraphSage(1, 16, 16, X, graph, DEV, agg_func="MAX").to(DEV)
+    with pytest.raises(IndexError):
+        model([0, 1])
+    mean = models.GraphSage(1, 16, 16, X, graph, DEV, agg_func="MEAN").to(DEV)
+    out = mean([0, 1])
+    assert torch.isnan(out[0]).all()  # relu(NaN) stays NaN, as torch's relu
+    assert torch.isfinite(out[1]).all()
+
+
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_native_train_step_vs_oracle(gs, agg):
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256))
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32))
+    tr = train.NativeTrainer(graph, X.to(DEV), labels.to(DEV), 16, fanouts=(25, 10), agg_func=agg, seed=824)
+    sage_w, cw, cb = train.reference_init(2, 256, 128, 16, False, 824)
+    W = [w.clone().requires_grad_(True) for w in sage_w]
+    cw, cb = cw.clone().requires_grad_(True), cb.clone().requires_grad_(True)
+    rng = gs.RNG(824)
+    random.seed(824)
+    adj = oracle.Adjacency(g["rmat_src"], g["rmat_dst"], n)
+    for step, roots in enumerate(train.rank_batches(np.nonzero(graph.degrees())[0], 64, 0, 1, 7)):
+        if step == 3:
+            break
+        s = gs.sample(graph, rng, roots, [25, 10])
+        ds = models.DeviceSample(s, DEV)
+        loss = tr.step(ds, torch.from_numpy(roots.astype(np.int32)).to(DEV))
+        ref_loss = oracle.train_step_dense(adj, roots.tolist(), [25, 10], X, W, cw, cb,
+                                           labels[torch.from_numpy(roots)].long(), agg=agg)
+        assert abs(float(loss) - ref_loss) < 1e-4
+    sd = tr.p.state_dict()
+    for i in (1, 2):
+        torch.testing.assert_close(sd[f"sage_layer{i}.weight"].cpu(), W[i - 1].detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(sd["layer.0.weight"].cpu(), cw.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(sd["layer.0.bias"].cpu(), cb.detach(), atol=1e-4, rtol=1e-4)
+
+
+def test_prefetcher_matches_synchronous(gs):
+    graph, g, n = _graph(gs, "rmat")
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 32, 0, 1, 3))[:6]
+    pf = train.Prefetcher(graph, gs.RNG(3), batches, [25, 10], False, DEV)
+    rng = gs.RNG(3)
+    for roots in batches:
+        ds, roots_dev, s = pf.next()
+        s2 = gs.sample(graph, rng, roots, [25, 10])
+        assert torch.equal(ds.buf[:s.pack_total].cpu(), s2.pack()[:s2.pack_total])
+        assert roots_dev.cpu().tolist() == roots.tolist()

@@ -1,0 +1,189 @@
+"""Native host side (no GPU needed): C-ABI exports, RNG / set known answers,
+CSR builder order, multi-hop sampler bit-exactness vs the reference's vectors
+and vs the oracle, error behaviour, and the device pack layout."""
+import ctypes
+import json
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+from oracle import Adjacency, sample_layers
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "tests", "golden")
+
+
+def test_library_exports_every_declared_symbol(gs):
+    hdr = open(os.path.join(ROOT, "include", "graphsage_amd.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|int64_t|void|const char\*|const int64_t\*|const int32_t\*)\s+\**(gs_\w+)\(",
+                              hdr, re.M))
+    assert len(declared) > 30
+    L = gs._lib.lib()
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(gs._lib.exported_symbols()) >= declared
+    assert b"gfx950" in L.gs_version()
+
+
+def test_rng_known_answers(gs):
+    for rec in json.load(open(os.path.join(G, "rng.json"))):
+        r = gs.RNG(rec["seed"])
+        assert r.getrandbits(32, 8).tolist() == rec["bits32"]
+        for k, v in rec["bits_k"]:
+            assert int(r.getrandbits(k)[0]) == v
+        for s in rec["samples"]:
+            assert r.sample_positions(s["n"], s["k"]).tolist() == s["out"], (rec["seed"], s["n"], s["k"])
+        for n, v in rec["choice"]:
+            assert r.choice_position(n) == v
+        for n, v in rec["randbelow"]:
+            assert int(r.randbelow(n)[0]) == v
+        mt, pos = r.getstate()
+        assert mt.tolist() + [pos] == rec["state_after"]
+
+
+def test_rng_python_state_roundtrip(gs):
+    random.seed(99)
+    random.random()
+    r = gs.RNG.from_python()
+    a = r.getrandbits(32, 5).tolist()
+    b = [random.getrandbits(32) for _ in range(5)]
+    assert a == b
+    r.to_python()
+    assert random.getrandbits(32) == int(r.getrandbits(32)[0])
+
+
+def test_sample_errors(gs):
+    r = gs.RNG(1)
+    with pytest.raises(ValueError, match="Sample larger"):
+        r.sample_positions(3, 4)
+    with pytest.raises(ValueError):
+        r.choice_position(0)
+
+
+def test_pyset_known_answers(gs):
+    for case in json.load(open(os.path.join(G, "pyset.json"))):
+        assert gs.pyset_union_of_lists(case["lists"]).tolist() == case["union"]
+
+
+def _graph(gs, name):
+    g = np.load(os.path.join(G, "graphs.npz"))
+    return gs.CSRGraph.from_pairs(g[f"{name}_src"], g[f"{name}_dst"], int(g[f"{name}_n"][0])), g
+
+
+@pytest.mark.parametrize("name", ["cora", "pubmed", "rmat"])
+def test_csr_rows_in_reference_set_order(gs, name):
+    G_, g = _graph(gs, name)
+    assert np.array_equal(G_.row_ptr(), g[f"{name}_row_ptr"])
+    assert np.array_equal(G_.col(), g[f"{name}_col"])
+
+
+@pytest.mark.parametrize("name", ["cora", "pubmed", "rmat"])
+@pytest.mark.parametrize("full", [False, True])
+def test_sampler_matches_reference_vectors(gs, name, full):
+    G_, _ = _graph(gs, name)
+    S = np.load(os.path.join(G, f"sample_{name}.npz"))
+    for key in sorted({k.split("__")[0] for k in S.files}):
+        seed = int(key.split("_")[0][1:])
+        fan = [int(x) for x in key.split("_f")[1].split("-")]
+        r = gs.RNG(seed)
+        s = gs.sample(G_, r, S[key + "__roots"], fan, full=full)
+        for j in range(1, len(fan) + 1):
+            h = s.hop(j)
+            if j < len(fan) or full:
+                assert np.array_equal(h.src_ids, S[f"{key}__h{j}_union"]), (key, j)
+                assert np.array_equal(h.set_ptr, S[f"{key}__h{j}_set_ptr"])
+                assert np.array_equal(h.set_items, S[f"{key}__h{j}_set_items"])
+        mt, pos = r.getstate()
+        assert np.array_equal(np.append(mt.astype(np.int64), pos), S[key + "__state"])
+
+
+def test_adj_lists_adoption_matches_pairs(gs):
+    from collections import defaultdict
+    g = np.load(os.path.join(G, "graphs.npz"))
+    adj = defaultdict(set)
+    for a, b in zip(g["pubmed_src"].tolist(), g["pubmed_dst"].tolist()):
+        adj[a].add(b)
+        adj[b].add(a)
+    G1 = gs.CSRGraph.from_adj_lists(adj, int(g["pubmed_n"][0]))
+    G2, _ = _graph(gs, "pubmed")
+    assert np.array_equal(G1.col(), G2.col()) and np.array_equal(G1.row_ptr(), G2.row_ptr())
+    # a set with dummies (after discard) still reproduces the reference's frontier
+    adj[7].discard(next(iter(adj[7])))
+    G3 = gs.CSRGraph.from_adj_lists(adj, int(g["pubmed_n"][0]))
+    roots = [7] + list(range(100, 140))
+    random.seed(3)
+    want = sample_layers(adj, roots, [10, 10])
+    s = gs.sample(G3, gs.RNG(3), roots, [10, 10], full=True)
+    assert s.hop(1).src_ids.tolist() == want[0][3]
+    assert s.hop(2).src_ids.tolist() == want[1][3]
+
+
+def test_sampler_vs_oracle_random_graphs(gs):
+    """Random skewed graphs, many seeds, fanouts incl. None (take all) and >setsize."""
+    rs = np.random.RandomState(0)
+    for trial in range(6):
+        n = int(rs.randint(50, 400))
+        m = int(rs.randint(n, 12 * n))
+        hub = rs.randint(0, n, size=m) * (rs.random_sample(m) < 0.3)
+        src = np.where(hub > 0, hub % 7, rs.randint(0, n, size=m))
+        dst = rs.randint(0, n, size=m)
+        keep = src != dst
+        src, dst = src[keep], dst[keep]
+        Gn = gs.CSRGraph.from_pairs(src, dst, n)
+        adj = Adjacency(src, dst, n)
+        deg = Gn.degrees()
+        roots = [int(v) for v in rs.permutation(np.nonzero(deg)[0])[:int(rs.randint(1, 60))]]
+        for fan in ([25, 10], [10, 10], [3, None], [100], [2, 2, 2]):
+            seed = int(rs.randint(0, 10 ** 6))
+            random.seed(seed)
+            want = sample_layers(adj, roots, fan)
+            s = gs.sample(Gn, gs.RNG(seed), roots, fan, full=True)
+            for j, (_, samp, _, union) in enumerate(want, start=1):
+                h = s.hop(j)
+                assert h.src_ids.tolist() == union
+                assert h.sets() == [list(x) for x in samp]
+            r2 = gs.RNG(seed)
+            gs.sample(Gn, r2, roots, fan)
+            assert r2.getstate()[0].tolist() + [r2.getstate()[1]] == list(random.getstate()[1])
+
+
+def test_sample_pack_layout(gs):
+    G_, _ = _graph(gs, "cora")
+    s = gs.sample(G_, gs.RNG(824), list(range(0, 200, 7)), [10, 10])
+    buf = s.pack()
+    assert buf.numel() >= s.pack_total
+    for j in range(1, 3):
+        for f in s.offsets[j - 1]:
+            assert f == -1 or f % 4 == 0  # 16-byte aligned arrays
+    h1, h2 = s.hop(1), s.hop(2)
+    off = s.offsets
+    b = buf.numpy()
+    assert np.array_equal(b[off[0][gs._lib.GS_PK_NBR_PTR]:][:h1.n_dst + 1], h1.nbr_ptr)
+    assert np.array_equal(b[off[0][gs._lib.GS_PK_NBR]:][:h1.n_nbr], h1.nbr)
+    assert np.array_equal(b[off[1][gs._lib.GS_PK_POS]:][:h2.n_pos], h2.pos)
+    assert np.array_equal(b[off[1][gs._lib.GS_PK_DST_IDS]:][:h2.n_dst], h1.src_ids)
+    tp = b[off[0][gs._lib.GS_PK_TPTR]:][:h1.n_src + 1]
+    ti = b[off[0][gs._lib.GS_PK_TIDX]:][:h1.n_nbr + h1.n_dst]
+    # every (dst, src) edge and every self row appears exactly once in the transpose
+    pairs = sorted((c, int(t)) for c in range(h1.n_src) for t in ti[tp[c]:tp[c + 1]])
+    want = sorted([(int(h1.self_local[r]), -(r + 1)) for r in range(h1.n_dst)] +
+                  [(int(c), r) for r in range(h1.n_dst) for c in h1.nbr[h1.nbr_ptr[r]:h1.nbr_ptr[r + 1]]])
+    assert pairs == want
+
+
+def test_unknown_node_raises(gs):
+    G_, _ = _graph(gs, "cora")
+    with pytest.raises(IndexError):
+        gs.sample(G_, gs.RNG(1), [5, 10 ** 6], [10, 10])
+
+
+def test_rmat_generator_deterministic(gs):
+    a = gs.rmat_pairs(12, 50000, seed=5, n_threads=1)
+    b = gs.rmat_pairs(12, 50000, seed=5, n_threads=7)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert (a[0] != a[1]).all() and a[0].max() < 4096
+    deg = np.bincount(np.concatenate(a), minlength=4096)
+    assert deg.max() > 20 * max(1, np.median(deg))  # power-law skew
