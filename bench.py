@@ -205,10 +205,15 @@ def main():
         dist.barrier()
     timer.active = True
     agg_bytes, n_edges = [], 0
+    t_wait = t_launch = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        ta = time.perf_counter()
         ds, roots_dev, s = pf.next()
+        tb = time.perf_counter()
         trainer.step(ds, roots_dev, world)
+        t_launch += time.perf_counter() - tb
+        t_wait += tb - ta
         agg_bytes.append(agg1_bytes(s, cfg["feat"], elem))
         n_edges += s.sizes(1)[1] + s.sizes(2)[1]
     torch.cuda.synchronize()
@@ -246,7 +251,10 @@ def main():
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
-                       "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5)},
+                       "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
+                       "host_ms_per_step": {"sampler": round(1e3 * float(np.median(pf.sample_s)), 3),
+                                            "wait_for_batch": round(1e3 * t_wait / args.steps, 3),
+                                            "launch": round(1e3 * t_launch / args.steps, 3)}},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -54,31 +54,44 @@ struct MT19937 {
         index = N;
     }
 
-    void twist() {
-        static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
-        int kk = 0;
-        uint32_t y;
-        for (; kk < N - M; ++kk) {
-            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + M] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        for (; kk < N - 1; ++kk) {
-            y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ mag01[y & 1u];
-        }
-        y = (mt[N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
-        mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ mag01[y & 1u];
-        index = 0;
-    }
+    // Output words of the current block, tempered once per block (the block's
+    // raw state stays in mt[], exactly what random.getstate() exposes).
+    alignas(64) uint32_t out[N];
 
-    inline uint32_t next() {
-        if (index >= N) twist();
-        uint32_t y = mt[index++];
+    static inline uint32_t temper(uint32_t y) {
         y ^= (y >> 11);
         y ^= (y << 7) & 0x9d2c5680u;
         y ^= (y << 15) & 0xefc60000u;
         y ^= (y >> 18);
         return y;
+    }
+
+    // Recompute out[] from mt[] (after setstate).
+    void refresh() {
+        for (int i = 0; i < N; ++i) out[i] = temper(mt[i]);
+    }
+
+    // genrand_uint32's block regeneration, written as three branch-free loops
+    // the compiler vectorises (the recurrence distances 1, 397 and 227 allow it).
+    void twist() {
+        constexpr uint32_t A = 0x9908b0dfu;
+        for (int kk = 0; kk < N - M; ++kk) {
+            const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        }
+        for (int kk = N - M; kk < N - 1; ++kk) {
+            const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        }
+        const uint32_t y = (mt[N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+        mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        refresh();
+        index = 0;
+    }
+
+    inline uint32_t next() {
+        if (index >= N) twist();
+        return out[index++];
     }
 
     // getrandbits(k) for 1 <= k <= 32 (the fast path of _random_Random_getrandbits).
@@ -109,52 +122,35 @@ inline int64_t sample_setsize(int64_t k) {
 }
 
 // random.sample(population, k) expressed on positions 0..n-1 of the
-// population: writes the k chosen positions in result order.  `scratch` must
-// hold 2*k entries.  Requires 0 <= k <= n.
-inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize,
-                             int64_t* out, int64_t* scratch) {
+// population: writes the k chosen positions in result order.  `pool` must
+// hold setsize entries.  Requires 0 <= k <= n.
+template <class OutT>
+inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize, OutT* out,
+                             int32_t* pool) {
     if (n <= setsize) {
         // pool branch: pool = list(population); j = randbelow(n-i);
-        // result[i] = pool[j]; pool[j] = pool[n-i-1].  The pool is tracked as
-        // a sparse overlay on the identity permutation (<= k entries moved).
-        int64_t* mkey = scratch;      // overridden pool slots
-        int64_t* mval = scratch + k;  // their contents
-        int64_t nm = 0;
-        auto pool_get = [&](int64_t idx) -> int64_t {
-            for (int64_t t = 0; t < nm; ++t)
-                if (mkey[t] == idx) return mval[t];
-            return idx;
-        };
-        auto pool_set = [&](int64_t idx, int64_t v) {
-            for (int64_t t = 0; t < nm; ++t)
-                if (mkey[t] == idx) {
-                    mval[t] = v;
-                    return;
-                }
-            mkey[nm] = idx;
-            mval[nm] = v;
-            ++nm;
-        };
+        // result[i] = pool[j]; pool[j] = pool[n-i-1]   (positions stand in
+        // for the population items).
+        for (int64_t t = 0; t < n; ++t) pool[t] = static_cast<int32_t>(t);
         for (int64_t i = 0; i < k; ++i) {
             const int64_t j = rng.randbelow(static_cast<uint64_t>(n - i));
-            out[i] = pool_get(j);
-            pool_set(j, pool_get(n - i - 1));
+            out[i] = static_cast<OutT>(pool[j]);
+            pool[j] = pool[n - i - 1];
         }
     } else {
-        // selected-set branch: redraw while j already selected.
-        for (int64_t i = 0; i < k; ++i) {
-            int64_t j;
-            bool dup;
-            do {
-                j = rng.randbelow(static_cast<uint64_t>(n));
-                dup = false;
-                for (int64_t t = 0; t < i; ++t)
-                    if (out[t] == j) {
-                        dup = true;
-                        break;
-                    }
-            } while (dup);
-            out[i] = j;
+        // selected-set branch: j = randbelow(n), redrawn while j in selected.
+        // Both a rejected word (r >= n) and a repeat are simply skipped, so
+        // the result is the stream's accepted-and-new values in order; the
+        // scan below keeps that exact word consumption without a
+        // data-dependent branch per word.
+        const int sh = 32 - (64 - __builtin_clzll(static_cast<uint64_t>(n)));
+        int64_t cnt = 0;
+        while (cnt < k) {
+            const uint32_t r = rng.next() >> sh;
+            bool fresh = static_cast<uint64_t>(r) < static_cast<uint64_t>(n);
+            for (int64_t t = 0; t < cnt; ++t) fresh &= static_cast<int64_t>(out[t]) != static_cast<int64_t>(r);
+            out[cnt] = static_cast<OutT>(r);  // kept only when fresh
+            cnt += fresh;
         }
     }
 }

@@ -7,9 +7,15 @@
 // Rules follow Objects/setobject.c: LINEAR_PROBES = 9, PERTURB_SHIFT = 5,
 // PySet_MINSIZE = 8, grow at fill*5 >= mask*3 to used*4 (used*2 above 50000),
 // set_merge's pre-resize / slot-copy / insert_clean fast paths.  The reference
-// never deletes from these sets, so there are no dummy entries (fill == used).
+// never deletes from these sets, so there are no dummy entries (fill == used);
+// a caller-built row with dummies is flagged by fill > used.
+//
+// Tables of up to kInline slots live inside the object (a sampled
+// neighbourhood of k <= 25 never exceeds 128 slots), so the per-node sets of
+// a hop are built without touching the heap.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -17,30 +23,63 @@
 namespace gs {
 
 struct PySet {
-    static constexpr int64_t EMPTY = -1;
+    static constexpr int32_t EMPTY = -1;
     static constexpr size_t MINSIZE = 8;
     static constexpr size_t LINEAR_PROBES = 9;
     static constexpr int PERTURB_SHIFT = 5;
+    static constexpr size_t kInline = 128;
 
-    std::vector<int64_t> tab;
+    int32_t small_[kInline];
+    std::vector<int32_t> big_;
+    int32_t* tab = small_;
     size_t mask = MINSIZE - 1;
     int64_t fill = 0;
     int64_t used = 0;
 
-    PySet() : tab(MINSIZE, EMPTY) {}
+    PySet() { std::fill_n(small_, MINSIZE, EMPTY); }
+    PySet(const PySet& o) { *this = o; }
+    PySet& operator=(const PySet& o) {
+        if (this == &o) return *this;
+        mask = o.mask;
+        fill = o.fill;
+        used = o.used;
+        if (mask + 1 <= kInline) {
+            std::memcpy(small_, o.tab, (mask + 1) * sizeof(int32_t));
+            tab = small_;
+        } else {
+            big_.assign(o.tab, o.tab + mask + 1);
+            tab = big_.data();
+        }
+        return *this;
+    }
 
     void reset() {
-        tab.assign(MINSIZE, EMPTY);
+        std::fill_n(small_, MINSIZE, EMPTY);
+        tab = small_;
         mask = MINSIZE - 1;
         fill = used = 0;
     }
 
+    size_t size() const { return mask + 1; }
+
+    // Point `tab` at an EMPTY table of `n` slots (inline when it fits).
+    void alloc_table(size_t n) {
+        if (n <= kInline) {
+            tab = small_;
+        } else {
+            big_.assign(n, EMPTY);
+            tab = big_.data();
+        }
+        if (tab == small_) std::memset(small_, 0xFF, n * sizeof(int32_t));  // EMPTY == -1
+        mask = n - 1;
+    }
+
     // set_insert_clean: key known absent, table known to have room.
-    static inline void insert_clean(int64_t* t, size_t m, int64_t key) {
+    static inline void insert_clean(int32_t* t, size_t m, int32_t key) {
         size_t perturb = static_cast<size_t>(key);
         size_t i = static_cast<size_t>(key) & m;
         for (;;) {
-            int64_t* e = t + i;
+            int32_t* e = t + i;
             if (*e == EMPTY) {
                 *e = key;
                 return;
@@ -63,22 +102,30 @@ struct PySet {
     void resize(int64_t minused) {
         size_t newsize = MINSIZE;
         while (newsize <= static_cast<size_t>(minused)) newsize <<= 1;
-        std::vector<int64_t> old;
-        old.swap(tab);
-        tab.assign(newsize, EMPTY);
-        mask = newsize - 1;
-        for (int64_t k : old)
-            if (k != EMPTY) insert_clean(tab.data(), mask, k);
+        int32_t keep_small[kInline];
+        std::vector<int32_t> keep_big;
+        const int32_t* old;
+        const size_t old_n = mask + 1;
+        if (tab == small_) {
+            std::memcpy(keep_small, small_, old_n * sizeof(int32_t));
+            old = keep_small;
+        } else {
+            keep_big.swap(big_);
+            old = keep_big.data();
+        }
+        alloc_table(newsize);
+        for (size_t s = 0; s < old_n; ++s)
+            if (old[s] != EMPTY) insert_clean(tab, mask, old[s]);
         fill = used;
     }
 
     // set_add_entry.  Returns true when the key was new.
-    bool add(int64_t key) {
+    bool add(int32_t key) {
         size_t perturb = static_cast<size_t>(key);
         size_t i = static_cast<size_t>(key) & mask;
-        int64_t* e;
+        int32_t* e;
         for (;;) {
-            e = tab.data() + i;
+            e = tab + i;
             size_t probes = (i + LINEAR_PROBES <= mask) ? LINEAR_PROBES : 0;
             for (;;) {
                 if (*e == EMPTY) goto found_unused;
@@ -99,11 +146,11 @@ struct PySet {
     }
 
     // Slot of a present key (same probe walk as add), or -1.
-    int64_t find_slot(int64_t key) const {
+    int64_t find_slot(int32_t key) const {
         size_t perturb = static_cast<size_t>(key);
         size_t i = static_cast<size_t>(key) & mask;
         for (;;) {
-            const int64_t* e = tab.data() + i;
+            const int32_t* e = tab + i;
             size_t probes = (i + LINEAR_PROBES <= mask) ? LINEAR_PROBES : 0;
             size_t s = i;
             for (;;) {
@@ -118,70 +165,82 @@ struct PySet {
         }
     }
 
+    // set_merge(this, other) where only other's iteration order and counts
+    // matter (this non-empty): pre-resize, then set_add_entry per key.
+    template <class K>
+    void merge_items(const K* keys, int64_t n_used) {
+        if (n_used == 0) return;
+        if ((fill + n_used) * 5 >= static_cast<int64_t>(mask) * 3) resize((used + n_used) * 2);
+        if (fill == 0) {  // cannot happen for the callers' non-empty targets
+            fill = used = n_used;
+            for (int64_t t = 0; t < n_used; ++t) insert_clean(tab, mask, keys[t]);
+            return;
+        }
+        for (int64_t t = 0; t < n_used; ++t) add(keys[t]);
+    }
+
     // set_merge(this, other).
     void merge(const PySet& o) {
         if (&o == this || o.used == 0) return;
         if ((fill + o.used) * 5 >= static_cast<int64_t>(mask) * 3) resize((used + o.used) * 2);
         if (fill == 0 && mask == o.mask && o.fill == o.used) {
-            tab = o.tab;
+            std::memcpy(tab, o.tab, (mask + 1) * sizeof(int32_t));
             fill = o.fill;
             used = o.used;
             return;
         }
         if (fill == 0) {
             fill = used = o.used;
-            for (int64_t k : o.tab)
-                if (k != EMPTY) insert_clean(tab.data(), mask, k);
+            for (size_t s = 0; s <= o.mask; ++s)
+                if (o.tab[s] != EMPTY) insert_clean(tab, mask, o.tab[s]);
             return;
         }
-        for (int64_t k : o.tab)
-            if (k != EMPTY) add(k);
+        for (size_t s = 0; s <= o.mask; ++s)
+            if (o.tab[s] != EMPTY) add(o.tab[s]);
     }
 
-    // set_merge with a one-element set {key} (the `| set([node])` of :285).
-    void merge_single(int64_t key) {
-        PySet one;
-        one.add(key);
-        merge(one);
+    // set_merge with a one-element set {key} (the `| set([node])` of :285):
+    // {key} has mask 7, used 1, key in slot key & 7.
+    void merge_single(int32_t key) {
+        if ((fill + 1) * 5 >= static_cast<int64_t>(mask) * 3) resize((used + 1) * 2);
+        if (fill == 0 && mask == MINSIZE - 1) {  // slot copy of {key}
+            std::fill_n(tab, MINSIZE, EMPTY);
+            tab[static_cast<size_t>(key) & 7] = key;
+            fill = used = 1;
+            return;
+        }
+        if (fill == 0) {
+            fill = used = 1;
+            insert_clean(tab, mask, key);
+            return;
+        }
+        add(key);
     }
 
     // A set whose table is given verbatim (an adjacency row's own layout).
-    void assign_layout(size_t m, const int64_t* keys, const uint32_t* slots, int64_t n) {
-        tab.assign(m + 1, EMPTY);
-        mask = m;
+    void assign_layout(size_t m, const int32_t* keys, const uint32_t* slots, int64_t n) {
+        alloc_table(m + 1);
         for (int64_t t = 0; t < n; ++t) tab[slots[t]] = keys[t];
         fill = used = n;
     }
 
     template <class F>
     void for_each(F&& f) const {
-        for (int64_t k : tab)
-            if (k != EMPTY) f(k);
+        for (size_t s = 0; s <= mask; ++s)
+            if (tab[s] != EMPTY) f(tab[s]);
     }
 };
 
 // set.copy() / make_new_set(iterable=set): an empty set merged with `o`.
+inline void copy_into(PySet& r, const PySet& o) {
+    r.reset();
+    r.merge(o);
+}
+
 inline PySet copy_of(const PySet& o) {
     PySet r;
     r.merge(o);
     return r;
-}
-
-// Final mask of a set grown by `n` distinct adds from empty (no deletions):
-// resizes depend only on the count of distinct keys.
-inline size_t grown_mask(int64_t n) {
-    size_t mask = PySet::MINSIZE - 1;
-    int64_t fill = 0;
-    for (int64_t u = 1; u <= n; ++u) {
-        fill = u;
-        if (static_cast<size_t>(fill) * 5 >= mask * 3) {
-            const int64_t minused = u > 50000 ? u * 2 : u * 4;
-            size_t ns = PySet::MINSIZE;
-            while (ns <= static_cast<size_t>(minused)) ns <<= 1;
-            mask = ns - 1;
-        }
-    }
-    return mask;
 }
 
 }  // namespace gs

@@ -48,23 +48,30 @@ struct Sample {
 static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
     h.pos_ptr.assign(n + 1, 0);
+    thread_local std::vector<int64_t> deg;
+    deg.resize(n);
     int64_t total = 0;
+    const int64_t* rp = g.row_ptr.data();
+    constexpr int64_t kAhead = 16;  // frontier ids are known: prefetch their row_ptr
+    for (int64_t r = 0; r < std::min(n, kAhead); ++r) __builtin_prefetch(rp + h.dst_ids[r]);
     for (int64_t r = 0; r < n; ++r) {
-        const int64_t d = g.degree(h.dst_ids[r]);
+        if (r + kAhead < n) __builtin_prefetch(rp + h.dst_ids[r + kAhead]);
+        const int64_t v = h.dst_ids[r];
+        const int64_t d = rp[v + 1] - rp[v];
+        deg[r] = d;
         total += (h.k > 0 && d >= h.k) ? h.k : d;
         GS_REQUIRE(total < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
         h.pos_ptr[r + 1] = static_cast<int32_t>(total);
     }
     h.pos.resize(total);
     const int64_t setsize = sample_setsize(h.k);
-    std::vector<int64_t> out(std::max<int64_t>(h.k, 1)), scratch(2 * std::max<int64_t>(h.k, 1));
+    thread_local std::vector<int32_t> pool;
+    pool.resize(std::max<int64_t>(setsize, 1));
     for (int64_t r = 0; r < n; ++r) {
-        const int64_t v = h.dst_ids[r];
-        const int64_t d = g.degree(v);
+        const int64_t d = deg[r];
         int32_t* dstp = h.pos.data() + h.pos_ptr[r];
         if (h.k > 0 && d >= h.k) {
-            sample_positions(rng, d, h.k, setsize, out.data(), scratch.data());
-            for (int64_t t = 0; t < h.k; ++t) dstp[t] = static_cast<int32_t>(out[t]);
+            sample_positions(rng, d, h.k, setsize, dstp, pool.data());
         } else {
             for (int64_t t = 0; t < d; ++t) dstp[t] = static_cast<int32_t>(t);
         }
@@ -89,8 +96,13 @@ static int64_t count_empty(const Graph& g, const Hop& h, bool gcn) {
 // transposed lists the backward pass gathers over.
 static void materialise(const Graph& g, Hop& h, bool gcn) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    std::vector<PySet> sets(n);
-    PySet s;
+    // samp_neighs[r] = S_r | {v}: built in a scratch set, kept only as its
+    // iteration order (set_items) — all the union needs from r >= 1 — plus
+    // the full table of r == 0, which the union copies.
+    PySet s, t, first;
+    h.set_ptr.assign(n + 1, 0);
+    h.set_items.clear();
+    h.set_items.reserve(h.pos.size() + n);
     for (int64_t r = 0; r < n; ++r) {
         const int64_t v = h.dst_ids[r];
         const int64_t rs = g.row_ptr[v], d = g.degree(v);
@@ -98,44 +110,46 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
         if (h.k > 0 && d >= h.k) {
             // set(random.sample(adj, k)) : adds in result order
             s.reset();
-            for (int64_t t = 0; t < cnt; ++t) s.add(g.col[rs + h.pos[h.pos_ptr[r] + t]]);
+            for (int64_t q = 0; q < cnt; ++q) s.add(g.col[rs + h.pos[h.pos_ptr[r] + q]]);
         } else {
             // the adjacency set object itself, with its own table layout
-            std::vector<int64_t> keys(d);
-            for (int64_t t = 0; t < d; ++t) keys[t] = g.col[rs + t];
-            s.assign_layout((size_t(1) << g.log2size[v]) - 1, keys.data(), g.slot.data() + rs, d);
+            s.assign_layout((size_t(1) << g.log2size[v]) - 1, g.col.data() + rs, g.slot.data() + rs, d);
             if (!g.dirty.empty() && g.dirty[v]) s.fill = s.used + 1;  // dummies: no slot-copy fast path
         }
-        sets[r] = copy_of(s);      // samp_neigh | set([v])  (:285)
-        sets[r].merge_single(v);
+        copy_into(t, s);  // samp_neigh | set([v])  (:285)
+        t.merge_single(v);
+        if (r == 0) first = t;
+        t.for_each([&](int64_t key) { h.set_items.push_back(key); });
+        h.set_ptr[r + 1] = static_cast<int32_t>(h.set_items.size());
     }
-    // samp_neighs as the reference holds them (API / parity views).
-    h.set_ptr.assign(n + 1, 0);
-    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] = h.set_ptr[r] + static_cast<int32_t>(sets[r].used);
-    h.set_items.resize(h.set_ptr[n]);
-    for (int64_t r = 0; r < n; ++r) {
-        int64_t w = h.set_ptr[r];
-        sets[r].for_each([&](int64_t key) { h.set_items[w++] = key; });
-    }
-    // list(set.union(*samp_neighs))  (:286)
+    // list(set.union(*samp_neighs))  (:286): copy of the first, then set_merge
+    // of each other set, which only walks that set's iteration order.
     PySet u;
     if (n > 0) {
-        u = copy_of(sets[0]);
-        for (int64_t r = 1; r < n; ++r) u.merge(sets[r]);
+        copy_into(u, first);
+        for (int64_t r = 1; r < n; ++r)
+            u.merge_items(h.set_items.data() + h.set_ptr[r], h.set_ptr[r + 1] - h.set_ptr[r]);
     }
-    std::vector<int32_t> slot_pos(u.mask + 1, -1);
+    // Union-local positions through a dense node -> position map (one int32
+    // per graph node per sampler thread, restored to -1 before returning).
+    thread_local std::vector<int32_t> pos_of;
+    if (static_cast<int64_t>(pos_of.size()) < g.n_nodes) pos_of.assign(g.n_nodes, -1);
     h.src_ids.clear();
     h.src_ids.reserve(u.used);
     for (size_t sl = 0; sl <= u.mask; ++sl) {
-        if (u.tab[sl] == PySet::EMPTY) continue;
-        slot_pos[sl] = static_cast<int32_t>(h.src_ids.size());
-        h.src_ids.push_back(u.tab[sl]);
+        const int32_t key = u.tab[sl];
+        if (key == PySet::EMPTY) continue;
+        pos_of[key] = static_cast<int32_t>(h.src_ids.size());
+        h.src_ids.push_back(key);
     }
-    auto local_of = [&](int64_t key) -> int32_t {
-        const int64_t sl = u.find_slot(key);
-        GS_REQUIRE(sl >= 0, GS_EINVAL, "internal: key missing from union");
-        return slot_pos[sl];
-    };
+    struct Restore {
+        std::vector<int32_t>& m;
+        const std::vector<int64_t>& keys;
+        ~Restore() {
+            for (int64_t k : keys) m[k] = -1;
+        }
+    } restore{pos_of, h.src_ids};
+    auto local_of = [&](int64_t key) -> int32_t { return pos_of[key]; };
     // Neighbourhoods in union-local ids, ascending (= the dense mask's column
     // order, :305-308); non-gcn removes self (:297-298).
     h.nbr_ptr.assign(n + 1, 0);
@@ -145,11 +159,17 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     for (int64_t r = 0; r < n; ++r) {
         const int64_t v = h.dst_ids[r];
         tmp.clear();
-        sets[r].for_each([&](int64_t key) {
-            if (!gcn && key == v) return;
+        for (int32_t q = h.set_ptr[r]; q < h.set_ptr[r + 1]; ++q) {
+            const int64_t key = h.set_items[q];
+            if (!gcn && key == v) continue;
             tmp.push_back(local_of(key));
-        });
-        std::sort(tmp.begin(), tmp.end());
+        }
+        for (size_t a = 1; a < tmp.size(); ++a) {  // insertion sort: lists are <= k+1 long
+            const int32_t x = tmp[a];
+            size_t b = a;
+            for (; b > 0 && tmp[b - 1] > x; --b) tmp[b] = tmp[b - 1];
+            tmp[b] = x;
+        }
         h.nbr.insert(h.nbr.end(), tmp.begin(), tmp.end());
         h.nbr_ptr[r + 1] = static_cast<int32_t>(h.nbr.size());
         h.self_local[r] = local_of(v);
@@ -228,6 +248,7 @@ int gs_rng_set_state(gs_rng* rng, const uint32_t* mt624, int64_t pos) {
     GS_REQUIRE(pos >= 0 && pos <= gs::MT19937::N, GS_EINVAL, "state index out of range");
     std::memcpy(rng->mt.mt, mt624, sizeof(rng->mt.mt));
     rng->mt.index = static_cast<int>(pos);
+    rng->mt.refresh();
     GS_API_END
 }
 
@@ -259,8 +280,9 @@ int gs_rng_sample_positions(gs_rng* rng, int64_t n, int64_t k, int64_t* out) {
     GS_REQUIRE(rng && (out || k == 0), GS_EINVAL, "bad arguments");
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 32), GS_EINVAL, "population size out of range");
     GS_REQUIRE(k >= 0 && k <= n, GS_ERANGE, "Sample larger than population or is negative");
-    std::vector<int64_t> scratch(2 * std::max<int64_t>(k, 1));
-    gs::sample_positions(rng->mt, n, k, gs::sample_setsize(k), out, scratch.data());
+    const int64_t setsize = gs::sample_setsize(k);
+    std::vector<int32_t> pool(static_cast<size_t>(std::max<int64_t>(std::min(setsize, n), 1)));
+    gs::sample_positions(rng->mt, n, k, setsize, out, pool.data());
     GS_API_END
 }
 

@@ -13,6 +13,7 @@ Initialisation reproduces the reference modules' init under torch.manual_seed
 import os
 import queue
 import threading
+import time
 
 import numpy as np
 import torch
@@ -148,6 +149,7 @@ class Prefetcher:
             self.free.put(i)
         self._it = iter(batches)
         self._stop = False
+        self.sample_s = []  # host sampler seconds per batch
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
 
@@ -156,7 +158,9 @@ class Prefetcher:
             for roots in self._it:
                 if self._stop:
                     break
+                t0 = time.perf_counter()
                 s = sample(self.graph, self.rng, roots, self.fanouts, gcn=self.gcn)
+                self.sample_s.append(time.perf_counter() - t0)
                 slot = self.free.get()
                 ev = self.events[slot]
                 if ev is not None:

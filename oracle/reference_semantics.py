@@ -137,4 +137,4 @@ def train_step_dense(adj, roots, fanouts, X, weights, cls_w, cls_b, labels, agg=
         for p in list(weights) + [cls_w, cls_b]:
             p.add_(p.grad, alpha=-lr)
             p.grad = None
-    return float(loss)
+    return float(loss.detach())
