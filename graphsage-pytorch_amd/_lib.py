@@ -90,7 +90,22 @@ _SIGS = {
                                   _vp]),
     "gs_clip_sgd": (_i32, [_i32, _vp, _vp, _vp, _f32, _f32, _f32, _vp, _vp]),
     "gs_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
+    "gs_trainer_create": (_i32, [_vp, _p(_vp)]),
+    "gs_trainer_destroy": (None, [_vp]),
+    "gs_trainer_n_params": (_i64, [_vp]),
+    "gs_trainer_ws_bytes": (_i64, [_vp, _vp]),
+    "gs_trainer_forward_backward": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "gs_trainer_update": (_i32, [_vp, _f32, _vp, _vp]),
 }
+
+
+class TrainerConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", _i32), ("hidden", _i32), ("n_classes", _i32), ("agg", _i32), ("gcn", _i32),
+        ("feat_dtype", _i32), ("feat_dim", _i64), ("feat_ld", _i64),
+        ("X", _vp), ("row_ptr", _vp), ("col", _vp), ("labels", _vp), ("params", _vp), ("grads", _vp),
+        ("lr", _f32), ("max_norm", _f32),
+    ]
 
 _lib = None
 

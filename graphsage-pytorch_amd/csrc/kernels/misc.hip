@@ -48,54 +48,49 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// One wavefront per row: logits, log_softmax (max-shifted, as torch), the
-// row's NLL term and dlogits = (softmax - onehot) / B.
+// One wavefront per row: logits (lanes over D, one wave reduction per class),
+// log_softmax (max-shifted, as torch), the row's NLL term, dlogits =
+// (softmax - onehot) / B, and dE[i] = dlogits · Wc (lanes over D again).
+constexpr int kClsMaxC = 1024;
 __global__ __launch_bounds__(kTb) void cls_rows_kernel(int B, int D, int C, const float* __restrict__ E,
                                                        const float* __restrict__ Wc, const float* __restrict__ bc,
                                                        const int* __restrict__ labels, float* __restrict__ dl,
-                                                       float* __restrict__ rowloss) {
-    const int lane = threadIdx.x & 63;
-    const int i = blockIdx.x * (kTb / 64) + (threadIdx.x >> 6);
+                                                       float* __restrict__ rowloss, float* __restrict__ dE) {
+    __shared__ float zs[kTb / 64][kClsMaxC];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = blockIdx.x * (kTb / 64) + w;
     if (i >= B) return;
     const float* e = E + static_cast<int64_t>(i) * D;
     const int y = labels[i];
     float mx = -INFINITY;
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        const int c = c0 + lane;
-        float z = -INFINITY;
-        if (c < C) {
-            z = bc[c];
-            const float* w = Wc + static_cast<int64_t>(c) * D;
-            for (int d = 0; d < D; ++d) z = fmaf(e[d], w[d], z);
-            dl[static_cast<int64_t>(i) * C + c] = z;
-        }
-        mx = fmaxf(mx, wave_max(z));
+    for (int c = 0; c < C; ++c) {
+        const float* wr = Wc + static_cast<int64_t>(c) * D;
+        float p = 0.f;
+        for (int d = lane; d < D; d += 64) p = fmaf(e[d], wr[d], p);
+        const float z = wave_sum(p) + bc[c];
+        if (lane == 0) zs[w][c] = z;
+        mx = fmaxf(mx, z);
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row's logits are in LDS
+    __builtin_amdgcn_wave_barrier();
     float se = 0.f;
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        const int c = c0 + lane;
-        se += wave_sum(c < C ? expf(dl[static_cast<int64_t>(i) * C + c] - mx) : 0.f);
-    }
-    const float lse = logf(se);
+    for (int c = lane; c < C; c += 64) se += expf(zs[w][c] - mx);
+    const float lse = logf(wave_sum(se));
     const float invB = 1.0f / static_cast<float>(B);
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        const int c = c0 + lane;
-        if (c >= C) continue;
-        const float lp = dl[static_cast<int64_t>(i) * C + c] - mx - lse;
+    for (int c = lane; c < C; c += 64) {
+        const float lp = zs[w][c] - mx - lse;
         if (c == y) rowloss[i] = -lp;
-        dl[static_cast<int64_t>(i) * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+        const float g = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+        dl[static_cast<int64_t>(i) * C + c] = g;
+        zs[w][c] = g;
     }
-}
-
-// dE[i][d] = Σ_c dl[i][c] · Wc[c][d]
-__global__ __launch_bounds__(kTb) void cls_dE_kernel(int B, int D, int C, const float* __restrict__ dl,
-                                                     const float* __restrict__ Wc, float* __restrict__ dE) {
-    const int64_t t = blockIdx.x * int64_t(kTb) + threadIdx.x;
-    if (t >= static_cast<int64_t>(B) * D) return;
-    const int i = static_cast<int>(t / D), d = static_cast<int>(t - static_cast<int64_t>(i) * D);
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s = fmaf(dl[static_cast<int64_t>(i) * C + c], Wc[static_cast<int64_t>(c) * D + d], s);
-    dE[t] = s;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (int d = lane; d < D; d += 64) {
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s = fmaf(zs[w][c], Wc[static_cast<int64_t>(c) * D + d], s);
+        dE[static_cast<int64_t>(i) * D + d] = s;
+    }
 }
 
 // Partial dWc / dbc over a 32-row chunk: slab[chunk][c][0..D) and [c][D] (bias).
@@ -109,6 +104,7 @@ __global__ __launch_bounds__(kTb) void cls_dW_partial_kernel(int B, int D, int C
     const int c = static_cast<int>(t / (D + 1)), d = static_cast<int>(t - static_cast<int64_t>(c) * (D + 1));
     const int i0 = chunk * kClsChunk, i1 = min(B, i0 + kClsChunk);
     float s = 0.f;
+#pragma unroll 8
     for (int i = i0; i < i1; ++i) {
         const float g = dl[static_cast<int64_t>(i) * C + c];
         s += (d < D) ? g * E[static_cast<int64_t>(i) * D + d] : g;
@@ -231,6 +227,7 @@ int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E, const fl
     GS_API_BEGIN
     using namespace gs;
     GS_REQUIRE(B >= 1 && D >= 1 && C >= 1 && B < (1 << 30), GS_EINVAL, "bad sizes");
+    GS_REQUIRE(C <= kClsMaxC, GS_EINVAL, "at most 1024 classes");
     GS_REQUIRE(E && Wc && bc && labels && loss && dE && dWc && dbc && ws, GS_EINVAL, "NULL device pointer");
     hipStream_t st = as_stream(stream);
     const int b = static_cast<int>(B), d = static_cast<int>(D), c = static_cast<int>(C);
@@ -238,8 +235,7 @@ int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E, const fl
     float* rowloss = ws + B * C;
     const int n_chunks = (b + kClsChunk - 1) / kClsChunk;
     float* slab = rowloss + B;
-    cls_rows_kernel<<<dim3((b + 3) / 4), kTb, 0, st>>>(b, d, c, E, Wc, bc, labels, dl, rowloss);
-    cls_dE_kernel<<<dim3(static_cast<unsigned>((B * D + kTb - 1) / kTb)), kTb, 0, st>>>(b, d, c, dl, Wc, dE);
+    cls_rows_kernel<<<dim3((b + 3) / 4), kTb, 0, st>>>(b, d, c, E, Wc, bc, labels, dl, rowloss, dE);
     const int64_t per = C * (D + 1);
     cls_dW_partial_kernel<<<dim3(static_cast<unsigned>((per + kTb - 1) / kTb), n_chunks), kTb, 0, st>>>(b, d, c, dl,
                                                                                                        E, slab);

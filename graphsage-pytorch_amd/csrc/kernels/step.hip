@@ -1,0 +1,215 @@
+// Native training-step runtime: the reference's per-batch loop body
+// (utils.py:157-191 — GraphSage forward, Classification + NLL, backward,
+// clip_grad_norm_ per model, SGD) issued as one stream of the kernels in this
+// library, with every intermediate carved from one caller-owned workspace.
+// The Python host makes two calls per step (forward_backward, update) and
+// puts the RCCL gradient all-reduce between them.
+#include <algorithm>
+#include <vector>
+
+#include "kcommon.hpp"
+
+struct gs_trainer {
+    gs_trainer_config cfg;
+    std::vector<int64_t> w_off;  // element offset of each parameter in the flat buffer
+    std::vector<int64_t> w_rows, w_cols;
+    int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
+};
+
+namespace gs {
+
+__global__ void gather_labels_kernel(const int* __restrict__ labels, const int* __restrict__ roots, int n,
+                                     int* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = labels[roots[i]];
+}
+
+// Bump allocator over the workspace (256-byte aligned carves).
+struct Carve {
+    char* base;
+    int64_t cap, at = 0;
+    template <class T>
+    T* take(int64_t n) {
+        at = (at + 255) & ~int64_t(255);
+        T* p = base ? reinterpret_cast<T*>(base + at) : nullptr;
+        at += n * static_cast<int64_t>(sizeof(T));
+        return p;
+    }
+};
+
+struct HopSz {
+    int64_t n_dst, n_pos, n_src, n_nbr;
+};
+
+static inline void ok(int rc) {
+    if (rc != GS_OK) fail(rc, gs_last_error());
+}
+
+// Runs (or, with ws == nullptr, only sizes) one forward + backward.
+static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+                        const int32_t* roots, int64_t B, char* ws, int64_t ws_bytes, float* loss,
+                        hipStream_t st) {
+    const gs_trainer_config& c = T.cfg;
+    const int L = c.n_layers;
+    const int64_t H = c.hidden, F = c.feat_dim;
+    const bool lowp = c.feat_dtype == GS_BF16;
+    const size_t xsz = lowp ? 2 : 4;
+    std::vector<HopSz> hs(L);
+    for (int j = 0; j < L; ++j) hs[j] = {hop_sizes[4 * j], hop_sizes[4 * j + 1], hop_sizes[4 * j + 2], hop_sizes[4 * j + 3]};
+    auto fld = [&](int hop, int f) -> const int32_t* {  // hop 1-based
+        const int64_t o = offsets[(hop - 1) * GS_PK_NFIELDS + f];
+        GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
+        return pack + o;
+    };
+    GS_REQUIRE(hs[0].n_dst == B, GS_EINVAL, "roots / hop-1 size mismatch");
+    Carve cv{ws, ws_bytes};
+    // ---- activations
+    std::vector<void*> agg(L);
+    std::vector<float*> h(L);
+    std::vector<int32_t*> am(L, nullptr);
+    std::vector<int64_t> rows(L), in_dim(L);
+    for (int l = 1; l <= L; ++l) {
+        const int j = L - l + 1;
+        rows[l - 1] = hs[j - 1].n_dst;
+        in_dim[l - 1] = l == 1 ? F : H;
+        if (l == 1) agg[0] = cv.take<char>(rows[0] * F * static_cast<int64_t>(xsz));
+        else agg[l - 1] = cv.take<float>(rows[l - 1] * H);
+        h[l - 1] = cv.take<float>(rows[l - 1] * H);
+        if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
+    }
+    void* w1lp = lowp ? cv.take<uint16_t>(T.w_rows[0] * T.w_cols[0]) : nullptr;
+    int32_t* y = cv.take<int32_t>(B);
+    float* demb = cv.take<float>(B * H);
+    float* cls_ws = cv.take<float>(gs_cls_nll_ws_floats(B, H, c.n_classes));
+    int64_t dw_need = 0, dx_rows = 0, dprev_rows = 0;
+    for (int l = 1; l <= L; ++l) {
+        dw_need = std::max(dw_need, gs_sage_linear_bwd_weight_ws(rows[l - 1], T.w_cols[l - 1], H));
+        if (l >= 2) {
+            dx_rows = std::max(dx_rows, rows[l - 1]);
+            dprev_rows = std::max(dprev_rows, rows[l - 2]);
+        }
+    }
+    char* dw_ws = cv.take<char>(dw_need);
+    float* dIn = cv.take<float>(dx_rows * (c.gcn ? H : 2 * H));
+    float* dbuf[2] = {cv.take<float>(dprev_rows * H), cv.take<float>(dprev_rows * H)};
+    if (!ws) return cv.at + 256;
+    GS_REQUIRE(cv.at <= ws_bytes, GS_EINVAL, "workspace too small");
+
+    float* P = c.params;
+    float* G = c.grads;
+    // ---- forward (models.py:255-267)
+    if (lowp) ok(gs_cast_f32_bf16(P + T.w_off[0], w1lp, T.w_rows[0] * T.w_cols[0], st));
+    const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
+    ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, rows[0],
+                  fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.row_ptr, c.col, dst_L, c.gcn, agg[0],
+                  static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
+                          dst_L, agg[0], F, lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]), h[0], H, 1, st));
+    for (int l = 2; l <= L; ++l) {
+        const int j = L - l + 1;
+        ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), GS_F32, h[l - 2], H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
+                      fld(j, GS_PK_NBR), nullptr, nullptr, nullptr, 0, agg[l - 1], GS_F32, H, am[l - 1], st));
+        ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
+                              agg[l - 1], H, P + T.w_off[l - 1], h[l - 1], H, 1, st));
+    }
+    // ---- loss head (models.py:8-27, utils.py:159-164)
+    gather_labels_kernel<<<dim3(static_cast<unsigned>((B + 255) / 256)), 256, 0, st>>>(c.labels, roots,
+                                                                                         static_cast<int>(B), y);
+    check_launch("gather_labels");
+    ok(gs_cls_nll_fwd_bwd(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off, y, loss, demb,
+                          G + T.cls_w_off, G + T.cls_b_off, cls_ws, st));
+    // ---- backward (utils.py:184)
+    const float* dH = demb;
+    int relu = 1;
+    int flip = 0;
+    for (int l = L; l >= 1; --l) {
+        const int j = L - l + 1;
+        const bool first = l == 1;
+        const void* x_in = first ? c.X : h[l - 2];
+        const int32_t* sidx = first ? dst_L : fld(j, GS_PK_SELF);
+        const int64_t fin = in_dim[l - 1], ldx = first ? c.feat_ld : H;
+        ok(gs_sage_linear_bwd_weight(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H,
+                                     c.gcn ? nullptr : x_in, ldx, sidx, agg[l - 1], fin, dH, h[l - 1], H, relu,
+                                     G + T.w_off[l - 1], dw_ws, dw_need, st));
+        if (first) break;
+        const int64_t ldd = c.gcn ? H : 2 * H;
+        float* dSelf = c.gcn ? nullptr : dIn;
+        float* dA = c.gcn ? dIn : dIn + H;
+        ok(gs_sage_linear_bwd_input(rows[l - 1], H, H, dH, h[l - 1], H, relu, P + T.w_off[l - 1], dSelf, dA, ldd,
+                                    st));
+        float* dprev = dbuf[flip];
+        flip ^= 1;
+        ok(gs_agg_bwd(static_cast<gs_agg>(c.agg), rows[l - 2], H, fld(j, GS_PK_TPTR), fld(j, GS_PK_TIDX),
+                      fld(j, GS_PK_NBR_PTR), dA, dSelf, ldd, am[l - 1], h[l - 2], H, dprev, st));
+        dH = dprev;
+        relu = 0;  // dprev is already masked by relu'(h_{l-1})
+    }
+    return cv.at;
+}
+
+}  // namespace gs
+
+extern "C" {
+
+int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(cfg && out, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(cfg->n_layers >= 1 && cfg->n_layers <= GS_MAX_HOPS, GS_EINVAL, "n_layers out of range");
+    GS_REQUIRE(cfg->hidden >= 16 && cfg->hidden <= 256 && cfg->hidden % 16 == 0, GS_EINVAL, "bad hidden size");
+    GS_REQUIRE(cfg->n_classes >= 1 && cfg->feat_dim >= 1 && cfg->feat_ld >= cfg->feat_dim, GS_EINVAL, "bad dims");
+    GS_REQUIRE(cfg->X && cfg->row_ptr && cfg->col && cfg->labels && cfg->params && cfg->grads, GS_EINVAL,
+               "NULL device pointer");
+    auto* T = new gs_trainer();
+    T->cfg = *cfg;
+    int64_t at = 0;
+    for (int l = 1; l <= cfg->n_layers; ++l) {
+        const int64_t in = l == 1 ? cfg->feat_dim : cfg->hidden;
+        T->w_off.push_back(at);
+        T->w_rows.push_back(cfg->hidden);
+        T->w_cols.push_back(cfg->gcn ? in : 2 * in);
+        at += cfg->hidden * T->w_cols.back();
+    }
+    T->cls_w_off = at;
+    at += static_cast<int64_t>(cfg->n_classes) * cfg->hidden;
+    T->cls_b_off = at;
+    at += cfg->n_classes;
+    T->total = at;
+    *out = T;
+    GS_API_END
+}
+
+void gs_trainer_destroy(gs_trainer* t) { delete t; }
+
+int64_t gs_trainer_n_params(const gs_trainer* t) { return t ? t->total : -1; }
+
+int64_t gs_trainer_ws_bytes(gs_trainer* t, const int64_t* hop_sizes) {
+    try {
+        std::vector<int64_t> off(GS_MAX_HOPS * GS_PK_NFIELDS, 0);
+        return gs::run_step(*t, nullptr, hop_sizes, off.data(), nullptr, hop_sizes[0], nullptr, 0, nullptr,
+                            nullptr);
+    } catch (const gs::Error& e) {
+        gs::set_error(e.what());
+        return -1;
+    }
+}
+
+int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                                const int64_t* offsets, const int32_t* roots, int64_t n_roots, void* ws,
+                                int64_t ws_bytes, float* loss, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && pack && hop_sizes && offsets && roots && ws && loss, GS_EINVAL, "NULL argument");
+    gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
+                 gs::as_stream(stream));
+    GS_API_END
+}
+
+int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
+    const int64_t goff[3] = {0, t->cls_w_off, t->total};
+    int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);
+    if (rc != GS_OK) return rc;
+    GS_API_END
+}
+
+}  // extern "C"

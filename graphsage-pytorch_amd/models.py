@@ -44,6 +44,15 @@ class DeviceSample:
             buf = host.to(device, non_blocking=True)
         self.buf = buf
 
+    def native_sizes(self):
+        """(hop sizes [L][4], pack offsets [GS_MAX_HOPS][NFIELDS]) as int64 arrays."""
+        if getattr(self, "_native", None) is None:
+            sizes = np.array(self.sizes, np.int64).reshape(-1)
+            offs = np.full((_lib.GS_MAX_HOPS, _lib.GS_PK_NFIELDS), -1, np.int64)
+            offs[:self.n_hops] = np.array(self.offsets, np.int64)
+            self._native = (sizes, offs.reshape(-1))
+        return self._native
+
     def field(self, hop, name):
         """int32 view of `name` for hop (1-based)."""
         n_dst, n_pos, n_src, n_nbr = self.sizes[hop - 1]

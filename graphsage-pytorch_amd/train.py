@@ -10,6 +10,7 @@ Parameter layout (one flat fp32 buffer, one all-reduce per step):
 Initialisation reproduces the reference modules' init under torch.manual_seed
 (SageLayer xavier_uniform_ per layer, then Linear + xavier on its weight).
 """
+import ctypes
 import os
 import queue
 import threading
@@ -19,8 +20,10 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from . import hip_ops as ops
-from .models import Classification, DeviceSample, SageLayer, sage_backward, sage_forward
+from ._lib import check, lib
+from .models import Classification, DeviceSample, SageLayer
 from .sampler import RNG, sample
 
 
@@ -74,43 +77,52 @@ class NativeTrainer:
         names = [f"sage_layer{i}.weight" for i in range(1, num_layers + 1)] + ["layer.0.weight", "layer.0.bias"]
         self.p = FlatParams(list(sage_w) + [cls_w, cls_b], names, [0, num_layers], self.device)
         self.row_ptr, self.col = graph.device_csr(self.device)
-        self.lowp = features.dtype == torch.bfloat16
-        self.W1lp = (torch.empty(self.p.shapes[0], dtype=torch.bfloat16, device=self.device)
-                     if self.lowp else None)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.clip_ws = torch.empty(65 * 2, dtype=torch.float32, device=self.device)
-        self._cls_ws = {}
+        X = self.X
+        cfg = _lib.TrainerConfig(
+            n_layers=num_layers, hidden=hidden, n_classes=n_classes, agg=ops.agg_op(agg_func), gcn=int(gcn),
+            feat_dtype=_lib.GS_BF16 if X.dtype == torch.bfloat16 else _lib.GS_F32,
+            feat_dim=X.shape[1], feat_ld=X.stride(0), X=X.data_ptr(), row_ptr=self.row_ptr.data_ptr(),
+            col=self.col.data_ptr(), labels=self.labels.data_ptr(), params=self.p.params.data_ptr(),
+            grads=self.p.grads.data_ptr(), lr=lr, max_norm=max_norm)
+        h = ctypes.c_void_p()
+        check(lib().gs_trainer_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        if lib().gs_trainer_n_params(h) != self.p.params.numel():
+            raise RuntimeError("flat parameter layout mismatch")
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
 
     def weights(self):
         return [self.p.view(i) for i in range(self.L)]
 
     def forward_backward(self, ds, roots_dev):
-        """Loss (device scalar) and gradients into self.p.grads for one batch."""
-        Ws = self.weights()
-        lowp = None
-        if self.lowp:
-            ops.cast_bf16(Ws[0], self.W1lp)
-            lowp = [self.W1lp]
-        hs, aggs, ams = sage_forward(ds, self.X, Ws, self.agg, self.gcn, self.row_ptr, self.col, lowp)
-        emb = hs[-1]
-        B = emb.shape[0]
-        ws = self._cls_ws.get(B)
-        if ws is None:
-            ws = self._cls_ws[B] = ops.cls_nll_workspace(B, self.H, self.C, self.device)
-        y = self.labels.index_select(0, roots_dev)
-        demb = torch.empty_like(emb)
-        ops.cls_nll_fwd_bwd(emb, self.p.view(self.L), self.p.view(self.L + 1), y, self.loss, demb,
-                            self.p.view(self.L, grad=True), self.p.view(self.L + 1, grad=True), ws)
-        dWs = [self.p.view(i, grad=True) for i in range(self.L)]
-        sage_backward(ds, self.X, Ws, self.agg, self.gcn, hs, aggs, ams, demb, dWs)
+        """Loss (device scalar) and gradients into self.p.grads for one batch:
+        one native call that issues every kernel of the step on the stream."""
+        sizes, offs = ds.native_sizes()
+        need = int(lib().gs_trainer_ws_bytes(self._h, sizes.ctypes.data))
+        if need < 0:
+            check(_lib.GS_EINVAL)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(int(need * 1.25) + (1 << 20), dtype=torch.uint8, device=self.device)
+        check(lib().gs_trainer_forward_backward(
+            self._h, ds.buf.data_ptr(), sizes.ctypes.data, offs.ctypes.data, roots_dev.data_ptr(),
+            roots_dev.numel(), self._ws.data_ptr(), self._ws.numel(), self.loss.data_ptr(),
+            _lib.stream_ptr(self.device)))
         return self.loss
 
     def apply_update(self, world_size=1, group=None):
         """All-reduce (sum) the flat gradients over ranks, then clip + SGD with 1/world."""
         if world_size > 1:
             dist.all_reduce(self.p.grads, group=group)
-        ops.clip_sgd(self.p.group_off, self.p.params, self.p.grads, 1.0 / world_size, self.max_norm,
-                     self.lr, self.clip_ws)
+        check(lib().gs_trainer_update(self._h, 1.0 / world_size, self.clip_ws.data_ptr(),
+                                      _lib.stream_ptr(self.device)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.gs_trainer_destroy(h)
+            self._h = None
 
     def step(self, ds, roots_dev, world_size=1, group=None):
         loss = self.forward_backward(ds, roots_dev)

@@ -263,6 +263,46 @@ int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params,
 /* f32 → bf16 (RNE) cast, n elements. */
 int gs_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
 
+/* ------------------------------------------------------- training runtime
+ * One supervised step of the reference loop (utils.py:144-191 without
+ * extend_nodes): GraphSage forward over a packed sample, Classification +
+ * NLL mean, backward into the flat gradient buffer, then (separate call, so
+ * the caller can all-reduce gradients in between) clip_grad_norm_(max_norm)
+ * per model and SGD.  Flat parameter layout:
+ *   [sage_layer1.weight | ... | sage_layerL.weight | layer.0.weight | layer.0.bias]
+ * Device pointers stay owned by the caller. */
+typedef struct {
+    int32_t n_layers, hidden, n_classes;
+    int32_t agg;        /* gs_agg */
+    int32_t gcn;
+    int32_t feat_dtype; /* gs_dtype of X */
+    int64_t feat_dim, feat_ld;
+    const void* X;          /* [N, feat_ld] raw features                 */
+    const int64_t* row_ptr; /* device CSR (gs_graph_row_ptr mirrored)    */
+    const int32_t* col;
+    const int32_t* labels;  /* [N] class ids                             */
+    float* params;          /* flat, gs_trainer_n_params floats          */
+    float* grads;
+    float lr, max_norm;     /* reference: 0.7, 5 (utils.py:136, :186)    */
+} gs_trainer_config;
+
+typedef struct gs_trainer gs_trainer;
+int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out);
+void gs_trainer_destroy(gs_trainer* t);
+int64_t gs_trainer_n_params(const gs_trainer* t);
+/* Workspace bytes for a sample with hop_sizes[L][4] = (n_dst, n_pos, n_src,
+ * n_nbr) per hop; -1 on error. */
+int64_t gs_trainer_ws_bytes(gs_trainer* t, const int64_t* hop_sizes);
+/* pack: the device copy of gs_sample_pack; offsets: gs_pack_layout.off
+ * flattened [GS_MAX_HOPS][GS_PK_NFIELDS]; roots: [n_roots] device ids.
+ * Writes loss[0] and overwrites every gradient. */
+int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
+                                const int64_t* hop_sizes, const int64_t* offsets,
+                                const int32_t* roots, int64_t n_roots, void* ws,
+                                int64_t ws_bytes, float* loss, void* stream);
+/* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
+int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
