@@ -72,35 +72,14 @@ def build_workload(cfg, device, seed=824):
                 t_graph=t_graph, deg=deg)
 
 
-class Agg1Timer:
-    """HIP events around the layer-1 gather-aggregate launch, on its stream."""
-
-    def __init__(self):
-        self.pairs = []
-        self.bytes = []
-        self.active = False
-        self._orig = None
-
-    def install(self, elem_bytes):
-        orig = ops.agg_fwd
-        timer = self
-
-        def timed(agg_func, X, ptr_, idx, out, **kw):
-            if not (timer.active and kw.get("row_ptr") is not None):
-                return orig(agg_func, X, ptr_, idx, out, **kw)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            r = orig(agg_func, X, ptr_, idx, out, **kw)
-            b.record()
-            timer.pairs.append((a, b))
-            return r
-
-        self._orig = orig
-        models.ops.agg_fwd = timed
-
-    def mean_ms(self):
-        torch.cuda.synchronize()
-        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+def agg1_times_ms(trainer, n):
+    """HIP-event durations of the layer-1 K-agg launches recorded by the native
+    step on its own stream (gs_trainer_time_agg)."""
+    out = np.zeros(max(n, 1), np.float32)
+    got = int(gs._lib.lib().gs_trainer_agg_times(trainer._h, out.ctypes.data, n))
+    if got < 0:
+        raise RuntimeError("event timing failed")
+    return out[:got]
 
 
 def agg1_bytes(s, F, elem):
@@ -169,6 +148,8 @@ def main():
     ap.add_argument("--seed", type=int, default=824)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--sampler-streams", type=int, default=1,
+                    help="independent bit-exact sampler streams per GPU (1 = the reference's single stream)")
     args = ap.parse_args()
 
     cfg = dict(CONFIGS[args.config])
@@ -184,7 +165,7 @@ def main():
     wl = build_workload(cfg, device, args.seed)
     trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2,
                                   hidden=128, fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=args.seed)
-    rng = train.make_rng(args.seed, rank)
+    rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
     total_steps = args.warmup + args.steps
     batches = []
     epoch = 0
@@ -192,9 +173,8 @@ def main():
         batches.extend(train.rank_batches(wl["candidates"], cfg["batch"], rank, world, args.seed + 1000, epoch))
         epoch += 1
     batches = batches[:total_steps]
-    pf = train.Prefetcher(wl["graph"], rng, batches, cfg["fanouts"], False, device)
-    timer = Agg1Timer()
-    timer.install(2 if cfg["dtype"] == "bf16" else 4)
+    pf = train.Prefetcher(wl["graph"], None, batches, cfg["fanouts"], False, device, rngs=rngs,
+                          fail_empty=cfg["agg"] == "MAX")
     elem = 2 if cfg["dtype"] == "bf16" else 4
 
     for _ in range(args.warmup):
@@ -203,7 +183,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.active = True
+    gs._lib.check(gs._lib.lib().gs_trainer_time_agg(trainer._h, args.steps))
     agg_bytes, n_edges = [], 0
     t_wait = t_launch = 0.0
     t0 = time.perf_counter()
@@ -220,13 +200,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timer.active = False
     loss = float(trainer.loss.item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    agg_ms = timer.mean_ms()
+    agg_ms = float(np.mean(agg1_times_ms(trainer, args.steps)))
     value = cfg["batch"] * args.steps * world / elapsed
 
     if rank == 0:
@@ -250,6 +229,7 @@ def main():
                                    f"({wl['n']} ids), {cfg['pairs']} pairs, feat {cfg['feat']}, "
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
+                       "sampler_streams_per_gpu": args.sampler_streams,
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
                        "host_ms_per_step": {"sampler": round(1e3 * float(np.median(pf.sample_s)), 3),

@@ -72,6 +72,8 @@ _SIGS = {
     "gs_sample_hop": (_i32, [_vp, _i32, _p(HopView)]),
     "gs_sample_pack_layout": (_i32, [_vp, _p(PackLayout)]),
     "gs_sample_pack": (_i32, [_vp, _vp, _i64]),
+    "gs_sample_pack_bound": (_i64, [_vp, _i64, _vp, _i32]),
+    "gs_sample_pack_run": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp, _p(_i64)]),
     "gs_fill_uniform": (_i32, [_vp, _i32, _i64, _i64, _i64, _u64, _vp]),
     "gs_uniform_host": (_i32, [_u64, _i64, _i64, _i64, _vp]),
     "gs_agg_fwd": (_i32, [_i32, _i32, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32,
@@ -96,6 +98,8 @@ _SIGS = {
     "gs_trainer_ws_bytes": (_i64, [_vp, _vp]),
     "gs_trainer_forward_backward": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gs_trainer_update": (_i32, [_vp, _f32, _vp, _vp]),
+    "gs_trainer_time_agg": (_i32, [_vp, _i64]),
+    "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
 }
 
 

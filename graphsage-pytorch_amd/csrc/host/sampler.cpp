@@ -393,6 +393,52 @@ int gs_sample_pack_layout(const gs_sample* sp, gs_pack_layout* out) {
     GS_API_END
 }
 
+int64_t gs_sample_pack_bound(const gs_graph* gp, int64_t n_roots, const int32_t* fanouts, int32_t n_hops) {
+    if (!gp || n_roots < 1 || n_hops < 1 || n_hops > GS_MAX_HOPS) return -1;
+    const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
+    auto al = [](int64_t n) { return (n + 3) & ~int64_t(3); };
+    int64_t nd = n_roots, total = 0;
+    for (int32_t j = 0; j < n_hops; ++j) {
+        const int64_t k = fanouts ? fanouts[j] : 10;
+        const int64_t per = (k > 0) ? std::min<int64_t>(k, g.max_degree) : g.max_degree;
+        const int64_t npos = nd * per;
+        const int64_t nsrc = std::min<int64_t>(g.n_nodes, nd + npos);
+        const int64_t nnbr = npos + nd;
+        if (j == n_hops - 1) total += al(nd + 1) + al(npos) + al(nd);
+        else total += al(nd + 1) + al(nnbr) + al(nd) + al(nsrc + 1) + al(nnbr + nd);
+        nd = nsrc;
+    }
+    return total + al(n_roots);
+}
+
+int gs_sample_pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots,
+                       const int32_t* fanouts, int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
+                       int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    GS_API_BEGIN
+    GS_REQUIRE(gp && rng && buf && hop_sizes && offsets && used, GS_EINVAL, "NULL argument");
+    const int64_t bound = gs_sample_pack_bound(gp, n_roots, fanouts, n_hops);
+    GS_REQUIRE(bound >= 0 && cap >= bound, GS_EINVAL, "buffer below gs_sample_pack_bound");
+    const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
+    std::unique_ptr<Sample> s(gs::run_sample(g, rng->mt, roots, n_roots, fanouts, n_hops, flags));
+    gs_pack_layout L;
+    layout_of(*s, &L);
+    gs_sample_pack(reinterpret_cast<const gs_sample*>(s.get()), buf, cap);
+    for (int32_t j = 0; j < n_hops; ++j) {
+        const Hop& h = s->hops[j];
+        hop_sizes[4 * j] = static_cast<int64_t>(h.dst_ids.size());
+        hop_sizes[4 * j + 1] = static_cast<int64_t>(h.pos.size());
+        hop_sizes[4 * j + 2] = h.materialised ? static_cast<int64_t>(h.src_ids.size()) : -1;
+        hop_sizes[4 * j + 3] = h.materialised ? static_cast<int64_t>(h.nbr.size()) : -1;
+        if (h.n_empty && (flags & GS_SAMPLE_FAIL_EMPTY)) gs::fail(GS_EEMPTY, "empty neighbourhood");
+    }
+    for (int32_t j = 0; j < GS_MAX_HOPS; ++j)
+        for (int f = 0; f < GS_PK_NFIELDS; ++f) offsets[j * GS_PK_NFIELDS + f] = L.off[j][f];
+    int32_t* r = buf + L.total;  // roots (int32) right after the pack
+    for (int64_t i = 0; i < n_roots; ++i) r[i] = static_cast<int32_t>(roots[i]);
+    *used = L.total + n_roots;
+    GS_API_END
+}
+
 int gs_sample_pack(const gs_sample* sp, int32_t* buf, int64_t cap) {
     GS_API_BEGIN
     GS_REQUIRE(sp && buf, GS_EINVAL, "NULL argument");

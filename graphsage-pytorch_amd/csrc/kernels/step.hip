@@ -14,6 +14,13 @@ struct gs_trainer {
     std::vector<int64_t> w_off;  // element offset of each parameter in the flat buffer
     std::vector<int64_t> w_rows, w_cols;
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
+    // optional HIP-event timing of the layer-1 gather-aggregate (bench roofline)
+    std::vector<hipEvent_t> ev0, ev1;
+    int64_t n_timed = 0;
+    ~gs_trainer() {
+        for (auto e : ev0) (void)hipEventDestroy(e);
+        for (auto e : ev1) (void)hipEventDestroy(e);
+    }
 };
 
 namespace gs {
@@ -100,9 +107,15 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     // ---- forward (models.py:255-267)
     if (lowp) ok(gs_cast_f32_bf16(P + T.w_off[0], w1lp, T.w_rows[0] * T.w_cols[0], st));
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
+    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
+    if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
     ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, rows[0],
                   fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.row_ptr, c.col, dst_L, c.gcn, agg[0],
                   static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    if (timed) {
+        GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+        ++T.n_timed;
+    }
     ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
                           dst_L, agg[0], F, lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]), h[0], H, 1, st));
     for (int l = 2; l <= L; ++l) {
@@ -201,6 +214,31 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_
     gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
                  gs::as_stream(stream));
     GS_API_END
+}
+
+int gs_trainer_time_agg(gs_trainer* t, int64_t capacity) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && capacity >= 0, GS_EINVAL, "bad arguments");
+    for (auto e : t->ev0) (void)hipEventDestroy(e);
+    for (auto e : t->ev1) (void)hipEventDestroy(e);
+    t->ev0.assign(capacity, nullptr);
+    t->ev1.assign(capacity, nullptr);
+    for (int64_t i = 0; i < capacity; ++i)
+        GS_REQUIRE(hipEventCreate(&t->ev0[i]) == hipSuccess && hipEventCreate(&t->ev1[i]) == hipSuccess, GS_EHIP,
+                   "hipEventCreate");
+    t->n_timed = 0;
+    GS_API_END
+}
+
+int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap) {
+    if (!t || !ms) return -1;
+    const int64_t n = std::min(cap, t->n_timed);
+    for (int64_t i = 0; i < n; ++i) {
+        if (hipEventSynchronize(t->ev1[i]) != hipSuccess ||
+            hipEventElapsedTime(&ms[i], t->ev0[i], t->ev1[i]) != hipSuccess)
+            return -1;
+    }
+    return n;
 }
 
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) {

@@ -141,68 +141,113 @@ def rank_batches(candidates, batch_size, rank, world_size, seed, epoch=0):
         yield perm[b * batch_size:(b + 1) * batch_size]
 
 
-def rank_seed(seed, rank):
-    """Sampler stream of a rank: random.seed(seed + rank) — rank 0 == the reference's stream."""
-    return seed + rank
+def rank_seed(seed, rank, stream=0):
+    """Sampler stream (rank, stream): random.seed(seed + rank + 64 * stream);
+    rank 0 stream 0 is exactly the reference's random.seed(seed) stream."""
+    return seed + rank + 64 * stream
 
 
-class Prefetcher:
-    """Samples batch i+1.. on a host thread (GIL released inside the native
-    sampler) into a ring of pinned buffers while the GPU runs batch i."""
+class SampleInfo:
+    """Sizes / pack offsets of one packed batch (what DeviceSample needs)."""
 
-    def __init__(self, graph, rng, batches, fanouts, gcn, device, depth=3):
-        self.graph, self.rng, self.fanouts, self.gcn = graph, rng, list(fanouts), gcn
-        self.device = torch.device(device)
+    def __init__(self, n_hops, sizes, offsets, used, n_roots):
+        self.n_hops = n_hops
+        self._sizes = [tuple(int(x) for x in sizes[4 * j:4 * j + 4]) for j in range(n_hops)]
+        self.offsets = offsets.reshape(_lib.GS_MAX_HOPS, _lib.GS_PK_NFIELDS)[:n_hops].tolist()
+        self.pack_total = int(used) - n_roots
+        self.n_roots = n_roots
+
+    def sizes(self, j):
+        return self._sizes[j - 1]
+
+
+class _SamplerWorker:
+    """One RNG stream: samples its batches in order on a host thread (the GIL
+    is released for the whole native sample+pack call) into a ring of pinned
+    buffers; the consumer copies each to the device and recycles the slot."""
+
+    def __init__(self, graph, rng, batches, fanouts, flags, depth):
+        self.graph, self.rng, self.batches, self.flags = graph, rng, batches, flags
+        self.fan = np.array([(-1 if k is None else int(k)) for k in fanouts], np.int32)
         self.q = queue.Queue(maxsize=depth)
         self.slots = [None] * (depth + 1)
         self.events = [None] * (depth + 1)
         self.free = queue.Queue()
         for i in range(depth + 1):
             self.free.put(i)
-        self._it = iter(batches)
-        self._stop = False
-        self.sample_s = []  # host sampler seconds per batch
+        self.sample_s = []
+        self.stop = False
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
 
     def _run(self):
+        L = len(self.fan)
         try:
-            for roots in self._it:
-                if self._stop:
+            for roots in self.batches:
+                if self.stop:
                     break
-                t0 = time.perf_counter()
-                s = sample(self.graph, self.rng, roots, self.fanouts, gcn=self.gcn)
-                self.sample_s.append(time.perf_counter() - t0)
+                roots = np.ascontiguousarray(roots, dtype=np.int64)
+                bound = int(lib().gs_sample_pack_bound(self.graph.handle, len(roots), self.fan.ctypes.data, L))
                 slot = self.free.get()
                 ev = self.events[slot]
                 if ev is not None:
                     ev.synchronize()  # the previous H2D copy out of this slot is done
-                need = s.pack_total + len(roots)
                 buf = self.slots[slot]
-                if buf is None or buf.numel() < need:
-                    buf = self.slots[slot] = torch.empty(int(need * 1.25) + 1024, dtype=torch.int32,
-                                                         pin_memory=True)
-                s.pack_into(buf)
-                buf[s.pack_total:need].copy_(torch.from_numpy(np.asarray(roots, np.int32)))
-                self.q.put((s, slot, need, len(roots)))
+                if buf is None or buf.numel() < bound:
+                    buf = self.slots[slot] = torch.empty(bound, dtype=torch.int32, pin_memory=True)
+                sizes = np.empty(4 * L, np.int64)
+                offs = np.empty(_lib.GS_MAX_HOPS * _lib.GS_PK_NFIELDS, np.int64)
+                used = ctypes.c_int64()
+                t0 = time.perf_counter()
+                check(lib().gs_sample_pack_run(self.graph.handle, self.rng._h, roots.ctypes.data, len(roots),
+                                               self.fan.ctypes.data, L, self.flags, buf.data_ptr(), buf.numel(),
+                                               sizes.ctypes.data, offs.ctypes.data, ctypes.byref(used)))
+                self.sample_s.append(time.perf_counter() - t0)
+                self.q.put((slot, SampleInfo(L, sizes, offs, used.value, len(roots)), offs, sizes))
         except BaseException as e:  # surface sampler errors in the consumer
             self.q.put(e)
         self.q.put(None)
 
+
+class Prefetcher:
+    """Host sampling pipelined with the GPU.  With one RNG (the default) the
+    batches are sampled in order from that single stream — exactly the
+    reference's sequence.  With `rngs` = S streams, stream w samples batches
+    w, w+S, ... (each stream individually bit-exact with the reference seeded
+    the same way, like S data-parallel ranks sharing this GPU); batches are
+    still consumed in order."""
+
+    def __init__(self, graph, rng, batches, fanouts, gcn, device, depth=3, rngs=None, fail_empty=False):
+        self.device = torch.device(device)
+        rngs = list(rngs) if rngs is not None else [rng]
+        S = len(rngs)
+        batches = list(batches)
+        flags = (_lib.GS_SAMPLE_GCN if gcn else 0) | (4 if fail_empty else 0)
+        self.workers = [_SamplerWorker(graph, rngs[w], batches[w::S], fanouts, flags, depth) for w in range(S)]
+        self.i = 0
+
+    @property
+    def sample_s(self):
+        return [t for w in self.workers for t in w.sample_s]
+
     def next(self):
-        item = self.q.get()
+        w = self.workers[self.i % len(self.workers)]
+        item = w.q.get()
         if item is None:
             raise StopIteration
         if isinstance(item, BaseException):
             raise item
-        s, slot, need, B = item
-        dev = self.slots[slot][:need].to(self.device, non_blocking=True)
+        self.i += 1
+        slot, info, offs, sizes = item
+        used = info.pack_total + info.n_roots
+        dev = w.slots[slot][:used].to(self.device, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self.events[slot] = ev
-        self.free.put(slot)
-        ds = DeviceSample(s, self.device, buf=dev)
-        return ds, dev[s.pack_total:need], s
+        w.events[slot] = ev
+        w.free.put(slot)
+        ds = DeviceSample(info, self.device, buf=dev)
+        ds._native = (sizes, offs)
+        return ds, dev[info.pack_total:used], info
 
     def __iter__(self):
         return self
@@ -211,7 +256,8 @@ class Prefetcher:
         return self.next()
 
     def close(self):
-        self._stop = True
+        for w in self.workers:
+            w.stop = True
 
 
 def init_distributed():
@@ -226,5 +272,5 @@ def init_distributed():
     return rank, world
 
 
-def make_rng(seed, rank=0):
-    return RNG(rank_seed(seed, rank))
+def make_rng(seed, rank=0, stream=0):
+    return RNG(rank_seed(seed, rank, stream))

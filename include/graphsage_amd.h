@@ -168,6 +168,20 @@ int gs_sample_pack_layout(const gs_sample* s, gs_pack_layout* out);
 /* Writes the layout's int32 image into buf (cap elements, typically pinned). */
 int gs_sample_pack(const gs_sample* s, int32_t* buf, int64_t cap);
 
+/* Streaming form for sampler threads: sample every hop and write the device
+ * image plus the roots (int32, at element `used - n_roots`) straight into a
+ * caller buffer of at least gs_sample_pack_bound() elements, with no handle
+ * to keep.  hop_sizes[4*j..] = (n_dst, n_pos, n_src, n_nbr) of hop j+1;
+ * offsets = gs_pack_layout.off flattened.  GS_SAMPLE_FAIL_EMPTY turns an
+ * empty neighbourhood into GS_EEMPTY (MAX aggregation). */
+#define GS_SAMPLE_FAIL_EMPTY 4
+int64_t gs_sample_pack_bound(const gs_graph* g, int64_t n_roots,
+                             const int32_t* fanouts, int32_t n_hops);
+int gs_sample_pack_run(const gs_graph* g, gs_rng* rng, const int64_t* roots,
+                       int64_t n_roots, const int32_t* fanouts, int32_t n_hops,
+                       int32_t flags, int32_t* buf, int64_t cap,
+                       int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+
 /* --------------------------------------------------------- device kernels */
 typedef enum { GS_F32 = 0, GS_BF16 = 1 } gs_dtype;
 typedef enum { GS_AGG_MEAN = 0, GS_AGG_MAX = 1 } gs_agg;
@@ -302,6 +316,11 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
                                 int64_t ws_bytes, float* loss, void* stream);
 /* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
+/* Measurement only (not on the graph-capturable path): record HIP events on
+ * the launch stream around the next `capacity` layer-1 gather-aggregate
+ * launches; gs_trainer_agg_times synchronises and returns their durations (ms). */
+int gs_trainer_time_agg(gs_trainer* t, int64_t capacity);
+int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 
 #ifdef __cplusplus
 }

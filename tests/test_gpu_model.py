@@ -197,3 +197,23 @@ def test_prefetcher_matches_synchronous(gs):
             for name in names:  # fields only: the pack's alignment padding is not initialised
                 assert torch.equal(ds.field(hop, name), ds2.field(hop, name)), (hop, name)
         assert roots_dev.cpu().tolist() == roots.tolist()
+
+
+def test_prefetcher_streams_each_bit_exact(gs):
+    """S sampler streams: stream w serves batches w, w+S, ... and equals a
+    synchronous sampler seeded rank_seed(seed, rank, w)."""
+    graph, g, n = _graph(gs, "rmat")
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 32, 0, 1, 4))[:8]
+    S = 3
+    pf = train.Prefetcher(graph, None, batches, [25, 10], False, DEV,
+                          rngs=[train.make_rng(5, 0, w) for w in range(S)])
+    sync = [train.make_rng(5, 0, w) for w in range(S)]
+    for i, roots in enumerate(batches):
+        ds, roots_dev, info = pf.next()
+        s2 = gs.sample(graph, sync[i % S], roots, [25, 10])
+        ds2 = models.DeviceSample(s2, DEV)
+        assert info.sizes(1) == s2.sizes(1) and info.sizes(2) == s2.sizes(2)
+        for hop, names in ((1, ("nbr_ptr", "nbr", "self", "tptr", "tidx")), (2, ("pos_ptr", "pos", "dst_ids"))):
+            for name in names:
+                assert torch.equal(ds.field(hop, name), ds2.field(hop, name)), (i, hop, name)
+        assert roots_dev.cpu().tolist() == roots.tolist()

@@ -187,3 +187,60 @@ def test_rmat_generator_deterministic(gs):
     assert (a[0] != a[1]).all() and a[0].max() < 4096
     deg = np.bincount(np.concatenate(a), minlength=4096)
     assert deg.max() > 20 * max(1, np.median(deg))  # power-law skew
+
+
+def test_pack_run_matches_sample_pack(gs):
+    """The streaming sample+pack call equals sample() + pack() and leaves the rng identical."""
+    import torch
+    G_, _ = _graph(gs, "rmat")
+    L = gs._lib
+    roots = np.nonzero(G_.degrees())[0][:40].astype(np.int64)
+    fan = np.array([25, 10], np.int32)
+    bound = int(L.lib().gs_sample_pack_bound(G_.handle, len(roots), fan.ctypes.data, 2))
+    buf = np.full(bound, -7, np.int32)
+    sizes = np.empty(8, np.int64)
+    offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+    used = ctypes.c_int64()
+    r1 = gs.RNG(42)
+    L.check(L.lib().gs_sample_pack_run(G_.handle, r1._h, roots.ctypes.data, len(roots), fan.ctypes.data, 2, 0,
+                                       buf.ctypes.data, bound, sizes.ctypes.data, offs.ctypes.data,
+                                       ctypes.byref(used)))
+    r2 = gs.RNG(42)
+    s = gs.sample(G_, r2, roots, [25, 10])
+    assert s.pack_total + len(roots) == used.value
+    assert [tuple(sizes[4 * j:4 * j + 4]) for j in range(2)] == [s.sizes(1), s.sizes(2)]
+    ref = s.pack().numpy()
+    for j in range(2):
+        for f in range(L.GS_PK_NFIELDS):
+            o = offs[j * L.GS_PK_NFIELDS + f]
+            assert o == s.offsets[j][f]
+    h1, h2 = s.hop(1), s.hop(2)
+    for j, f, n in [(0, L.GS_PK_NBR, h1.n_nbr), (0, L.GS_PK_TIDX, h1.n_nbr + h1.n_dst), (1, L.GS_PK_POS, h2.n_pos)]:
+        o = s.offsets[j][f]
+        assert np.array_equal(buf[o:o + n], ref[o:o + n])
+    assert np.array_equal(buf[s.pack_total:used.value], roots.astype(np.int32))
+    assert r1.getstate()[0].tolist() == r2.getstate()[0].tolist() and r1.getstate()[1] == r2.getstate()[1]
+    with pytest.raises(ValueError):  # below the bound: refused before any rng word is drawn
+        L.check(L.lib().gs_sample_pack_run(G_.handle, r1._h, roots.ctypes.data, len(roots), fan.ctypes.data, 2,
+                                           0, buf.ctypes.data, 10, sizes.ctypes.data, offs.ctypes.data,
+                                           ctypes.byref(used)))
+
+
+def test_stream_seeds_are_reference_seeds(gs):
+    """Stream (rank, w) draws exactly what random.seed(seed + rank + 64 w) would."""
+    import importlib
+    train = importlib.import_module("graphsage-pytorch_amd.train")
+    assert train.rank_seed(824, 0, 0) == 824
+    G_, g = _graph(gs, "cora")
+    adj = Adjacency(g["cora_src"], g["cora_dst"], int(g["cora_n"][0]))
+    batches = list(train.rank_batches(np.arange(2708), 20, 1, 2, 5))[:6]
+    S = 2
+    for w in range(S):
+        seed = train.rank_seed(824, 1, w)
+        r = train.make_rng(824, 1, w)
+        random.seed(seed)
+        for roots in batches[w::S]:
+            s = gs.sample(G_, r, roots, [10, 10], full=True)
+            want = sample_layers(adj, roots.tolist(), [10, 10])
+            assert s.hop(2).src_ids.tolist() == want[1][3]
+        assert r.getstate()[0].tolist() + [r.getstate()[1]] == list(random.getstate()[1])
