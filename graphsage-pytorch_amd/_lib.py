@@ -88,8 +88,8 @@ _SIGS = {
     "gs_agg_bwd": (_i32, [_i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp,
                           _vp]),
     "gs_cls_nll_ws_floats": (_i64, [_i64, _i64, _i64]),
-    "gs_cls_nll_fwd_bwd": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                  _vp]),
+    "gs_cls_nll_fwd_bwd": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
+                                  _vp, _vp, _vp]),
     "gs_clip_sgd": (_i32, [_i32, _vp, _vp, _vp, _f32, _f32, _f32, _vp, _vp]),
     "gs_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
     "gs_trainer_create": (_i32, [_vp, _p(_vp)]),

@@ -13,21 +13,37 @@
 // through a double-buffered LDS ring whose next chunk is fetched while the
 // MFMAs of the current one run.
 #include <algorithm>
+#include <mutex>
+#include <unordered_set>
 
 #include "kcommon.hpp"
 
 namespace gs {
 
 constexpr int kThreads = 256;  // 4 wavefronts
-constexpr int kLdsMax = 160 * 1024;
+// Dynamic-LDS budget per workgroup: the runtime torch ships rejects requests
+// near the 160 KiB hardware size (hipFuncSetAttribute: invalid argument at
+// ~156 KB), so every layout below stays within 128 KiB.
+constexpr int kLdsMax = 128 * 1024;
 
+// Raise a kernel's dynamic-LDS limit once (the attribute call costs host
+// time on every launch otherwise); kLdsMax is always requested so one call
+// covers every shape.
 template <typename K>
 static void allow_smem(K kernel, size_t bytes) {
-    if (bytes > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
-        if (e != hipSuccess) fail(GS_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    if (bytes <= 64 * 1024) return;
+    GS_REQUIRE(bytes <= static_cast<size_t>(kLdsMax), GS_EINVAL, "LDS request above budget");
+    static std::mutex mu;
+    static std::unordered_set<const void*> done;
+    const void* key = reinterpret_cast<const void*>(kernel);
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count(key)) return;
+    const hipError_t e = hipFuncSetAttribute(key, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // do not leave a sticky error for the caller's next HIP call
+        fail(GS_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
     }
+    done.insert(key);
 }
 
 // 16 B of row `row` at element k of the virtual concat [self | agg] (zeros
@@ -81,7 +97,7 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
     int n, int F, int H, int K, int KP, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo) {
     constexpr int EPV = 16 / sizeof(T);
-    constexpr int CH = 16;  // 16-byte chunks per W row per step
+    constexpr int CH = NTW <= 2 ? 16 : 8;  // 16-byte chunks per W row per step (LDS budget at H = 256)
     constexpr int BK = CH * EPV;
     constexpr int BM = 16;
     constexpr int SW = BK + EPV;
@@ -198,7 +214,8 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
 // columns are loaded into LDS in one burst, then the MFMA "k" runs over rows,
 // both operands read straight from row-major LDS tiles.  Splits write fp32
 // partials that sum_slabs_kernel adds in a fixed order (no atomics).
-constexpr int kRS = 128;
+constexpr int kRS = 128;  // slab rows for H <= 128; 64 above (LDS budget)
+static inline int dw_rows(int64_t H) { return H <= 128 ? kRS : kRS / 2; }
 constexpr int kBKC = 64;
 constexpr int kSAc = kBKC + 16;
 
@@ -210,7 +227,8 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int SZ = ((H + 31) / 32) * 32 + 16;  // bank-spread rows for the b32 fragment reads
     float* sZ = reinterpret_cast<float*>(smem);
-    float* sA = sZ + kRS * SZ;
+    const int RS = rows_per_split;  // LDS slab height
+    float* sA = sZ + RS * SZ;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int kc0 = blockIdx.x * kBKC;
     const int i_beg = blockIdx.y * rows_per_split;
@@ -220,7 +238,7 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     // dZ slab [rows][H]
     if (zvec) {
         const int q4 = H / 4;
-        const int total = kRS * q4;
+        const int total = RS * q4;
         for (int base = tid; base < total; base += 8 * kThreads) {
             float4 z[8], o[8];  // 8 (16 with the relu mask) loads in flight per lane
 #pragma unroll
@@ -250,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
             }
         }
     } else {
-        for (int e = tid; e < kRS * H; e += kThreads) {
+        for (int e = tid; e < RS * H; e += kThreads) {
             const int ii = e / H, h = e - ii * H;
             float z = 0.f;
             if (ii < rows) {
@@ -263,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     }
     // input slab [rows][64 columns of the concat]
 #pragma unroll 8
-    for (int e = tid; e < kRS * (kBKC / 4); e += kThreads) {
+    for (int e = tid; e < RS * (kBKC / 4); e += kThreads) {
         const int ii = e >> 4, c = (e & 15) * 4, k = kc0 + c;
         float v[4] = {0.f, 0.f, 0.f, 0.f};
         if (ii < rows) {
@@ -398,12 +416,17 @@ __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
     }
 }
 
-static int dw_splits(int64_t n) { return static_cast<int>(std::max<int64_t>(1, (n + kRS - 1) / kRS)); }
+static int dw_splits(int64_t n, int64_t H) {
+    const int rs = dw_rows(H);
+    return static_cast<int>(std::max<int64_t>(1, (n + rs - 1) / rs));
+}
 
 // Phase width of the forward's LDS-resident A tile (elements, multiple of the
 // W chunk) so that A + two W buffers fit in 160 KiB.
+static int fwd_chunks(int H) { return H <= 128 ? 16 : 8; }
+
 static int fwd_phase(int K, int H, size_t esz) {
-    const int EPV = static_cast<int>(16 / esz), BK = 16 * EPV;
+    const int EPV = static_cast<int>(16 / esz), BK = fwd_chunks(H) * EPV;
     const size_t w_bytes = 2 * static_cast<size_t>(H) * (BK + EPV) * esz;
     const size_t a_budget = kLdsMax - w_bytes - 1024;
     int KP = ((K + BK - 1) / BK) * BK;
@@ -433,7 +456,8 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                        aligned16(A) && aligned16(Wd);
     const size_t esz = dt == GS_F32 ? 4 : 2;
     const int KP = fwd_phase(K, static_cast<int>(H), esz);
-    const size_t smem = (16 * static_cast<size_t>(KP + EPV) + 2 * static_cast<size_t>(H) * (16 * EPV + EPV)) * esz;
+    const size_t smem =
+        (16 * static_cast<size_t>(KP + EPV) + 2 * static_cast<size_t>(H) * (fwd_chunks(static_cast<int>(H)) * EPV + EPV)) * esz;
     const dim3 grid(static_cast<unsigned>((n + 15) / 16));
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
@@ -465,7 +489,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
 }
 
 int64_t gs_sage_linear_bwd_weight_ws(int64_t n, int64_t K, int64_t H) {
-    const int S = gs::dw_splits(n);
+    const int S = gs::dw_splits(n, H);
     return S > 1 ? static_cast<int64_t>(S) * K * H * 4 : 0;
 }
 
@@ -485,21 +509,22 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
         return GS_OK;
     }
     GS_REQUIRE(A && dout && out && dW, GS_EINVAL, "NULL device pointer");
-    const int S = dw_splits(n);
+    const int S = dw_splits(n, H);
     const int64_t need = gs_sage_linear_bwd_weight_ws(n, K, H);
     GS_REQUIRE(ws_bytes >= need && (need == 0 || ws), GS_EINVAL, "workspace too small");
     float* target = (S > 1) ? static_cast<float*>(ws) : dW;
     const bool vload = F % 4 == 0 && lda % 4 == 0 && aligned16(A) && (!self || (ldxs % 4 == 0 && aligned16(Xs)));
     const bool zvec = H % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && aligned16(out);
     const int SZ = static_cast<int>(((H + 31) / 32) * 32 + 16);
-    const size_t smem = static_cast<size_t>(kRS) * (SZ + kSAc) * sizeof(float);
+    const int RS = dw_rows(H);
+    const size_t smem = static_cast<size_t>(RS) * (SZ + kSAc) * sizeof(float);
     const dim3 grid(static_cast<unsigned>((K + kBKC - 1) / kBKC), static_cast<unsigned>(S));
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
 #define GS_LDW1(TT, SELF, RELU, VL, HW)                                                                   \
     do {                                                                                                  \
         auto kern = linear_dw_kernel<TT, SELF, RELU, VL, HW>;                                             \
         allow_smem(kern, smem);                                                                           \
-        kern<<<grid, kThreads, smem, st>>>(nn, ff, hh, kk, kRS, static_cast<const TT*>(Xs), ldxs, sidx,   \
+        kern<<<grid, kThreads, smem, st>>>(nn, ff, hh, kk, RS, static_cast<const TT*>(Xs), ldxs, sidx,    \
                                            static_cast<const TT*>(A), lda, dout, out, ldo, zvec, target,  \
                                            H * K);                                                        \
     } while (0)

@@ -37,102 +37,132 @@ __global__ __launch_bounds__(kTb) void cast_bf16_kernel(const float* in, bf16_t*
         out[i] = f2bf(in[i]);
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-// One wavefront per row: logits (lanes over D, one wave reduction per class),
-// log_softmax (max-shifted, as torch), the row's NLL term, dlogits =
-// (softmax - onehot) / B, and dE[i] = dlogits · Wc (lanes over D again).
-constexpr int kClsMaxC = 1024;
-__global__ __launch_bounds__(kTb) void cls_rows_kernel(int B, int D, int C, const float* __restrict__ E,
-                                                       const float* __restrict__ Wc, const float* __restrict__ bc,
-                                                       const int* __restrict__ labels, float* __restrict__ dl,
-                                                       float* __restrict__ rowloss, float* __restrict__ dE) {
-    __shared__ float zs[kTb / 64][kClsMaxC];
+// ------------------------------------------------------- classifier + NLL
+// One block of 16 waves per R rows, one wave per row.  Wc is staged in LDS
+// when it fits (C·D <= 8192 floats); per row: logits with lanes over D and one
+// wave reduction per class, log_softmax (max-shifted, as torch), the row's
+// NLL term, dlogits = (softmax - onehot) / B and dE = dlogits · Wc, optionally
+// masked by E > 0 (the relu of the layer that produced E, so the caller gets
+// dZ directly).  Labels are read through the roots (labels[roots[i]]).  The
+// block then reduces its rows' dWc / dbc / loss into one partial slab;
+// cls_reduce_kernel adds the slabs in a fixed order.
+constexpr int kClsThreads = 1024;
+constexpr int64_t kClsLdsFloats = 16 * 1024;  // 64 KiB
+constexpr int64_t kClsWcLds = 8 * 1024;
+
+struct ClsPlan {
+    int rows;
+    bool wc_lds;
+    size_t smem;
+};
+
+inline ClsPlan cls_plan(int64_t C, int64_t D) {
+    ClsPlan p;
+    p.wc_lds = C * D <= kClsWcLds;
+    const int64_t fixed = p.wc_lds ? C * D : 0;
+    p.rows = 1;
+    for (int r = kClsThreads / 64; r > 1; r >>= 1)
+        if (fixed + r * (C + D + 1) <= kClsLdsFloats) {
+            p.rows = r;
+            break;
+        }
+    p.smem = static_cast<size_t>(fixed + p.rows * (C + D + 1)) * sizeof(float);
+    return p;
+}
+
+__global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
+    int B, int D, int C, int R, int wc_lds, const float* __restrict__ E, const float* __restrict__ Wc,
+    const float* __restrict__ bc, const int* __restrict__ labels, const int* __restrict__ roots, int mask_relu,
+    float* __restrict__ dE, float* __restrict__ slab) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* sdl = sm;             // [R][C]
+    float* sE = sdl + R * C;     // [R][D]
+    float* sloss = sE + R * D;   // [R]
+    float* sW = sloss + R;       // [C][D] when wc_lds
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int i = blockIdx.x * (kTb / 64) + w;
-    if (i >= B) return;
-    const float* e = E + static_cast<int64_t>(i) * D;
-    const int y = labels[i];
-    float mx = -INFINITY;
-    for (int c = 0; c < C; ++c) {
-        const float* wr = Wc + static_cast<int64_t>(c) * D;
-        float p = 0.f;
-        for (int d = lane; d < D; d += 64) p = fmaf(e[d], wr[d], p);
-        const float z = wave_sum(p) + bc[c];
-        if (lane == 0) zs[w][c] = z;
-        mx = fmaxf(mx, z);
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the row's logits are in LDS
-    __builtin_amdgcn_wave_barrier();
-    float se = 0.f;
-    for (int c = lane; c < C; c += 64) se += expf(zs[w][c] - mx);
-    const float lse = logf(wave_sum(se));
+    const int r0 = blockIdx.x * R;
+    const int nr = min(R, B - r0);
     const float invB = 1.0f / static_cast<float>(B);
-    for (int c = lane; c < C; c += 64) {
-        const float lp = zs[w][c] - mx - lse;
-        if (c == y) rowloss[i] = -lp;
-        const float g = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
-        dl[static_cast<int64_t>(i) * C + c] = g;
-        zs[w][c] = g;
+    for (int t = threadIdx.x; t < R * D; t += kClsThreads) {
+        const int ii = t / D;
+        sE[t] = ii < nr ? E[static_cast<int64_t>(r0) * D + t] : 0.f;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    for (int d = lane; d < D; d += 64) {
+    if (wc_lds)
+        for (int t = threadIdx.x; t < C * D; t += kClsThreads) sW[t] = Wc[t];
+    __syncthreads();
+    const float* W = wc_lds ? sW : Wc;
+    for (int ii = w; ii < nr; ii += kClsThreads / 64) {
+        const float* e = sE + ii * D;
+        const int y = labels[roots ? roots[r0 + ii] : r0 + ii];
+        float mx = -INFINITY;
+        for (int c = 0; c < C; ++c) {
+            const float* wr = W + static_cast<int64_t>(c) * D;
+            float p = 0.f;
+            for (int d = lane; d < D; d += 64) p = fmaf(e[d], wr[d], p);
+            const float z = wave_sum(p) + bc[c];
+            if (lane == 0) sdl[ii * C + c] = z;
+            mx = fmaxf(mx, z);
+        }
+        __builtin_amdgcn_wave_barrier();
+        float se = 0.f;
+        for (int c = lane; c < C; c += 64) se += expf(sdl[ii * C + c] - mx);
+        const float lse = logf(wave_sum(se));
+        for (int c = lane; c < C; c += 64) {
+            const float lp = sdl[ii * C + c] - mx - lse;
+            if (c == y) sloss[ii] = -lp;
+            sdl[ii * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int d = lane; d < D; d += 64) {
+            float s = 0.f;
+            for (int c = 0; c < C; ++c) s = fmaf(sdl[ii * C + c], W[static_cast<int64_t>(c) * D + d], s);
+            if (mask_relu && !(e[d] > 0.f)) s = 0.f;
+            dE[static_cast<int64_t>(r0 + ii) * D + d] = s;
+        }
+    }
+    __syncthreads();
+    // block partials: [C][D+1] (column D = bias) + 1 loss term
+    const int per = C * (D + 1);
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
+    for (int t = threadIdx.x; t < per; t += kClsThreads) {
+        const int c = t / (D + 1), d = t - c * (D + 1);
         float s = 0.f;
-        for (int c = 0; c < C; ++c) s = fmaf(zs[w][c], Wc[static_cast<int64_t>(c) * D + d], s);
-        dE[static_cast<int64_t>(i) * D + d] = s;
+        for (int ii = 0; ii < nr; ++ii) s = fmaf(sdl[ii * C + c], d < D ? sE[ii * D + d] : 1.f, s);
+        out[t] = s;
+    }
+    if (threadIdx.x < 64) {
+        float s = 0.f;
+        for (int ii = threadIdx.x; ii < nr; ii += 64) s += sloss[ii];
+        s = wave_sum(s);
+        if (threadIdx.x == 0) out[per] = s;
     }
 }
 
-// Partial dWc / dbc over a 32-row chunk: slab[chunk][c][0..D) and [c][D] (bias).
-constexpr int kClsChunk = 32;
-__global__ __launch_bounds__(kTb) void cls_dW_partial_kernel(int B, int D, int C, const float* __restrict__ dl,
-                                                             const float* __restrict__ E, float* __restrict__ slab) {
-    const int chunk = blockIdx.y;
-    const int64_t t = blockIdx.x * int64_t(kTb) + threadIdx.x;
-    const int64_t per = static_cast<int64_t>(C) * (D + 1);
-    if (t >= per) return;
-    const int c = static_cast<int>(t / (D + 1)), d = static_cast<int>(t - static_cast<int64_t>(c) * (D + 1));
-    const int i0 = chunk * kClsChunk, i1 = min(B, i0 + kClsChunk);
+__global__ __launch_bounds__(kTb) void cls_reduce_kernel(int B, int D, int C, int n_blocks,
+                                                         const float* __restrict__ slab, float* __restrict__ dWc,
+                                                         float* __restrict__ dbc, float* __restrict__ loss) {
+    const int per = C * (D + 1);
+    const int t = blockIdx.x * kTb + threadIdx.x;
+    if (t > per) return;
     float s = 0.f;
 #pragma unroll 8
-    for (int i = i0; i < i1; ++i) {
-        const float g = dl[static_cast<int64_t>(i) * C + c];
-        s += (d < D) ? g * E[static_cast<int64_t>(i) * D + d] : g;
+    for (int k = 0; k < n_blocks; ++k) s += slab[static_cast<int64_t>(k) * (per + 1) + t];
+    if (t == per) {
+        loss[0] = s / static_cast<float>(B);  // -sum(logp[i, y_i]) / B  (utils.py:162-163)
+        return;
     }
-    slab[chunk * per + t] = s;
+    const int c = t / (D + 1), d = t - c * (D + 1);
+    if (d < D) dWc[static_cast<int64_t>(c) * D + d] = s;
+    else dbc[c] = s;
 }
 
-__global__ __launch_bounds__(kTb) void cls_dW_reduce_kernel(int B, int D, int C, int n_chunks,
-                                                            const float* __restrict__ slab,
-                                                            const float* __restrict__ rowloss, float* __restrict__ dWc,
-                                                            float* __restrict__ dbc, float* __restrict__ loss) {
-    const int64_t t = blockIdx.x * int64_t(kTb) + threadIdx.x;
-    const int64_t per = static_cast<int64_t>(C) * (D + 1);
-    if (t < per) {
-        float s = 0.f;
-        for (int k = 0; k < n_chunks; ++k) s += slab[k * per + t];
-        const int c = static_cast<int>(t / (D + 1)), d = static_cast<int>(t - static_cast<int64_t>(c) * (D + 1));
-        if (d < D) dWc[static_cast<int64_t>(c) * D + d] = s;
-        else dbc[c] = s;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < 64) {  // -sum(logp[i, y_i]) / B  (utils.py:162-163)
-        float s = 0.f;
-        for (int i = threadIdx.x; i < B; i += 64) s += rowloss[i];
-        s = wave_sum(s);
-        if (threadIdx.x == 0) loss[0] = s / static_cast<float>(B);
-    }
-}
-
+// ------------------------------------------------------- clip + SGD
 struct Groups {
     int64_t off[9];
     int n;
@@ -159,20 +189,21 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
     }
 }
 
-// clip_coef = max_norm / (||scale·g|| + 1e-6), clamped to 1; mult = scale · coef.
-__global__ void group_coef_kernel(int n, const float* __restrict__ part, float scale, float max_norm,
-                                  float* __restrict__ mult) {
-    const int grp = threadIdx.x;
-    if (grp >= n) return;
-    float t = 0.f;
-    for (int b = 0; b < kNormBlocks; ++b) t += part[grp * kNormBlocks + b];
-    const float norm = sqrtf(t) * scale;
-    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
-    mult[grp] = scale * coef;
-}
-
+// Each block first folds the per-group partial sums (same fixed order in
+// every block) into clip_coef = max_norm / (||scale·g|| + 1e-6) clamped to 1,
+// then p -= lr · (scale · coef) · g and g is left scaled like torch's in-place
+// clip.
 __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
-                                                  const float* __restrict__ mult, float lr) {
+                                                  const float* __restrict__ part, float scale, float max_norm,
+                                                  float lr) {
+    __shared__ float mult[8];
+    if (threadIdx.x < G.n) {
+        float t = 0.f;
+        for (int b = 0; b < kNormBlocks; ++b) t += part[threadIdx.x * kNormBlocks + b];
+        const float norm = sqrtf(t) * scale;
+        mult[threadIdx.x] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+    }
+    __syncthreads();
     const int64_t total = G.off[G.n];
     for (int64_t i = blockIdx.x * int64_t(kTb) + threadIdx.x; i < total; i += int64_t(gridDim.x) * kTb) {
         int grp = 0;
@@ -221,33 +252,30 @@ int gs_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
     GS_API_END
 }
 
+int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C) {
+    const int r = gs::cls_plan(C, D).rows;
+    const int64_t nb = (B + r - 1) / r;
+    return nb * (C * (D + 1) + 1);
+}
+
 int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,
-                       const int32_t* labels, float* loss, float* dE, float* dWc, float* dbc, float* ws,
-                       void* stream) {
+                       const int32_t* labels, const int32_t* roots, int32_t mask_relu, float* loss, float* dE,
+                       float* dWc, float* dbc, float* ws, void* stream) {
     GS_API_BEGIN
     using namespace gs;
     GS_REQUIRE(B >= 1 && D >= 1 && C >= 1 && B < (1 << 30), GS_EINVAL, "bad sizes");
-    GS_REQUIRE(C <= kClsMaxC, GS_EINVAL, "at most 1024 classes");
+    GS_REQUIRE(C + D + 1 <= kClsLdsFloats, GS_EINVAL, "classes + embedding dims too large");
     GS_REQUIRE(E && Wc && bc && labels && loss && dE && dWc && dbc && ws, GS_EINVAL, "NULL device pointer");
     hipStream_t st = as_stream(stream);
     const int b = static_cast<int>(B), d = static_cast<int>(D), c = static_cast<int>(C);
-    float* dl = ws;
-    float* rowloss = ws + B * C;
-    const int n_chunks = (b + kClsChunk - 1) / kClsChunk;
-    float* slab = rowloss + B;
-    cls_rows_kernel<<<dim3((b + 3) / 4), kTb, 0, st>>>(b, d, c, E, Wc, bc, labels, dl, rowloss, dE);
-    const int64_t per = C * (D + 1);
-    cls_dW_partial_kernel<<<dim3(static_cast<unsigned>((per + kTb - 1) / kTb), n_chunks), kTb, 0, st>>>(b, d, c, dl,
-                                                                                                       E, slab);
-    cls_dW_reduce_kernel<<<dim3(static_cast<unsigned>((per + kTb - 1) / kTb)), kTb, 0, st>>>(b, d, c, n_chunks, slab,
-                                                                                             rowloss, dWc, dbc, loss);
+    const ClsPlan plan = cls_plan(C, D);
+    const int nb = (b + plan.rows - 1) / plan.rows;
+    cls_rows_kernel<<<dim3(nb), kClsThreads, plan.smem, st>>>(b, d, c, plan.rows, plan.wc_lds ? 1 : 0, E, Wc, bc,
+                                                              labels, roots, mask_relu, dE, ws);
+    const int per = c * (d + 1) + 1;
+    cls_reduce_kernel<<<dim3((per + kTb - 1) / kTb), kTb, 0, st>>>(b, d, c, nb, ws, dWc, dbc, loss);
     check_launch("gs_cls_nll_fwd_bwd");
     GS_API_END
-}
-
-int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C) {
-    const int64_t n_chunks = (B + gs::kClsChunk - 1) / gs::kClsChunk;
-    return B * C + B + n_chunks * C * (D + 1);
 }
 
 int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params, float* grads, float grad_scale,
@@ -261,13 +289,10 @@ int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params, float
     for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
     for (int i = 0; i < n_groups; ++i) GS_REQUIRE(G.off[i] <= G.off[i + 1], GS_EINVAL, "group offsets not sorted");
     hipStream_t st = as_stream(stream);
-    float* part = ws;
-    float* mult = ws + n_groups * kNormBlocks;
-    group_sumsq_kernel<<<dim3(kNormBlocks, n_groups), kTb, 0, st>>>(G, grads, part);
-    group_coef_kernel<<<1, 64, 0, st>>>(n_groups, part, grad_scale, max_norm, mult);
+    group_sumsq_kernel<<<dim3(kNormBlocks, n_groups), kTb, 0, st>>>(G, grads, ws);
     const int64_t total = G.off[n_groups];
-    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 1024))));
-    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, mult, lr);
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
+    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, ws, grad_scale, max_norm, lr);
     check_launch("gs_clip_sgd");
     GS_API_END
 }

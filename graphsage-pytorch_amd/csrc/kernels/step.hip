@@ -25,12 +25,6 @@ struct gs_trainer {
 
 namespace gs {
 
-__global__ void gather_labels_kernel(const int* __restrict__ labels, const int* __restrict__ roots, int n,
-                                     int* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = labels[roots[i]];
-}
-
 // Bump allocator over the workspace (256-byte aligned carves).
 struct Carve {
     char* base;
@@ -85,7 +79,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
     }
     void* w1lp = lowp ? cv.take<uint16_t>(T.w_rows[0] * T.w_cols[0]) : nullptr;
-    int32_t* y = cv.take<int32_t>(B);
     float* demb = cv.take<float>(B * H);
     float* cls_ws = cv.take<float>(gs_cls_nll_ws_floats(B, H, c.n_classes));
     int64_t dw_need = 0, dx_rows = 0, dprev_rows = 0;
@@ -125,15 +118,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
                               agg[l - 1], H, P + T.w_off[l - 1], h[l - 1], H, 1, st));
     }
-    // ---- loss head (models.py:8-27, utils.py:159-164)
-    gather_labels_kernel<<<dim3(static_cast<unsigned>((B + 255) / 256)), 256, 0, st>>>(c.labels, roots,
-                                                                                         static_cast<int>(B), y);
-    check_launch("gather_labels");
-    ok(gs_cls_nll_fwd_bwd(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off, y, loss, demb,
-                          G + T.cls_w_off, G + T.cls_b_off, cls_ws, st));
-    // ---- backward (utils.py:184)
+    // ---- loss head (models.py:8-27, utils.py:159-164); labels gathered through
+    // the roots, and demb comes back already masked by relu'(h_L), i.e. dZ_L
+    ok(gs_cls_nll_fwd_bwd(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off, c.labels, roots, 1, loss,
+                          demb, G + T.cls_w_off, G + T.cls_b_off, cls_ws, st));
+    // ---- backward (utils.py:184); every dH below is pre-masked, so relu = 0
     const float* dH = demb;
-    int relu = 1;
+    const int relu = 0;
     int flip = 0;
     for (int l = L; l >= 1; --l) {
         const int j = L - l + 1;
@@ -154,8 +145,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         flip ^= 1;
         ok(gs_agg_bwd(static_cast<gs_agg>(c.agg), rows[l - 2], H, fld(j, GS_PK_TPTR), fld(j, GS_PK_TIDX),
                       fld(j, GS_PK_NBR_PTR), dA, dSelf, ldd, am[l - 1], h[l - 2], H, dprev, st));
-        dH = dprev;
-        relu = 0;  // dprev is already masked by relu'(h_{l-1})
+        dH = dprev;  // agg_bwd masks by relu'(h_{l-1})
     }
     return cv.at;
 }

@@ -123,11 +123,14 @@ def cls_nll_workspace(B, D, C, device):
     return torch.empty(int(lib().gs_cls_nll_ws_floats(B, D, C)), dtype=torch.float32, device=device)
 
 
-def cls_nll_fwd_bwd(E, Wc, bc, labels, loss, dE, dWc, dbc, ws):
-    _dev(E, Wc, bc, labels, loss, dE, dWc, dbc, ws)
+def cls_nll_fwd_bwd(E, Wc, bc, labels, loss, dE, dWc, dbc, ws, roots=None, mask_relu=False):
+    """Classification + NLL forward/backward; labels[roots[i]] is row i's label
+    (labels[i] without roots).  mask_relu zeroes dE where E <= 0."""
+    _dev(E, Wc, bc, labels, loss, dE, dWc, dbc, ws, roots)
     B, D = E.shape
     C = Wc.shape[0]
-    check(lib().gs_cls_nll_fwd_bwd(B, D, C, ptr(E), ptr(Wc), ptr(bc), ptr(_i32(labels)), ptr(loss),
+    check(lib().gs_cls_nll_fwd_bwd(B, D, C, ptr(E), ptr(Wc), ptr(bc), ptr(_i32(labels)), ptr(_i32(roots)),
+                                   int(bool(mask_relu)), ptr(loss),
                                    ptr(dE), ptr(dWc), ptr(dbc), ptr(ws), _stream(E)))
 
 

@@ -256,20 +256,25 @@ int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr,
 
 /* Classification (models.py:8-27) + NLL mean (utils.py:159-164), fused
  * forward + backward: logits = E·Wcᵀ + bc, logp = log_softmax (max-shifted),
- * loss = -Σ_i logp[i, y_i] / B; writes loss[0], dE[B,D], dWc[C,D], dbc[C]
- * (all overwritten).  ws: gs_cls_nll_ws_floats(B, D, C) floats.
- * Deterministic (fixed-order partial sums, no atomics). */
+ * loss = -Σ_i logp[i, y_i] / B with y_i = labels[roots[i]] (labels[i] when
+ * roots is NULL, utils.py:161); writes loss[0], dE[B,D], dWc[C,D], dbc[C]
+ * (all overwritten).  mask_relu != 0 zeroes dE where E <= 0 (E = relu output
+ * of the last SageLayer, so dE is that layer's dZ).  C + D < 16384.
+ * ws: gs_cls_nll_ws_floats(B, D, C) floats.  Deterministic (fixed-order
+ * partial sums, no atomics); two launches. */
 int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C);
 int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E,
                        const float* Wc, const float* bc, const int32_t* labels,
-                       float* loss, float* dE, float* dWc, float* dbc, float* ws,
+                       const int32_t* roots, int32_t mask_relu, float* loss,
+                       float* dE, float* dWc, float* dbc, float* ws,
                        void* stream);
 
 /* clip_grad_norm_(params, max_norm) per group (utils.py:185-186) then SGD
  * (utils.py:136,187): p -= lr * g * min(1, max_norm / (||g_group|| + 1e-6)).
  * grads scaled by `grad_scale` first (1/world_size after an RCCL sum).
  * Groups are contiguous ranges [goff[i], goff[i+1]) of the flat buffers.
- * ws: fp32 workspace of >= 65 * n_groups floats.  Up to 8 groups. */
+ * ws: fp32 workspace of >= 64 * n_groups floats.  Up to 8 groups; two
+ * launches (per-group partial sums, then coefficient + update). */
 int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params,
                 float* grads, float grad_scale, float max_norm, float lr,
                 float* ws, void* stream);

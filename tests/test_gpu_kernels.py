@@ -153,22 +153,33 @@ def test_agg_bwd_matches_autograd(agg, F):
     torch.testing.assert_close(dH, Ht.grad, atol=1e-5, rtol=1e-5)
 
 
-def test_cls_nll_matches_torch():
+@pytest.mark.parametrize("B,D,C,use_roots,mask", [
+    (512, 128, 16, False, False),
+    (512, 128, 16, True, True),
+    (37, 64, 7, True, False),        # ragged last block, Cora-sized head
+    (100, 256, 200, True, True),     # Wc too large for LDS -> read from global
+    (1, 8, 1, False, False),
+])
+def test_cls_nll_matches_torch(B, D, C, use_roots, mask):
     torch.manual_seed(0)
-    B, D, C = 512, 128, 16
-    E = torch.randn(B, D, device=DEV, requires_grad=True)
+    n_nodes = 3 * B + 5
+    H = torch.randn(B, D, device=DEV)
+    E = (torch.relu(H) if mask else H).requires_grad_(True)
     Wc = (torch.randn(C, D, device=DEV) * 0.1).requires_grad_(True)
     bc = torch.randn(C, device=DEV, requires_grad=True)
-    y = torch.randint(0, C, (B,), device=DEV)
+    labels = torch.randint(0, C, (n_nodes,), device=DEV, dtype=torch.int32)
+    roots = torch.randperm(n_nodes, device=DEV)[:B].int() if use_roots else None
+    y = (labels[roots.long()] if use_roots else labels[:B]).long()
     logp = torch.log_softmax(E @ Wc.t() + bc, 1)
     loss = -torch.sum(logp[range(B), y], 0) / B
     loss.backward()
+    dE_ref = E.grad * (E.detach() > 0) if mask else E.grad
     out = [torch.empty(1, device=DEV), torch.empty(B, D, device=DEV), torch.empty(C, D, device=DEV),
            torch.empty(C, device=DEV)]
     ws = ops.cls_nll_workspace(B, D, C, DEV)
-    ops.cls_nll_fwd_bwd(E.detach(), Wc.detach(), bc.detach(), y.int(), *out, ws)
+    ops.cls_nll_fwd_bwd(E.detach(), Wc.detach(), bc.detach(), labels, *out, ws, roots=roots, mask_relu=mask)
     torch.testing.assert_close(out[0][0], loss.detach(), atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(out[1], E.grad, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(out[1], dE_ref, atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(out[2], Wc.grad, atol=1e-6, rtol=1e-4)
     torch.testing.assert_close(out[3], bc.grad, atol=1e-6, rtol=1e-4)
 
