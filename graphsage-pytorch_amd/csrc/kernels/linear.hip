@@ -1,352 +1,327 @@
 // SageLayer (models.py:189-220) on CDNA4 matrix cores.
 //   forward : out = relu([Xs[sidx] | A] · Wᵀ)      (:216 cat self-first, :219)
 //   backward: dW = dZᵀ · [Xs[sidx] | A],  dIn = dZ · W,  dZ = dOut ⊙ (out > 0)
-// The concat is never materialised: the K loop reads its first F columns from
+// The concat is never materialised: a K chunk reads its first F columns from
 // the gathered self rows and the rest from the aggregate.  fp32 inputs run on
 // v_mfma_f32_16x16x4_f32 (exact f32 products, fp32 accumulate); bf16 inputs on
 // v_mfma_f32_16x16x32_bf16 with fp32 accumulate.
 //
-// These GEMMs are skinny (n ~ 0.5-30k rows, H = 128) and so latency-bound,
-// not MFMA-bound, when written as a K loop of dependent chunk loads.  Both
-// kernels therefore issue the block's whole row tile in one burst (every
-// load in flight at once) and only stream the small, L2-resident weight
-// through a double-buffered LDS ring whose next chunk is fetched while the
-// MFMAs of the current one run.
+// These GEMMs are skinny (n ~ 0.5-30k rows, H <= 256, K <= a few thousand),
+// so what sets their time is how many dependent memory round trips a wave
+// waits through, not MFMA issue.  Every load below is therefore branch-free
+// (addresses clamped into range, values masked with a select afterwards) so
+// the compiler can keep a whole chunk's loads in flight, and each K (or row)
+// chunk's loads are issued one chunk ahead, under the MFMAs of the current
+// one, with a single workgroup barrier per chunk.
 #include <algorithm>
-#include <mutex>
-#include <unordered_set>
 
 #include "kcommon.hpp"
 
 namespace gs {
 
 constexpr int kThreads = 256;  // 4 wavefronts
-// Dynamic-LDS budget per workgroup: the runtime torch ships rejects requests
-// near the 160 KiB hardware size (hipFuncSetAttribute: invalid argument at
-// ~156 KB), so every layout below stays within 128 KiB.
-constexpr int kLdsMax = 128 * 1024;
+constexpr int kSlots = 16;     // 16-byte slots per row per K chunk (64 fp32 / 128 bf16)
 
-// Raise a kernel's dynamic-LDS limit once (the attribute call costs host
-// time on every launch otherwise); kLdsMax is always requested so one call
-// covers every shape.
-template <typename K>
-static void allow_smem(K kernel, size_t bytes) {
-    if (bytes <= 64 * 1024) return;
-    GS_REQUIRE(bytes <= static_cast<size_t>(kLdsMax), GS_EINVAL, "LDS request above budget");
-    static std::mutex mu;
-    static std::unordered_set<const void*> done;
-    const void* key = reinterpret_cast<const void*>(kernel);
-    std::lock_guard<std::mutex> lock(mu);
-    if (done.count(key)) return;
-    const hipError_t e = hipFuncSetAttribute(key, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();  // do not leave a sticky error for the caller's next HIP call
-        fail(GS_EHIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-    }
-    done.insert(key);
-}
-
-// 16 B of row `row` at element k of the virtual concat [self | agg] (zeros
-// past K or past n).  VLOAD: F, K, strides and bases are 16-byte aligned.
+// One 16-byte slot of the virtual concat row [self | agg] starting at element
+// k; zeros at and past K.  VLOAD: F, strides and bases are 16-byte aligned,
+// so a slot never straddles the self/agg seam.
 template <typename T, bool HAS_SELF, bool VLOAD>
-__device__ __forceinline__ uint4 concat_chunk(const T* self_row, const T* agg_row, int F, int K, int k,
-                                              bool ok) {
+__device__ __forceinline__ uint4 concat_slot(const T* srow, const T* arow, int F, int K, int k) {
     constexpr int EPV = 16 / sizeof(T);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (!ok) return v;
-    if (VLOAD) {
-        if (k < K) {
-            const T* src = (HAS_SELF && k < F) ? self_row + k : agg_row + (HAS_SELF ? k - F : k);
-            v = *reinterpret_cast<const uint4*>(src);
-        }
+    if constexpr (VLOAD) {
+        const bool in = k < K;
+        const int kk = in ? k : 0;
+        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        return in ? v : make_uint4(0, 0, 0, 0);
     } else {
         T e[EPV];
 #pragma unroll
         for (int q = 0; q < EPV; ++q) {
-            const int kk = k + q;
-            e[q] = kk < K ? ((HAS_SELF && kk < F) ? self_row[kk] : agg_row[HAS_SELF ? kk - F : kk]) : T(0);
+            const int k1 = k + q;
+            const bool in = k1 < K;
+            const int kk = in ? k1 : 0;
+            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
+            e[q] = in ? x : T(0);
         }
+        uint4 v;
         __builtin_memcpy(&v, e, 16);
+        return v;
     }
+}
+
+// 4 consecutive elements of the concat row as floats (dW operand).
+template <typename T, bool HAS_SELF, bool VLOAD>
+__device__ __forceinline__ float4 concat_quad(const T* srow, const T* arow, int F, int K, int k) {
+    float v[4];
+    if constexpr (VLOAD) {
+        const bool in = k < K;
+        const int kk = in ? k : 0;
+        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
+        if constexpr (sizeof(T) == 4) {
+            const float4 q = *reinterpret_cast<const float4*>(p);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2*>(p);
+            v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+            v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+        }
+        if (!in) v[0] = v[1] = v[2] = v[3] = 0.f;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k1 = k + q;
+            const bool in = k1 < K;
+            const int kk = in ? k1 : 0;
+            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
+            float f;
+            if constexpr (sizeof(T) == 4) f = x;
+            else f = bf2f(x);
+            v[q] = in ? f : 0.f;
+        }
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// 4 consecutive floats of a row at column c (< lim masked to 0).  VEC: the
+// row, c and lim are multiples of 4 floats.
+template <bool VEC>
+__device__ __forceinline__ float4 row_quad(const float* row, int c, int lim) {
+    if constexpr (VEC) {
+        const bool in = c < lim;
+        const float4 v = *reinterpret_cast<const float4*>(row + (in ? c : 0));
+        return in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = c + q < lim;
+            const float x = row[in ? c + q : 0];
+            v[q] = in ? x : 0.f;
+        }
+        return make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// Unmasked variants for loops that issue loads well before using them: the
+// address is clamped into range and mask_quad zeroes the out-of-range
+// elements at the point of use (a select right after the load would force a
+// wait for it there).
+template <bool VEC>
+__device__ __forceinline__ float4 row_quad_raw(const float* row, int c, int lim) {
+    if constexpr (VEC) {
+        return *reinterpret_cast<const float4*>(row + (c < lim ? c : 0));
+    } else {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = row[c + q < lim ? c + q : 0];
+        return make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+template <typename T, bool HAS_SELF, bool VLOAD>
+__device__ __forceinline__ float4 concat_quad_raw(const T* srow, const T* arow, int F, int K, int k) {
+    float v[4];
+    if constexpr (VLOAD) {
+        const int kk = k < K ? k : 0;
+        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
+        if constexpr (sizeof(T) == 4) {
+            const float4 q = *reinterpret_cast<const float4*>(p);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2*>(p);
+            v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+            v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int kk = k + q < K ? k + q : 0;
+            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
+            if constexpr (sizeof(T) == 4) v[q] = x;
+            else v[q] = bf2f(x);
+        }
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float4 mask_quad(float4 v, int c, int lim) {
+    v.x = c < lim ? v.x : 0.f; v.y = c + 1 < lim ? v.y : 0.f;
+    v.z = c + 2 < lim ? v.z : 0.f; v.w = c + 3 < lim ? v.w : 0.f;
     return v;
 }
 
-template <typename T, bool VLOAD>
-__device__ __forceinline__ uint4 w_chunk(const T* W, int K, int h, int k) {
-    constexpr int EPV = 16 / sizeof(T);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (VLOAD) {
-        if (k < K) v = *reinterpret_cast<const uint4*>(W + static_cast<int64_t>(h) * K + k);
+__device__ __forceinline__ float4 relu_mask(float4 z, float4 o) {
+    z.x = o.x > 0.f ? z.x : 0.f; z.y = o.y > 0.f ? z.y : 0.f;
+    z.z = o.z > 0.f ? z.z : 0.f; z.w = o.w > 0.f ? z.w : 0.f;
+    return z;
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma_slot(uint4 a, uint4 b, f32x4 acc) {
+    if constexpr (sizeof(T) == 4) {
+        // k-slots permuted identically on both operands: MFMA j sums element j
+        // of the four kq lanes' slots, so the four MFMAs cover all 16 k.
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
     } else {
-        T e[EPV];
-#pragma unroll
-        for (int q = 0; q < EPV; ++q) e[q] = (k + q < K) ? W[static_cast<int64_t>(h) * K + k + q] : T(0);
-        __builtin_memcpy(&v, e, 16);
+        s16x8 a8, b8;
+        __builtin_memcpy(&a8, &a, 16);
+        __builtin_memcpy(&b8, &b, 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, acc, 0, 0, 0);
     }
-    return v;
+    return acc;
 }
 
 // ---------------------------------------------------------------- forward
-// Block = 16 output rows x all H columns; wave w owns column tiles w, w+4, ...
-// The A tile (16 rows x KP columns of the concat) sits in LDS; W streams in
-// 256-byte-per-row chunks (64 fp32 / 128 bf16) through two LDS buffers.  Each
-// lane reads 16 B of a row and feeds 4 fp32 MFMAs (k-slots permuted
-// identically for both operands) or one bf16 MFMA.
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, int NTW>
+// Block = 16 rows x 64 output columns (wave w: columns 16·(4·by + w) ..).
+// Per K chunk each thread loads one slot of the 16-row concat tile into a
+// two-buffer LDS ring (shared by the 4 waves) and each lane loads the four
+// W slots its MFMAs consume straight into registers (W rows are private to a
+// wave).  Lane (r, kq) feeds MFMA group g with slot 4g + kq of row r.
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD>
 __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
-    int n, int F, int H, int K, int KP, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
+    int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo) {
     constexpr int EPV = 16 / sizeof(T);
-    constexpr int CH = NTW <= 2 ? 16 : 8;  // 16-byte chunks per W row per step (LDS budget at H = 256)
-    constexpr int BK = CH * EPV;
-    constexpr int BM = 16;
-    constexpr int SW = BK + EPV;
-    const int SA = KP + EPV;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    T* sA = reinterpret_cast<T*>(smem);
-    T* sW[2] = {sA + BM * SA, sA + BM * SA + H * SW};
+    constexpr int BK = kSlots * EPV;
+    constexpr int SA = kSlots + 1;  // LDS row pitch in slots: rows land 4 banks apart
+    __shared__ uint4 sA[2][16 * SA];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = blockIdx.x * BM;
-    const int nW = (K + BK - 1) / BK;
-    const int wper = (H * CH) / kThreads;  // W chunks (16 B) per thread per step: H/16
-
-    uint4 wreg[16];
-    auto fetch_w = [&](int c) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if (q >= wper) break;
-            const int i = tid + q * kThreads;
-            wreg[q] = w_chunk<T, VLOAD>(W, K, i / CH, c * BK + (i % CH) * EPV);
-        }
-    };
-    auto stash_w = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if (q >= wper) break;
-            const int i = tid + q * kThreads;
-            *reinterpret_cast<uint4*>(sW[buf] + (i / CH) * SW + (i % CH) * EPV) = wreg[q];
-        }
-    };
-
-    f32x4 acc[NTW];
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    fetch_w(0);
     const int r = lane & 15, kq = lane >> 4;
-    int c = 0;
-    for (int p0 = 0; p0 < K; p0 += KP) {
-        // the whole A tile of this phase, every load in flight at once
-        const int a_chunks = KP / EPV;
-        const int a_total = BM * a_chunks;
-        for (int base = tid; base < a_total; base += 8 * kThreads) {
-            uint4 v[8];  // 8 loads in flight per lane before the first LDS store
+    const int m0 = blockIdx.x * 16;
+    const int ct = blockIdx.y * 4 + wave;
+    const int ar = tid >> 4, as = tid & 15;
+    const int arow_i = min(m0 + ar, n - 1);
+    const T* arow = A + static_cast<int64_t>(arow_i) * lda;
+    const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
+    const T* wrow = W + static_cast<int64_t>(min(ct * 16 + r, H - 1)) * K;
+    const int nC = (K + BK - 1) / BK;
+
+    uint4 a_nx = concat_slot<T, HAS_SELF, VLOAD>(srow, arow, F, K, as * EPV);
+    uint4 w_nx[4];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = base + u * kThreads;
-                const int row = i / a_chunks, cc = i - row * a_chunks;
-                const bool ok = i < a_total && m0 + row < n;
-                const T* srow = nullptr;
-                const T* arow = nullptr;
-                if (ok) {
-                    if (HAS_SELF) srow = Xs + static_cast<int64_t>(sidx ? sidx[m0 + row] : m0 + row) * ldxs;
-                    arow = A + static_cast<int64_t>(m0 + row) * lda;
-                }
-                v[u] = concat_chunk<T, HAS_SELF, VLOAD>(srow, arow, F, K, p0 + cc * EPV, ok);
-            }
+    for (int g = 0; g < 4; ++g) w_nx[g] = concat_slot<T, false, VLOAD>(nullptr, wrow, K, K, (4 * g + kq) * EPV);
+    sA[0][ar * SA + as] = a_nx;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nC; ++c) {
+        uint4 w_cur[4];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = base + u * kThreads;
-                if (i >= a_total) break;
-                const int row = i / a_chunks, cc = i - row * a_chunks;
-                *reinterpret_cast<uint4*>(sA + row * SA + cc * EPV) = v[u];
-            }
-        }
-        const int c_end = min(nW, (p0 + KP) / BK);
-        for (; c < c_end; ++c) {
-            stash_w(c & 1);
-            __syncthreads();
-            if (c + 1 < nW) fetch_w(c + 1);  // in flight under this chunk's MFMAs
-            const T* a_base = sA + r * SA + (c * BK - p0);
-            const T* w_base = sW[c & 1];
+        for (int g = 0; g < 4; ++g) w_cur[g] = w_nx[g];
+        __syncthreads();
+        // next chunk (the last iteration re-reads its own chunk; discarded)
+        const int kn = min(c + 1, nC - 1) * BK;
+        a_nx = concat_slot<T, HAS_SELF, VLOAD>(srow, arow, F, K, kn + as * EPV);
 #pragma unroll
-            for (int g = 0; g < CH / 4; ++g) {
-                const uint4 av = *reinterpret_cast<const uint4*>(a_base + (g * 4 + kq) * EPV);
+        for (int g = 0; g < 4; ++g) w_nx[g] = concat_slot<T, false, VLOAD>(nullptr, wrow, K, K, kn + (4 * g + kq) * EPV);
+        __builtin_amdgcn_sched_barrier(0);  // prefetch issued ahead of the chunk's LDS reads and MFMAs
+        const uint4* tile = sA[c & 1];
+        uint4 av[4];
 #pragma unroll
-                for (int t = 0; t < NTW; ++t) {
-                    const int ct = wave + 4 * t;
-                    if (ct * 16 >= H) break;
-                    const uint4 bv = *reinterpret_cast<const uint4*>(w_base + (ct * 16 + r) * SW + (g * 4 + kq) * EPV);
-                    if constexpr (sizeof(T) == 4) {
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.x), __uint_as_float(bv.x), acc[t], 0, 0, 0);
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.y), __uint_as_float(bv.y), acc[t], 0, 0, 0);
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.z), __uint_as_float(bv.z), acc[t], 0, 0, 0);
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av.w), __uint_as_float(bv.w), acc[t], 0, 0, 0);
-                    } else {
-                        s16x8 a8, b8;
-                        __builtin_memcpy(&a8, &av, 16);
-                        __builtin_memcpy(&b8, &bv, 16);
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, acc[t], 0, 0, 0);
-                    }
-                }
-            }
-        }
-        __syncthreads();  // before the next phase overwrites sA
+        for (int g = 0; g < 4; ++g) av[g] = tile[r * SA + 4 * g + kq];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], w_cur[g], acc);
+        __builtin_amdgcn_sched_barrier(0);  // keep the wait for the prefetch behind every MFMA
+        sA[(c + 1) & 1][ar * SA + as] = a_nx;
     }
+    if (ct * 16 >= H) return;
+    const int col = ct * 16 + r;
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-        const int ct = wave + 4 * t;
-        if (ct * 16 >= H) break;
-        const int col = ct * 16 + (lane & 15);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int row = m0 + 4 * (lane >> 4) + j;
-            if (row < n) {
-                const float v = acc[t][j];
-                out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;  // NaN kept, as torch.relu
-            }
+    for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 4 * kq + j;
+        if (row < n) {
+            const float v = acc[j];
+            out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;  // NaN kept, as torch.relu
         }
     }
 }
 
 // ------------------------------------------------------------ weight grad
-// dW[h][k] = Σ_i dZ[i][h] · In[i][k].  Block = one 64-column tile of K over a
-// slab of up to kRS rows (split s): the slab's dZ (relu-masked dOut) and input
-// columns are loaded into LDS in one burst, then the MFMA "k" runs over rows,
-// both operands read straight from row-major LDS tiles.  Splits write fp32
-// partials that sum_slabs_kernel adds in a fixed order (no atomics).
-constexpr int kRS = 128;  // slab rows for H <= 128; 64 above (LDS budget)
-static inline int dw_rows(int64_t H) { return H <= 128 ? kRS : kRS / 2; }
-constexpr int kBKC = 64;
-constexpr int kSAc = kBKC + 16;
+// dW[h][k] = Σ_i dZ[i][h] · In[i][k].  Block = 64 h x 64 k over one slab of
+// rows (blockIdx.z); wave w owns h rows 16w.. of the tile and 4 k tiles.  Rows
+// stream in chunks of 16 through a two-buffer LDS ring (thread: 4 dZ values
+// and 4 inputs of one row per chunk); the MFMA "k" runs over rows.  Slabs
+// write fp32 partials that sum_slabs_kernel adds in a fixed order.
+constexpr int kDwPitch = 64 + 4;
+constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are staged in LDS)
 
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, int HTW>
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
 __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
     const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
-    const float* __restrict__ out, int64_t ldo, bool zvec, float* __restrict__ dst, int64_t split_stride) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int SZ = ((H + 31) / 32) * 32 + 16;  // bank-spread rows for the b32 fragment reads
-    float* sZ = reinterpret_cast<float*>(smem);
-    const int RS = rows_per_split;  // LDS slab height
-    float* sA = sZ + RS * SZ;
+    const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
+    __shared__ float sZ[2][16 * kDwPitch];
+    __shared__ float sI[2][16 * kDwPitch];
+    __shared__ int sIdx[HAS_SELF ? kDwMaxSlab : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kc0 = blockIdx.x * kBKC;
-    const int i_beg = blockIdx.y * rows_per_split;
-    const int rows = min(n, i_beg + rows_per_split) - i_beg;
-    const int HT = (H + 15) / 16;
-
-    // dZ slab [rows][H]
-    if (zvec) {
-        const int q4 = H / 4;
-        const int total = RS * q4;
-        for (int base = tid; base < total; base += 8 * kThreads) {
-            float4 z[8], o[8];  // 8 (16 with the relu mask) loads in flight per lane
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = base + u * kThreads;
-                const int ii = e / q4, h = (e - ii * q4) * 4;
-                z[u] = o[u] = make_float4(1.f, 1.f, 1.f, 1.f);
-                if (e < total && ii < rows) {
-                    const int64_t off = static_cast<int64_t>(i_beg + ii) * ldo + h;
-                    z[u] = *reinterpret_cast<const float4*>(dout + off);
-                    if (RELU) o[u] = *reinterpret_cast<const float4*>(out + off);
-                } else {
-                    z[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = base + u * kThreads;
-                if (e >= total) break;
-                const int ii = e / q4, h = (e - ii * q4) * 4;
-                float4 zz = z[u];
-                if (RELU) {
-                    zz.x = o[u].x > 0.f ? zz.x : 0.f; zz.y = o[u].y > 0.f ? zz.y : 0.f;
-                    zz.z = o[u].z > 0.f ? zz.z : 0.f; zz.w = o[u].w > 0.f ? zz.w : 0.f;
-                }
-                *reinterpret_cast<float4*>(sZ + ii * SZ + h) = zz;
-            }
-        }
-    } else {
-        for (int e = tid; e < RS * H; e += kThreads) {
-            const int ii = e / H, h = e - ii * H;
-            float z = 0.f;
-            if (ii < rows) {
-                const int64_t off = static_cast<int64_t>(i_beg + ii) * ldo + h;
-                z = dout[off];
-                if (RELU && !(out[off] > 0.f)) z = 0.f;
-            }
-            sZ[ii * SZ + h] = z;
-        }
-    }
-    // input slab [rows][64 columns of the concat]
-#pragma unroll 8
-    for (int e = tid; e < RS * (kBKC / 4); e += kThreads) {
-        const int ii = e >> 4, c = (e & 15) * 4, k = kc0 + c;
-        float v[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ii < rows) {
-            const int i = i_beg + ii;
-            const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[i] : i) * ldxs : nullptr;
-            const T* arow = A + static_cast<int64_t>(i) * lda;
-            if (VLOAD && k < K) {
-                const T* src = (HAS_SELF && k < F) ? srow + k : arow + (HAS_SELF ? k - F : k);
-                if constexpr (sizeof(T) == 4) {
-                    const float4 q = *reinterpret_cast<const float4*>(src);
-                    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-                } else {
-                    const uint2 q = *reinterpret_cast<const uint2*>(src);
-                    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-                    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
-                }
-            } else if (!VLOAD) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int kk = k + q;
-                    if (kk >= K) break;
-                    const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
-                    if constexpr (sizeof(T) == 4) v[q] = x;
-                    else v[q] = bf2f(x);
-                }
-            }
-        }
-        *reinterpret_cast<float4*>(sA + ii * kSAc + c) = make_float4(v[0], v[1], v[2], v[3]);
-    }
+    const int r = lane & 15, kq = lane >> 4;
+    const int k0 = blockIdx.x * 64, h0 = blockIdx.y * 64;
+    const int i_beg = blockIdx.z * rows_per_split;
+    const int i_end = min(n, i_beg + rows_per_split);
+    const int nC = (i_end - i_beg + 15) / 16;
+    const int lr = tid >> 4, lq = (tid & 15) * 4;
+    if (HAS_SELF)
+        for (int t = tid; t < i_end - i_beg; t += kThreads) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
     __syncthreads();
 
-    f32x4 acc[HTW][4];
+    // Rows past the slab read a valid row and are zeroed at the LDS store
+    // (both operands: 0 · NaN would not vanish).
+    auto load = [&](int c, float4& z, float4& o, float4& x) {
+        const int t = min(16 * c + lr, i_end - i_beg - 1);
+        const int ic = i_beg + t;
+        z = row_quad_raw<ZVEC>(dout + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
+        if (RELU) o = row_quad_raw<ZVEC>(out + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
+        const T* arow = A + static_cast<int64_t>(ic) * lda;
+        const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sIdx[t]) * ldxs : nullptr;
+        x = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
+    };
+    auto stash = [&](int c, int buf, float4 z, float4 o, float4 x) {
+        z = mask_quad(z, h0 + lq, H);
+        if (RELU) z = relu_mask(z, o);
+        x = mask_quad(x, k0 + lq, K);
+        if (16 * c + lr >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(&sZ[buf][lr * kDwPitch + lq]) = z;
+        *reinterpret_cast<float4*>(&sI[buf][lr * kDwPitch + lq]) = x;
+    };
+    float4 z, o, x;
+    load(0, z, o, x);
+    stash(0, 0, z, o, x);
+    f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < HTW; ++t)
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nC; ++c) {
+        __syncthreads();
+        const int cn = min(c + 1, nC - 1);
+        load(cn, z, o, x);
+        __builtin_amdgcn_sched_barrier(0);  // loads issue before the chunk's LDS reads and MFMAs
+        const float* tz = sZ[c & 1];
+        const float* ti = sI[c & 1];
+        float a[4], b[4][4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int steps = (rows + 3) / 4;
-    for (int s = 0; s < steps; ++s) {
-        const int ri = 4 * s + (lane >> 4);
-        float b[4];
+        for (int s = 0; s < 4; ++s) {
+            const int row = 4 * s + kq;
+            a[s] = tz[row * kDwPitch + wave * 16 + r];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) b[c] = sA[ri * kSAc + c * 16 + (lane & 15)];
-#pragma unroll
-        for (int t = 0; t < HTW; ++t) {
-            const int ht = wave + 4 * t;
-            if (ht >= HT) break;
-            const float a = sZ[ri * SZ + ht * 16 + (lane & 15)];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[c], acc[t][c], 0, 0, 0);
+            for (int t = 0; t < 4; ++t) b[s][t] = ti[row * kDwPitch + t * 16 + r];
         }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        stash(cn, (c + 1) & 1, z, o, x);
     }
-    float* slab = dst + static_cast<int64_t>(blockIdx.y) * split_stride;
+    float* slab = dst + static_cast<int64_t>(blockIdx.z) * split_stride;
 #pragma unroll
-    for (int t = 0; t < HTW; ++t) {
-        const int ht = wave + 4 * t;
-        if (ht >= HT) break;
+    for (int t = 0; t < 4; ++t) {
+        const int k = k0 + t * 16 + r;
+        if (k >= K) continue;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int k = kc0 + c * 16 + (lane & 15);
-            if (k >= K) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int h = ht * 16 + 4 * (lane >> 4) + j;
-                if (h < H) slab[static_cast<int64_t>(h) * K + k] = acc[t][c][j];
-            }
+        for (int j = 0; j < 4; ++j) {
+            const int h = h0 + wave * 16 + 4 * kq + j;
+            if (h < H) slab[static_cast<int64_t>(h) * K + k] = acc[t][j];
         }
     }
 }
@@ -357,6 +332,7 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
     const int64_t n4 = len / 4;
     for (int64_t i = blockIdx.x * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * kThreads) {
         float4 s = *reinterpret_cast<const float4*>(slabs + 4 * i);
+#pragma unroll 4
         for (int t = 1; t < S; ++t) {
             const float4 v = *reinterpret_cast<const float4*>(slabs + t * len + 4 * i);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -371,67 +347,73 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
 }
 
 // ------------------------------------------------------------- input grad
-// dIn[i][k] = Σ_h dZ[i][h] · W[h][k]; block = 16 rows x 64 columns of K.
-template <bool HAS_SELF, bool RELU>
+// dIn[i][k] = Σ_h dZ[i][h] · W[h][k].  Wave = 16 rows x 16 k columns, block =
+// 4 waves along k, no LDS: lane (r, kq) loads dZ[r][16g + 4kq ..+4] as one
+// quad and the matching four W[h][k] values, 8 groups of h in flight at once.
+template <bool HAS_SELF, bool RELU, bool ZVEC>
 __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
     int n, int F, int H, int K, const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo,
     const float* __restrict__ W, float* __restrict__ dSelf, float* __restrict__ dA, int64_t ldd) {
-    constexpr int BM = 16, BH = 32, BKC = 64, SZ = BH + 2, SW = BKC + 16;
-    __shared__ float sZ[BM * SZ];
-    __shared__ float sW[BH * SW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = blockIdx.x * BM, kc0 = blockIdx.y * BKC;
+    constexpr int G = 8;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int m0 = blockIdx.x * 16;
+    const int kt = blockIdx.y * 4 + wave;
+    const int kc = min(kt * 16 + r, K - 1);
+    const int row = min(m0 + r, n - 1);
+    const float* zrow = dout + static_cast<int64_t>(row) * ldo;
+    const float* orow = out + static_cast<int64_t>(row) * ldo;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int h0 = 0; h0 < H; h0 += BH) {
-        for (int e = tid; e < BM * BH; e += kThreads) {
-            const int ii = e / BH, hh = e - ii * BH, i = m0 + ii, h = h0 + hh;
-            float z = 0.f;
-            if (i < n && h < H) {
-                z = dout[static_cast<int64_t>(i) * ldo + h];
-                if (RELU && !(out[static_cast<int64_t>(i) * ldo + h] > 0.f)) z = 0.f;
-            }
-            sZ[ii * SZ + hh] = z;
-        }
-        for (int e = tid; e < BH * BKC; e += kThreads) {
-            const int hh = e / BKC, c = e - hh * BKC, h = h0 + hh, k = kc0 + c;
-            sW[hh * SW + c] = (h < H && k < K) ? W[static_cast<int64_t>(h) * K + k] : 0.f;
-        }
-        __syncthreads();
+    for (int h0 = 0; h0 < H; h0 += 16 * G) {
+        float4 z[G];
+        float w[G][4];
 #pragma unroll
-        for (int hh = 0; hh < BH; hh += 4) {
-            const float a = sZ[(lane & 15) * SZ + hh + (lane >> 4)];
-            const float b = sW[(hh + (lane >> 4)) * SW + wave * 16 + (lane & 15)];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        for (int g = 0; g < G; ++g) {
+            const int hb = h0 + 16 * g + 4 * kq;
+            z[g] = row_quad<ZVEC>(zrow, hb, H);
+            if (RELU) z[g] = relu_mask(z[g], row_quad<ZVEC>(orow, hb, H));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool in = hb + j < H;
+                const float v = W[static_cast<int64_t>(in ? hb + j : 0) * K + kc];
+                w[g][j] = in ? v : 0.f;
+            }
         }
-        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].x, w[g][0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].y, w[g][1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].z, w[g][2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].w, w[g][3], acc, 0, 0, 0);
+        }
     }
-    const int k = kc0 + wave * 16 + (lane & 15);
+    const int k = kt * 16 + r;
     if (k >= K) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int i = m0 + 4 * (lane >> 4) + j;
+        const int i = m0 + 4 * kq + j;
         if (i >= n) continue;
         if (HAS_SELF && k < F) dSelf[static_cast<int64_t>(i) * ldd + k] = acc[j];
         else dA[static_cast<int64_t>(i) * ldd + (HAS_SELF ? k - F : k)] = acc[j];
     }
 }
 
-static int dw_splits(int64_t n, int64_t H) {
-    const int rs = dw_rows(H);
-    return static_cast<int>(std::max<int64_t>(1, (n + rs - 1) / rs));
+// Row slabs of the weight gradient: enough (64 h x 64 k) x slab workgroups to
+// fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
+constexpr int kDwTargetBlocks = 256;
+
+static int dw_rows_per_split(int64_t n, int64_t K, int64_t H) {
+    const int64_t tiles = ((K + 63) / 64) * ((H + 63) / 64);
+    const int64_t want = std::max<int64_t>(1, (kDwTargetBlocks + tiles - 1) / tiles);
+    const int64_t cap = std::max<int64_t>(1, n / 64);
+    const int64_t S = std::max(std::min(want, cap), (n + kDwMaxSlab - 1) / kDwMaxSlab);
+    const int64_t rows = (n + S - 1) / S;
+    return static_cast<int>(std::min<int64_t>(kDwMaxSlab, std::max<int64_t>(16, (rows + 15) / 16 * 16)));
 }
 
-// Phase width of the forward's LDS-resident A tile (elements, multiple of the
-// W chunk) so that A + two W buffers fit in 160 KiB.
-static int fwd_chunks(int H) { return H <= 128 ? 16 : 8; }
-
-static int fwd_phase(int K, int H, size_t esz) {
-    const int EPV = static_cast<int>(16 / esz), BK = fwd_chunks(H) * EPV;
-    const size_t w_bytes = 2 * static_cast<size_t>(H) * (BK + EPV) * esz;
-    const size_t a_budget = kLdsMax - w_bytes - 1024;
-    int KP = ((K + BK - 1) / BK) * BK;
-    while (KP > BK && 16 * static_cast<size_t>(KP + EPV) * esz > a_budget) KP -= BK;
-    return KP;
+static int dw_splits(int64_t n, int64_t K, int64_t H) {
+    const int rps = dw_rows_per_split(n, K, H);
+    return static_cast<int>(std::max<int64_t>(1, (n + rps - 1) / rps));
 }
 
 }  // namespace gs
@@ -454,25 +436,15 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     const int EPV = dt == GS_F32 ? 4 : 8;
     const bool vload = F % EPV == 0 && lda % EPV == 0 && (!self || (ldxs % EPV == 0 && aligned16(Xs))) &&
                        aligned16(A) && aligned16(Wd);
-    const size_t esz = dt == GS_F32 ? 4 : 2;
-    const int KP = fwd_phase(K, static_cast<int>(H), esz);
-    const size_t smem =
-        (16 * static_cast<size_t>(KP + EPV) + 2 * static_cast<size_t>(H) * (fwd_chunks(static_cast<int>(H)) * EPV + EPV)) * esz;
-    const dim3 grid(static_cast<unsigned>((n + 15) / 16));
+    const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 63) / 64));
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
-#define GS_LFWD1(TT, SELF, RELU, VL, NT)                                                                  \
-    do {                                                                                                  \
-        auto kern = linear_fwd_kernel<TT, SELF, RELU, VL, NT>;                                            \
-        allow_smem(kern, smem);                                                                           \
-        kern<<<grid, kThreads, smem, st>>>(nn, ff, hh, K, KP, static_cast<const TT*>(Xs), ldxs, sidx,     \
-                                           static_cast<const TT*>(A), lda, static_cast<const TT*>(Wd),    \
-                                           out, ldo);                                                     \
-    } while (0)
-#define GS_LFWD(TT, SELF, RELU, VL) \
-    do { if (hh <= 128) GS_LFWD1(TT, SELF, RELU, VL, 2); else GS_LFWD1(TT, SELF, RELU, VL, 4); } while (0)
+#define GS_LFWD1(TT, SELF, RELU, VL)                                                                     \
+    linear_fwd_kernel<TT, SELF, RELU, VL><<<grid, kThreads, 0, st>>>(                                   \
+        nn, ff, hh, K, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,          \
+        static_cast<const TT*>(Wd), out, ldo)
 #define GS_LFWD_V(TT, SELF, RELU) \
-    do { if (vload) GS_LFWD(TT, SELF, RELU, true); else GS_LFWD(TT, SELF, RELU, false); } while (0)
+    do { if (vload) GS_LFWD1(TT, SELF, RELU, true); else GS_LFWD1(TT, SELF, RELU, false); } while (0)
 #define GS_LFWD_R(TT, SELF) \
     do { if (relu) GS_LFWD_V(TT, SELF, true); else GS_LFWD_V(TT, SELF, false); } while (0)
 #define GS_LFWD_S(TT) \
@@ -482,14 +454,13 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
 #undef GS_LFWD_S
 #undef GS_LFWD_R
 #undef GS_LFWD_V
-#undef GS_LFWD
 #undef GS_LFWD1
     check_launch("gs_sage_linear_fwd");
     GS_API_END
 }
 
 int64_t gs_sage_linear_bwd_weight_ws(int64_t n, int64_t K, int64_t H) {
-    const int S = gs::dw_splits(n, H);
+    const int S = gs::dw_splits(n, K, H);
     return S > 1 ? static_cast<int64_t>(S) * K * H * 4 : 0;
 }
 
@@ -500,7 +471,7 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
     GS_API_BEGIN
     using namespace gs;
     GS_REQUIRE(dt == GS_F32 || dt == GS_BF16, GS_EINVAL, "dtype must be f32 or bf16");
-    GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1 && H <= 256, GS_EINVAL, "bad sizes");
+    GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1 && H <= 4096, GS_EINVAL, "bad sizes");
     const bool self = Xs != nullptr;
     const int64_t K = self ? 2 * F : F;
     hipStream_t st = as_stream(stream);
@@ -508,30 +479,29 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
         GS_REQUIRE(hipMemsetAsync(dW, 0, H * K * 4, st) == hipSuccess, GS_EHIP, "memset failed");
         return GS_OK;
     }
-    GS_REQUIRE(A && dout && out && dW, GS_EINVAL, "NULL device pointer");
-    const int S = dw_splits(n, H);
+    GS_REQUIRE(A && dout && dW && (out || !relu), GS_EINVAL, "NULL device pointer");
+    const int S = dw_splits(n, K, H);
+    const int rps = dw_rows_per_split(n, K, H);
     const int64_t need = gs_sage_linear_bwd_weight_ws(n, K, H);
     GS_REQUIRE(ws_bytes >= need && (need == 0 || ws), GS_EINVAL, "workspace too small");
     float* target = (S > 1) ? static_cast<float*>(ws) : dW;
-    const bool vload = F % 4 == 0 && lda % 4 == 0 && aligned16(A) && (!self || (ldxs % 4 == 0 && aligned16(Xs)));
-    const bool zvec = H % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && aligned16(out);
-    const int SZ = static_cast<int>(((H + 31) / 32) * 32 + 16);
-    const int RS = dw_rows(H);
-    const size_t smem = static_cast<size_t>(RS) * (SZ + kSAc) * sizeof(float);
-    const dim3 grid(static_cast<unsigned>((K + kBKC - 1) / kBKC), static_cast<unsigned>(S));
+    // 4-element input reads: 16 B (fp32) / 8 B (bf16) aligned
+    const uintptr_t amask = dt == GS_F32 ? 15u : 7u;
+    const bool vload = F % 4 == 0 && lda % 4 == 0 && (!self || ldxs % 4 == 0) &&
+                       (reinterpret_cast<uintptr_t>(A) & amask) == 0 &&
+                       (!self || (reinterpret_cast<uintptr_t>(Xs) & amask) == 0);
+    const bool zvec = H % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && (!relu || aligned16(out));
+    const dim3 grid(static_cast<unsigned>((K + 63) / 64), static_cast<unsigned>((H + 63) / 64),
+                    static_cast<unsigned>(S));
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
-#define GS_LDW1(TT, SELF, RELU, VL, HW)                                                                   \
-    do {                                                                                                  \
-        auto kern = linear_dw_kernel<TT, SELF, RELU, VL, HW>;                                             \
-        allow_smem(kern, smem);                                                                           \
-        kern<<<grid, kThreads, smem, st>>>(nn, ff, hh, kk, RS, static_cast<const TT*>(Xs), ldxs, sidx,    \
-                                           static_cast<const TT*>(A), lda, dout, out, ldo, zvec, target,  \
-                                           H * K);                                                        \
-    } while (0)
-#define GS_LDW(TT, SELF, RELU, VL) \
-    do { if (hh <= 128) GS_LDW1(TT, SELF, RELU, VL, 2); else GS_LDW1(TT, SELF, RELU, VL, 4); } while (0)
+#define GS_LDW1(TT, SELF, RELU, VL, ZV)                                                                  \
+    linear_dw_kernel<TT, SELF, RELU, VL, ZV><<<grid, kThreads, 0, st>>>(                                \
+        nn, ff, hh, kk, rps, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,    \
+        dout, out, ldo, target, H * K)
+#define GS_LDW_Z(TT, SELF, RELU, VL) \
+    do { if (zvec) GS_LDW1(TT, SELF, RELU, VL, true); else GS_LDW1(TT, SELF, RELU, VL, false); } while (0)
 #define GS_LDW_V(TT, SELF, RELU) \
-    do { if (vload) GS_LDW(TT, SELF, RELU, true); else GS_LDW(TT, SELF, RELU, false); } while (0)
+    do { if (vload) GS_LDW_Z(TT, SELF, RELU, true); else GS_LDW_Z(TT, SELF, RELU, false); } while (0)
 #define GS_LDW_R(TT, SELF) \
     do { if (relu) GS_LDW_V(TT, SELF, true); else GS_LDW_V(TT, SELF, false); } while (0)
 #define GS_LDW_S(TT) \
@@ -541,7 +511,7 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
 #undef GS_LDW_S
 #undef GS_LDW_R
 #undef GS_LDW_V
-#undef GS_LDW
+#undef GS_LDW_Z
 #undef GS_LDW1
     check_launch("gs_sage_linear_bwd_weight");
     if (S > 1) {
@@ -559,16 +529,20 @@ int gs_sage_linear_bwd_input(int64_t n, int64_t F, int64_t H, const float* dout,
     using namespace gs;
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1, GS_EINVAL, "bad sizes");
     if (n == 0) return GS_OK;
-    GS_REQUIRE(dout && out && W && dA, GS_EINVAL, "NULL device pointer");
+    GS_REQUIRE(dout && W && dA && (out || !relu), GS_EINVAL, "NULL device pointer");
     const bool self = dSelf != nullptr;
     const int64_t K = self ? 2 * F : F;
+    const bool zvec = H % 4 == 0 && ldo % 4 == 0 && aligned16(dout) && (!relu || aligned16(out));
     const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((K + 63) / 64));
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
-#define GS_LDX(SELF, RELU) \
-    linear_dx_kernel<SELF, RELU><<<grid, kThreads, 0, st>>>(nn, ff, hh, kk, dout, out, ldo, W, dSelf, dA, ldd)
-    if (self) { if (relu) GS_LDX(true, true); else GS_LDX(true, false); }
-    else { if (relu) GS_LDX(false, true); else GS_LDX(false, false); }
+#define GS_LDX(SELF, RELU, ZV) \
+    linear_dx_kernel<SELF, RELU, ZV><<<grid, kThreads, 0, st>>>(nn, ff, hh, kk, dout, out, ldo, W, dSelf, dA, ldd)
+#define GS_LDX_Z(SELF, RELU) \
+    do { if (zvec) GS_LDX(SELF, RELU, true); else GS_LDX(SELF, RELU, false); } while (0)
+    if (self) { if (relu) GS_LDX_Z(true, true); else GS_LDX_Z(true, false); }
+    else { if (relu) GS_LDX_Z(false, true); else GS_LDX_Z(false, false); }
+#undef GS_LDX_Z
 #undef GS_LDX
     check_launch("gs_sage_linear_bwd_input");
     GS_API_END

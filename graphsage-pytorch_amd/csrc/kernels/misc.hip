@@ -45,13 +45,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 // ------------------------------------------------------- classifier + NLL
 // One block of 16 waves per R rows, one wave per row.  Wc is staged in LDS
-// when it fits (C·D <= 8192 floats); per row: logits with lanes over D and one
-// wave reduction per class, log_softmax (max-shifted, as torch), the row's
-// NLL term, dlogits = (softmax - onehot) / B and dE = dlogits · Wc, optionally
-// masked by E > 0 (the relu of the layer that produced E, so the caller gets
-// dZ directly).  Labels are read through the roots (labels[roots[i]]).  The
-// block then reduces its rows' dWc / dbc / loss into one partial slab;
-// cls_reduce_kernel adds the slabs in a fixed order.
+// (row pitch D + 1) when it fits.  Per row, lane (cl, dq) = (lane & 15,
+// lane >> 4) computes the dot product of class c0 + cl over one quarter of D
+// and two xor-shuffles add the quarters, so a group of 16 classes costs one
+// short FMA chain instead of a wave reduction per class.  Then log_softmax
+// (max-shifted, as torch), the row's NLL term, dlogits = (softmax - onehot)
+// / B and dE = dlogits · Wc, optionally masked by E > 0 (the relu of the layer
+// that produced E, so the caller gets dZ directly).  Labels are read through
+// the roots (labels[roots[i]]).  The block then reduces its rows' dWc / dbc /
+// loss into one partial slab; cls_reduce_kernel adds the slabs in a fixed
+// order.
 constexpr int kClsThreads = 1024;
 constexpr int64_t kClsLdsFloats = 16 * 1024;  // 64 KiB
 constexpr int64_t kClsWcLds = 8 * 1024;
@@ -64,8 +67,8 @@ struct ClsPlan {
 
 inline ClsPlan cls_plan(int64_t C, int64_t D) {
     ClsPlan p;
-    p.wc_lds = C * D <= kClsWcLds;
-    const int64_t fixed = p.wc_lds ? C * D : 0;
+    p.wc_lds = C * (D + 1) <= kClsWcLds;
+    const int64_t fixed = p.wc_lds ? C * (D + 1) : 0;
     p.rows = 1;
     for (int r = kClsThreads / 64; r > 1; r >>= 1)
         if (fixed + r * (C + D + 1) <= kClsLdsFloats) {
@@ -84,31 +87,48 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
     float* sdl = sm;             // [R][C]
     float* sE = sdl + R * C;     // [R][D]
     float* sloss = sE + R * D;   // [R]
-    float* sW = sloss + R;       // [C][D] when wc_lds
+    float* sW = sloss + R;       // [C][D + 1] when wc_lds
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane & 15, dq = lane >> 4;
     const int r0 = blockIdx.x * R;
     const int nr = min(R, B - r0);
     const float invB = 1.0f / static_cast<float>(B);
+    // every global read is issued before the first barrier: the label chain
+    // (roots -> labels) and the bias overlap the E / Wc tile loads
+    int y_w = 0;
+    if (w < nr) y_w = labels[roots ? roots[r0 + w] : r0 + w];
+    const float b_lane = bc[min(cl, C - 1)];
     for (int t = threadIdx.x; t < R * D; t += kClsThreads) {
         const int ii = t / D;
         sE[t] = ii < nr ? E[static_cast<int64_t>(r0) * D + t] : 0.f;
     }
     if (wc_lds)
-        for (int t = threadIdx.x; t < C * D; t += kClsThreads) sW[t] = Wc[t];
+        for (int t = threadIdx.x; t < C * D; t += kClsThreads) {
+            const int c = t / D;
+            sW[t + c] = Wc[t];
+        }
     __syncthreads();
     const float* W = wc_lds ? sW : Wc;
+    const int wp = wc_lds ? D + 1 : D;  // row pitch of W
+    const int DQ = (D + 3) / 4;
+    const int d_lo = min(D, dq * DQ), d_hi = min(D, d_lo + DQ);
     for (int ii = w; ii < nr; ii += kClsThreads / 64) {
         const float* e = sE + ii * D;
-        const int y = labels[roots ? roots[r0 + ii] : r0 + ii];
+        const int y = ii == w ? y_w : labels[roots ? roots[r0 + ii] : r0 + ii];
         float mx = -INFINITY;
-        for (int c = 0; c < C; ++c) {
-            const float* wr = W + static_cast<int64_t>(c) * D;
+        for (int c0 = 0; c0 < C; c0 += 16) {
+            const int c = c0 + cl;
+            const float* wr = W + static_cast<int64_t>(min(c, C - 1)) * wp;
             float p = 0.f;
-            for (int d = lane; d < D; d += 64) p = fmaf(e[d], wr[d], p);
-            const float z = wave_sum(p) + bc[c];
-            if (lane == 0) sdl[ii * C + c] = z;
-            mx = fmaxf(mx, z);
+            for (int d = d_lo; d < d_hi; ++d) p = fmaf(e[d], wr[d], p);
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            const float z = p + (c0 == 0 ? b_lane : bc[min(c, C - 1)]);
+            if (dq == 0 && c < C) sdl[ii * C + c] = z;
+            if (c < C) mx = fmaxf(mx, z);
         }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
         __builtin_amdgcn_wave_barrier();
         float se = 0.f;
         for (int c = lane; c < C; c += 64) se += expf(sdl[ii * C + c] - mx);
@@ -121,7 +141,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
         __builtin_amdgcn_wave_barrier();
         for (int d = lane; d < D; d += 64) {
             float s = 0.f;
-            for (int c = 0; c < C; ++c) s = fmaf(sdl[ii * C + c], W[static_cast<int64_t>(c) * D + d], s);
+            for (int c = 0; c < C; ++c) s = fmaf(sdl[ii * C + c], W[static_cast<int64_t>(c) * wp + d], s);
             if (mask_relu && !(e[d] > 0.f)) s = 0.f;
             dE[static_cast<int64_t>(r0 + ii) * D + d] = s;
         }

@@ -88,7 +88,8 @@ def test_agg_fwd_explicit_max_argmax_first_index(gs, F):
 
 
 @pytest.mark.parametrize("n,F,H", [(1, 256, 128), (37, 128, 128), (300, 100, 64), (4321, 256, 128),
-                                   (50, 1433, 128), (64, 8, 16), (129, 256, 256)])
+                                   (50, 1433, 128), (64, 8, 16), (129, 256, 256), (5000, 64, 48),
+                                   (3000, 20, 16)])
 @pytest.mark.parametrize("gcn", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_sage_linear_fwd_bwd(n, F, H, gcn, dtype):
