@@ -6,9 +6,15 @@
 // so the state here is word-for-word interchangeable with random.getstate().
 #pragma once
 
+#include <immintrin.h>
+
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+
+#ifndef GS_SELECT_SMALL
+#define GS_SELECT_SMALL 1
+#endif
 
 namespace gs {
 
@@ -121,6 +127,72 @@ inline int64_t sample_setsize(int64_t k) {
     return setsize;
 }
 
+// The selected-set branch for k <= 32, eight stream words at a time.  A
+// word is a repeat exactly when it equals an already selected value or an
+// earlier in-range word of the same call (an earlier in-range word was either
+// selected or itself a repeat of a selected value), so the freshness of the
+// eight words of a chunk follows from comparisons alone, without a
+// data-dependent branch per word.  The first (k - cnt) fresh words are taken,
+// and the stream advances by exactly the words up to the last one taken —
+// the same consumption as redrawing word by word.  Near the end of a block
+// (fewer than 8 words left) words are taken one at a time through next().
+template <class OutT>
+inline void select_chunked(MT19937& rng, int64_t n, int64_t k, OutT* out) {
+    const int sh = 32 - (64 - __builtin_clzll(static_cast<uint64_t>(n)));
+    const __m128i shv = _mm_cvtsi32_si128(sh);
+    const __m256i nv = _mm256_set1_epi32(static_cast<int32_t>(n));
+    alignas(32) int32_t sel[32];
+    const __m256i none = _mm256_set1_epi32(-1);
+    for (int q = 0; q < 4; ++q) _mm256_store_si256(reinterpret_cast<__m256i*>(sel) + q, none);
+    int32_t cnt = 0;
+    while (cnt < k) {
+        if (rng.index + 8 <= MT19937::N) {
+            const __m256i w = _mm256_srl_epi32(
+                _mm256_loadu_si256(reinterpret_cast<const __m256i*>(rng.out + rng.index)), shv);
+            const int inr = _mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(nv, w)));
+            const __m256i s0 = _mm256_load_si256(reinterpret_cast<const __m256i*>(sel));
+            const __m256i s1 = _mm256_load_si256(reinterpret_cast<const __m256i*>(sel) + 1);
+            const __m256i s2 = _mm256_load_si256(reinterpret_cast<const __m256i*>(sel) + 2);
+            const __m256i s3 = _mm256_load_si256(reinterpret_cast<const __m256i*>(sel) + 3);
+            uint32_t fresh = 0;
+#pragma GCC unroll 8
+            for (int i = 0; i < 8; ++i) {
+                const __m256i b = _mm256_permutevar8x32_epi32(w, _mm256_set1_epi32(i));
+                const int earlier = _mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpeq_epi32(b, w))) & inr &
+                                    ((1 << i) - 1);
+                const __m256i h = _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi32(b, s0), _mm256_cmpeq_epi32(b, s1)),
+                                                  _mm256_or_si256(_mm256_cmpeq_epi32(b, s2), _mm256_cmpeq_epi32(b, s3)));
+                const uint32_t ok = ((inr >> i) & 1) & (earlier == 0) & _mm256_testz_si256(h, h);
+                fresh |= ok << i;
+            }
+            const int need = static_cast<int>(k) - cnt;
+            int consumed = 8;
+            if (__builtin_popcount(fresh) >= need) {
+                const int last = __builtin_ctz(_pdep_u32(1u << (need - 1), fresh));
+                consumed = last + 1;
+                fresh &= (2u << last) - 1;
+            }
+            alignas(32) int32_t wv[8];
+            _mm256_store_si256(reinterpret_cast<__m256i*>(wv), w);
+            while (fresh) {
+                const int i = __builtin_ctz(fresh);
+                sel[cnt] = wv[i];
+                out[cnt] = static_cast<OutT>(wv[i]);
+                ++cnt;
+                fresh &= fresh - 1;
+            }
+            rng.index += consumed;
+        } else {
+            const uint32_t r = rng.next() >> sh;
+            bool ok = r < static_cast<uint32_t>(n);
+            for (int32_t t = 0; t < cnt; ++t) ok &= sel[t] != static_cast<int32_t>(r);
+            sel[cnt] = ok ? static_cast<int32_t>(r) : -1;
+            out[cnt] = static_cast<OutT>(r);  // kept only when fresh
+            cnt += ok;
+        }
+    }
+}
+
 // random.sample(population, k) expressed on positions 0..n-1 of the
 // population: writes the k chosen positions in result order.  `pool` must
 // hold setsize entries.  Requires 0 <= k <= n.
@@ -137,6 +209,8 @@ inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize
             out[i] = static_cast<OutT>(pool[j]);
             pool[j] = pool[n - i - 1];
         }
+    } else if (GS_SELECT_SMALL && k <= 32 && n < (int64_t(1) << 31)) {
+        select_chunked(rng, n, k, out);
     } else {
         // selected-set branch: j = randbelow(n), redrawn while j in selected.
         // Both a rejected word (r >= n) and a repeat are simply skipped, so

@@ -23,6 +23,10 @@ struct gs_rng {
     gs::MT19937 mt;
 };
 
+#ifndef GS_PHASE  // phase marks for tools/sampler_prof.cpp; no-ops in the library
+#define GS_PHASE(i)
+#endif
+
 namespace gs {
 
 struct Hop {
@@ -99,6 +103,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     // samp_neighs[r] = S_r | {v}: built in a scratch set, kept only as its
     // iteration order (set_items) — all the union needs from r >= 1 — plus
     // the full table of r == 0, which the union copies.
+    GS_PHASE(0);
     PySet s, t, first;
     h.set_ptr.assign(n + 1, 0);
     h.set_items.clear();
@@ -122,6 +127,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
         t.for_each([&](int64_t key) { h.set_items.push_back(key); });
         h.set_ptr[r + 1] = static_cast<int32_t>(h.set_items.size());
     }
+    GS_PHASE(1);
     // list(set.union(*samp_neighs))  (:286): copy of the first, then set_merge
     // of each other set, which only walks that set's iteration order.
     PySet u;
@@ -132,6 +138,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     }
     // Union-local positions through a dense node -> position map (one int32
     // per graph node per sampler thread, restored to -1 before returning).
+    GS_PHASE(2);
     thread_local std::vector<int32_t> pos_of;
     if (static_cast<int64_t>(pos_of.size()) < g.n_nodes) pos_of.assign(g.n_nodes, -1);
     h.src_ids.clear();
@@ -152,6 +159,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     auto local_of = [&](int64_t key) -> int32_t { return pos_of[key]; };
     // Neighbourhoods in union-local ids, ascending (= the dense mask's column
     // order, :305-308); non-gcn removes self (:297-298).
+    GS_PHASE(3);
     h.nbr_ptr.assign(n + 1, 0);
     h.nbr.clear();
     h.self_local.resize(n);
@@ -176,6 +184,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     }
     // Transposed lists over Fj: for source c, the destinations reading it
     // (r >= 0) and the destinations whose self row it is (-(r+1)), r ascending.
+    GS_PHASE(4);
     const int64_t ns = static_cast<int64_t>(h.src_ids.size());
     h.tptr.assign(ns + 1, 0);
     for (int32_t c : h.nbr) ++h.tptr[c + 1];
@@ -189,6 +198,7 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
             h.tidx[cur[h.nbr[e]]++] = static_cast<int32_t>(r);
     }
     h.materialised = true;
+    GS_PHASE(5);
 }
 
 static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,

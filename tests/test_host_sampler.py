@@ -244,3 +244,23 @@ def test_stream_seeds_are_reference_seeds(gs):
             want = sample_layers(adj, roots.tolist(), [10, 10])
             assert s.hop(2).src_ids.tolist() == want[1][3]
         assert r.getstate()[0].tolist() + [r.getstate()[1]] == list(random.getstate()[1])
+
+
+def test_sample_positions_match_cpython_random_sample(gs):
+    """random.sample over both branches (pool / selected-set, incl. the
+    chunked k <= 32 scan) and across MT block refills: positions and the
+    stream state must equal CPython's own random.Random."""
+    rs = np.random.RandomState(7)
+    ks = [1, 2, 5, 6, 10, 16, 25, 31, 32, 33, 40]
+    for seed in (0, 1, 824):
+        py = random.Random(seed)
+        r = gs.RNG(seed)
+        for _ in range(2500):
+            k = int(rs.choice(ks))
+            n = int(rs.choice([k, k + 1, 50, 85, 86, 100, 128, 129, 277, 278, 1000, 65536, 100003, (1 << 20) + 3]))
+            if n < k:
+                continue
+            assert r.sample_positions(n, k).tolist() == py.sample(range(n), k), (seed, n, k)
+        mt, pos = r.getstate()
+        st = py.getstate()[1]
+        assert mt.tolist() == list(st[:624]) and pos == st[624]
