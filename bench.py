@@ -52,8 +52,21 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
+def host_cores():
+    """CPUs this process may use: affinity, capped by a cgroup-v2 CPU quota
+    (the GPU boxes grant 16 CPUs per GPU while showing every core)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def host_threads():
-    return max(1, min(16, os.cpu_count() or 1))
+    return max(1, min(16, host_cores()))
 
 
 def build_workload(cfg, device, seed=824):
@@ -82,13 +95,22 @@ def agg1_times_ms(trainer, n):
     return out[:got]
 
 
-def agg1_bytes(s, F, elem):
+def cgroup_throttle():
+    """Cumulative CPU-quota throttling of this cgroup (us), or None."""
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            if line.startswith("throttled_usec"):
+                return int(line.split()[1])
+    except OSError:
+        pass
+    return None
+
+
+def agg1_bytes(n_dst, n_pos, F, elem):
     """Algorithmic HBM bytes of one layer-1 K-agg launch:
     neighbour feature rows once per sampled edge + sampled positions and CSR
     column entries (4 B each) + one output row per destination + per-destination
     metadata (dst id 4 B, row_ptr 8 B, pos_ptr 4 B)."""
-    L = s.n_hops
-    n_dst, n_pos, _, _ = s.sizes(L)
     return n_pos * (F * elem + 8) + n_dst * (F * elem + 16)
 
 
@@ -148,9 +170,13 @@ def main():
     ap.add_argument("--seed", type=int, default=824)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
-    ap.add_argument("--sampler-streams", type=int, default=1,
-                    help="independent bit-exact sampler streams per GPU (1 = the reference's single stream)")
+    ap.add_argument("--sampler-streams", type=int, default=None,
+                    help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
+                         "default: min(8, host cores per GPU - 2))")
     args = ap.parse_args()
+    if args.sampler_streams is None:
+        per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+        args.sampler_streams = max(1, min(8, per_gpu - 2))
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -173,33 +199,26 @@ def main():
         batches.extend(train.rank_batches(wl["candidates"], cfg["batch"], rank, world, args.seed + 1000, epoch))
         epoch += 1
     batches = batches[:total_steps]
-    pf = train.Prefetcher(wl["graph"], None, batches, cfg["fanouts"], False, device, rngs=rngs,
-                          fail_empty=cfg["agg"] == "MAX")
+    comm = train.Communicator(rank, world, device) if world > 1 else None
+    runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
+                          fail_empty=cfg["agg"] == "MAX", comm=comm)
     elem = 2 if cfg["dtype"] == "bf16" else 4
 
-    for _ in range(args.warmup):
-        ds, roots_dev, s = pf.next()
-        trainer.step(ds, roots_dev, world)
+    runner.run(args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    runner.stats(reset=True)
     gs._lib.check(gs._lib.lib().gs_trainer_time_agg(trainer._h, args.steps))
-    agg_bytes, n_edges = [], 0
-    t_wait = t_launch = 0.0
+    thr0 = cgroup_throttle()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ta = time.perf_counter()
-        ds, roots_dev, s = pf.next()
-        tb = time.perf_counter()
-        trainer.step(ds, roots_dev, world)
-        t_launch += time.perf_counter() - tb
-        t_wait += tb - ta
-        agg_bytes.append(agg1_bytes(s, cfg["feat"], elem))
-        n_edges += s.sizes(1)[1] + s.sizes(2)[1]
+    runner.run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    thr1 = cgroup_throttle()
+    st = runner.stats()
     loss = float(trainer.loss.item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -207,15 +226,19 @@ def main():
     elapsed = float(t.item())
     agg_ms = float(np.mean(agg1_times_ms(trainer, args.steps)))
     value = cfg["batch"] * args.steps * world / elapsed
+    L = len(cfg["fanouts"])
+    sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
+    n_edges = float(sizes[:L, 1].sum()) * args.steps
+    agg_bytes = agg1_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem)
 
     if rank == 0:
-        achieved = float(np.mean(agg_bytes)) / (agg_ms * 1e-3) / 1e9
+        achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9
         tr = load_traffic(args.config)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": (tr["agg1_hbm_bytes_per_launch"] if tr else None),
                 "kernel": "agg_fwd_kernel (layer-1 expand gather-mean)", "avg_launch_us": round(agg_ms * 1e3, 2),
-                "algo_bytes_per_launch": int(np.mean(agg_bytes))}
+                "algo_bytes_per_launch": int(agg_bytes)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(wl, cfg, args.cpu_budget, args.seed)
@@ -232,14 +255,21 @@ def main():
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
-                       "host_ms_per_step": {"sampler": round(1e3 * float(np.median(pf.sample_s)), 3),
-                                            "wait_for_batch": round(1e3 * t_wait / args.steps, 3),
-                                            "launch": round(1e3 * t_launch / args.steps, 3)}},
+                       "host_ms_per_step": {"sampler": round(1e3 * st["sample_s"] / max(1, st["steps"]), 3),
+                                            "wait_for_batch": round(1e3 * st["wait_s"] / max(1, st["steps"]), 3),
+                                            "issue": round(1e3 * st["issue_s"] / max(1, st["steps"]), 3),
+                                            "issue_copy": round(1e3 * st["copy_s"] / max(1, st["steps"]), 3),
+                                            "issue_fwd_bwd": round(1e3 * st["fwd_bwd_s"] / max(1, st["steps"]), 3),
+                                            "issue_update": round(1e3 * st["update_s"] / max(1, st["steps"]), 3),
+                                            "max_step": round(1e3 * st["max_step_s"], 3)},
+                       "cgroup_throttled_ms": (round((thr1 - thr0) / 1e3, 3) if thr0 is not None else None)},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    pf.close()
+    runner.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

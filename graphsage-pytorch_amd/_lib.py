@@ -100,6 +100,16 @@ _SIGS = {
     "gs_trainer_update": (_i32, [_vp, _f32, _vp, _vp]),
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
+    "gs_trainer_grads": (_vp, [_vp]),
+    "gs_comm_unique_id": (_i32, [_vp]),
+    "gs_comm_create": (_i32, [_vp, _i32, _i32, _p(_vp)]),
+    "gs_comm_destroy": (None, [_vp]),
+    "gs_comm_allreduce_sum": (_i32, [_vp, _vp, _i64, _vp]),
+    "gs_runner_create": (_i32, [_vp, _p(_vp)]),
+    "gs_runner_run": (_i32, [_vp, _i64, _vp, _vp]),
+    "gs_runner_stats_get": (_i32, [_vp, _vp]),
+    "gs_runner_stats_reset": (None, [_vp]),
+    "gs_runner_destroy": (None, [_vp]),
 }
 
 
@@ -110,6 +120,24 @@ class TrainerConfig(ctypes.Structure):
         ("X", _vp), ("row_ptr", _vp), ("col", _vp), ("labels", _vp), ("params", _vp), ("grads", _vp),
         ("lr", _f32), ("max_norm", _f32),
     ]
+
+
+class RunnerConfig(ctypes.Structure):
+    _fields_ = [
+        ("graph", _vp), ("trainer", _vp), ("batches", _vp), ("n_batches", _i64), ("batch", _i64),
+        ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
+        ("depth", _i32), ("comm", _vp), ("world", _i32),
+    ]
+
+
+class RunnerStats(ctypes.Structure):
+    _fields_ = [
+        ("steps", _i64), ("wait_s", ctypes.c_double), ("issue_s", ctypes.c_double),
+        ("sample_s", ctypes.c_double), ("hop_sizes", ctypes.c_double * (4 * GS_MAX_HOPS)),
+        ("copy_s", ctypes.c_double), ("fwd_bwd_s", ctypes.c_double), ("update_s", ctypes.c_double),
+        ("max_step_s", ctypes.c_double),
+    ]
+
 
 _lib = None
 

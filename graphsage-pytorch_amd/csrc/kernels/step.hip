@@ -185,6 +185,8 @@ void gs_trainer_destroy(gs_trainer* t) { delete t; }
 
 int64_t gs_trainer_n_params(const gs_trainer* t) { return t ? t->total : -1; }
 
+float* gs_trainer_grads(const gs_trainer* t) { return t ? t->cfg.grads : nullptr; }
+
 int64_t gs_trainer_ws_bytes(gs_trainer* t, const int64_t* hop_sizes) {
     try {
         std::vector<int64_t> off(GS_MAX_HOPS * GS_PK_NFIELDS, 0);

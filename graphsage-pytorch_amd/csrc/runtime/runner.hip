@@ -1,0 +1,335 @@
+// Native pipeline runner: the reference's per-epoch batch loop
+// (utils.py:144-191) with its two halves overlapped instead of alternating —
+// host neighbour sampling on S threads and the device step on one stream —
+// so that no Python code runs per step.
+//
+//   sampler thread w : batches w, w+S, ... in order, each into a free pinned
+//                      slot of its ring (gs_sample_pack_run, its own rng)
+//   gs_runner_run    : batch i from stream i % S, in order: H2D copy into
+//                      device pack buffer i % 2, forward/backward, all-reduce
+//                      (world > 1) and update, all on the caller's stream.
+// A pinned slot returns to its sampler once the copy that read it has
+// completed.  Only the driver thread makes HIP calls: it polls the copy events
+// of consumed slots (hipEventQuery) and hands finished slots back, and waits
+// on the oldest copy only when a stream has no slot left to sample into.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../kernels/kcommon.hpp"
+
+namespace gs {
+
+using Clock = std::chrono::steady_clock;
+
+static double secs(Clock::time_point a, Clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+}
+
+static void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct PackSlot {
+    int32_t* host = nullptr;  // pinned
+    hipEvent_t copied = nullptr;
+    int64_t batch = -1;
+    int64_t hop_sizes[4 * GS_MAX_HOPS];
+    int64_t offsets[GS_MAX_HOPS * GS_PK_NFIELDS];
+    int64_t used = 0;
+    double sample_s = 0;
+    int status = GS_OK;
+    std::string error;
+};
+
+struct SamplerStream {
+    gs_rng* rng = nullptr;
+    std::vector<int64_t> batches;  // global batch indices, in order
+    std::vector<PackSlot> slots;
+    std::deque<int> free, ready;  // guarded by mu
+    std::deque<int> copying;      // driver-only: consumed, H2D copy in flight
+    std::mutex mu;
+    std::condition_variable cv;
+    std::thread th;
+};
+
+}  // namespace gs
+
+struct gs_runner {
+    gs_runner_config cfg{};
+    std::vector<int32_t> fanouts;
+    std::vector<int64_t> roots;  // n_batches x batch
+    int64_t cap = 0;             // int32 words per pack slot (pack bound + roots)
+    std::vector<std::unique_ptr<gs::SamplerStream>> streams;
+    bool stop = false;
+    int64_t next_batch = 0;
+    int32_t* dev[2] = {nullptr, nullptr};  // device packs, alternating (stream-ordered reuse)
+    void* ws = nullptr;
+    int64_t ws_bytes = 0;
+    float* clip_ws = nullptr;
+    int device = 0;
+    gs_runner_stats stats{};
+
+    ~gs_runner();
+    void sampler_loop(gs::SamplerStream& s);
+    void recycle(gs::SamplerStream& s, bool block);
+};
+
+// Hand the slots whose copy has completed back to their sampler; with
+// `block`, wait for the oldest one when none is free yet.
+void gs_runner::recycle(gs::SamplerStream& s, bool block) {
+    int n_back = 0;
+    while (!s.copying.empty()) {
+        const int q = s.copying.front();
+        const hipError_t e = (block && n_back == 0) ? hipEventSynchronize(s.slots[q].copied)
+                                                     : hipEventQuery(s.slots[q].copied);
+        if (e == hipErrorNotReady) break;
+        gs::hip_ok(e, "copy event");
+        s.copying.pop_front();
+        {
+            std::lock_guard<std::mutex> lk(s.mu);
+            s.free.push_back(q);
+        }
+        ++n_back;
+    }
+    if (n_back) s.cv.notify_all();
+}
+
+void gs_runner::sampler_loop(gs::SamplerStream& s) {
+    for (int64_t b : s.batches) {
+        int slot_id;
+        {
+            std::unique_lock<std::mutex> lk(s.mu);
+            s.cv.wait(lk, [&] { return stop || !s.free.empty(); });
+            if (stop) return;
+            slot_id = s.free.front();
+            s.free.pop_front();
+        }
+        gs::PackSlot& slot = s.slots[slot_id];
+        const auto t0 = gs::Clock::now();
+        slot.batch = b;
+        slot.status = gs_sample_pack_run(cfg.graph, s.rng, roots.data() + b * cfg.batch, cfg.batch, fanouts.data(),
+                                         cfg.n_hops, cfg.flags, slot.host, cap, slot.hop_sizes, slot.offsets,
+                                         &slot.used);
+        if (slot.status != GS_OK) slot.error = gs_last_error();
+        slot.sample_s = gs::secs(t0, gs::Clock::now());
+        {
+            std::lock_guard<std::mutex> lk(s.mu);
+            s.ready.push_back(slot_id);
+        }
+        s.cv.notify_all();
+        if (slot.status != GS_OK) return;  // the driver reports it when it reaches this batch
+    }
+}
+
+gs_runner::~gs_runner() {
+    for (auto& s : streams) {
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            stop = true;
+        }
+        s->cv.notify_all();
+    }
+    for (auto& s : streams)
+        if (s->th.joinable()) s->th.join();
+    for (auto& s : streams)
+        for (int q : s->copying) (void)hipEventSynchronize(s->slots[q].copied);
+    for (auto& s : streams)
+        for (auto& slot : s->slots) {
+            if (slot.copied) (void)hipEventDestroy(slot.copied);
+            if (slot.host) (void)hipHostFree(slot.host);
+        }
+    for (int d = 0; d < 2; ++d)
+        if (dev[d]) (void)hipFree(dev[d]);
+    if (ws) (void)hipFree(ws);
+    if (clip_ws) (void)hipFree(clip_ws);
+}
+
+extern "C" {
+
+int gs_comm_unique_id(uint8_t id[128]) {
+    GS_API_BEGIN
+    GS_REQUIRE(id, GS_EINVAL, "NULL argument");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    GS_REQUIRE(ncclGetUniqueId(&u) == ncclSuccess, GS_EHIP, "ncclGetUniqueId failed");
+    std::memcpy(id, &u, 128);
+    GS_API_END
+}
+
+int gs_comm_create(const uint8_t id[128], int32_t n_ranks, int32_t rank, void** comm) {
+    GS_API_BEGIN
+    GS_REQUIRE(id && comm && n_ranks >= 1 && rank >= 0 && rank < n_ranks, GS_EINVAL, "bad arguments");
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, n_ranks, u, rank);
+    GS_REQUIRE(r == ncclSuccess, GS_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    *comm = c;
+    GS_API_END
+}
+
+void gs_comm_destroy(void* comm) {
+    if (comm) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm));
+}
+
+int gs_comm_allreduce_sum(void* comm, float* buf, int64_t n, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(comm && buf && n >= 0, GS_EINVAL, "bad arguments");
+    const ncclResult_t r = ncclAllReduce(buf, buf, static_cast<size_t>(n), ncclFloat32, ncclSum,
+                                         static_cast<ncclComm_t>(comm), gs::as_stream(stream));
+    GS_REQUIRE(r == ncclSuccess, GS_EHIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    GS_API_END
+}
+
+int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
+    GS_API_BEGIN
+    using namespace gs;
+    GS_REQUIRE(cfg && out, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(cfg->graph && cfg->trainer && cfg->batches && cfg->rngs, GS_EINVAL, "NULL pointer in config");
+    GS_REQUIRE(cfg->n_batches >= 1 && cfg->batch >= 1 && cfg->batch < (int64_t(1) << 30), GS_EINVAL,
+               "bad batch shape");
+    GS_REQUIRE(cfg->n_hops >= 1 && cfg->n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
+    GS_REQUIRE(cfg->n_streams >= 1 && cfg->n_streams <= 64 && cfg->depth >= 1 && cfg->depth <= 64, GS_EINVAL,
+               "n_streams / depth out of range");
+    GS_REQUIRE(cfg->world >= 1 && (cfg->world == 1 || cfg->comm), GS_EINVAL, "world > 1 needs a communicator");
+    for (int32_t w = 0; w < cfg->n_streams; ++w) GS_REQUIRE(cfg->rngs[w], GS_EINVAL, "NULL rng");
+    std::unique_ptr<gs_runner> r(new gs_runner());
+    r->cfg = *cfg;
+    r->fanouts.assign(cfg->fanouts ? cfg->fanouts : nullptr, cfg->fanouts ? cfg->fanouts + cfg->n_hops : nullptr);
+    if (r->fanouts.empty()) r->fanouts.assign(cfg->n_hops, 10);
+    r->cfg.fanouts = r->fanouts.data();
+    r->roots.assign(cfg->batches, cfg->batches + cfg->n_batches * cfg->batch);
+    r->cfg.batches = r->roots.data();
+    const int64_t bound = gs_sample_pack_bound(cfg->graph, cfg->batch, r->fanouts.data(), cfg->n_hops);
+    GS_REQUIRE(bound > 0, GS_EINVAL, "pack bound failed");
+    r->cap = bound + cfg->batch;
+    hip_ok(hipGetDevice(&r->device), "hipGetDevice");
+    for (int d = 0; d < 2; ++d) {
+        hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
+    }
+    hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
+    const int32_t S = cfg->n_streams;
+    for (int32_t w = 0; w < S; ++w) {
+        auto s = std::make_unique<SamplerStream>();
+        s->rng = cfg->rngs[w];
+        for (int64_t b = w; b < cfg->n_batches; b += S) s->batches.push_back(b);
+        s->slots.resize(cfg->depth);
+        for (int32_t q = 0; q < cfg->depth; ++q) {
+            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s->slots[q].host), r->cap * sizeof(int32_t),
+                                 hipHostMallocDefault),
+                   "hipHostMalloc");
+            hip_ok(hipEventCreateWithFlags(&s->slots[q].copied, hipEventDisableTiming), "hipEventCreate");
+            s->free.push_back(q);
+        }
+        r->streams.push_back(std::move(s));
+    }
+    for (auto& s : r->streams) {
+        SamplerStream* sp = s.get();
+        gs_runner* rp = r.get();
+        s->th = std::thread([rp, sp] { rp->sampler_loop(*sp); });
+    }
+    *out = r.release();
+    GS_API_END
+}
+
+int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
+    GS_API_BEGIN
+    using namespace gs;
+    GS_REQUIRE(r && loss && n_steps >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(r->next_batch + n_steps <= r->cfg.n_batches, GS_ERANGE, "runner has fewer batches left");
+    hipStream_t st = as_stream(stream);
+    const int32_t S = r->cfg.n_streams;
+    const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
+    float* grads = gs_trainer_grads(r->cfg.trainer);
+    for (int64_t step = 0; step < n_steps; ++step) {
+        const int64_t b = r->next_batch;
+        SamplerStream& s = *r->streams[b % S];
+        const auto t0 = Clock::now();
+        for (auto& o : r->streams) r->recycle(*o, false);
+        int slot_id;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(s.mu);
+            // a sampled batch, or a sampler starved of slots while copies are in flight
+            s.cv.wait(lk, [&] { return !s.ready.empty() || (s.free.empty() && !s.copying.empty()); });
+            if (!s.ready.empty()) {
+                slot_id = s.ready.front();
+                s.ready.pop_front();
+                break;
+            }
+            lk.unlock();
+            r->recycle(s, true);
+        }
+        PackSlot& slot = s.slots[slot_id];
+        const auto t1 = Clock::now();
+        GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
+        if (slot.status != GS_OK) fail(slot.status, slot.error);
+        // H2D on the step's own stream: a separate copy stream waiting on the
+        // step that last read the buffer made hipMemcpyAsync block the host
+        // (measured 0.2-0.35 ms per step), far more than the ~10 us of copy
+        // it could hide.
+        const int d = static_cast<int>(b & 1);
+        hip_ok(hipMemcpyAsync(r->dev[d], slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, st),
+               "hipMemcpyAsync(pack)");
+        hip_ok(hipEventRecord(slot.copied, st), "hipEventRecord");
+        const auto t2 = Clock::now();
+        const int64_t need = gs_trainer_ws_bytes(r->cfg.trainer, slot.hop_sizes);
+        GS_REQUIRE(need >= 0, GS_EINVAL, gs_last_error());
+        if (need > r->ws_bytes) {
+            hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+            if (r->ws) hip_ok(hipFree(r->ws), "hipFree");
+            r->ws = nullptr;
+            r->ws_bytes = need + need / 4 + (1 << 20);
+            hip_ok(hipMalloc(&r->ws, r->ws_bytes), "hipMalloc(ws)");
+        }
+        const int64_t pack_total = slot.used - r->cfg.batch;
+        int rc = gs_trainer_forward_backward(r->cfg.trainer, r->dev[d], slot.hop_sizes, slot.offsets,
+                                             r->dev[d] + pack_total, r->cfg.batch, r->ws, r->ws_bytes, loss, st);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+        const auto t3 = Clock::now();
+        if (r->cfg.world > 1) {
+            rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+        }
+        rc = gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+        for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);
+        r->stats.sample_s += slot.sample_s;
+        s.copying.push_back(slot_id);
+        ++r->next_batch;
+        ++r->stats.steps;
+        const auto t4 = Clock::now();
+        r->stats.wait_s += secs(t0, t1);
+        r->stats.issue_s += secs(t1, t4);
+        r->stats.copy_s += secs(t1, t2);
+        r->stats.fwd_bwd_s += secs(t2, t3);
+        r->stats.update_s += secs(t3, t4);
+        r->stats.max_step_s = std::max(r->stats.max_step_s, secs(t0, t4));
+    }
+    GS_API_END
+}
+
+int gs_runner_stats_get(const gs_runner* r, gs_runner_stats* out) {
+    GS_API_BEGIN
+    GS_REQUIRE(r && out, GS_EINVAL, "NULL argument");
+    *out = r->stats;
+    GS_API_END
+}
+
+void gs_runner_stats_reset(gs_runner* r) {
+    if (r) r->stats = gs_runner_stats{};
+}
+
+void gs_runner_destroy(gs_runner* r) { delete r; }
+
+}  // extern "C"

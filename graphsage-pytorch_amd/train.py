@@ -274,3 +274,78 @@ def init_distributed():
 
 def make_rng(seed, rank=0, stream=0):
     return RNG(rank_seed(seed, rank, stream))
+
+
+# ------------------------------------------------------------ native runner
+class Communicator:
+    """Native RCCL communicator for the runner's gradient all-reduce; the
+    128-byte id is created on rank 0 and broadcast over torch.distributed."""
+
+    def __init__(self, rank, world, device):
+        self.world = world
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            check(lib().gs_comm_unique_id(uid.numpy().ctypes.data))
+        t = uid.to(device)
+        dist.broadcast(t, 0)
+        uid = t.cpu().contiguous()
+        h = ctypes.c_void_p()
+        check(lib().gs_comm_create(uid.numpy().ctypes.data, world, rank, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            lib().gs_comm_destroy(self._h)
+        self._h = None
+
+
+class Runner:
+    """The training loop as one native pipeline (gs_runner): S sampler
+    threads, pinned pack rings, H2D copies on a copy stream and the fused
+    step, all without Python per step.  `batches`: iterable of equal-size
+    int64 root arrays consumed in order; `rngs`: one RNG per sampler stream
+    (stream w samples batches w, w+S, ...)."""
+
+    def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
+                 comm=None):
+        self.trainer, self.graph = trainer, graph
+        self.rngs = list(rngs)
+        self.batches = np.ascontiguousarray(np.stack([np.asarray(b, np.int64) for b in batches]))
+        self.fanouts = np.ascontiguousarray(fanouts, dtype=np.int32)
+        self._rng_ptrs = (ctypes.c_void_p * len(self.rngs))(*[r._h.value for r in self.rngs])
+        self.comm = comm
+        flags = (_lib.GS_SAMPLE_GCN if gcn else 0) | (4 if fail_empty else 0)
+        cfg = _lib.RunnerConfig(
+            graph=graph._h.value, trainer=trainer._h.value, batches=self.batches.ctypes.data,
+            n_batches=self.batches.shape[0], batch=self.batches.shape[1], fanouts=self.fanouts.ctypes.data,
+            n_hops=len(self.fanouts), flags=flags, n_streams=len(self.rngs),
+            rngs=ctypes.cast(self._rng_ptrs, ctypes.c_void_p), depth=depth,
+            comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1)
+        h = ctypes.c_void_p()
+        check(lib().gs_runner_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    def run(self, n_steps):
+        """Issue the next n_steps training steps (asynchronous on the device)."""
+        check(lib().gs_runner_run(self._h, int(n_steps), self.trainer.loss.data_ptr(),
+                                  _lib.stream_ptr(self.trainer.device)))
+        return self.trainer.loss
+
+    def stats(self, reset=False):
+        st = _lib.RunnerStats()
+        check(lib().gs_runner_stats_get(self._h, ctypes.byref(st)))
+        if reset:
+            lib().gs_runner_stats_reset(self._h)
+        sizes = np.array(st.hop_sizes[:], dtype=np.float64).reshape(_lib.GS_MAX_HOPS, 4)
+        return {"steps": st.steps, "wait_s": st.wait_s, "issue_s": st.issue_s, "sample_s": st.sample_s,
+                "copy_s": st.copy_s, "fwd_bwd_s": st.fwd_bwd_s, "update_s": st.update_s,
+                "max_step_s": st.max_step_s, "hop_sizes_sum": sizes}
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.gs_runner_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        self.close()

@@ -326,6 +326,63 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
  * launches; gs_trainer_agg_times synchronises and returns their durations (ms). */
 int gs_trainer_time_agg(gs_trainer* t, int64_t capacity);
 int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
+/* The flat gradient buffer (cfg.grads), gs_trainer_n_params floats. */
+float* gs_trainer_grads(const gs_trainer* t);
+
+/* ------------------------------------------------------- RCCL communicator
+ * One communicator per data-parallel rank for the gradient all-reduce of the
+ * native runner (utils.py:184-187 per rank, then an average over ranks).
+ * Rank 0 creates the id; the caller broadcasts its 128 bytes. */
+int gs_comm_unique_id(uint8_t id[128]);
+int gs_comm_create(const uint8_t id[128], int32_t n_ranks, int32_t rank, void** comm);
+void gs_comm_destroy(void* comm);
+/* In-place sum over ranks of n fp32 values on `stream`. */
+int gs_comm_allreduce_sum(void* comm, float* buf, int64_t n, void* stream);
+
+/* ------------------------------------------------------- pipeline runner
+ * The reference's epoch loop over batches (utils.py:144-191 called from
+ * main.py per epoch) as a native pipeline: S sampler threads (stream w owns
+ * batches w, w+S, ... and its own rng — S = 1 is the reference's single
+ * random stream) fill rings of pinned pack buffers with gs_sample_pack_run;
+ * gs_runner_run consumes the batches in order, issuing on `stream` the pack's
+ * H2D copy (two device buffers, reused in stream order), forward_backward,
+ * the optional all-reduce and the update.  Sampler threads make no HIP calls;
+ * the calling thread recycles a pinned slot once its copy event completes.
+ * The rngs, graph and trainer are borrowed and must outlive the runner;
+ * `batches` (n_batches x batch int64 ids) is copied. */
+typedef struct {
+    const gs_graph* graph;
+    gs_trainer* trainer;
+    const int64_t* batches;
+    int64_t n_batches, batch;
+    const int32_t* fanouts;
+    int32_t n_hops;
+    int32_t flags;          /* GS_SAMPLE_* */
+    int32_t n_streams;
+    gs_rng* const* rngs;    /* [n_streams] */
+    int32_t depth;          /* pinned slots per stream (>= 1) */
+    void* comm;             /* gs_comm_create handle or NULL */
+    int32_t world;          /* gradient scale 1/world after the all-reduce */
+} gs_runner_config;
+
+typedef struct {
+    int64_t steps;          /* steps issued since the last reset */
+    double wait_s;          /* host time blocked on a not-yet-sampled batch */
+    double issue_s;         /* host time issuing copies and launches */
+    double sample_s;        /* summed sampler-thread time of those batches */
+    double hop_sizes[4 * GS_MAX_HOPS]; /* summed (n_dst, n_pos, n_src, n_nbr) */
+    double copy_s, fwd_bwd_s, update_s; /* parts of issue_s */
+    double max_step_s;      /* longest single step (wait + issue) */
+} gs_runner_stats;
+
+typedef struct gs_runner gs_runner;
+int gs_runner_create(const gs_runner_config* cfg, gs_runner** out);
+/* Issue the next n_steps steps (GPU work asynchronous on `stream`); fails
+ * with the sampler's error (e.g. GS_EEMPTY) or GS_ERANGE past n_batches. */
+int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream);
+int gs_runner_stats_get(const gs_runner* r, gs_runner_stats* out);
+void gs_runner_stats_reset(gs_runner* r);
+void gs_runner_destroy(gs_runner* r);
 
 #ifdef __cplusplus
 }

@@ -217,3 +217,35 @@ def test_prefetcher_streams_each_bit_exact(gs):
             for name in names:
                 assert torch.equal(ds.field(hop, name), ds2.field(hop, name)), (i, hop, name)
         assert roots_dev.cpu().tolist() == roots.tolist()
+
+
+@pytest.mark.parametrize("S", [1, 3])
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_native_runner_matches_python_loop(gs, S, agg):
+    """gs_runner (native sampler threads + pinned ring + copy stream + fused
+    step) leaves exactly the parameters of the Python loop over the same
+    sampler streams (same kernels, same order: bitwise equal)."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:7]
+    a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
+    b = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
+    pf = train.Prefetcher(graph, None, batches, [25, 10], False, DEV,
+                          rngs=[train.make_rng(11, 0, w) for w in range(S)], fail_empty=agg == "MAX")
+    for _ in batches:
+        ds, roots_dev, _info = pf.next()
+        a.step(ds, roots_dev)
+    pf.close()
+    runner = train.Runner(b, graph, batches, [train.make_rng(11, 0, w) for w in range(S)], [25, 10],
+                          fail_empty=agg == "MAX", depth=2)
+    runner.run(3)
+    runner.run(len(batches) - 3)
+    torch.cuda.synchronize()
+    st = runner.stats()
+    assert st["steps"] == len(batches)
+    assert torch.equal(a.p.params, b.p.params)
+    assert float(a.loss) == float(b.loss)
+    with pytest.raises(IndexError):
+        runner.run(1)  # past the last batch
+    runner.close()
