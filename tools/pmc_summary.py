@@ -1,0 +1,49 @@
+"""Summarise two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into mean HBM
+bytes per dispatch per kernel.  gfx950 FETCH_SIZE counts half the bytes of
+16 B/lane coalesced reads (MI355X_MICROARCH.md, HBM section), so reads are
+reported doubled; WRITE_SIZE is exact for 16 B/lane stores."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def per_kernel(path, counter):
+    files = glob.glob(f"{path}/{counter}/**/*counter_collection.csv", recursive=True)
+    acc = collections.defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0]
+            acc[name].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+
+
+def main():
+    out_dir, config = sys.argv[1], sys.argv[2]
+    fetch = per_kernel(out_dir, "FETCH_SIZE")
+    write = per_kernel(out_dir, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, (0.0, 0))[0] * 1024.0  # rocprofv3 reports KiB
+        w = write.get(k, (0.0, 0))[0] * 1024.0
+        kernels[k] = {"fetch_bytes_raw": round(f), "read_bytes": round(2 * f), "write_bytes": round(w),
+                      "hbm_bytes": round(2 * f + w), "dispatches": fetch.get(k, write.get(k, (0, 0)))[1]}
+    agg = [k for k in kernels if "agg_fwd_kernel" in k and k.endswith("true>")]
+    bench = {}
+    for line in open(f"{out_dir}/bench_FETCH_SIZE.log"):
+        if line.startswith('{"metric"'):
+            bench = json.loads(line)
+    summary = {"config": config, "kernels": kernels,
+               "note": "read_bytes = 2 x FETCH_SIZE (gfx950 half-count of wide reads); bytes per dispatch"}
+    if agg:
+        summary["agg1_kernel"] = agg[0]
+        summary["agg1_hbm_bytes_per_launch"] = kernels[agg[0]]["hbm_bytes"]
+        summary["agg1_algo_bytes_per_launch"] = bench.get("roofline", {}).get("algo_bytes_per_launch")
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
