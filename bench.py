@@ -106,6 +106,16 @@ def cgroup_throttle():
     return None
 
 
+def layer1_fused_bytes(n_dst, n_pos, F, H, elem, gcn=False):
+    """Algorithmic HBM bytes of one fused layer-1 launch (gs_sage1_fwd,
+    DESIGN.md §4): per sampled edge the neighbour row + entry + col id; per
+    destination the self row (not in gcn), the aggregate row written back, the
+    fp32 output row and its pos_ptr / dst id; W once."""
+    K = F if gcn else 2 * F
+    per_dst = (0 if gcn else F * elem) + F * elem + H * 4 + 8
+    return n_pos * (F * elem + 8) + n_dst * per_dst + H * K * elem
+
+
 def agg1_bytes(n_dst, n_pos, F, elem):
     """Algorithmic HBM bytes of one layer-1 K-agg launch:
     neighbour feature rows once per sampled edge + sampled positions and CSR
@@ -147,15 +157,17 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
                       f"pair-list indexing {t_adj:.1f} s excluded"}
 
 
-def load_traffic(config_name):
-    """Per-launch HBM bytes of K-agg from a committed rocprofv3 --pmc summary."""
+def load_traffic(config_name, kernel):
+    """Per-launch HBM bytes of the timed layer-1 kernel from the newest
+    committed rocprofv3 --pmc summary for this config (profiles/*pmc*.json)."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("config") == config_name and "agg1_hbm_bytes_per_launch" in d:
+        if d.get("config") == config_name and kernel in d.get("layer1_kernel", "") and \
+                "layer1_hbm_bytes_per_launch" in d:
             best = d
     return best
 
@@ -229,15 +241,21 @@ def main():
     L = len(cfg["fanouts"])
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
     n_edges = float(sizes[:L, 1].sum()) * args.steps
-    agg_bytes = agg1_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem)
+    fused1 = bool(gs._lib.lib().gs_trainer_layer1_fused(trainer._h))
+    if fused1:
+        agg_bytes = layer1_fused_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], 128, elem)
+        kname = "sage1_fwd_kernel (layer-1 gather-mean + concat-linear-relu, fused)"
+    else:
+        agg_bytes = agg1_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem)
+        kname = "agg_fwd_kernel (layer-1 expand gather-mean)"
 
     if rank == 0:
         achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9
-        tr = load_traffic(args.config)
+        tr = load_traffic(args.config, kname.split(" ")[0])
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": (tr["agg1_hbm_bytes_per_launch"] if tr else None),
-                "kernel": "agg_fwd_kernel (layer-1 expand gather-mean)", "avg_launch_us": round(agg_ms * 1e3, 2),
+                "traffic": (tr["layer1_hbm_bytes_per_launch"] if tr else None),
+                "kernel": kname, "avg_launch_us": round(agg_ms * 1e3, 2),
                 "algo_bytes_per_launch": int(agg_bytes)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

@@ -87,6 +87,9 @@ _SIGS = {
                                         _i64, _vp]),
     "gs_agg_bwd": (_i32, [_i32, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp,
                           _vp]),
+    "gs_sage1_fwd_supported": (_i32, [_i32, _i64, _i64, _i32]),
+    "gs_sage1_fwd": (_i32, [_i32, _i32, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i32,
+                            _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
     "gs_cls_nll_ws_floats": (_i64, [_i64, _i64, _i64]),
     "gs_cls_nll_fwd_bwd": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
@@ -101,6 +104,7 @@ _SIGS = {
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_grads": (_vp, [_vp]),
+    "gs_trainer_layer1_fused": (_i32, [_vp]),
     "gs_comm_unique_id": (_i32, [_vp]),
     "gs_comm_create": (_i32, [_vp, _i32, _i32, _p(_vp)]),
     "gs_comm_destroy": (None, [_vp]),

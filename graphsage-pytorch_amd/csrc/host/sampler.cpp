@@ -34,6 +34,7 @@ struct Hop {
     bool materialised = false;
     std::vector<int64_t> dst_ids;
     std::vector<int32_t> pos_ptr, pos;
+    std::vector<int64_t> row_start;  // row_ptr[dst] per destination (absolute entries in the pack)
     std::vector<int64_t> src_ids;
     std::vector<int32_t> nbr_ptr, nbr, self_local;
     std::vector<int32_t> set_ptr;
@@ -54,6 +55,7 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
     h.pos_ptr.assign(n + 1, 0);
     thread_local std::vector<int64_t> deg;
     deg.resize(n);
+    h.row_start.resize(n);
     int64_t total = 0;
     const int64_t* rp = g.row_ptr.data();
     constexpr int64_t kAhead = 16;  // frontier ids are known: prefetch their row_ptr
@@ -63,6 +65,7 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
         const int64_t v = h.dst_ids[r];
         const int64_t d = rp[v + 1] - rp[v];
         deg[r] = d;
+        h.row_start[r] = rp[v];
         total += (h.k > 0 && d >= h.k) ? h.k : d;
         GS_REQUIRE(total < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
         h.pos_ptr[r + 1] = static_cast<int32_t>(total);
@@ -205,6 +208,7 @@ static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, in
                           const int32_t* fanouts, int32_t n_hops, int32_t flags) {
     GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
     GS_REQUIRE(n_roots >= 1 && roots, GS_EINVAL, "empty nodes_batch");
+    GS_REQUIRE(g.n_entries < (int64_t(1) << 31), GS_ERANGE, "graph has >= 2^31 CSR entries (int32 pack entries)");
     for (int64_t i = 0; i < n_roots; ++i)
         GS_REQUIRE(roots[i] >= 0 && roots[i] < g.n_nodes, GS_ERANGE, "node id out of range");
     std::unique_ptr<Sample> s(new Sample());
@@ -463,7 +467,14 @@ int gs_sample_pack(const gs_sample* sp, int32_t* buf, int64_t cap) {
         const Hop& h = s.hops[j];
         if (j == s.n_hops - 1) {
             cpy(j, GS_PK_POS_PTR, h.pos_ptr.data(), h.pos_ptr.size());
-            cpy(j, GS_PK_POS, h.pos.data(), h.pos.size());
+            // absolute CSR entries row_ptr[dst] + position: the device gather
+            // then reads col[] without first looking up row_ptr[dst]
+            int32_t* e = buf + L.off[j][GS_PK_POS];
+            const int64_t nd = static_cast<int64_t>(h.dst_ids.size());
+            for (int64_t r = 0; r < nd; ++r) {
+                const int64_t rs = h.row_start[r];
+                for (int32_t t = h.pos_ptr[r]; t < h.pos_ptr[r + 1]; ++t) e[t] = static_cast<int32_t>(rs + h.pos[t]);
+            }
             int32_t* d = buf + L.off[j][GS_PK_DST_IDS];
             for (size_t r = 0; r < h.dst_ids.size(); ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
         } else {

@@ -10,13 +10,28 @@
 namespace gs {
 
 constexpr int kBlock = 256;
-constexpr int kUnroll = 4;  // neighbour rows in flight per lane group
+constexpr int kRows = 16;  // neighbour rows in flight per lane group (8 for 8-element bf16 vectors)
+
+// Lanes [lo, lo + G) of the wave's ballot.
+template <int G>
+__device__ __forceinline__ uint64_t group_bits(bool p) {
+    const uint64_t m = __ballot(p);
+    if constexpr (G == 64) return m;
+    const int lo = (threadIdx.x & 63) & ~(G - 1);
+    return (m >> lo) & ((uint64_t(1) << G) - 1);
+}
 
 // One group of G lanes per destination r.  EXPAND: the neighbourhood is the
 // sampled positions idx[ptr[r]..ptr[r+1]) of node dst_ids[r]'s CSR row,
-// expanded on the fly (col[row_ptr[node] + pos]); self is skipped unless gcn,
+// expanded on the fly (col[row_ptr[node] + pos], or col[idx] when row_ptr is
+// NULL and idx already holds absolute entries, as in the packed sample);
+// self is skipped unless gcn,
 // and gcn adds it once (models.py:285, :297-298).  Otherwise idx holds the
 // source rows of X directly (already self-filtered and ascending).
+//
+// Every load is unconditional: slots past the neighbourhood re-read the
+// chunk's first row (already in flight) and are masked when accumulated, so a
+// group keeps all kRows rows of a chunk in flight instead of waiting on each.
 template <int OP, typename T, int VEC, int G, bool EXPAND>
 __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
     const T* __restrict__ X, int64_t ldx, int F, int n_dst, const int* __restrict__ ptr,
@@ -31,11 +46,15 @@ __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
     int64_t rs = 0;
     if (EXPAND) {
         node = dst_ids[r];
-        rs = row_ptr[node];
+        if (row_ptr) rs = row_ptr[node];
     }
+    constexpr int NR = VEC > 4 ? kRows / 2 : kRows;
     const bool want_am = (OP == GS_AGG_MAX) && (argmax != nullptr);
-    for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
+    const int nf = (F + G * VEC - 1) / (G * VEC);
+    for (int fi = 0; fi < nf; ++fi) {
+        const int f0 = fi * G * VEC + gl * VEC;
         const bool act = f0 < F;
+        const int f0c = act ? f0 : 0;
         float acc[VEC];
         int am[VEC];
 #pragma unroll
@@ -44,60 +63,56 @@ __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
             am[v] = -1;
         }
         int cnt = 0;
+        bool self_seen = false;
         for (int base = beg; base < end; base += G) {
             const int m = min(G, end - base);
-            int my = -1;
-            if (gl < m) {
-                const int e = idx[base + gl];
-                if (EXPAND) {
-                    const int nb = col[rs + e];
-                    my = (gcn || nb != node) ? nb : -1;
-                } else {
-                    my = e;
-                }
+            const bool mine = gl < m;
+            const int e = idx[mine ? base + gl : base];
+            int my;
+            if (EXPAND) {
+                const int nb = col[rs + e];
+                self_seen |= group_bits<G>(mine && nb == node) != 0;
+                my = (mine && (gcn || nb != node)) ? nb : -1;
+            } else {
+                my = mine ? e : -1;
             }
-            for (int j = 0; j < m; j += kUnroll) {
-                int rows[kUnroll];
-                float x[kUnroll][VEC];
+            for (int j = 0; j < m; j += NR) {
+                int rows[NR];
+                bool ok[NR];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    rows[u] = __shfl(my, j + u < m ? j + u : 0, G);
-                    if (j + u >= m) rows[u] = -1;
+                for (int u = 0; u < NR; ++u) {
+                    rows[u] = __shfl(my, j + u < m ? j + u : j, G);
+                    ok[u] = (j + u < m) && rows[u] >= 0;
                 }
+                const int fallback = rows[0] >= 0 ? rows[0] : (EXPAND ? node : 0);
+                float x[NR][VEC];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u)
-                    if (rows[u] >= 0 && act) RowIO<T, VEC>::load(X + static_cast<int64_t>(rows[u]) * ldx + f0, x[u]);
+                for (int u = 0; u < NR; ++u)
+                    RowIO<T, VEC>::load(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0c, x[u]);
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    if (rows[u] < 0) continue;
-                    ++cnt;
-                    if (!act) continue;
+                for (int u = 0; u < NR; ++u) {
+                    cnt += ok[u];
 #pragma unroll
                     for (int v = 0; v < VEC; ++v) {
                         if (OP == GS_AGG_MEAN) {
-                            acc[v] += x[u][v];
-                        } else if (x[u][v] > acc[v]) {  // strict: first index wins ties
-                            acc[v] = x[u][v];
-                            am[v] = rows[u];
+                            acc[v] += ok[u] ? x[u][v] : 0.f;
+                        } else {
+                            const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
+                            acc[v] = take ? x[u][v] : acc[v];
+                            am[v] = take ? rows[u] : am[v];
                         }
                     }
                 }
             }
         }
-        if (EXPAND && gcn) {
-            bool self_seen = false;  // gcn keeps self exactly once (set semantics)
-            for (int e = beg; e < end; ++e) self_seen |= (col[rs + idx[e]] == node);
-            if (!self_seen) {
-                ++cnt;
-                if (act) {
-                    float x[VEC];
-                    RowIO<T, VEC>::load(X + static_cast<int64_t>(node) * ldx + f0, x);
+        if (EXPAND && gcn && !self_seen) {  // gcn keeps self exactly once (set semantics)
+            ++cnt;
+            float x[VEC];
+            RowIO<T, VEC>::load(X + static_cast<int64_t>(node) * ldx + f0c, x);
 #pragma unroll
-                    for (int v = 0; v < VEC; ++v) {
-                        if (OP == GS_AGG_MEAN) acc[v] += x[v];
-                        else if (x[v] > acc[v]) { acc[v] = x[v]; am[v] = node; }
-                    }
-                }
+            for (int v = 0; v < VEC; ++v) {
+                if (OP == GS_AGG_MEAN) acc[v] += x[v];
+                else if (x[v] > acc[v]) { acc[v] = x[v]; am[v] = node; }
             }
         }
         if (!act) continue;
@@ -230,8 +245,8 @@ int gs_agg_fwd(gs_agg op, gs_dtype xdt, const void* X, int64_t ldx, int64_t F, i
     GS_REQUIRE(ldx >= F && ldo >= F, GS_EINVAL, "leading dimension smaller than F");
     if (n_dst == 0) return GS_OK;
     GS_REQUIRE(X && ptr && idx && out, GS_EINVAL, "NULL device pointer");
-    const bool expand = row_ptr != nullptr;
-    GS_REQUIRE(!expand || (col && dst_ids), GS_EINVAL, "expand mode needs col and dst_ids");
+    const bool expand = col != nullptr;
+    GS_REQUIRE(!expand || dst_ids, GS_EINVAL, "expand mode needs dst_ids");
     GS_REQUIRE(!(argmax && expand), GS_EINVAL, "argmax is only produced in explicit mode");
     const int V = xdt == GS_F32 ? 4 : 8;
     const int vec = (F % V == 0 && ldx % V == 0 && ldo % V == 0 && aligned16(X) && aligned16(out)) ? V : 1;

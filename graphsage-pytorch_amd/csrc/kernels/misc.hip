@@ -95,18 +95,33 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
     const float invB = 1.0f / static_cast<float>(B);
     // every global read is issued before the first barrier: the label chain
     // (roots -> labels) and the bias overlap the E / Wc tile loads
-    int y_w = 0;
-    if (w < nr) y_w = labels[roots ? roots[r0 + w] : r0 + w];
+    // (addresses clamped, values selected afterwards: no load sits behind a
+    // branch, so they all overlap instead of each waiting for the previous)
+    const int wr_ = min(w, nr - 1);
+    const int y_w = labels[roots ? roots[r0 + wr_] : r0 + wr_];
     const float b_lane = bc[min(cl, C - 1)];
-    for (int t = threadIdx.x; t < R * D; t += kClsThreads) {
-        const int ii = t / D;
-        sE[t] = ii < nr ? E[static_cast<int64_t>(r0) * D + t] : 0.f;
-    }
-    if (wc_lds)
-        for (int t = threadIdx.x; t < C * D; t += kClsThreads) {
-            const int c = t / D;
-            sW[t + c] = Wc[t];
+    const int nE = nr * D, nW = wc_lds ? C * D : 0;
+    const int tid = static_cast<int>(threadIdx.x);
+    for (int t0 = 0; t0 < R * D; t0 += 4 * kClsThreads) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = E[static_cast<int64_t>(r0) * D + min(t0 + q * kClsThreads + tid, nE - 1)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = t0 + q * kClsThreads + tid;
+            if (t < R * D) sE[t] = t < nE ? v[q] : 0.f;
         }
+    }
+    for (int t0 = 0; t0 < nW; t0 += 4 * kClsThreads) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = Wc[min(t0 + q * kClsThreads + tid, nW - 1)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = t0 + q * kClsThreads + tid;
+            if (t < nW) sW[t + t / D] = v[q];
+        }
+    }
     __syncthreads();
     const float* W = wc_lds ? sW : Wc;
     const int wp = wc_lds ? D + 1 : D;  // row pitch of W

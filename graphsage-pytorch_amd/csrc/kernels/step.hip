@@ -5,6 +5,7 @@
 // The Python host makes two calls per step (forward_backward, update) and
 // puts the RCCL gradient all-reduce between them.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "kcommon.hpp"
@@ -14,6 +15,7 @@ struct gs_trainer {
     std::vector<int64_t> w_off;  // element offset of each parameter in the flat buffer
     std::vector<int64_t> w_rows, w_cols;
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
+    bool fused1 = false;  // layer 1 through gs_sage1_fwd (gather + linear in one launch)
     // optional HIP-event timing of the layer-1 gather-aggregate (bench roofline)
     std::vector<hipEvent_t> ev0, ev1;
     int64_t n_timed = 0;
@@ -101,16 +103,24 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     if (lowp) ok(gs_cast_f32_bf16(P + T.w_off[0], w1lp, T.w_rows[0] * T.w_cols[0], st));
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
     const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
+    const void* W1 = lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]);
     if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
-    ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, rows[0],
-                  fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.row_ptr, c.col, dst_L, c.gcn, agg[0],
-                  static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    if (T.fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
+        ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
+                        rows[0], fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.col, dst_L, c.gcn, W1, agg[0], F, h[0],
+                        H, 1, st));
+    } else {
+        ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, rows[0],
+                      fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), nullptr, c.col, dst_L, c.gcn, agg[0],
+                      static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    }
     if (timed) {
         GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
         ++T.n_timed;
     }
-    ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
-                          dst_L, agg[0], F, lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]), h[0], H, 1, st));
+    if (!T.fused1)
+        ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
+                              dst_L, agg[0], F, W1, h[0], H, 1, st));
     for (int l = 2; l <= L; ++l) {
         const int j = L - l + 1;
         ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), GS_F32, h[l - 2], H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
@@ -160,7 +170,7 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
     GS_REQUIRE(cfg->n_layers >= 1 && cfg->n_layers <= GS_MAX_HOPS, GS_EINVAL, "n_layers out of range");
     GS_REQUIRE(cfg->hidden >= 16 && cfg->hidden <= 256 && cfg->hidden % 16 == 0, GS_EINVAL, "bad hidden size");
     GS_REQUIRE(cfg->n_classes >= 1 && cfg->feat_dim >= 1 && cfg->feat_ld >= cfg->feat_dim, GS_EINVAL, "bad dims");
-    GS_REQUIRE(cfg->X && cfg->row_ptr && cfg->col && cfg->labels && cfg->params && cfg->grads, GS_EINVAL,
+    GS_REQUIRE(cfg->X && cfg->col && cfg->labels && cfg->params && cfg->grads, GS_EINVAL,
                "NULL device pointer");
     auto* T = new gs_trainer();
     T->cfg = *cfg;
@@ -177,6 +187,10 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
     T->cls_b_off = at;
     at += cfg->n_classes;
     T->total = at;
+    T->fused1 = gs_sage1_fwd_supported(static_cast<gs_dtype>(cfg->feat_dtype), cfg->feat_dim, cfg->hidden,
+                                       cfg->gcn) != 0 &&
+                cfg->feat_ld % (cfg->feat_dtype == GS_F32 ? 4 : 8) == 0 && gs::aligned16(cfg->X) &&
+                std::getenv("GS_FUSED1") != nullptr;  // opt-in: measured slower than agg + linear
     *out = T;
     GS_API_END
 }
@@ -186,6 +200,8 @@ void gs_trainer_destroy(gs_trainer* t) { delete t; }
 int64_t gs_trainer_n_params(const gs_trainer* t) { return t ? t->total : -1; }
 
 float* gs_trainer_grads(const gs_trainer* t) { return t ? t->cfg.grads : nullptr; }
+
+int32_t gs_trainer_layer1_fused(const gs_trainer* t) { return t && t->fused1 ? 1 : 0; }
 
 int64_t gs_trainer_ws_bytes(gs_trainer* t, const int64_t* hop_sizes) {
     try {

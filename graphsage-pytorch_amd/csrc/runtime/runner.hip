@@ -5,9 +5,11 @@
 //
 //   sampler thread w : batches w, w+S, ... in order, each into a free pinned
 //                      slot of its ring (gs_sample_pack_run, its own rng)
-//   gs_runner_run    : batch i from stream i % S, in order: H2D copy into
-//                      device pack buffer i % 2, forward/backward, all-reduce
-//                      (world > 1) and update, all on the caller's stream.
+//   gs_runner_run    : batch i from stream i % S, in order: H2D copy on a
+//                      dedicated copy stream into device pack buffer i % 3,
+//                      then forward/backward, all-reduce (world > 1) and
+//                      update on the caller's stream (which waits, GPU-side,
+//                      for the copy).
 // A pinned slot returns to its sampler once the copy that read it has
 // completed.  Only the driver thread makes HIP calls: it polls the copy events
 // of consumed slots (hipEventQuery) and hands finished slots back, and waits
@@ -38,6 +40,17 @@ static double secs(Clock::time_point a, Clock::time_point b) {
 
 static void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Device-side pull of a pinned host pack (hipHostMalloc memory is mapped into
+// the device address space): the host pays one kernel launch instead of
+// hipMemcpyAsync's host-side cost (measured ~50 us per 0.3 MB pack).
+__global__ __launch_bounds__(256) void pull_pack_kernel(const int4* __restrict__ src, int4* __restrict__ dst,
+                                                        int64_t n16, const int32_t* __restrict__ src_tail,
+                                                        int32_t* __restrict__ dst_tail, int n_tail) {
+    const int64_t i = blockIdx.x * int64_t(256) + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+    if (i < n_tail) dst_tail[i] = src_tail[i];
 }
 
 struct PackSlot {
@@ -73,7 +86,11 @@ struct gs_runner {
     std::vector<std::unique_ptr<gs::SamplerStream>> streams;
     bool stop = false;
     int64_t next_batch = 0;
-    int32_t* dev[2] = {nullptr, nullptr};  // device packs, alternating (stream-ordered reuse)
+    static constexpr int kDev = 3;         // device pack ring
+    int32_t* dev[kDev] = {};
+    hipEvent_t dev_done[kDev] = {};        // recorded after the step that read dev[k]
+    bool dev_busy[kDev] = {};
+    hipStream_t copy_stream = nullptr;     // H2D only; never waits on anything
     void* ws = nullptr;
     int64_t ws_bytes = 0;
     float* clip_ws = nullptr;
@@ -149,8 +166,13 @@ gs_runner::~gs_runner() {
             if (slot.copied) (void)hipEventDestroy(slot.copied);
             if (slot.host) (void)hipHostFree(slot.host);
         }
-    for (int d = 0; d < 2; ++d)
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    for (int d = 0; d < kDev; ++d) {
+        if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
+        if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
         if (dev[d]) (void)hipFree(dev[d]);
+    }
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (ws) (void)hipFree(ws);
     if (clip_ws) (void)hipFree(clip_ws);
 }
@@ -215,7 +237,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(bound > 0, GS_EINVAL, "pack bound failed");
     r->cap = bound + cfg->batch;
     hip_ok(hipGetDevice(&r->device), "hipGetDevice");
-    for (int d = 0; d < 2; ++d) {
+    hip_ok(hipStreamCreateWithFlags(&r->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
+    for (int d = 0; d < gs_runner::kDev; ++d) {
+        hip_ok(hipEventCreateWithFlags(&r->dev_done[d], hipEventDisableTiming), "hipEventCreate");
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     }
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
@@ -274,14 +298,23 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         const auto t1 = Clock::now();
         GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
         if (slot.status != GS_OK) fail(slot.status, slot.error);
-        // H2D on the step's own stream: a separate copy stream waiting on the
-        // step that last read the buffer made hipMemcpyAsync block the host
-        // (measured 0.2-0.35 ms per step), far more than the ~10 us of copy
-        // it could hide.
-        const int d = static_cast<int>(b & 1);
-        hip_ok(hipMemcpyAsync(r->dev[d], slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, st),
-               "hipMemcpyAsync(pack)");
-        hip_ok(hipEventRecord(slot.copied, st), "hipEventRecord");
+        // H2D (device pull) on a stream that never waits: device buffer d is reused only
+        // once the host has seen the step that last read it complete (three
+        // steps back, normally long done).  A copy queued behind GPU work
+        // (same stream, or a copy stream waiting on an event) made
+        // hipMemcpyAsync block the host until that work drained.
+        const int d = static_cast<int>(b % gs_runner::kDev);
+        if (r->dev_busy[d]) hip_ok(hipEventSynchronize(r->dev_done[d]), "hipEventSynchronize");
+        {
+            const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
+            const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
+            pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, r->copy_stream>>>(
+                reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(r->dev[d]), n16,
+                slot.host + 4 * n16, r->dev[d] + 4 * n16, static_cast<int>(tail));
+            hip_ok(hipGetLastError(), "pull_pack_kernel");
+        }
+        hip_ok(hipEventRecord(slot.copied, r->copy_stream), "hipEventRecord");
+        hip_ok(hipStreamWaitEvent(st, slot.copied, 0), "hipStreamWaitEvent");
         const auto t2 = Clock::now();
         const int64_t need = gs_trainer_ws_bytes(r->cfg.trainer, slot.hop_sizes);
         GS_REQUIRE(need >= 0, GS_EINVAL, gs_last_error());
@@ -303,6 +336,8 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         rc = gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st);
         if (rc != GS_OK) fail(rc, gs_last_error());
+        hip_ok(hipEventRecord(r->dev_done[d], st), "hipEventRecord");
+        r->dev_busy[d] = true;
         for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);
         r->stats.sample_s += slot.sample_s;
         s.copying.push_back(slot_id);

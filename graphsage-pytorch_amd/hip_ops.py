@@ -70,6 +70,26 @@ def sage_linear_fwd(A, Wd, out, *, Xs=None, sidx=None, relu=True):
     return out
 
 
+def sage1_supported(dtype, F, H, gcn):
+    return bool(lib().gs_sage1_fwd_supported(_DT[dtype], F, H, int(bool(gcn))))
+
+
+def sage1_fwd(agg_func, X, ptr_, ent, col, dst_ids, W, agg_out, out, *, gcn=False, relu=True):
+    """Fused layer 1 (gs_sage1_fwd): gather-aggregate over absolute CSR
+    entries + relu([X[dst] | agg] · Wᵀ); fills agg_out and out."""
+    _dev(X, ptr_, ent, col, dst_ids, W, agg_out, out)
+    n_dst = ptr_.numel() - 1
+    F = X.shape[1]
+    H = W.shape[0]
+    if W.dtype != X.dtype or agg_out.dtype != X.dtype or out.dtype != torch.float32:
+        raise TypeError("W / agg_out must share X's dtype; out is fp32")
+    check(lib().gs_sage1_fwd(agg_op(agg_func), _DT[X.dtype], ptr(X), X.stride(0), F, H, n_dst, ptr(_i32(ptr_)),
+                             ptr(_i32(ent)), ptr(_i32(col)), ptr(_i32(dst_ids)), int(bool(gcn)), ptr(W),
+                             ptr(agg_out), agg_out.stride(0), ptr(out), out.stride(0), int(bool(relu)),
+                             _stream(X)))
+    return out
+
+
 def linear_dw_workspace(n, K, H, device):
     nbytes = int(lib().gs_sage_linear_bwd_weight_ws(n, K, H))
     return torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device), nbytes

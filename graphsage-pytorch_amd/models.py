@@ -75,11 +75,17 @@ def sage_forward(ds, X, weights, agg_func, gcn, row_ptr, col, weights_lowp=None)
     n_dst = ds.sizes[L - 1][0]
     dst = ds.field(L, "dst_ids")
     a1 = torch.empty(n_dst, X.shape[1], dtype=X.dtype, device=X.device)
-    ops.agg_fwd(agg_func, X, ds.field(L, "pos_ptr"), ds.field(L, "pos"), a1,
-                row_ptr=row_ptr, col=col, dst_ids=dst, gcn=gcn)
     W1 = weights_lowp[0] if weights_lowp is not None else weights[0]
     h = torch.empty(n_dst, weights[0].shape[0], dtype=torch.float32, device=X.device)
-    ops.sage_linear_fwd(a1, W1, h, Xs=None if gcn else X, sidx=dst)
+    W1c = W1.detach().contiguous()
+    if (ops.sage1_supported(X.dtype, X.shape[1], W1c.shape[0], gcn) and X.stride(1) == 1
+            and X.stride(0) % (16 // X.element_size()) == 0 and X.data_ptr() % 16 == 0):
+        # gather + concat-linear in one launch; the pack holds absolute CSR entries
+        ops.sage1_fwd(agg_func, X, ds.field(L, "pos_ptr"), ds.field(L, "pos"), col, dst, W1c, a1, h, gcn=gcn)
+    else:
+        ops.agg_fwd(agg_func, X, ds.field(L, "pos_ptr"), ds.field(L, "pos"), a1,
+                    row_ptr=None, col=col, dst_ids=dst, gcn=gcn)
+        ops.sage_linear_fwd(a1, W1, h, Xs=None if gcn else X, sidx=dst)
     hs.append(h)
     aggs.append(a1)
     ams.append(None)

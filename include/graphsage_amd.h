@@ -141,7 +141,9 @@ typedef struct {
 /* Device pack: everything the kernels read for one batch, one int32 buffer. */
 enum {
     GS_PK_POS_PTR = 0, /* last hop: [n_dst+1]                                 */
-    GS_PK_POS,         /* last hop: [n_pos]                                   */
+    GS_PK_POS,         /* last hop: [n_pos] absolute CSR entries
+                          row_ptr[dst] + position (the hop view's pos + row
+                          start), so the device gather skips row_ptr      */
     GS_PK_DST_IDS,     /* last hop: [n_dst] global ids of F(L-1)              */
     GS_PK_NBR_PTR,     /* hops < L: [n_dst+1]                                 */
     GS_PK_NBR,         /* hops < L: [n_nbr]                                   */
@@ -196,10 +198,11 @@ int gs_uniform_host(uint64_t seed, int64_t row0, int64_t F, int64_t n_rows,
 
 /* GraphSage.aggregate (models.py:291-330): mean (mask/rowsum @ X, :311-314)
  * or element-wise max (:316-326) of source rows per destination.
- *   explicit mode (row_ptr == NULL): sources of dst r are rows idx[ptr[r]..ptr[r+1]).
- *   expand mode (row_ptr != NULL): node = dst_ids[r]; sources are
- *     col[row_ptr[node] + idx[e]], minus node itself unless gcn; gcn adds node
- *     once (models.py:285, :297-298).
+ *   explicit mode (col == NULL): sources of dst r are rows idx[ptr[r]..ptr[r+1]).
+ *   expand mode (col != NULL): node = dst_ids[r]; sources are
+ *     col[row_ptr[node] + idx[e]] (positions), or col[idx[e]] when row_ptr is
+ *     NULL (absolute CSR entries, as gs_sample_pack writes them), minus node
+ *     itself unless gcn; gcn adds node once (models.py:285, :297-298).
  * MEAN of an empty neighbourhood is NaN like the reference (0/0); MAX of one
  * is reported as GS_EEMPTY by the host before launch.  argmax (MAX, optional)
  * receives the winning source row per element, first index on ties. */
@@ -254,6 +257,21 @@ int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr,
                const int32_t* argmax, const float* Hprev, int64_t ldh,
                float* dH, void* stream);
 
+/* Layer 1 of GraphSage.forward (models.py:255-260) fused: the expand-mode
+ * gather-aggregate of gs_agg_fwd (absolute CSR entries `ent`, self dropped
+ * unless gcn) feeding gs_sage_linear_fwd's relu([X[dst] | agg] · Wᵀ) through
+ * LDS, in one launch.  Writes the aggregate rows to agg_out (dtype dt, kept
+ * for the weight gradient) and out[n_dst, H] (fp32).  Results equal the
+ * two-kernel path bitwise.  gs_sage1_fwd_supported: 1 when the 16-row A tile
+ * fits 64 KiB of LDS (F <= 512 fp32 / 1024 bf16 with self) and F is a
+ * multiple of the 16-byte vector. */
+int gs_sage1_fwd_supported(gs_dtype dt, int64_t F, int64_t H, int32_t gcn);
+int gs_sage1_fwd(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F,
+                 int64_t H, int64_t n_dst, const int32_t* ptr, const int32_t* ent,
+                 const int32_t* col, const int32_t* dst_ids, int32_t gcn,
+                 const void* W, void* agg_out, int64_t ld_agg, float* out,
+                 int64_t ldo, int32_t relu, void* stream);
+
 /* Classification (models.py:8-27) + NLL mean (utils.py:159-164), fused
  * forward + backward: logits = E·Wcᵀ + bc, logp = log_softmax (max-shifted),
  * loss = -Σ_i logp[i, y_i] / B with y_i = labels[roots[i]] (labels[i] when
@@ -297,7 +315,7 @@ typedef struct {
     int32_t feat_dtype; /* gs_dtype of X */
     int64_t feat_dim, feat_ld;
     const void* X;          /* [N, feat_ld] raw features                 */
-    const int64_t* row_ptr; /* device CSR (gs_graph_row_ptr mirrored)    */
+    const int64_t* row_ptr; /* device CSR (optional: packs carry absolute entries) */
     const int32_t* col;
     const int32_t* labels;  /* [N] class ids                             */
     float* params;          /* flat, gs_trainer_n_params floats          */
@@ -321,13 +339,16 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
                                 int64_t ws_bytes, float* loss, void* stream);
 /* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
-/* Measurement only (not on the graph-capturable path): record HIP events on
- * the launch stream around the next `capacity` layer-1 gather-aggregate
- * launches; gs_trainer_agg_times synchronises and returns their durations (ms). */
+/* Measurement only: record HIP events on the launch stream around the next
+ * `capacity` layer-1 launches — the fused gather + linear kernel when
+ * gs_trainer_layer1_fused(t), else the gather-aggregate; gs_trainer_agg_times
+ * synchronises and returns their durations (ms). */
 int gs_trainer_time_agg(gs_trainer* t, int64_t capacity);
 int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 /* The flat gradient buffer (cfg.grads), gs_trainer_n_params floats. */
 float* gs_trainer_grads(const gs_trainer* t);
+/* 1 when layer 1 runs through gs_sage1_fwd (opt-in: GS_FUSED1 set at create). */
+int32_t gs_trainer_layer1_fused(const gs_trainer* t);
 
 /* ------------------------------------------------------- RCCL communicator
  * One communicator per data-parallel rank for the gradient all-reduce of the

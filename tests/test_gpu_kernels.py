@@ -55,9 +55,20 @@ def test_agg_fwd_expand(gs, F, agg, dtype, gcn):
     rp, cl = graph.device_csr(DEV)
     n_dst = s.sizes(2)[0]
     out = torch.empty(n_dst, F, dtype=dtype, device=DEV)
-    ops.agg_fwd(agg, X, ds.field(2, "pos_ptr"), ds.field(2, "pos"), out, row_ptr=rp, col=cl,
-                dst_ids=ds.field(2, "dst_ids"), gcn=gcn)
+    ops.agg_fwd(agg, X, ds.field(2, "pos_ptr"), ds.field(2, "pos"), out, row_ptr=None, col=cl,
+                dst_ids=ds.field(2, "dst_ids"), gcn=gcn)  # pack: absolute entries
     ref = _expand_ref(graph, s, 2, X, agg, gcn)
+    got = out.float().cpu()
+    if dtype == torch.float32:
+        torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-5, equal_nan=True)
+    else:
+        torch.testing.assert_close(got, ref.to(torch.bfloat16).float(), atol=2e-2, rtol=1e-2, equal_nan=True)
+    # relative positions through row_ptr (hop view layout)
+    h = s.hop(2)
+    pos_rel = torch.from_numpy(h.pos.astype(np.int32)).to(DEV)
+    out.zero_()
+    ops.agg_fwd(agg, X, ds.field(2, "pos_ptr"), pos_rel, out, row_ptr=rp, col=cl,
+                dst_ids=ds.field(2, "dst_ids"), gcn=gcn)
     got = out.float().cpu()
     if dtype == torch.float32:
         torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-5, equal_nan=True)
@@ -211,3 +222,36 @@ def test_fill_uniform_matches_host_hash():
     Xb = torch.empty(1000, 77, dtype=torch.bfloat16, device=DEV)
     ops.fill_uniform(Xb, 824)
     assert torch.equal(Xb.cpu(), X.cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("F,H", [(256, 128), (128, 64), (64, 256), (512, 128), (40, 16)])
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("gcn", [False, True])
+def test_sage1_fused_equals_two_kernel_path(gs, F, H, agg, dtype, gcn):
+    """gs_sage1_fwd == gs_agg_fwd (expand) + gs_sage_linear_fwd, bitwise."""
+    if not ops.sage1_supported(dtype, F, H, gcn):
+        pytest.skip("shape outside the fused kernel's LDS tile")
+    graph = _rand_graph(gs, 700, 9000, F)
+    X = torch.randn(700, F, device=DEV).to(dtype)
+    roots = np.nonzero(graph.degrees())[0][:120]
+    s = gs.sample(graph, gs.RNG(F + H), roots, [25, 70], gcn=gcn)  # > 64 entries per dst reach the slow path
+    if agg == "MAX" and s.n_empty(2):
+        pytest.skip("empty neighbourhood (MAX raises in the model layer)")
+    models = importlib.import_module("graphsage-pytorch_amd.models")
+    ds = models.DeviceSample(s, DEV)
+    _, cl = graph.device_csr(DEV)
+    n_dst = s.sizes(2)[0]
+    K = F if gcn else 2 * F
+    W = (torch.randn(H, K, device=DEV) * 0.05).to(dtype)
+    ptr_, ent, dst = ds.field(2, "pos_ptr"), ds.field(2, "pos"), ds.field(2, "dst_ids")
+    a_ref = torch.empty(n_dst, F, dtype=dtype, device=DEV)
+    ops.agg_fwd(agg, X, ptr_, ent, a_ref, row_ptr=None, col=cl, dst_ids=dst, gcn=gcn)
+    h_ref = torch.empty(n_dst, H, device=DEV)
+    ops.sage_linear_fwd(a_ref, W, h_ref, Xs=None if gcn else X, sidx=dst)
+    a = torch.empty_like(a_ref)
+    h = torch.empty_like(h_ref)
+    ops.sage1_fwd(agg, X, ptr_, ent, cl, dst, W, a, h, gcn=gcn)
+    assert torch.equal(a.view(torch.int16) if dtype == torch.bfloat16 else a,
+                       a_ref.view(torch.int16) if dtype == torch.bfloat16 else a_ref)
+    assert torch.equal(h, h_ref)

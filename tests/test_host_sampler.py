@@ -163,7 +163,8 @@ def test_sample_pack_layout(gs):
     b = buf.numpy()
     assert np.array_equal(b[off[0][gs._lib.GS_PK_NBR_PTR]:][:h1.n_dst + 1], h1.nbr_ptr)
     assert np.array_equal(b[off[0][gs._lib.GS_PK_NBR]:][:h1.n_nbr], h1.nbr)
-    assert np.array_equal(b[off[1][gs._lib.GS_PK_POS]:][:h2.n_pos], h2.pos)
+    rs = G_.row_ptr()[h2.dst_ids]  # the pack holds absolute entries row_ptr[dst] + pos
+    assert np.array_equal(b[off[1][gs._lib.GS_PK_POS]:][:h2.n_pos], np.repeat(rs, np.diff(h2.pos_ptr)) + h2.pos)
     assert np.array_equal(b[off[1][gs._lib.GS_PK_DST_IDS]:][:h2.n_dst], h1.src_ids)
     tp = b[off[0][gs._lib.GS_PK_TPTR]:][:h1.n_src + 1]
     ti = b[off[0][gs._lib.GS_PK_TIDX]:][:h1.n_nbr + h1.n_dst]

@@ -31,7 +31,8 @@ def main():
         w = write.get(k, (0.0, 0))[0] * 1024.0
         kernels[k] = {"fetch_bytes_raw": round(f), "read_bytes": round(2 * f), "write_bytes": round(w),
                       "hbm_bytes": round(2 * f + w), "dispatches": fetch.get(k, write.get(k, (0, 0)))[1]}
-    agg = [k for k in kernels if "agg_fwd_kernel" in k and k.endswith("true>")]
+    agg = [k for k in kernels if "sage1_fwd_kernel" in k] or \
+        [k for k in kernels if "agg_fwd_kernel" in k and k.endswith("true>")]
     bench = {}
     for line in open(f"{out_dir}/bench_FETCH_SIZE.log"):
         if line.startswith('{"metric"'):
@@ -39,9 +40,9 @@ def main():
     summary = {"config": config, "kernels": kernels,
                "note": "read_bytes = 2 x FETCH_SIZE (gfx950 half-count of wide reads); bytes per dispatch"}
     if agg:
-        summary["agg1_kernel"] = agg[0]
-        summary["agg1_hbm_bytes_per_launch"] = kernels[agg[0]]["hbm_bytes"]
-        summary["agg1_algo_bytes_per_launch"] = bench.get("roofline", {}).get("algo_bytes_per_launch")
+        summary["layer1_kernel"] = agg[0]
+        summary["layer1_hbm_bytes_per_launch"] = kernels[agg[0]]["hbm_bytes"]
+        summary["layer1_algo_bytes_per_launch"] = bench.get("roofline", {}).get("algo_bytes_per_launch")
     print(json.dumps(summary, indent=1))
 
 

@@ -7,7 +7,7 @@ OUT=$ROOT/gpurun_out/prof_mb_${TAG:-x}
 mkdir -p "$OUT"
 cd "$ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT" -o run --output-format csv -- \
-    python3 tools/mb_linear.py ${MB_ARGS} > "$OUT/mb.log" 2>&1 || exit $?
+    python3 ${MB:-tools/mb_linear.py} ${MB_ARGS} > "$OUT/mb.log" 2>&1 || exit $?
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
