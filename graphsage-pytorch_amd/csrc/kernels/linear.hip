@@ -244,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
 // stream in chunks of 16 through a two-buffer LDS ring (thread: 4 dZ values
 // and 4 inputs of one row per chunk); the MFMA "k" runs over rows.  Slabs
 // write fp32 partials that sum_slabs_kernel adds in a fixed order.
-constexpr int kDwPitch = 64 + 4;
+constexpr int kDwPitch = 64 + 16;  // rows 16 banks apart: (kq, r) reads of a column hit distinct banks
 constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are staged in LDS)
 
 template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
