@@ -276,7 +276,10 @@ def main():
                        "host_ms_per_step": {"sampler": round(1e3 * st["sample_s"] / max(1, st["steps"]), 3),
                                             "wait_for_batch": round(1e3 * st["wait_s"] / max(1, st["steps"]), 3),
                                             "issue": round(1e3 * st["issue_s"] / max(1, st["steps"]), 3),
-                                            "issue_copy": round(1e3 * st["copy_s"] / max(1, st["steps"]), 3),
+                                            "wait_sample": round(1e3 * st["wait_sample_s"] / max(1, st["steps"]), 3),
+                                            "wait_ring": round(1e3 * st["wait_ring_s"] / max(1, st["steps"]), 3),
+                                            "wait_gather": round(1e3 * st["wait_gather_s"] / max(1, st["steps"]), 3),
+                                            "lookahead_misses": st["lookahead_misses"],
                                             "issue_fwd_bwd": round(1e3 * st["fwd_bwd_s"] / max(1, st["steps"]), 3),
                                             "issue_update": round(1e3 * st["update_s"] / max(1, st["steps"]), 3),
                                             "max_step": round(1e3 * st["max_step_s"], 3)},

@@ -101,6 +101,9 @@ _SIGS = {
     "gs_trainer_ws_bytes": (_i64, [_vp, _vp]),
     "gs_trainer_forward_backward": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gs_trainer_update": (_i32, [_vp, _f32, _vp, _vp]),
+    "gs_trainer_gather_reserve": (_i32, [_vp, _i64]),
+    "gs_trainer_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),
+    "gs_trainer_forward_backward_gathered": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_grads": (_vp, [_vp]),
@@ -138,8 +141,9 @@ class RunnerStats(ctypes.Structure):
     _fields_ = [
         ("steps", _i64), ("wait_s", ctypes.c_double), ("issue_s", ctypes.c_double),
         ("sample_s", ctypes.c_double), ("hop_sizes", ctypes.c_double * (4 * GS_MAX_HOPS)),
-        ("copy_s", ctypes.c_double), ("fwd_bwd_s", ctypes.c_double), ("update_s", ctypes.c_double),
-        ("max_step_s", ctypes.c_double),
+        ("wait_sample_s", ctypes.c_double), ("wait_ring_s", ctypes.c_double),
+        ("wait_gather_s", ctypes.c_double), ("fwd_bwd_s", ctypes.c_double), ("update_s", ctypes.c_double),
+        ("max_step_s", ctypes.c_double), ("lookahead_misses", _i64),
     ]
 
 

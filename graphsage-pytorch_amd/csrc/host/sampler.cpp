@@ -34,7 +34,7 @@ struct Hop {
     bool materialised = false;
     std::vector<int64_t> dst_ids;
     std::vector<int32_t> pos_ptr, pos;
-    std::vector<int64_t> row_start;  // row_ptr[dst] per destination (absolute entries in the pack)
+    std::vector<int32_t> ent;  // absolute CSR entries row_ptr[dst] + pos (what the pack carries)
     std::vector<int64_t> src_ids;
     std::vector<int32_t> nbr_ptr, nbr, self_local;
     std::vector<int32_t> set_ptr;
@@ -55,7 +55,6 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
     h.pos_ptr.assign(n + 1, 0);
     thread_local std::vector<int64_t> deg;
     deg.resize(n);
-    h.row_start.resize(n);
     int64_t total = 0;
     const int64_t* rp = g.row_ptr.data();
     constexpr int64_t kAhead = 16;  // frontier ids are known: prefetch their row_ptr
@@ -65,23 +64,27 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
         const int64_t v = h.dst_ids[r];
         const int64_t d = rp[v + 1] - rp[v];
         deg[r] = d;
-        h.row_start[r] = rp[v];
         total += (h.k > 0 && d >= h.k) ? h.k : d;
         GS_REQUIRE(total < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
         h.pos_ptr[r + 1] = static_cast<int32_t>(total);
     }
     h.pos.resize(total);
+    h.ent.resize(total);
     const int64_t setsize = sample_setsize(h.k);
     thread_local std::vector<int32_t> pool;
     pool.resize(std::max<int64_t>(setsize, 1));
     for (int64_t r = 0; r < n; ++r) {
         const int64_t d = deg[r];
         int32_t* dstp = h.pos.data() + h.pos_ptr[r];
+        const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
         if (h.k > 0 && d >= h.k) {
             sample_positions(rng, d, h.k, setsize, dstp, pool.data());
         } else {
             for (int64_t t = 0; t < d; ++t) dstp[t] = static_cast<int32_t>(t);
         }
+        const int32_t rs = static_cast<int32_t>(rp[h.dst_ids[r]]);  // < 2^31 (checked in run_sample)
+        int32_t* ep = h.ent.data() + h.pos_ptr[r];
+        for (int64_t t = 0; t < cnt; ++t) ep[t] = rs + dstp[t];
     }
 }
 
@@ -111,7 +114,25 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     h.set_ptr.assign(n + 1, 0);
     h.set_items.clear();
     h.set_items.reserve(h.pos.size() + n);
+    // the rows read below are known ahead (positions are drawn): prefetch the
+    // col / slot lines of the row kAhead destinations on (random row reads
+    // dominate this loop on large graphs)
+    constexpr int64_t kAhead = 4;
+    auto prefetch_row = [&](int64_t q) {
+        const int64_t v = h.dst_ids[q];
+        const int64_t rs = g.row_ptr[v], d = g.row_ptr[v + 1] - rs;
+        if (h.k > 0 && d >= h.k) {
+            for (int32_t t = h.pos_ptr[q]; t < h.pos_ptr[q + 1]; ++t) __builtin_prefetch(g.col.data() + rs + h.pos[t]);
+        } else {
+            for (int64_t t = 0; t < d; t += 16) {
+                __builtin_prefetch(g.col.data() + rs + t);
+                __builtin_prefetch(g.slot.data() + rs + t);
+            }
+        }
+    };
+    for (int64_t q = 0; q < std::min(n, kAhead); ++q) prefetch_row(q);
     for (int64_t r = 0; r < n; ++r) {
+        if (r + kAhead < n) prefetch_row(r + kAhead);
         const int64_t v = h.dst_ids[r];
         const int64_t rs = g.row_ptr[v], d = g.degree(v);
         const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
@@ -469,12 +490,7 @@ int gs_sample_pack(const gs_sample* sp, int32_t* buf, int64_t cap) {
             cpy(j, GS_PK_POS_PTR, h.pos_ptr.data(), h.pos_ptr.size());
             // absolute CSR entries row_ptr[dst] + position: the device gather
             // then reads col[] without first looking up row_ptr[dst]
-            int32_t* e = buf + L.off[j][GS_PK_POS];
-            const int64_t nd = static_cast<int64_t>(h.dst_ids.size());
-            for (int64_t r = 0; r < nd; ++r) {
-                const int64_t rs = h.row_start[r];
-                for (int32_t t = h.pos_ptr[r]; t < h.pos_ptr[r + 1]; ++t) e[t] = static_cast<int32_t>(rs + h.pos[t]);
-            }
+            cpy(j, GS_PK_POS, h.ent.data(), h.ent.size());
             int32_t* d = buf + L.off[j][GS_PK_DST_IDS];
             for (size_t r = 0; r < h.dst_ids.size(); ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
         } else {

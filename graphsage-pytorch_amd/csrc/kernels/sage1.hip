@@ -62,6 +62,11 @@ __global__ __launch_bounds__(kS1Threads) void sage1_fwd_kernel(
         }
         // neighbour ids of both destinations (first 64 of each; longer
         // neighbourhoods continue in the loop below)
+        // expand mode (col != NULL): ent holds absolute CSR entries, self is
+        // dropped unless gcn; explicit mode (col == NULL): ent holds the
+        // source rows themselves, already self-filtered (gcn lists include self)
+        const bool expand = col != nullptr;
+        if (!expand) gcn = 0;
         int my[2];
         bool selfhit[2];
 #pragma unroll
@@ -69,8 +74,8 @@ __global__ __launch_bounds__(kS1Threads) void sage1_fwd_kernel(
             const int m = min(64, end[q] - beg[q]);
             const bool mine = lane < m;
             const int e = m > 0 ? ent[mine ? beg[q] + lane : beg[q]] : 0;
-            const int nb = col[e];
-            my[q] = (mine && (gcn || nb != node[q])) ? nb : -1;
+            const int nb = expand ? col[e] : e;
+            my[q] = (mine && (!expand || gcn || nb != node[q])) ? nb : -1;
             selfhit[q] = __ballot(mine && nb == node[q]) != 0;
         }
         for (int q = 0; q < 2; ++q) {
@@ -95,8 +100,9 @@ __global__ __launch_bounds__(kS1Threads) void sage1_fwd_kernel(
                     int mine_id = my[q];
                     if (base != beg[q]) {  // rare: more than 64 sampled entries
                         const bool mine = lane < m;
-                        const int nb = col[ent[mine ? base + lane : base]];
-                        mine_id = (mine && (gcn || nb != node[q])) ? nb : -1;
+                        const int e = ent[mine ? base + lane : base];
+                        const int nb = expand ? col[e] : e;
+                        mine_id = (mine && (!expand || gcn || nb != node[q])) ? nb : -1;
                         self_seen |= __ballot(mine && nb == node[q]) != 0;
                     }
                     for (int j = 0; j < m; j += NR) {
@@ -232,7 +238,7 @@ int gs_sage1_fwd(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, 
     GS_REQUIRE(n_dst >= 0 && n_dst < (int64_t(1) << 31) && F < (1 << 28), GS_EINVAL, "bad sizes");
     if (n_dst == 0) return GS_OK;
     const int64_t EPV = dt == GS_F32 ? 4 : 8;
-    GS_REQUIRE(X && ptr && ent && col && dst_ids && W && agg_out && out, GS_EINVAL, "NULL device pointer");
+    GS_REQUIRE(X && ptr && ent && dst_ids && W && agg_out && out, GS_EINVAL, "NULL device pointer");
     GS_REQUIRE(ldx % EPV == 0 && ld_agg % EPV == 0 && aligned16(X) && aligned16(W) && aligned16(agg_out),
                GS_EINVAL, "X / W / agg_out must be 16-byte aligned with aligned strides");
     GS_REQUIRE(ldx >= F && ld_agg >= F && ldo >= H, GS_EINVAL, "leading dimension too small");

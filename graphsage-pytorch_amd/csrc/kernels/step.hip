@@ -16,12 +16,20 @@ struct gs_trainer {
     std::vector<int64_t> w_rows, w_cols;
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
     bool fused1 = false;  // layer 1 through gs_sage1_fwd (gather + linear in one launch)
+    bool fused2 = false;  // layers >= 2 likewise (explicit lists; MEAN)
     // optional HIP-event timing of the layer-1 gather-aggregate (bench roofline)
     std::vector<hipEvent_t> ev0, ev1;
     int64_t n_timed = 0;
+    // layer-1 aggregate slots for gathers issued ahead of their step
+    // (gs_trainer_gather), so the next batch's gather overlaps this backward
+    static constexpr int kSlots = 3;
+    void* a1_slot[kSlots] = {};
+    int64_t a1_rows = 0;
     ~gs_trainer() {
         for (auto e : ev0) (void)hipEventDestroy(e);
         for (auto e : ev1) (void)hipEventDestroy(e);
+        for (void* p : a1_slot)
+            if (p) (void)hipFree(p);
     }
 };
 
@@ -48,10 +56,34 @@ static inline void ok(int rc) {
     if (rc != GS_OK) fail(rc, gs_last_error());
 }
 
-// Runs (or, with ws == nullptr, only sizes) one forward + backward.
+// The layer-1 gather-aggregate of one packed sample (models.py:291-330 at
+// layer 1) into `out`, bracketed by the timing events when armed.
+static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+                    void* out, hipStream_t st) {
+    const gs_trainer_config& c = T.cfg;
+    const int L = c.n_layers;
+    const int64_t F = c.feat_dim;
+    auto fld = [&](int f) -> const int32_t* {
+        const int64_t o = offsets[(L - 1) * GS_PK_NFIELDS + f];
+        GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
+        return pack + o;
+    };
+    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
+    if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+    ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F,
+                  hop_sizes[4 * (L - 1)], fld(GS_PK_POS_PTR), fld(GS_PK_POS), nullptr, c.col, fld(GS_PK_DST_IDS),
+                  c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    if (timed) {
+        GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+        ++T.n_timed;
+    }
+}
+
+// Runs (or, with ws == nullptr, only sizes) one forward + backward.  With
+// a1_slot >= 0 the layer-1 aggregate was produced by gs_trainer_gather.
 static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
                         const int32_t* roots, int64_t B, char* ws, int64_t ws_bytes, float* loss,
-                        hipStream_t st) {
+                        hipStream_t st, int a1_slot = -1) {
     const gs_trainer_config& c = T.cfg;
     const int L = c.n_layers;
     const int64_t H = c.hidden, F = c.feat_dim;
@@ -75,7 +107,14 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         const int j = L - l + 1;
         rows[l - 1] = hs[j - 1].n_dst;
         in_dim[l - 1] = l == 1 ? F : H;
-        if (l == 1) agg[0] = cv.take<char>(rows[0] * F * static_cast<int64_t>(xsz));
+        if (l == 1) {
+            if (a1_slot >= 0) {
+                GS_REQUIRE(rows[0] <= T.a1_rows && T.a1_slot[a1_slot], GS_EINVAL, "gather slot too small");
+                agg[0] = T.a1_slot[a1_slot];
+            } else {
+                agg[0] = cv.take<char>(rows[0] * F * static_cast<int64_t>(xsz));
+            }
+        }
         else agg[l - 1] = cv.take<float>(rows[l - 1] * H);
         h[l - 1] = cv.take<float>(rows[l - 1] * H);
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
@@ -102,27 +141,32 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     // ---- forward (models.py:255-267)
     if (lowp) ok(gs_cast_f32_bf16(P + T.w_off[0], w1lp, T.w_rows[0] * T.w_cols[0], st));
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
-    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
     const void* W1 = lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]);
-    if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
-    if (T.fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
+    const bool fused1 = T.fused1 && a1_slot < 0;
+    if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
+        const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
+        if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
         ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
                         rows[0], fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.col, dst_L, c.gcn, W1, agg[0], F, h[0],
                         H, 1, st));
-    } else {
-        ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, rows[0],
-                      fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), nullptr, c.col, dst_L, c.gcn, agg[0],
-                      static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+        if (timed) {
+            GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+            ++T.n_timed;
+        }
+    } else if (a1_slot < 0) {
+        gather1(T, pack, hop_sizes, offsets, agg[0], st);
     }
-    if (timed) {
-        GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
-        ++T.n_timed;
-    }
-    if (!T.fused1)
+    if (!fused1)
         ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
                               dst_L, agg[0], F, W1, h[0], H, 1, st));
     for (int l = 2; l <= L; ++l) {
         const int j = L - l + 1;
+        if (T.fused2 && c.agg == GS_AGG_MEAN) {  // MAX needs the argmax the fused kernel does not keep
+            ok(gs_sage1_fwd(GS_AGG_MEAN, GS_F32, h[l - 2], H, H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
+                            fld(j, GS_PK_NBR), nullptr, fld(j, GS_PK_SELF), c.gcn, P + T.w_off[l - 1], agg[l - 1], H,
+                            h[l - 1], H, 1, st));
+            continue;
+        }
         ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), GS_F32, h[l - 2], H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
                       fld(j, GS_PK_NBR), nullptr, nullptr, nullptr, 0, agg[l - 1], GS_F32, H, am[l - 1], st));
         ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
@@ -191,6 +235,8 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
                                        cfg->gcn) != 0 &&
                 cfg->feat_ld % (cfg->feat_dtype == GS_F32 ? 4 : 8) == 0 && gs::aligned16(cfg->X) &&
                 std::getenv("GS_FUSED1") != nullptr;  // opt-in: measured slower than agg + linear
+    T->fused2 = gs_sage1_fwd_supported(GS_F32, cfg->hidden, cfg->hidden, cfg->gcn) != 0 &&
+                std::getenv("GS_FUSED2") != nullptr;  // opt-in: measured slower than agg + linear
     *out = T;
     GS_API_END
 }
@@ -221,6 +267,43 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_
     GS_REQUIRE(t && pack && hop_sizes && offsets && roots && ws && loss, GS_EINVAL, "NULL argument");
     gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
                  gs::as_stream(stream));
+    GS_API_END
+}
+
+int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && max_rows >= 0, GS_EINVAL, "bad arguments");
+    if (max_rows <= t->a1_rows) return GS_OK;
+    const int64_t bytes = max_rows * t->cfg.feat_dim * (t->cfg.feat_dtype == GS_BF16 ? 2 : 4);
+    for (void*& p : t->a1_slot) {
+        if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
+        p = nullptr;
+        GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(bytes, 256)) == hipSuccess, GS_ENOMEM, "hipMalloc(gather slot)");
+    }
+    t->a1_rows = max_rows;
+    GS_API_END
+}
+
+int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+                      int32_t slot, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && pack && hop_sizes && offsets && slot >= 0 && slot < gs_trainer::kSlots, GS_EINVAL,
+               "bad arguments");
+    const int L = t->cfg.n_layers;
+    GS_REQUIRE(hop_sizes[4 * (L - 1)] <= t->a1_rows && t->a1_slot[slot], GS_EINVAL,
+               "gather slot too small (gs_trainer_gather_reserve)");
+    gs::gather1(*t, pack, hop_sizes, offsets, t->a1_slot[slot], gs::as_stream(stream));
+    GS_API_END
+}
+
+int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                                         const int64_t* offsets, const int32_t* roots, int64_t n_roots,
+                                         int32_t slot, void* ws, int64_t ws_bytes, float* loss, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && pack && hop_sizes && offsets && roots && ws && loss && slot >= 0 && slot < gs_trainer::kSlots,
+               GS_EINVAL, "bad arguments");
+    gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
+                 gs::as_stream(stream), slot);
     GS_API_END
 }
 

@@ -5,11 +5,12 @@
 //
 //   sampler thread w : batches w, w+S, ... in order, each into a free pinned
 //                      slot of its ring (gs_sample_pack_run, its own rng)
-//   gs_runner_run    : batch i from stream i % S, in order: H2D copy on a
-//                      dedicated copy stream into device pack buffer i % 3,
-//                      then forward/backward, all-reduce (world > 1) and
-//                      update on the caller's stream (which waits, GPU-side,
-//                      for the copy).
+//   gs_runner_run    : batch i from stream i % S, in order: device pull of
+//                      its pack (ring entry i % 3) and its layer-1 gather on
+//                      a side stream, issued one batch ahead when sampled so
+//                      they run under step i-1; then forward/backward from
+//                      the gathered slot, all-reduce (world > 1) and update
+//                      on the caller's stream.
 // A pinned slot returns to its sampler once the copy that read it has
 // completed.  Only the driver thread makes HIP calls: it polls the copy events
 // of consumed slots (hipEventQuery) and hands finished slots back, and waits
@@ -86,11 +87,23 @@ struct gs_runner {
     std::vector<std::unique_ptr<gs::SamplerStream>> streams;
     bool stop = false;
     int64_t next_batch = 0;
-    static constexpr int kDev = 3;         // device pack ring
+    // Ring of 3 per batch in flight (b % 3): device pack buffer, trainer
+    // gather slot, events.  The side stream pulls batch b's pack and gathers
+    // its layer 1 (reads only X and the pack) while the main stream runs
+    // batch b-1.  No stream ever waits on another's event (a cross-queue wait
+    // measured ~17 us of idle GPU here): the host checks instead that the step
+    // three batches back released the ring entry, and that the gather of the
+    // batch it is about to issue has completed.
+    static constexpr int kDev = 3;
     int32_t* dev[kDev] = {};
-    hipEvent_t dev_done[kDev] = {};        // recorded after the step that read dev[k]
+    hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
-    hipStream_t copy_stream = nullptr;     // H2D only; never waits on anything
+    hipEvent_t gathered[kDev] = {};        // side: pull + gather of the batch in entry k
+    hipStream_t side = nullptr;
+    struct Inflight {
+        int stream = -1, slot = -1;
+    } inflight[kDev];
+    int64_t issued = 0;                    // batches whose pull + gather are issued
     void* ws = nullptr;
     int64_t ws_bytes = 0;
     float* clip_ws = nullptr;
@@ -100,6 +113,7 @@ struct gs_runner {
     ~gs_runner();
     void sampler_loop(gs::SamplerStream& s);
     void recycle(gs::SamplerStream& s, bool block);
+    bool issue(int64_t b, bool block);
 };
 
 // Hand the slots whose copy has completed back to their sampler; with
@@ -149,6 +163,50 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
     }
 }
 
+// Pull batch b's pack to the device and gather its layer 1, both on the side
+// stream.  block == false: return false if b is not sampled yet.
+bool gs_runner::issue(int64_t b, bool block) {
+    using namespace gs;
+    SamplerStream& s = *streams[b % cfg.n_streams];
+    int slot_id;
+    const auto tw = Clock::now();
+    for (;;) {
+        std::unique_lock<std::mutex> lk(s.mu);
+        if (!s.ready.empty()) {
+            slot_id = s.ready.front();
+            s.ready.pop_front();
+            break;
+        }
+        if (!block) return false;
+        // wait for a sampled batch, or free a slot for a starved sampler
+        s.cv.wait(lk, [&] { return !s.ready.empty() || (s.free.empty() && !s.copying.empty()); });
+        if (!s.ready.empty()) continue;
+        lk.unlock();
+        recycle(s, true);
+    }
+    const auto tr = Clock::now();
+    stats.wait_sample_s += secs(tw, tr);
+    PackSlot& slot = s.slots[slot_id];
+    GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
+    if (slot.status != GS_OK) fail(slot.status, slot.error);
+    const int k = static_cast<int>(b % kDev);
+    if (dev_busy[k]) hip_ok(hipEventSynchronize(dev_done[k]), "hipEventSynchronize");  // batch b-3 done
+    stats.wait_ring_s += secs(tr, Clock::now());
+    const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
+    const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
+    pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
+        reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(dev[k]), n16, slot.host + 4 * n16,
+        dev[k] + 4 * n16, static_cast<int>(tail));
+    hip_ok(hipGetLastError(), "pull_pack_kernel");
+    hip_ok(hipEventRecord(slot.copied, side), "hipEventRecord");
+    const int rc = gs_trainer_gather(cfg.trainer, dev[k], slot.hop_sizes, slot.offsets, k, side);
+    if (rc != GS_OK) fail(rc, gs_last_error());
+    hip_ok(hipEventRecord(gathered[k], side), "hipEventRecord");
+    inflight[k] = {static_cast<int>(b % cfg.n_streams), slot_id};
+    issued = b + 1;
+    return true;
+}
+
 gs_runner::~gs_runner() {
     for (auto& s : streams) {
         {
@@ -166,13 +224,14 @@ gs_runner::~gs_runner() {
             if (slot.copied) (void)hipEventDestroy(slot.copied);
             if (slot.host) (void)hipHostFree(slot.host);
         }
-    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    if (side) (void)hipStreamSynchronize(side);
     for (int d = 0; d < kDev; ++d) {
         if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
+        if (gathered[d]) (void)hipEventDestroy(gathered[d]);
         if (dev[d]) (void)hipFree(dev[d]);
     }
-    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (side) (void)hipStreamDestroy(side);
     if (ws) (void)hipFree(ws);
     if (clip_ws) (void)hipFree(clip_ws);
 }
@@ -237,12 +296,25 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(bound > 0, GS_EINVAL, "pack bound failed");
     r->cap = bound + cfg->batch;
     hip_ok(hipGetDevice(&r->device), "hipGetDevice");
-    hip_ok(hipStreamCreateWithFlags(&r->copy_stream, hipStreamNonBlocking), "hipStreamCreate");
+    hip_ok(hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking), "hipStreamCreate");
     for (int d = 0; d < gs_runner::kDev; ++d) {
         hip_ok(hipEventCreateWithFlags(&r->dev_done[d], hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipEventCreateWithFlags(&r->gathered[d], hipEventDisableTiming), "hipEventCreate");
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     }
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
+    {  // layer-1 destinations bound (the last hop's frontier), for the gather slots
+        int64_t nn = 0, ne = 0, md = 0;
+        GS_REQUIRE(gs_graph_dims(cfg->graph, &nn, &ne, &md) == GS_OK, GS_EINVAL, "gs_graph_dims");
+        int64_t nd = cfg->batch;
+        for (int32_t j = 0; j + 1 < cfg->n_hops; ++j) {
+            const int64_t k = r->fanouts[j];
+            const int64_t per = k > 0 ? std::min<int64_t>(k, md) : md;
+            nd = std::min<int64_t>(nn, nd + nd * per);
+        }
+        const int rc = gs_trainer_gather_reserve(cfg->trainer, nd);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+    }
     const int32_t S = cfg->n_streams;
     for (int32_t w = 0; w < S; ++w) {
         auto s = std::make_unique<SamplerStream>();
@@ -273,49 +345,28 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     GS_REQUIRE(r && loss && n_steps >= 0, GS_EINVAL, "bad arguments");
     GS_REQUIRE(r->next_batch + n_steps <= r->cfg.n_batches, GS_ERANGE, "runner has fewer batches left");
     hipStream_t st = as_stream(stream);
-    const int32_t S = r->cfg.n_streams;
     const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
     float* grads = gs_trainer_grads(r->cfg.trainer);
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
-        SamplerStream& s = *r->streams[b % S];
         const auto t0 = Clock::now();
         for (auto& o : r->streams) r->recycle(*o, false);
-        int slot_id;
-        for (;;) {
-            std::unique_lock<std::mutex> lk(s.mu);
-            // a sampled batch, or a sampler starved of slots while copies are in flight
-            s.cv.wait(lk, [&] { return !s.ready.empty() || (s.free.empty() && !s.copying.empty()); });
-            if (!s.ready.empty()) {
-                slot_id = s.ready.front();
-                s.ready.pop_front();
-                break;
-            }
-            lk.unlock();
-            r->recycle(s, true);
+        if (r->issued <= b) {
+            ++r->stats.lookahead_misses;
+            r->issue(b, true);
         }
-        PackSlot& slot = s.slots[slot_id];
+        // look ahead: batch b+1's pull + gather run on the side stream under
+        // this step (never block here: with a slow sampler that would idle the GPU)
+        if (b + 1 < r->cfg.n_batches && r->issued == b + 1) r->issue(b + 1, false);
+        const int k = static_cast<int>(b % gs_runner::kDev);
+        const auto tg = Clock::now();
+        hip_ok(hipEventSynchronize(r->gathered[k]), "hipEventSynchronize");  // normally long done
         const auto t1 = Clock::now();
-        GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
-        if (slot.status != GS_OK) fail(slot.status, slot.error);
-        // H2D (device pull) on a stream that never waits: device buffer d is reused only
-        // once the host has seen the step that last read it complete (three
-        // steps back, normally long done).  A copy queued behind GPU work
-        // (same stream, or a copy stream waiting on an event) made
-        // hipMemcpyAsync block the host until that work drained.
-        const int d = static_cast<int>(b % gs_runner::kDev);
-        if (r->dev_busy[d]) hip_ok(hipEventSynchronize(r->dev_done[d]), "hipEventSynchronize");
-        {
-            const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
-            const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
-            pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, r->copy_stream>>>(
-                reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(r->dev[d]), n16,
-                slot.host + 4 * n16, r->dev[d] + 4 * n16, static_cast<int>(tail));
-            hip_ok(hipGetLastError(), "pull_pack_kernel");
-        }
-        hip_ok(hipEventRecord(slot.copied, r->copy_stream), "hipEventRecord");
-        hip_ok(hipStreamWaitEvent(st, slot.copied, 0), "hipStreamWaitEvent");
-        const auto t2 = Clock::now();
+        r->stats.wait_gather_s += secs(tg, t1);
+        const gs_runner::Inflight f = r->inflight[k];
+        SamplerStream& s = *r->streams[f.stream];
+        PackSlot& slot = s.slots[f.slot];
+        const auto t2 = t1;
         const int64_t need = gs_trainer_ws_bytes(r->cfg.trainer, slot.hop_sizes);
         GS_REQUIRE(need >= 0, GS_EINVAL, gs_last_error());
         if (need > r->ws_bytes) {
@@ -326,8 +377,9 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             hip_ok(hipMalloc(&r->ws, r->ws_bytes), "hipMalloc(ws)");
         }
         const int64_t pack_total = slot.used - r->cfg.batch;
-        int rc = gs_trainer_forward_backward(r->cfg.trainer, r->dev[d], slot.hop_sizes, slot.offsets,
-                                             r->dev[d] + pack_total, r->cfg.batch, r->ws, r->ws_bytes, loss, st);
+        int32_t* pk = r->dev[k];
+        int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets,
+                                                      pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss, st);
         if (rc != GS_OK) fail(rc, gs_last_error());
         const auto t3 = Clock::now();
         if (r->cfg.world > 1) {
@@ -336,17 +388,16 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         rc = gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st);
         if (rc != GS_OK) fail(rc, gs_last_error());
-        hip_ok(hipEventRecord(r->dev_done[d], st), "hipEventRecord");
-        r->dev_busy[d] = true;
+        hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
+        r->dev_busy[k] = true;
         for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);
         r->stats.sample_s += slot.sample_s;
-        s.copying.push_back(slot_id);
+        s.copying.push_back(f.slot);
         ++r->next_batch;
         ++r->stats.steps;
         const auto t4 = Clock::now();
         r->stats.wait_s += secs(t0, t1);
         r->stats.issue_s += secs(t1, t4);
-        r->stats.copy_s += secs(t1, t2);
         r->stats.fwd_bwd_s += secs(t2, t3);
         r->stats.update_s += secs(t3, t4);
         r->stats.max_step_s = std::max(r->stats.max_step_s, secs(t0, t4));

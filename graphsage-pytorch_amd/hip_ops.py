@@ -77,7 +77,7 @@ def sage1_supported(dtype, F, H, gcn):
 def sage1_fwd(agg_func, X, ptr_, ent, col, dst_ids, W, agg_out, out, *, gcn=False, relu=True):
     """Fused layer 1 (gs_sage1_fwd): gather-aggregate over absolute CSR
     entries + relu([X[dst] | agg] · Wᵀ); fills agg_out and out."""
-    _dev(X, ptr_, ent, col, dst_ids, W, agg_out, out)
+    _dev(X, ptr_, ent, col, dst_ids, W, agg_out, out)  # col None: explicit lists (layers >= 2)
     n_dst = ptr_.numel() - 1
     F = X.shape[1]
     H = W.shape[0]

@@ -338,8 +338,9 @@ class Runner:
             lib().gs_runner_stats_reset(self._h)
         sizes = np.array(st.hop_sizes[:], dtype=np.float64).reshape(_lib.GS_MAX_HOPS, 4)
         return {"steps": st.steps, "wait_s": st.wait_s, "issue_s": st.issue_s, "sample_s": st.sample_s,
-                "copy_s": st.copy_s, "fwd_bwd_s": st.fwd_bwd_s, "update_s": st.update_s,
-                "max_step_s": st.max_step_s, "hop_sizes_sum": sizes}
+                "wait_sample_s": st.wait_sample_s, "wait_ring_s": st.wait_ring_s,
+                "wait_gather_s": st.wait_gather_s, "fwd_bwd_s": st.fwd_bwd_s, "update_s": st.update_s,
+                "max_step_s": st.max_step_s, "lookahead_misses": st.lookahead_misses, "hop_sizes_sum": sizes}
 
     def close(self):
         h = getattr(self, "_h", None)

@@ -262,7 +262,10 @@ int gs_agg_bwd(gs_agg op, int64_t n_src, int64_t F, const int32_t* tptr,
  * unless gcn) feeding gs_sage_linear_fwd's relu([X[dst] | agg] · Wᵀ) through
  * LDS, in one launch.  Writes the aggregate rows to agg_out (dtype dt, kept
  * for the weight gradient) and out[n_dst, H] (fp32).  Results equal the
- * two-kernel path bitwise.  gs_sage1_fwd_supported: 1 when the 16-row A tile
+ * two-kernel path bitwise.  col == NULL selects explicit mode (layers >= 2):
+ * ent holds the source rows of X themselves (the pack's NBR lists, already
+ * self-filtered) and dst_ids the self rows (SELF field), like gs_agg_fwd's
+ * explicit mode.  gs_sage1_fwd_supported: 1 when the 16-row A tile
  * fits 64 KiB of LDS (F <= 512 fp32 / 1024 bf16 with self) and F is a
  * multiple of the 16-byte vector. */
 int gs_sage1_fwd_supported(gs_dtype dt, int64_t F, int64_t H, int32_t gcn);
@@ -337,6 +340,19 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
                                 const int64_t* hop_sizes, const int64_t* offsets,
                                 const int32_t* roots, int64_t n_roots, void* ws,
                                 int64_t ws_bytes, float* loss, void* stream);
+/* Split form of forward_backward for overlapping consecutive steps: the
+ * layer-1 gather-aggregate of a batch (which reads only X and the pack) into
+ * trainer slot 0..2 on any stream, then the rest of the step reading that
+ * slot.  The caller orders them (event) and keeps a slot until the step that
+ * reads it has finished its backward.  gs_trainer_gather_reserve allocates
+ * the three slots for up to max_rows layer-1 destinations. */
+int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows);
+int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                      const int64_t* offsets, int32_t slot, void* stream);
+int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack,
+                                         const int64_t* hop_sizes, const int64_t* offsets,
+                                         const int32_t* roots, int64_t n_roots, int32_t slot,
+                                         void* ws, int64_t ws_bytes, float* loss, void* stream);
 /* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
 /* Measurement only: record HIP events on the launch stream around the next
@@ -388,12 +404,16 @@ typedef struct {
 
 typedef struct {
     int64_t steps;          /* steps issued since the last reset */
-    double wait_s;          /* host time blocked on a not-yet-sampled batch */
-    double issue_s;         /* host time issuing copies and launches */
+    double wait_s;          /* host time blocked, = the three parts below */
+    double issue_s;         /* host time issuing launches */
     double sample_s;        /* summed sampler-thread time of those batches */
     double hop_sizes[4 * GS_MAX_HOPS]; /* summed (n_dst, n_pos, n_src, n_nbr) */
-    double copy_s, fwd_bwd_s, update_s; /* parts of issue_s */
+    double wait_sample_s;   /* ... on a not-yet-sampled batch */
+    double wait_ring_s;     /* ... on the step three batches back (ring entry reuse) */
+    double wait_gather_s;   /* ... on this batch's side-stream pull + gather */
+    double fwd_bwd_s, update_s; /* parts of issue_s */
     double max_step_s;      /* longest single step (wait + issue) */
+    int64_t lookahead_misses; /* steps whose batch was not issued one step ahead */
 } gs_runner_stats;
 
 typedef struct gs_runner gs_runner;

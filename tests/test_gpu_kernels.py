@@ -255,3 +255,27 @@ def test_sage1_fused_equals_two_kernel_path(gs, F, H, agg, dtype, gcn):
     assert torch.equal(a.view(torch.int16) if dtype == torch.bfloat16 else a,
                        a_ref.view(torch.int16) if dtype == torch.bfloat16 else a_ref)
     assert torch.equal(h, h_ref)
+
+
+@pytest.mark.parametrize("gcn", [False, True])
+@pytest.mark.parametrize("H", [128, 64])
+def test_sage1_explicit_equals_two_kernel_path(gs, gcn, H):
+    """Explicit mode (layers >= 2): gs_sage1_fwd over the pack's NBR/SELF
+    fields == gs_agg_fwd (explicit) + gs_sage_linear_fwd, bitwise."""
+    graph = _rand_graph(gs, 600, 7000, 16)
+    roots = np.nonzero(graph.degrees())[0][:100]
+    s = gs.sample(graph, gs.RNG(H), roots, [25, 10], gcn=gcn)
+    models = importlib.import_module("graphsage-pytorch_amd.models")
+    ds = models.DeviceSample(s, DEV)
+    n_src = s.sizes(1)[2]
+    n_dst = s.sizes(1)[0]
+    Hp = torch.randn(n_src, H, device=DEV)
+    W = torch.randn(H, H if gcn else 2 * H, device=DEV) * 0.05
+    ptr_, nbr, slf = ds.field(1, "nbr_ptr"), ds.field(1, "nbr"), ds.field(1, "self")
+    a_ref = torch.empty(n_dst, H, device=DEV)
+    ops.agg_fwd("MEAN", Hp, ptr_, nbr, a_ref)
+    h_ref = torch.empty(n_dst, H, device=DEV)
+    ops.sage_linear_fwd(a_ref, W, h_ref, Xs=None if gcn else Hp, sidx=slf)
+    a, h = torch.empty_like(a_ref), torch.empty_like(h_ref)
+    ops.sage1_fwd("MEAN", Hp, ptr_, nbr, None, slf, W, a, h, gcn=gcn)
+    assert torch.equal(a, a_ref) and torch.equal(h, h_ref)
