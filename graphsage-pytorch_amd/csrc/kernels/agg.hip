@@ -1,190 +1,7 @@
-// Segmented gather-aggregate for GraphSage.aggregate (models.py:291-330) and
-// its backward.  The reference builds a dense [n_dst, n_src] 0/1 mask and
-// multiplies (MEAN, :305-314) or loops rows in Python (MAX, :316-326); here
-// each destination is owned by a group of G lanes of one wavefront that
-// streams its neighbours' feature rows straight from HBM (16 B per lane, so a
-// 1 KiB fp32 F=256 row is one coalesced wave load) and reduces in registers.
-// Nothing of size n_dst x n_src is ever formed.
-#include "kcommon.hpp"
+// C-ABI launchers of the gather-aggregate kernels (kernels/agg_dev.hpp).
+#include "agg_dev.hpp"
 
 namespace gs {
-
-constexpr int kBlock = 256;
-constexpr int kRows = 16;  // neighbour rows in flight per lane group (8 for 8-element bf16 vectors)
-
-// Lanes [lo, lo + G) of the wave's ballot.
-template <int G>
-__device__ __forceinline__ uint64_t group_bits(bool p) {
-    const uint64_t m = __ballot(p);
-    if constexpr (G == 64) return m;
-    const int lo = (threadIdx.x & 63) & ~(G - 1);
-    return (m >> lo) & ((uint64_t(1) << G) - 1);
-}
-
-// One group of G lanes per destination r.  EXPAND: the neighbourhood is the
-// sampled positions idx[ptr[r]..ptr[r+1]) of node dst_ids[r]'s CSR row,
-// expanded on the fly (col[row_ptr[node] + pos], or col[idx] when row_ptr is
-// NULL and idx already holds absolute entries, as in the packed sample);
-// self is skipped unless gcn,
-// and gcn adds it once (models.py:285, :297-298).  Otherwise idx holds the
-// source rows of X directly (already self-filtered and ascending).
-//
-// Every load is unconditional: slots past the neighbourhood re-read the
-// chunk's first row (already in flight) and are masked when accumulated, so a
-// group keeps all kRows rows of a chunk in flight instead of waiting on each.
-template <int OP, typename T, int VEC, int G, bool EXPAND>
-__global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
-    const T* __restrict__ X, int64_t ldx, int F, int n_dst, const int* __restrict__ ptr,
-    const int* __restrict__ idx, const int64_t* __restrict__ row_ptr, const int* __restrict__ col,
-    const int* __restrict__ dst_ids, int gcn, T* __restrict__ out, int64_t ldo,
-    int* __restrict__ argmax) {
-    const int gl = threadIdx.x % G;
-    const int r = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-    if (r >= n_dst) return;  // whole lane groups leave together
-    const int beg = ptr[r], end = ptr[r + 1];
-    int node = 0;
-    int64_t rs = 0;
-    if (EXPAND) {
-        node = dst_ids[r];
-        if (row_ptr) rs = row_ptr[node];
-    }
-    constexpr int NR = VEC > 4 ? kRows / 2 : kRows;
-    const bool want_am = (OP == GS_AGG_MAX) && (argmax != nullptr);
-    const int nf = (F + G * VEC - 1) / (G * VEC);
-    for (int fi = 0; fi < nf; ++fi) {
-        const int f0 = fi * G * VEC + gl * VEC;
-        const bool act = f0 < F;
-        const int f0c = act ? f0 : 0;
-        float acc[VEC];
-        int am[VEC];
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-            acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
-            am[v] = -1;
-        }
-        int cnt = 0;
-        bool self_seen = false;
-        for (int base = beg; base < end; base += G) {
-            const int m = min(G, end - base);
-            const bool mine = gl < m;
-            const int e = idx[mine ? base + gl : base];
-            int my;
-            if (EXPAND) {
-                const int nb = col[rs + e];
-                self_seen |= group_bits<G>(mine && nb == node) != 0;
-                my = (mine && (gcn || nb != node)) ? nb : -1;
-            } else {
-                my = mine ? e : -1;
-            }
-            for (int j = 0; j < m; j += NR) {
-                int rows[NR];
-                bool ok[NR];
-#pragma unroll
-                for (int u = 0; u < NR; ++u) {
-                    rows[u] = __shfl(my, j + u < m ? j + u : j, G);
-                    ok[u] = (j + u < m) && rows[u] >= 0;
-                }
-                const int fallback = rows[0] >= 0 ? rows[0] : (EXPAND ? node : 0);
-                float x[NR][VEC];
-#pragma unroll
-                for (int u = 0; u < NR; ++u)
-                    RowIO<T, VEC>::load(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0c, x[u]);
-#pragma unroll
-                for (int u = 0; u < NR; ++u) {
-                    cnt += ok[u];
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) {
-                        if (OP == GS_AGG_MEAN) {
-                            acc[v] += ok[u] ? x[u][v] : 0.f;
-                        } else {
-                            const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
-                            acc[v] = take ? x[u][v] : acc[v];
-                            am[v] = take ? rows[u] : am[v];
-                        }
-                    }
-                }
-            }
-        }
-        if (EXPAND && gcn && !self_seen) {  // gcn keeps self exactly once (set semantics)
-            ++cnt;
-            float x[VEC];
-            RowIO<T, VEC>::load(X + static_cast<int64_t>(node) * ldx + f0c, x);
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                if (OP == GS_AGG_MEAN) acc[v] += x[v];
-                else if (x[v] > acc[v]) { acc[v] = x[v]; am[v] = node; }
-            }
-        }
-        if (!act) continue;
-        if (OP == GS_AGG_MEAN) {
-            const float inv = 1.0f / static_cast<float>(cnt);  // cnt == 0 -> NaN row, as 0/0 in :313
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) acc[v] *= inv;
-        }
-        RowIO<T, VEC>::store(out + static_cast<int64_t>(r) * ldo + f0, acc);
-        if (want_am) {
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) argmax[static_cast<int64_t>(r) * F + f0 + v] = am[v];
-        }
-    }
-}
-
-// Backward over source rows c (transposed neighbourhood lists, GS_PK_TIDX
-// encoding): self-row gradient + mean/max routing, then the relu mask of the
-// layer that produced these rows.  Fixed order, no atomics.
-template <int OP, int VEC, int G>
-__global__ __launch_bounds__(kBlock) void agg_bwd_kernel(
-    int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,
-    const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
-    int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
-    float* __restrict__ dH) {
-    const int gl = threadIdx.x % G;
-    const int c = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-    if (c >= n_src) return;
-    const int beg = tptr[c], end = tptr[c + 1];
-    for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
-        const bool act = f0 < F;
-        float g[VEC];
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) g[v] = 0.f;
-        for (int t = beg; t < end; ++t) {
-            const int e = tidx[t];
-            if (!act) continue;
-            float x[VEC];
-            if (e < 0) {
-                if (!dSelf) continue;  // gcn: self rows feed no linear input
-                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0, x);
-#pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += x[v];
-            } else if (OP == GS_AGG_MEAN) {
-                const float w = 1.0f / static_cast<float>(ptr[e + 1] - ptr[e]);
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
-#pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += x[v] * w;
-            } else {
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
-#pragma unroll
-                for (int v = 0; v < VEC; ++v)
-                    if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += x[v];
-            }
-        }
-        if (!act) continue;
-        if (Hprev) {
-            float h[VEC];
-            RowIO<float, VEC>::load(Hprev + static_cast<int64_t>(c) * ldh + f0, h);
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) g[v] = h[v] > 0.f ? g[v] : 0.f;
-        }
-        RowIO<float, VEC>::store(dH + static_cast<int64_t>(c) * ldh + f0, g);
-    }
-}
-
-static int pick_group(int F, int vec) {
-    const int lanes = (F + vec - 1) / vec;
-    int g = 16;
-    while (g < lanes && g < 64) g <<= 1;
-    return g;
-}
 
 template <int OP, typename T, bool EXPAND>
 static void launch_fwd(int vec, const T* X, int64_t ldx, int F, int n_dst, const int* ptr,
@@ -193,15 +10,15 @@ static void launch_fwd(int vec, const T* X, int64_t ldx, int F, int n_dst, const
     constexpr int V = sizeof(T) == 4 ? 4 : 8;
     if (vec == 1) {
         const dim3 grid((n_dst + (kBlock / 64) - 1) / (kBlock / 64));
-        agg_fwd_kernel<OP, T, 1, 64, EXPAND><<<grid, kBlock, 0, st>>>(X, ldx, F, n_dst, ptr, idx, row_ptr,
-                                                                       col, dst_ids, gcn, out, ldo, am);
+        launch_k(agg_fwd_kernel<OP, T, 1, 64, EXPAND>, grid, dim3(kBlock), 0, st, X, ldx, F, n_dst, ptr, idx, row_ptr,
+                 col, dst_ids, gcn, out, ldo, am);
         return;
     }
     const int G = pick_group(F, V);
     const dim3 grid((n_dst + (kBlock / G) - 1) / (kBlock / G));
-#define GS_AGG_FWD(GG)                                                                              \
-    agg_fwd_kernel<OP, T, V, GG, EXPAND><<<grid, kBlock, 0, st>>>(X, ldx, F, n_dst, ptr, idx, row_ptr, \
-                                                                   col, dst_ids, gcn, out, ldo, am)
+#define GS_AGG_FWD(GG)                                                                                   \
+    launch_k(agg_fwd_kernel<OP, T, V, GG, EXPAND>, grid, dim3(kBlock), 0, st, X, ldx, F, n_dst, ptr, idx, row_ptr, \
+             col, dst_ids, gcn, out, ldo, am)
     if (G == 16) GS_AGG_FWD(16);
     else if (G == 32) GS_AGG_FWD(32);
     else GS_AGG_FWD(64);

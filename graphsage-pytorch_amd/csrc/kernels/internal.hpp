@@ -1,0 +1,67 @@
+#pragma once
+// Internal launchers shared between the kernel translation units and the
+// trainer (step.hip).  Not part of the C-ABI: they throw gs::Error and take
+// hipStream_t directly.
+#include "kcommon.hpp"
+
+namespace gs {
+
+// linear.hip
+int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
+                    const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
+                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st);
+void sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
+int sum_slabs_grid(int64_t len);
+
+// misc.hip
+int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,
+                    const int32_t* labels, const int32_t* roots, int32_t mask_relu, float* dE, float* ws,
+                    hipStream_t st);
+void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart, int pstride, float* params,
+                    float* grads, const float* part, float grad_scale, float max_norm, float lr, hipStream_t st);
+
+// bwd.hip: the backward of one layer l >= 2 (fp32 activations, relu already
+// folded into dZ) in two launches, each running independent kernels side by
+// side in one grid (every boundary between dependent launches costs the
+// stream a drain and a dispatch, ~2-3 us measured):
+//   A: dW_l row slabs | dIn_l = dZ_l · W_l | (top layer) classifier reduce
+//   B: dW_l = Σ slabs (+ its norm partials) | agg backward into dH_{l-1}
+struct LayerBwd {
+    int64_t n, fin, H;                    // rows, input width per concat half, output width
+    const float* Xs;                      // self rows source (nullptr: gcn), row stride ldxs
+    int64_t ldxs;
+    const int32_t* sidx;                  // self row of each output row
+    const float* A;                       // aggregate [n][fin]
+    const float* dZ;                      // [n][H], already masked by relu'
+    const float* W;                       // [H][K]
+    float* dW;                            // [H][K] gradient
+    float* slabs;                         // dW row slabs workspace
+    int64_t slab_bytes;
+    float* dIn;                           // [n][K] input gradient ([dSelf | dA], or dA when gcn)
+    int agg;                              // GS_AGG_MEAN / GS_AGG_MAX
+    int64_t n_src;                        // rows of the previous layer
+    const int32_t* tptr;                  // transposed neighbourhoods (GS_PK_TPTR / TIDX)
+    const int32_t* tidx;
+    const int32_t* ptr;                   // forward neighbourhood offsets (mean weights)
+    const int32_t* argmax;                // MAX routing, [n][H]
+    const float* Hprev;                   // previous layer's output (relu mask), [n_src][H]
+    float* dH;                            // [n_src][H] gradient of the previous layer's output (masked)
+};
+
+struct ClsReduce {
+    int64_t B, D, C;
+    int n_row_blocks;
+    const float* slab;
+    float* dWc;
+    float* dbc;
+    float* loss;
+    float* part;                          // norm partials of (dWc, dbc), one per reduce block
+};
+
+bool layer_bwd_fusable(const LayerBwd& a);
+int cls_reduce_grid(int64_t C, int64_t D);
+// Returns the number of norm partials written to `part` (0 when the weight
+// gradient fits one slab and was written directly: no partials).
+int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t st);
+
+}  // namespace gs

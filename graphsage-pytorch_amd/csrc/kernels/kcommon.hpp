@@ -3,6 +3,7 @@
 // the launch-status check used by every C-ABI launcher.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -74,6 +75,26 @@ struct RowIO<bf16_t, 1> {
     static __device__ __forceinline__ void store(bf16_t* p, const float (&v)[1]) { *p = f2bf(v[0]); }
 };
 
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Sum of v over the (<= 1024-thread) block, written by thread 0 to *dst.
+// Every thread of the block must call it.
+__device__ __forceinline__ void block_sum_to(float v, float* dst) {
+    __shared__ float red[16];
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < static_cast<int>(blockDim.x + 63) / 64; ++w) t += red[w];
+        *dst = t;
+    }
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline void check_launch(const char* what) {
@@ -82,5 +103,26 @@ inline void check_launch(const char* what) {
 }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Kernel-bound timing: when armed (by the trainer's roofline timer), the next
+// launch through launch_k binds the two events to its own dispatch packet
+// (hipExtLaunchKernel), so their elapsed time is the kernel's begin-to-end
+// span, the quantity rocprofv3's kernel trace reports, without the marker
+// packets' dispatch overhead.  Cleared by that launch.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+inline thread_local LaunchEvents g_launch_events;
+
+template <typename... KArgs, typename... Args>
+inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
+    LaunchEvents ev = g_launch_events;
+    if (ev.start) {
+        g_launch_events = {};
+        hipExtLaunchKernelGGL(kernel, grid, block, smem, st, ev.start, ev.stop, 0, static_cast<KArgs>(args)...);
+    } else {
+        kernel<<<grid, block, smem, st>>>(static_cast<KArgs>(args)...);
+    }
+}
 
 }  // namespace gs

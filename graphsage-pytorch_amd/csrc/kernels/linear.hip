@@ -1,419 +1,13 @@
-// SageLayer (models.py:189-220) on CDNA4 matrix cores.
-//   forward : out = relu([Xs[sidx] | A] · Wᵀ)      (:216 cat self-first, :219)
-//   backward: dW = dZᵀ · [Xs[sidx] | A],  dIn = dZ · W,  dZ = dOut ⊙ (out > 0)
-// The concat is never materialised: a K chunk reads its first F columns from
-// the gathered self rows and the rest from the aggregate.  fp32 inputs run on
-// v_mfma_f32_16x16x4_f32 (exact f32 products, fp32 accumulate); bf16 inputs on
-// v_mfma_f32_16x16x32_bf16 with fp32 accumulate.
-//
-// These GEMMs are skinny (n ~ 0.5-30k rows, H <= 256, K <= a few thousand),
-// so what sets their time is how many dependent memory round trips a wave
-// waits through, not MFMA issue.  Every load below is therefore branch-free
-// (addresses clamped into range, values masked with a select afterwards) so
-// the compiler can keep a whole chunk's loads in flight, and each K (or row)
-// chunk's loads are issued one chunk ahead, under the MFMAs of the current
-// one, with a single workgroup barrier per chunk.
-#include <algorithm>
-
-#include "kcommon.hpp"
+// C-ABI launchers of the SageLayer kernels (kernels/linear_dev.hpp).
+#include "internal.hpp"
+#include "linear_dev.hpp"
 
 namespace gs {
 
-constexpr int kThreads = 256;  // 4 wavefronts
-constexpr int kSlots = 16;     // 16-byte slots per row per K chunk (64 fp32 / 128 bf16)
-
-// One 16-byte slot of the virtual concat row [self | agg] starting at element
-// k; zeros at and past K.  VLOAD: F, strides and bases are 16-byte aligned,
-// so a slot never straddles the self/agg seam.
-template <typename T, bool HAS_SELF, bool VLOAD>
-__device__ __forceinline__ uint4 concat_slot(const T* srow, const T* arow, int F, int K, int k) {
-    constexpr int EPV = 16 / sizeof(T);
-    if constexpr (VLOAD) {
-        const bool in = k < K;
-        const int kk = in ? k : 0;
-        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
-        const uint4 v = *reinterpret_cast<const uint4*>(p);
-        return in ? v : make_uint4(0, 0, 0, 0);
-    } else {
-        T e[EPV];
-#pragma unroll
-        for (int q = 0; q < EPV; ++q) {
-            const int k1 = k + q;
-            const bool in = k1 < K;
-            const int kk = in ? k1 : 0;
-            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
-            e[q] = in ? x : T(0);
-        }
-        uint4 v;
-        __builtin_memcpy(&v, e, 16);
-        return v;
-    }
-}
-
-// 4 consecutive elements of the concat row as floats (dW operand).
-template <typename T, bool HAS_SELF, bool VLOAD>
-__device__ __forceinline__ float4 concat_quad(const T* srow, const T* arow, int F, int K, int k) {
-    float v[4];
-    if constexpr (VLOAD) {
-        const bool in = k < K;
-        const int kk = in ? k : 0;
-        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
-        if constexpr (sizeof(T) == 4) {
-            const float4 q = *reinterpret_cast<const float4*>(p);
-            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2*>(p);
-            v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-            v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
-        }
-        if (!in) v[0] = v[1] = v[2] = v[3] = 0.f;
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k1 = k + q;
-            const bool in = k1 < K;
-            const int kk = in ? k1 : 0;
-            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
-            float f;
-            if constexpr (sizeof(T) == 4) f = x;
-            else f = bf2f(x);
-            v[q] = in ? f : 0.f;
-        }
-    }
-    return make_float4(v[0], v[1], v[2], v[3]);
-}
-
-// 4 consecutive floats of a row at column c (< lim masked to 0).  VEC: the
-// row, c and lim are multiples of 4 floats.
-template <bool VEC>
-__device__ __forceinline__ float4 row_quad(const float* row, int c, int lim) {
-    if constexpr (VEC) {
-        const bool in = c < lim;
-        const float4 v = *reinterpret_cast<const float4*>(row + (in ? c : 0));
-        return in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool in = c + q < lim;
-            const float x = row[in ? c + q : 0];
-            v[q] = in ? x : 0.f;
-        }
-        return make_float4(v[0], v[1], v[2], v[3]);
-    }
-}
-
-// Unmasked variants for loops that issue loads well before using them: the
-// address is clamped into range and mask_quad zeroes the out-of-range
-// elements at the point of use (a select right after the load would force a
-// wait for it there).
-template <bool VEC>
-__device__ __forceinline__ float4 row_quad_raw(const float* row, int c, int lim) {
-    if constexpr (VEC) {
-        return *reinterpret_cast<const float4*>(row + (c < lim ? c : 0));
-    } else {
-        float v[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = row[c + q < lim ? c + q : 0];
-        return make_float4(v[0], v[1], v[2], v[3]);
-    }
-}
-
-template <typename T, bool HAS_SELF, bool VLOAD>
-__device__ __forceinline__ float4 concat_quad_raw(const T* srow, const T* arow, int F, int K, int k) {
-    float v[4];
-    if constexpr (VLOAD) {
-        const int kk = k < K ? k : 0;
-        const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
-        if constexpr (sizeof(T) == 4) {
-            const float4 q = *reinterpret_cast<const float4*>(p);
-            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2*>(p);
-            v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-            v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int kk = k + q < K ? k + q : 0;
-            const T x = (HAS_SELF && kk < F) ? srow[kk] : arow[HAS_SELF ? kk - F : kk];
-            if constexpr (sizeof(T) == 4) v[q] = x;
-            else v[q] = bf2f(x);
-        }
-    }
-    return make_float4(v[0], v[1], v[2], v[3]);
-}
-
-__device__ __forceinline__ float4 mask_quad(float4 v, int c, int lim) {
-    v.x = c < lim ? v.x : 0.f; v.y = c + 1 < lim ? v.y : 0.f;
-    v.z = c + 2 < lim ? v.z : 0.f; v.w = c + 3 < lim ? v.w : 0.f;
-    return v;
-}
-
-__device__ __forceinline__ float4 relu_mask(float4 z, float4 o) {
-    z.x = o.x > 0.f ? z.x : 0.f; z.y = o.y > 0.f ? z.y : 0.f;
-    z.z = o.z > 0.f ? z.z : 0.f; z.w = o.w > 0.f ? z.w : 0.f;
-    return z;
-}
-
-template <typename T>
-__device__ __forceinline__ f32x4 mfma_slot(uint4 a, uint4 b, f32x4 acc) {
-    if constexpr (sizeof(T) == 4) {
-        // k-slots permuted identically on both operands: MFMA j sums element j
-        // of the four kq lanes' slots, so the four MFMAs cover all 16 k.
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-    } else {
-        s16x8 a8, b8;
-        __builtin_memcpy(&a8, &a, 16);
-        __builtin_memcpy(&b8, &b, 16);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, b8, acc, 0, 0, 0);
-    }
-    return acc;
-}
-
-// ---------------------------------------------------------------- forward
-// Block = 16 rows x 64 output columns (wave w: columns 16·(4·by + w) ..).
-// Per K chunk each thread loads one slot of the 16-row concat tile into a
-// two-buffer LDS ring (shared by the 4 waves) and each lane loads the four
-// W slots its MFMAs consume straight into registers (W rows are private to a
-// wave).  Lane (r, kq) feeds MFMA group g with slot 4g + kq of row r.
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD>
-__global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
-    int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
-    const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo) {
-    constexpr int EPV = 16 / sizeof(T);
-    constexpr int BK = kSlots * EPV;
-    constexpr int SA = kSlots + 1;  // LDS row pitch in slots: rows land 4 banks apart
-    __shared__ uint4 sA[2][16 * SA];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 15, kq = lane >> 4;
-    const int m0 = blockIdx.x * 16;
-    const int ct = blockIdx.y * 4 + wave;
-    const int ar = tid >> 4, as = tid & 15;
-    const int arow_i = min(m0 + ar, n - 1);
-    const T* arow = A + static_cast<int64_t>(arow_i) * lda;
-    const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
-    const T* wrow = W + static_cast<int64_t>(min(ct * 16 + r, H - 1)) * K;
-    const int nC = (K + BK - 1) / BK;
-
-    uint4 a_nx = concat_slot<T, HAS_SELF, VLOAD>(srow, arow, F, K, as * EPV);
-    uint4 w_nx[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) w_nx[g] = concat_slot<T, false, VLOAD>(nullptr, wrow, K, K, (4 * g + kq) * EPV);
-    sA[0][ar * SA + as] = a_nx;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nC; ++c) {
-        uint4 w_cur[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) w_cur[g] = w_nx[g];
-        __syncthreads();
-        // next chunk (the last iteration re-reads its own chunk; discarded)
-        const int kn = min(c + 1, nC - 1) * BK;
-        a_nx = concat_slot<T, HAS_SELF, VLOAD>(srow, arow, F, K, kn + as * EPV);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) w_nx[g] = concat_slot<T, false, VLOAD>(nullptr, wrow, K, K, kn + (4 * g + kq) * EPV);
-        __builtin_amdgcn_sched_barrier(0);  // prefetch issued ahead of the chunk's LDS reads and MFMAs
-        const uint4* tile = sA[c & 1];
-        uint4 av[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) av[g] = tile[r * SA + 4 * g + kq];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], w_cur[g], acc);
-        __builtin_amdgcn_sched_barrier(0);  // keep the wait for the prefetch behind every MFMA
-        sA[(c + 1) & 1][ar * SA + as] = a_nx;
-    }
-    if (ct * 16 >= H) return;
-    const int col = ct * 16 + r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = m0 + 4 * kq + j;
-        if (row < n) {
-            const float v = acc[j];
-            out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;  // NaN kept, as torch.relu
-        }
-    }
-}
-
-// ------------------------------------------------------------ weight grad
-// dW[h][k] = Σ_i dZ[i][h] · In[i][k].  Block = 64 h x 64 k over one slab of
-// rows (blockIdx.z); wave w owns h rows 16w.. of the tile and 4 k tiles.  Rows
-// stream in chunks of 16 through a two-buffer LDS ring (thread: 4 dZ values
-// and 4 inputs of one row per chunk); the MFMA "k" runs over rows.  Slabs
-// write fp32 partials that sum_slabs_kernel adds in a fixed order.
-constexpr int kDwPitch = 64 + 16;  // rows 16 banks apart: (kq, r) reads of a column hit distinct banks
-constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are staged in LDS)
-
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
-__global__ __launch_bounds__(kThreads) void linear_dw_kernel(
-    int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
-    const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
-    const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
-    __shared__ float sZ[2][16 * kDwPitch];
-    __shared__ float sI[2][16 * kDwPitch];
-    __shared__ int sIdx[HAS_SELF ? kDwMaxSlab : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 15, kq = lane >> 4;
-    const int k0 = blockIdx.x * 64, h0 = blockIdx.y * 64;
-    const int i_beg = blockIdx.z * rows_per_split;
-    const int i_end = min(n, i_beg + rows_per_split);
-    const int nC = (i_end - i_beg + 15) / 16;
-    const int lr = tid >> 4, lq = (tid & 15) * 4;
-    if (HAS_SELF)
-        for (int t = tid; t < i_end - i_beg; t += kThreads) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
-    __syncthreads();
-
-    // Rows past the slab read a valid row and are zeroed at the LDS store
-    // (both operands: 0 · NaN would not vanish).
-    auto load = [&](int c, float4& z, float4& o, float4& x) {
-        const int t = min(16 * c + lr, i_end - i_beg - 1);
-        const int ic = i_beg + t;
-        z = row_quad_raw<ZVEC>(dout + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
-        if (RELU) o = row_quad_raw<ZVEC>(out + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
-        const T* arow = A + static_cast<int64_t>(ic) * lda;
-        const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sIdx[t]) * ldxs : nullptr;
-        x = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
-    };
-    auto stash = [&](int c, int buf, float4 z, float4 o, float4 x) {
-        z = mask_quad(z, h0 + lq, H);
-        if (RELU) z = relu_mask(z, o);
-        x = mask_quad(x, k0 + lq, K);
-        if (16 * c + lr >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(&sZ[buf][lr * kDwPitch + lq]) = z;
-        *reinterpret_cast<float4*>(&sI[buf][lr * kDwPitch + lq]) = x;
-    };
-    float4 z, o, x;
-    load(0, z, o, x);
-    stash(0, 0, z, o, x);
-    f32x4 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nC; ++c) {
-        __syncthreads();
-        const int cn = min(c + 1, nC - 1);
-        load(cn, z, o, x);
-        __builtin_amdgcn_sched_barrier(0);  // loads issue before the chunk's LDS reads and MFMAs
-        const float* tz = sZ[c & 1];
-        const float* ti = sI[c & 1];
-        float a[4], b[4][4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int row = 4 * s + kq;
-            a[s] = tz[row * kDwPitch + wave * 16 + r];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) b[s][t] = ti[row * kDwPitch + t * 16 + r];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        stash(cn, (c + 1) & 1, z, o, x);
-    }
-    float* slab = dst + static_cast<int64_t>(blockIdx.z) * split_stride;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const int k = k0 + t * 16 + r;
-        if (k >= K) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int h = h0 + wave * 16 + 4 * kq + j;
-            if (h < H) slab[static_cast<int64_t>(h) * K + k] = acc[t][j];
-        }
-    }
-}
-
-// out[i] = Σ_s slabs[s][i], fixed order; 4 elements per thread.
 __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __restrict__ slabs, int S,
-                                                             int64_t len, float* __restrict__ out) {
-    const int64_t n4 = len / 4;
-    for (int64_t i = blockIdx.x * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * kThreads) {
-        float4 s = *reinterpret_cast<const float4*>(slabs + 4 * i);
-#pragma unroll 4
-        for (int t = 1; t < S; ++t) {
-            const float4 v = *reinterpret_cast<const float4*>(slabs + t * len + 4 * i);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-        }
-        *reinterpret_cast<float4*>(out + 4 * i) = s;
-    }
-    for (int64_t i = 4 * n4 + blockIdx.x * int64_t(kThreads) + threadIdx.x; i < len; i += int64_t(gridDim.x) * kThreads) {
-        float s = 0.f;
-        for (int t = 0; t < S; ++t) s += slabs[t * len + i];
-        out[i] = s;
-    }
-}
-
-// ------------------------------------------------------------- input grad
-// dIn[i][k] = Σ_h dZ[i][h] · W[h][k].  Wave = 16 rows x 16 k columns, block =
-// 4 waves along k, no LDS: lane (r, kq) loads dZ[r][16g + 4kq ..+4] as one
-// quad and the matching four W[h][k] values, 8 groups of h in flight at once.
-template <bool HAS_SELF, bool RELU, bool ZVEC>
-__global__ __launch_bounds__(kThreads) void linear_dx_kernel(
-    int n, int F, int H, int K, const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo,
-    const float* __restrict__ W, float* __restrict__ dSelf, float* __restrict__ dA, int64_t ldd) {
-    constexpr int G = 8;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r = lane & 15, kq = lane >> 4;
-    const int m0 = blockIdx.x * 16;
-    const int kt = blockIdx.y * 4 + wave;
-    const int kc = min(kt * 16 + r, K - 1);
-    const int row = min(m0 + r, n - 1);
-    const float* zrow = dout + static_cast<int64_t>(row) * ldo;
-    const float* orow = out + static_cast<int64_t>(row) * ldo;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int h0 = 0; h0 < H; h0 += 16 * G) {
-        float4 z[G];
-        float w[G][4];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int hb = h0 + 16 * g + 4 * kq;
-            z[g] = row_quad<ZVEC>(zrow, hb, H);
-            if (RELU) z[g] = relu_mask(z[g], row_quad<ZVEC>(orow, hb, H));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool in = hb + j < H;
-                const float v = W[static_cast<int64_t>(in ? hb + j : 0) * K + kc];
-                w[g][j] = in ? v : 0.f;
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].x, w[g][0], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].y, w[g][1], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].z, w[g][2], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(z[g].w, w[g][3], acc, 0, 0, 0);
-        }
-    }
-    const int k = kt * 16 + r;
-    if (k >= K) return;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int i = m0 + 4 * kq + j;
-        if (i >= n) continue;
-        if (HAS_SELF && k < F) dSelf[static_cast<int64_t>(i) * ldd + k] = acc[j];
-        else dA[static_cast<int64_t>(i) * ldd + (HAS_SELF ? k - F : k)] = acc[j];
-    }
-}
-
-// Row slabs of the weight gradient: enough (64 h x 64 k) x slab workgroups to
-// fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
-constexpr int kDwTargetBlocks = 256;
-
-static int dw_rows_per_split(int64_t n, int64_t K, int64_t H) {
-    const int64_t tiles = ((K + 63) / 64) * ((H + 63) / 64);
-    const int64_t want = std::max<int64_t>(1, (kDwTargetBlocks + tiles - 1) / tiles);
-    const int64_t cap = std::max<int64_t>(1, n / 64);
-    const int64_t S = std::max(std::min(want, cap), (n + kDwMaxSlab - 1) / kDwMaxSlab);
-    const int64_t rows = (n + S - 1) / S;
-    return static_cast<int>(std::min<int64_t>(kDwMaxSlab, std::max<int64_t>(16, (rows + 15) / 16 * 16)));
-}
-
-static int dw_splits(int64_t n, int64_t K, int64_t H) {
-    const int rps = dw_rows_per_split(n, K, H);
-    return static_cast<int>(std::max<int64_t>(1, (n + rps - 1) / rps));
+                                                             int64_t len, float* __restrict__ out,
+                                                             float* __restrict__ part) {
+    sum_slabs_body(blockIdx.x, gridDim.x, slabs, S, len, out, part);
 }
 
 }  // namespace gs
@@ -464,20 +58,23 @@ int64_t gs_sage_linear_bwd_weight_ws(int64_t n, int64_t K, int64_t H) {
     return S > 1 ? static_cast<int64_t>(S) * K * H * 4 : 0;
 }
 
-int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
-                              const int32_t* sidx, const void* A, int64_t lda, const float* dout,
-                              const float* out, int64_t ldo, int32_t relu, float* dW, void* ws,
-                              int64_t ws_bytes, void* stream) {
-    GS_API_BEGIN
-    using namespace gs;
+}  // extern "C"
+
+namespace gs {
+
+// The row-slab launch of the weight gradient.  Returns the slab count S:
+// S == 1 wrote dW directly, S > 1 left S partial slabs in ws for the caller
+// to add (sum_slabs_kernel, or a fused launch in bwd.hip).
+int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
+                    const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
+                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st) {
     GS_REQUIRE(dt == GS_F32 || dt == GS_BF16, GS_EINVAL, "dtype must be f32 or bf16");
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1 && H <= 4096, GS_EINVAL, "bad sizes");
     const bool self = Xs != nullptr;
     const int64_t K = self ? 2 * F : F;
-    hipStream_t st = as_stream(stream);
     if (n == 0) {
         GS_REQUIRE(hipMemsetAsync(dW, 0, H * K * 4, st) == hipSuccess, GS_EHIP, "memset failed");
-        return GS_OK;
+        return 1;
     }
     GS_REQUIRE(A && dout && dW && (out || !relu), GS_EINVAL, "NULL device pointer");
     const int S = dw_splits(n, K, H);
@@ -514,12 +111,27 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
 #undef GS_LDW_Z
 #undef GS_LDW1
     check_launch("gs_sage_linear_bwd_weight");
-    if (S > 1) {
-        const int64_t len = H * K;
-        const dim3 g2(static_cast<unsigned>(std::min<int64_t>((len / 4 + kThreads - 1) / kThreads + 1, 2048)));
-        sum_slabs_kernel<<<g2, kThreads, 0, st>>>(target, S, len, dW);
-        check_launch("gs_sage_linear_bwd_weight(sum)");
-    }
+    return S;
+}
+
+void sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st) {
+    sum_slabs_kernel<<<dim3(sum_slabs_blocks(len)), kThreads, 0, st>>>(slabs, S, len, out, part);
+    check_launch("sum_slabs");
+}
+
+}  // namespace gs
+
+extern "C" {
+
+int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
+                              const int32_t* sidx, const void* A, int64_t lda, const float* dout,
+                              const float* out, int64_t ldo, int32_t relu, float* dW, void* ws,
+                              int64_t ws_bytes, void* stream) {
+    GS_API_BEGIN
+    using namespace gs;
+    hipStream_t st = as_stream(stream);
+    const int S = linear_dw_slabs(dt, n, F, H, Xs, ldxs, sidx, A, lda, dout, out, ldo, relu, dW, ws, ws_bytes, st);
+    if (S > 1) sum_slabs_launch(static_cast<const float*>(ws), S, H * (Xs ? 2 * F : F), dW, nullptr, st);
     GS_API_END
 }
 

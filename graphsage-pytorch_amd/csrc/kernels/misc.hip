@@ -4,7 +4,7 @@
 #include <algorithm>
 #include <cmath>
 
-#include "kcommon.hpp"
+#include "cls_dev.hpp"
 
 namespace gs {
 
@@ -37,11 +37,6 @@ __global__ __launch_bounds__(kTb) void cast_bf16_kernel(const float* in, bf16_t*
         out[i] = f2bf(in[i]);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 // ------------------------------------------------------- classifier + NLL
 // One block of 16 waves per R rows, one wave per row.  Wc is staged in LDS
@@ -79,6 +74,11 @@ inline ClsPlan cls_plan(int64_t C, int64_t D) {
     return p;
 }
 
+// FAST: the block's E rows and Wc are at most one float4 per thread each and
+// 16-byte aligned, so the prologue is straight-line: the roots load, the E
+// and Wc loads and the bias issue together, the labels load follows the roots
+// alone, and nothing waits before the LDS stores (two dependent rounds).
+template <bool FAST>
 __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
     int B, int D, int C, int R, int wc_lds, const float* __restrict__ E, const float* __restrict__ Wc,
     const float* __restrict__ bc, const int* __restrict__ labels, const int* __restrict__ roots, int mask_relu,
@@ -98,10 +98,35 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
     // (addresses clamped, values selected afterwards: no load sits behind a
     // branch, so they all overlap instead of each waiting for the previous)
     const int wr_ = min(w, nr - 1);
-    const int y_w = labels[roots ? roots[r0 + wr_] : r0 + wr_];
-    const float b_lane = bc[min(cl, C - 1)];
     const int nE = nr * D, nW = wc_lds ? C * D : 0;
     const int tid = static_cast<int>(threadIdx.x);
+    int y_w;
+    float b_lane;
+    if constexpr (FAST) {
+        // stores are unconditional (out-of-range threads write a dump slot):
+        // a predicated store would let the compiler sink its load behind a
+        // branch, and the branch join would wait for every load in flight
+        __shared__ float dump[4];
+        const int root = roots[r0 + wr_];
+        const float4 ev = reinterpret_cast<const float4*>(E + static_cast<int64_t>(r0) * D)[min(tid, nE / 4 - 1)];
+        const float4 wv = reinterpret_cast<const float4*>(Wc)[min(tid, C * D / 4 - 1)];
+        b_lane = bc[min(cl, C - 1)];
+        y_w = labels[root];
+        const int t = 4 * tid;
+        const bool in = t < nE;
+        float* de = t < R * D ? sE + t : dump;
+        de[0] = in ? ev.x : 0.f;
+        de[1] = in ? ev.y : 0.f;
+        de[2] = in ? ev.z : 0.f;
+        de[3] = in ? ev.w : 0.f;
+        float* dw = t < nW ? sW + t + t / D : dump;  // D % 4 == 0: the quad stays in one row
+        dw[0] = wv.x;
+        dw[1] = wv.y;
+        dw[2] = wv.z;
+        dw[3] = wv.w;
+    } else {
+    y_w = labels[roots ? roots[r0 + wr_] : r0 + wr_];
+    b_lane = bc[min(cl, C - 1)];
     for (int t0 = 0; t0 < R * D; t0 += 4 * kClsThreads) {
         float v[4];
 #pragma unroll
@@ -121,6 +146,7 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
             const int t = t0 + q * kClsThreads + tid;
             if (t < nW) sW[t + t / D] = v[q];
         }
+    }
     }
     __syncthreads();
     const float* W = wc_lds ? sW : Wc;
@@ -179,30 +205,14 @@ __global__ __launch_bounds__(kClsThreads) void cls_rows_kernel(
     }
 }
 
-__global__ __launch_bounds__(kTb) void cls_reduce_kernel(int B, int D, int C, int n_blocks,
-                                                         const float* __restrict__ slab, float* __restrict__ dWc,
-                                                         float* __restrict__ dbc, float* __restrict__ loss) {
-    const int per = C * (D + 1);
-    const int t = blockIdx.x * kTb + threadIdx.x;
-    if (t > per) return;
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < n_blocks; ++k) s += slab[static_cast<int64_t>(k) * (per + 1) + t];
-    if (t == per) {
-        loss[0] = s / static_cast<float>(B);  // -sum(logp[i, y_i]) / B  (utils.py:162-163)
-        return;
-    }
-    const int c = t / (D + 1), d = t - c * (D + 1);
-    if (d < D) dWc[static_cast<int64_t>(c) * D + d] = s;
-    else dbc[c] = s;
+__global__ __launch_bounds__(kClsRedThreads) void cls_reduce_kernel(int B, int D, int C, int n_blocks,
+                                                                    const float* __restrict__ slab,
+                                                                    float* __restrict__ dWc, float* __restrict__ dbc,
+                                                                    float* __restrict__ loss) {
+    cls_reduce_body(blockIdx.x, B, D, C, n_blocks, slab, dWc, dbc, loss, nullptr);
 }
 
 // ------------------------------------------------------- clip + SGD
-struct Groups {
-    int64_t off[9];
-    int n;
-};
-
 constexpr int kNormBlocks = 64;
 
 __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float* __restrict__ g, float* __restrict__ part) {
@@ -210,6 +220,7 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
     const int grp = blockIdx.y;
     const int64_t lo = G.off[grp], hi = G.off[grp + 1];
     float s = 0.f;
+#pragma unroll 8
     for (int64_t i = lo + blockIdx.x * int64_t(kTb) + threadIdx.x; i < hi; i += int64_t(kNormBlocks) * kTb) {
         const float v = g[i];
         s = fmaf(v, v, s);
@@ -220,7 +231,7 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
     if (threadIdx.x == 0) {
         float t = 0.f;
         for (int w = 0; w < kTb / 64; ++w) t += red[w];
-        part[grp * kNormBlocks + blockIdx.x] = t;
+        part[grp * G.pstride + blockIdx.x] = t;
     }
 }
 
@@ -232,11 +243,20 @@ __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ 
                                                   const float* __restrict__ part, float scale, float max_norm,
                                                   float lr) {
     __shared__ float mult[8];
-    if (threadIdx.x < G.n) {
+    // wave w folds group w (lane-strided loads, all in flight, then a fixed
+    // xor-tree): the same order in every block
+    const int lane = threadIdx.x & 63;
+    for (int grp = threadIdx.x >> 6; grp < G.n; grp += kTb / 64) {
+        const float* pg = part + grp * G.pstride;
+        const int np = G.npart[grp];
         float t = 0.f;
-        for (int b = 0; b < kNormBlocks; ++b) t += part[threadIdx.x * kNormBlocks + b];
-        const float norm = sqrtf(t) * scale;
-        mult[threadIdx.x] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+#pragma unroll 4
+        for (int b = lane; b < np; b += 64) t += pg[b];
+        t = wave_sum(t);
+        if (lane == 0) {
+            const float norm = sqrtf(t) * scale;
+            mult[grp] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+        }
     }
     __syncthreads();
     const int64_t total = G.off[G.n];
@@ -293,6 +313,49 @@ int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C) {
     return nb * (C * (D + 1) + 1);
 }
 
+}  // extern "C"
+
+namespace gs {
+
+int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,
+                    const int32_t* labels, const int32_t* roots, int32_t mask_relu, float* dE, float* ws,
+                    hipStream_t st) {
+    GS_REQUIRE(B >= 1 && D >= 1 && C >= 1 && B < (1 << 30), GS_EINVAL, "bad sizes");
+    GS_REQUIRE(C + D + 1 <= kClsLdsFloats, GS_EINVAL, "classes + embedding dims too large");
+    GS_REQUIRE(E && Wc && bc && labels && dE && ws, GS_EINVAL, "NULL device pointer");
+    const int b = static_cast<int>(B), d = static_cast<int>(D), c = static_cast<int>(C);
+    const ClsPlan plan = cls_plan(C, D);
+    const int nb = (b + plan.rows - 1) / plan.rows;
+    const bool fast = roots && D % 4 == 0 && plan.rows * D <= 4 * kClsThreads && C * D <= 4 * kClsThreads &&
+                      aligned16(E) && aligned16(Wc);
+    if (fast)
+        cls_rows_kernel<true><<<dim3(nb), kClsThreads, plan.smem, st>>>(b, d, c, plan.rows, plan.wc_lds ? 1 : 0, E, Wc,
+                                                                        bc, labels, roots, mask_relu, dE, ws);
+    else
+        cls_rows_kernel<false><<<dim3(nb), kClsThreads, plan.smem, st>>>(b, d, c, plan.rows, plan.wc_lds ? 1 : 0, E,
+                                                                         Wc, bc, labels, roots, mask_relu, dE, ws);
+    check_launch("cls_rows");
+    return nb;
+}
+
+void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart, int pstride, float* params,
+                    float* grads, const float* part, float grad_scale, float max_norm, float lr, hipStream_t st) {
+    GS_REQUIRE(n_groups >= 1 && n_groups <= 8, GS_EINVAL, "1..8 parameter groups");
+    Groups G;
+    G.n = n_groups;
+    G.pstride = pstride;
+    for (int i = 0; i < n_groups; ++i) G.npart[i] = npart[i];
+    for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
+    const int64_t total = G.off[n_groups];
+    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
+    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+    check_launch("sgd");
+}
+
+}  // namespace gs
+
+extern "C" {
+
 int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,
                        const int32_t* labels, const int32_t* roots, int32_t mask_relu, float* loss, float* dE,
                        float* dWc, float* dbc, float* ws, void* stream) {
@@ -303,12 +366,8 @@ int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E, const fl
     GS_REQUIRE(E && Wc && bc && labels && loss && dE && dWc && dbc && ws, GS_EINVAL, "NULL device pointer");
     hipStream_t st = as_stream(stream);
     const int b = static_cast<int>(B), d = static_cast<int>(D), c = static_cast<int>(C);
-    const ClsPlan plan = cls_plan(C, D);
-    const int nb = (b + plan.rows - 1) / plan.rows;
-    cls_rows_kernel<<<dim3(nb), kClsThreads, plan.smem, st>>>(b, d, c, plan.rows, plan.wc_lds ? 1 : 0, E, Wc, bc,
-                                                              labels, roots, mask_relu, dE, ws);
-    const int per = c * (d + 1) + 1;
-    cls_reduce_kernel<<<dim3((per + kTb - 1) / kTb), kTb, 0, st>>>(b, d, c, nb, ws, dWc, dbc, loss);
+    const int nb = cls_rows_launch(B, D, C, E, Wc, bc, labels, roots, mask_relu, dE, ws, st);
+    cls_reduce_kernel<<<dim3(cls_reduce_blocks(C, D)), kClsRedThreads, 0, st>>>(b, d, c, nb, ws, dWc, dbc, loss);
     check_launch("gs_cls_nll_fwd_bwd");
     GS_API_END
 }
@@ -321,6 +380,8 @@ int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params, float
     GS_REQUIRE(params && grads && ws, GS_EINVAL, "NULL device pointer");
     Groups G;
     G.n = n_groups;
+    G.pstride = kNormBlocks;
+    for (int i = 0; i < n_groups; ++i) G.npart[i] = kNormBlocks;
     for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
     for (int i = 0; i < n_groups; ++i) GS_REQUIRE(G.off[i] <= G.off[i + 1], GS_EINVAL, "group offsets not sorted");
     hipStream_t st = as_stream(stream);

@@ -248,9 +248,9 @@ int gs_sage1_fwd(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, 
     hipStream_t st = as_stream(stream);
     const int f = static_cast<int>(F), h = static_cast<int>(H), n = static_cast<int>(n_dst);
 #define GS_S1(OPV, TT, SELF, RELU)                                                                       \
-    sage1_fwd_kernel<OPV, TT, SELF, RELU><<<grid, kS1Threads, smem, st>>>(                                \
-        static_cast<const TT*>(X), ldx, f, h, n, ptr, ent, col, dst_ids, gcn, static_cast<const TT*>(W),  \
-        static_cast<TT*>(agg_out), ld_agg, out, ldo)
+    launch_k(sage1_fwd_kernel<OPV, TT, SELF, RELU>, grid, dim3(kS1Threads), static_cast<uint32_t>(smem), st, \
+             static_cast<const TT*>(X), ldx, f, h, n, ptr, ent, col, dst_ids, gcn, static_cast<const TT*>(W), \
+             static_cast<TT*>(agg_out), ld_agg, out, ldo)
 #define GS_S1_R(OPV, TT, SELF) \
     do { if (relu) GS_S1(OPV, TT, SELF, true); else GS_S1(OPV, TT, SELF, false); } while (0)
 #define GS_S1_S(OPV, TT) \

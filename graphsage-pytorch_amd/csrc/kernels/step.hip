@@ -8,7 +8,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "kcommon.hpp"
+#include "internal.hpp"
 
 struct gs_trainer {
     gs_trainer_config cfg;
@@ -25,7 +25,16 @@ struct gs_trainer {
     static constexpr int kSlots = 3;
     void* a1_slot[kSlots] = {};
     int64_t a1_rows = 0;
+    // clip-norm partials produced by the fused backward's reduce launches
+    // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
+    // consumed by gs_trainer_update_local when no all-reduce came between
+    bool fuse_bwd = true;
+    float* norm_part = nullptr;
+    int pstride = 0;
+    int npart[2] = {0, 0};
+    bool norm_ready = false;
     ~gs_trainer() {
+        if (norm_part) (void)hipFree(norm_part);
         for (auto e : ev0) (void)hipEventDestroy(e);
         for (auto e : ev1) (void)hipEventDestroy(e);
         for (void* p : a1_slot)
@@ -69,12 +78,12 @@ static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes
         return pack + o;
     };
     const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
-    if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+    if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
     ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F,
                   hop_sizes[4 * (L - 1)], fld(GS_PK_POS_PTR), fld(GS_PK_POS), nullptr, c.col, fld(GS_PK_DST_IDS),
                   c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
     if (timed) {
-        GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+        GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
         ++T.n_timed;
     }
 }
@@ -145,12 +154,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const bool fused1 = T.fused1 && a1_slot < 0;
     if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
         const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
-        if (timed) GS_REQUIRE(hipEventRecord(T.ev0[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+        if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
         ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
                         rows[0], fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.col, dst_L, c.gcn, W1, agg[0], F, h[0],
                         H, 1, st));
         if (timed) {
-            GS_REQUIRE(hipEventRecord(T.ev1[T.n_timed], st) == hipSuccess, GS_EHIP, "hipEventRecord");
+            GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
             ++T.n_timed;
         }
     } else if (a1_slot < 0) {
@@ -171,6 +180,70 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                       fld(j, GS_PK_NBR), nullptr, nullptr, nullptr, 0, agg[l - 1], GS_F32, H, am[l - 1], st));
         ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
                               agg[l - 1], H, P + T.w_off[l - 1], h[l - 1], H, 1, st));
+    }
+    T.norm_ready = false;
+    // ---- fused backward (bwd.hip): same kernels and summation order as the
+    // sequence below, two launches per layer >= 2 instead of five
+    if (T.fuse_bwd && L >= 2) {
+        std::vector<LayerBwd> lb;
+        int flip_f = 0;
+        bool fusable = true;
+        for (int l = L; l >= 2; --l) {
+            const int j = L - l + 1;
+            LayerBwd a{};
+            a.n = rows[l - 1];
+            a.fin = H;
+            a.H = H;
+            a.Xs = c.gcn ? nullptr : h[l - 2];
+            a.ldxs = H;
+            a.sidx = fld(j, GS_PK_SELF);
+            a.A = static_cast<const float*>(agg[l - 1]);
+            a.dZ = l == L ? demb : dbuf[flip_f ^ 1];
+            a.W = P + T.w_off[l - 1];
+            a.dW = G + T.w_off[l - 1];
+            a.slabs = reinterpret_cast<float*>(dw_ws);
+            a.slab_bytes = dw_need;
+            a.dIn = dIn;
+            a.agg = c.agg;
+            a.n_src = rows[l - 2];
+            a.tptr = fld(j, GS_PK_TPTR);
+            a.tidx = fld(j, GS_PK_TIDX);
+            a.ptr = fld(j, GS_PK_NBR_PTR);
+            a.argmax = am[l - 1];
+            a.Hprev = h[l - 2];
+            a.dH = dbuf[flip_f];
+            flip_f ^= 1;
+            fusable = fusable && layer_bwd_fusable(a);
+            lb.push_back(a);
+        }
+        if (fusable) {
+            const int cls_rows = cls_rows_launch(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off,
+                                                 c.labels, roots, 1, demb, cls_ws, st);
+            const ClsReduce cr{B, H, c.n_classes, cls_rows, cls_ws, G + T.cls_w_off, G + T.cls_b_off, loss,
+                               T.norm_part + T.pstride};
+            int np = 0;
+            bool parts = true;
+            for (size_t i = 0; i < lb.size(); ++i) {
+                const int n = layer_bwd(lb[i], i == 0 ? &cr : nullptr, T.norm_part + np, st);
+                parts = parts && n > 0;
+                np += n;
+            }
+            const int64_t K1 = T.w_cols[0];
+            const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
+                                           c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0],
+                                           dw_ws, dw_need, st);
+            if (S1 > 1) {
+                sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0], T.norm_part + np,
+                                 st);
+                np += sum_slabs_grid(H * K1);
+            } else {
+                parts = false;
+            }
+            T.npart[0] = np;
+            T.npart[1] = cls_reduce_grid(c.n_classes, H);
+            T.norm_ready = parts && np <= T.pstride && T.npart[1] <= T.pstride;
+            return cv.at;
+        }
     }
     // ---- loss head (models.py:8-27, utils.py:159-164); labels gathered through
     // the roots, and demb comes back already masked by relu'(h_L), i.e. dZ_L
@@ -231,6 +304,17 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
     T->cls_b_off = at;
     at += cfg->n_classes;
     T->total = at;
+    {
+        int64_t np = 0;
+        for (int l = 1; l <= cfg->n_layers; ++l) np += gs::sum_slabs_grid(cfg->hidden * T->w_cols[l - 1]);
+        np = std::max<int64_t>({np, gs::cls_reduce_grid(cfg->n_classes, cfg->hidden), 64});
+        T->pstride = static_cast<int>((np + 63) / 64 * 64);
+        if (hipMalloc(&T->norm_part, 2 * T->pstride * sizeof(float)) != hipSuccess) {
+            delete T;
+            gs::fail(GS_ENOMEM, "hipMalloc(norm partials)");
+        }
+    }
+    T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
     T->fused1 = gs_sage1_fwd_supported(static_cast<gs_dtype>(cfg->feat_dtype), cfg->feat_dim, cfg->hidden,
                                        cfg->gcn) != 0 &&
                 cfg->feat_ld % (cfg->feat_dtype == GS_F32 ? 4 : 8) == 0 && gs::aligned16(cfg->X) &&
@@ -332,9 +416,26 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap) {
     return n;
 }
 
+int gs_trainer_update_local(gs_trainer* t, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t, GS_EINVAL, "NULL argument");
+    const int64_t goff[3] = {0, t->cls_w_off, t->total};
+    if (t->norm_ready) {
+        gs::sgd_with_parts(2, goff, t->npart, t->pstride, t->cfg.params, t->cfg.grads, t->norm_part, 1.0f,
+                           t->cfg.max_norm, t->cfg.lr, gs::as_stream(stream));
+    } else {
+        const int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, 1.0f, t->cfg.max_norm, t->cfg.lr,
+                                   t->norm_part, stream);
+        if (rc != GS_OK) return rc;
+    }
+    t->norm_ready = false;
+    GS_API_END
+}
+
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) {
     GS_API_BEGIN
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
+    t->norm_ready = false;
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);
     if (rc != GS_OK) return rc;

@@ -386,7 +386,9 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
             if (rc != GS_OK) fail(rc, gs_last_error());
         }
-        rc = gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st);
+        rc = r->cfg.world > 1
+                 ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
+                 : gs_trainer_update_local(r->cfg.trainer, st);
         if (rc != GS_OK) fail(rc, gs_last_error());
         hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
         r->dev_busy[k] = true;

@@ -115,8 +115,10 @@ class NativeTrainer:
         """All-reduce (sum) the flat gradients over ranks, then clip + SGD with 1/world."""
         if world_size > 1:
             dist.all_reduce(self.p.grads, group=group)
-        check(lib().gs_trainer_update(self._h, 1.0 / world_size, self.clip_ws.data_ptr(),
-                                      _lib.stream_ptr(self.device)))
+            check(lib().gs_trainer_update(self._h, 1.0 / world_size, self.clip_ws.data_ptr(),
+                                          _lib.stream_ptr(self.device)))
+        else:
+            check(lib().gs_trainer_update_local(self._h, _lib.stream_ptr(self.device)))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -355,6 +355,11 @@ int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack,
                                          void* ws, int64_t ws_bytes, float* loss, void* stream);
 /* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
+/* Single-process update (no all-reduce between the step and the update):
+ * clip per model + SGD from the gradient-norm partials the last forward/
+ * backward left with its gradient reductions (one launch), or as
+ * gs_trainer_update(t, 1, ...) when that backward could not produce them. */
+int gs_trainer_update_local(gs_trainer* t, void* stream);
 /* Measurement only: record HIP events on the launch stream around the next
  * `capacity` layer-1 launches — the fused gather + linear kernel when
  * gs_trainer_layer1_fused(t), else the gather-aggregate; gs_trainer_agg_times
