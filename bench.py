@@ -184,11 +184,12 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=25.0)
     ap.add_argument("--sampler-streams", type=int, default=None,
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
-                         "default: min(8, host cores per GPU - 2))")
+                         "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
+                         "each for the issuing thread, the HIP runtime and RCCL's proxy)")
     args = ap.parse_args()
     if args.sampler_streams is None:
         per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-        args.sampler_streams = max(1, min(8, per_gpu - 2))
+        args.sampler_streams = max(1, min(12, per_gpu - 3))
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:

@@ -160,27 +160,22 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
         for (int64_t r = 1; r < n; ++r)
             u.merge_items(h.set_items.data() + h.set_ptr[r], h.set_ptr[r + 1] - h.set_ptr[r]);
     }
-    // Union-local positions through a dense node -> position map (one int32
-    // per graph node per sampler thread, restored to -1 before returning).
+    // Union-local positions = rank of the key's slot in the union's table
+    // (its iteration order): a probe of that cache-resident table instead of
+    // a graph-sized node -> position array (random DRAM reads and writes).
     GS_PHASE(2);
-    thread_local std::vector<int32_t> pos_of;
-    if (static_cast<int64_t>(pos_of.size()) < g.n_nodes) pos_of.assign(g.n_nodes, -1);
+    thread_local std::vector<int32_t> slot_local;
+    slot_local.resize(u.mask + 1);
     h.src_ids.clear();
     h.src_ids.reserve(u.used);
     for (size_t sl = 0; sl <= u.mask; ++sl) {
         const int32_t key = u.tab[sl];
-        if (key == PySet::EMPTY) continue;
-        pos_of[key] = static_cast<int32_t>(h.src_ids.size());
-        h.src_ids.push_back(key);
+        slot_local[sl] = static_cast<int32_t>(h.src_ids.size());
+        if (key != PySet::EMPTY) h.src_ids.push_back(key);
     }
-    struct Restore {
-        std::vector<int32_t>& m;
-        const std::vector<int64_t>& keys;
-        ~Restore() {
-            for (int64_t k : keys) m[k] = -1;
-        }
-    } restore{pos_of, h.src_ids};
-    auto local_of = [&](int64_t key) -> int32_t { return pos_of[key]; };
+    auto local_of = [&](int64_t key) -> int32_t {
+        return slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(key)))];
+    };
     // Neighbourhoods in union-local ids, ascending (= the dense mask's column
     // order, :305-308); non-gcn removes self (:297-298).
     GS_PHASE(3);
