@@ -1,4 +1,7 @@
 // C-ABI launchers of the SageLayer kernels (kernels/linear_dev.hpp).
+#include <cstdlib>
+#include <string>
+
 #include "internal.hpp"
 #include "linear_dev.hpp"
 
@@ -30,9 +33,25 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     const int EPV = dt == GS_F32 ? 4 : 8;
     const bool vload = F % EPV == 0 && lda % EPV == 0 && (!self || (ldxs % EPV == 0 && aligned16(Xs))) &&
                        aligned16(A) && aligned16(Wd);
-    const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 63) / 64));
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
+    static const bool wide_on = std::getenv("GS_LIN_FWD") && std::string(std::getenv("GS_LIN_FWD")) == "wide";
+    if (wide_on && dt == GS_F32 && vload) {
+        const dim3 gw(static_cast<unsigned>((n + kWideRows - 1) / kWideRows), static_cast<unsigned>((H + 63) / 64));
+        const float* xs = static_cast<const float*>(Xs);
+        const float* a = static_cast<const float*>(A);
+        const float* w = static_cast<const float*>(Wd);
+        if (self) {
+            if (relu) linear_fwd_wide_kernel<true, true><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else linear_fwd_wide_kernel<true, false><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+        } else {
+            if (relu) linear_fwd_wide_kernel<false, true><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else linear_fwd_wide_kernel<false, false><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+        }
+        check_launch("gs_sage_linear_fwd(wide)");
+        return GS_OK;
+    }
+    const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 63) / 64));
 #define GS_LFWD1(TT, SELF, RELU, VL)                                                                     \
     linear_fwd_kernel<TT, SELF, RELU, VL><<<grid, kThreads, 0, st>>>(                                   \
         nn, ff, hh, K, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,          \

@@ -9,7 +9,7 @@
 //                      its pack (ring entry i % 3) and its layer-1 gather on
 //                      a side stream, issued one batch ahead when sampled so
 //                      they run under step i-1; then forward/backward from
-//                      the gathered slot, all-reduce (world > 1) and update
+//                      the gathered slot, all-reduce (with a communicator) and update
 //                      on the caller's stream.
 // A pinned slot returns to its sampler once the copy that read it has
 // completed.  Only the driver thread makes HIP calls: it polls the copy events
@@ -382,11 +382,14 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                                                       pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss, st);
         if (rc != GS_OK) fail(rc, gs_last_error());
         const auto t3 = Clock::now();
-        if (r->cfg.world > 1) {
+        // with a communicator (any world size, so one rank exercises the same
+        // path): sum the gradients, then clip the averaged sum; without one
+        // the clip uses the norm partials of the step's own reductions
+        if (r->cfg.comm) {
             rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
             if (rc != GS_OK) fail(rc, gs_last_error());
         }
-        rc = r->cfg.world > 1
+        rc = r->cfg.comm
                  ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
                  : gs_trainer_update_local(r->cfg.trainer, st);
         if (rc != GS_OK) fail(rc, gs_last_error());

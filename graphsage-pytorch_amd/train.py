@@ -288,9 +288,10 @@ class Communicator:
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             check(lib().gs_comm_unique_id(uid.numpy().ctypes.data))
-        t = uid.to(device)
-        dist.broadcast(t, 0)
-        uid = t.cpu().contiguous()
+        if world > 1:
+            t = uid.to(device)
+            dist.broadcast(t, 0)
+            uid = t.cpu().contiguous()
         h = ctypes.c_void_p()
         check(lib().gs_comm_create(uid.numpy().ctypes.data, world, rank, ctypes.byref(h)))
         self._h = h

@@ -285,3 +285,44 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers):
         b.apply_update()
         torch.testing.assert_close(a.p.params, b.p.params, atol=2e-6, rtol=1e-5)
         b.p.params.copy_(a.p.params)  # keep both on one trajectory
+
+
+def test_rccl_communicator_single_rank(gs):
+    """The native RCCL communicator (gs_comm_*, torch's librccl) on one rank:
+    unique id, init, an in-place sum all-reduce (identity at world 1)."""
+    comm = train.Communicator(0, 1, DEV)
+    x = torch.randn(100003, device=DEV)
+    y = x.clone()
+    from importlib import import_module
+    _l = import_module("graphsage-pytorch_amd._lib")
+    _l.check(_l.lib().gs_comm_allreduce_sum(comm._h, y.data_ptr(), y.numel(), _l.stream_ptr(DEV)))
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    comm.close()
+
+
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_runner_distributed_path_single_rank(gs, agg):
+    """The runner's data-parallel update path (RCCL all-reduce of the flat
+    gradients, clip of the averaged sum via gs_trainer_update) run with a
+    one-rank communicator equals the single-process path (clip from the
+    reductions' norm partials) to fp32 rounding of the norm."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:6]
+    a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
+    b = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
+    ra = train.Runner(a, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
+                      fail_empty=agg == "MAX", depth=2)
+    comm = train.Communicator(0, 1, DEV)
+    rb = train.Runner(b, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
+                      fail_empty=agg == "MAX", depth=2, comm=comm)
+    ra.run(len(batches))
+    rb.run(len(batches))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.p.params, b.p.params, atol=2e-6, rtol=1e-5)
+    assert abs(float(a.loss) - float(b.loss)) < 1e-5
+    ra.close()
+    rb.close()
+    comm.close()

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--F", type=int, default=256)
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--nodes", type=int, default=1 << 21)
+    ap.add_argument("--self-rows", choices=["random", "contiguous"], default="random",
+                    help="layer-1 self rows: random rows of the 2M-row table, or a contiguous n-row block")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -49,6 +51,9 @@ def main():
         A = torch.rand(n, fin, device=dev) - 0.5
         Xs = X if gather else torch.rand(4 * n, fin, device=dev) - 0.5
         sidx = torch.randint(0, Xs.shape[0], (n,), device=dev, dtype=torch.int32)
+        if gather and args.self_rows == "contiguous":
+            Xs = X[:n].clone()
+            sidx = torch.arange(n, device=dev, dtype=torch.int32)
         W = (torch.rand(H, 2 * fin, device=dev) - 0.5) * 0.1
         out = torch.empty(n, H, device=dev)
         dout = torch.randn(n, H, device=dev)
