@@ -35,7 +35,23 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                        aligned16(A) && aligned16(Wd);
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
-    static const bool wide_on = std::getenv("GS_LIN_FWD") && std::string(std::getenv("GS_LIN_FWD")) == "wide";
+    static const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
+    static const bool wide_on = fwd_mode == "wide";
+    if (fwd_mode == "sk" && dt == GS_F32 && vload) {
+        const dim3 gs2(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 31) / 32));
+        const float* xs = static_cast<const float*>(Xs);
+        const float* a = static_cast<const float*>(A);
+        const float* w = static_cast<const float*>(Wd);
+        if (self) {
+            if (relu) linear_fwd_sk_kernel<true, true><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else linear_fwd_sk_kernel<true, false><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+        } else {
+            if (relu) linear_fwd_sk_kernel<false, true><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else linear_fwd_sk_kernel<false, false><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+        }
+        check_launch("gs_sage_linear_fwd(sk)");
+        return GS_OK;
+    }
     if (wide_on && dt == GS_F32 && vload) {
         const dim3 gw(static_cast<unsigned>((n + kWideRows - 1) / kWideRows), static_cast<unsigned>((H + 63) / 64));
         const float* xs = static_cast<const float*>(Xs);

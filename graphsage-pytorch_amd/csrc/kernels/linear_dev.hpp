@@ -303,6 +303,81 @@ __global__ __launch_bounds__(kWideThreads) void linear_fwd_wide_kernel(
     }
 }
 
+// Forward, fp32, split-K inside the block ("sk").  Block = 16 rows x 32
+// output columns, 4 waves; wave w owns K quarter w for both 16-column tiles
+// and issues all of that quarter's A and W slots (up to kSkChunks chunks of 64)
+// before its first MFMA, so a wave waits through one load round, not one per
+// chunk.  The four partial tiles are added in LDS in wave order (fixed, no
+// atomics) and wave 0 applies relu and stores.  Many small blocks (n/16 ·
+// H/32) keep ~4 waves per SIMD to overlap those rounds.
+constexpr int kSkChunks = 2;  // chunks of 64 per wave issued at once (K <= 512 in one round)
+template <bool HAS_SELF, bool RELU>
+__global__ __launch_bounds__(kThreads) void linear_fwd_sk_kernel(
+    int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
+    const float* __restrict__ A, int64_t lda, const float* __restrict__ W, float* __restrict__ out, int64_t ldo) {
+    __shared__ f32x4 red[3][2][64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int m0 = blockIdx.x * 16, c0 = blockIdx.y * 32;
+    const int row_i = min(m0 + r, n - 1);
+    const float* arow = A + static_cast<int64_t>(row_i) * lda;
+    const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[row_i] : row_i) * ldxs : nullptr;
+    const float* w0 = W + static_cast<int64_t>(min(c0 + r, H - 1)) * K;
+    const float* w1 = W + static_cast<int64_t>(min(c0 + 16 + r, H - 1)) * K;
+    const int nC = (K + 63) / 64;
+    const int cq = (nC + 3) / 4;  // chunks per quarter
+    const int cb = wave * cq, ce = min(nC, cb + cq);
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int c = cb; c < ce; c += kSkChunks) {
+        uint4 a[kSkChunks][4], b0[kSkChunks][4], b1[kSkChunks][4];
+#pragma unroll
+        for (int u = 0; u < kSkChunks; ++u) {
+            const int k0 = min(c + u, ce - 1) * 64;  // a chunk past the quarter re-reads the last one (masked below)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int k = k0 + (4 * g + kq) * 4;
+                a[u][g] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, k);
+                b0[u][g] = concat_slot<float, false, true>(nullptr, w0, K, K, k);
+                b1[u][g] = concat_slot<float, false, true>(nullptr, w1, K, K, k);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kSkChunks; ++u) {
+            if (c + u >= ce) break;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                acc0 = mfma_slot<float>(a[u][g], b0[u][g], acc0);
+                acc1 = mfma_slot<float>(a[u][g], b1[u][g], acc1);
+            }
+        }
+    }
+    if (wave > 0) {
+        red[wave - 1][0][lane] = acc0;
+        red[wave - 1][1][lane] = acc1;
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        acc0 += red[q][0][lane];
+        acc1 += red[q][1][lane];
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int col = c0 + 16 * t + r;
+        if (col >= H) continue;
+        const f32x4 v4 = t ? acc1 : acc0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = m0 + 4 * kq + j;
+            if (row < n) {
+                const float v = v4[j];
+                out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------ weight grad
 // dW[h][k] = Σ_i dZ[i][h] · In[i][k].  Block = 64 h x 64 k over one slab of
 // rows (blockIdx.z); wave w owns h rows 16w.. of the tile and 4 k tiles.  Rows

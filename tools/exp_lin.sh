@@ -1,6 +1,6 @@
-# A/B of the linear kernels in the microbenchmark under the rocprof kernel trace.
+# A/B of the linear forward variants: parity tests, then the rocprof kernel trace of the microbenchmark.
 set -o pipefail
 export TMPDIR=/tmp
+GS_LIN_FWD=sk timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -m gpu -q -x -k "linear" -p no:cacheprovider > gpurun_out/t_lin_sk.log 2>&1; rc=$?; tail -1 gpurun_out/t_lin_sk.log; [ $rc -eq 0 ] || exit $rc
 TAG=lrand MB_ARGS="--reps 100" timeout -k 10 300 bash tools/prof_mb.sh > /dev/null && \
-TAG=lcont MB_ARGS="--reps 100 --self-rows contiguous" timeout -k 10 300 bash tools/prof_mb.sh > /dev/null && \
-GS_LIN_FWD=wide TAG=lwcont MB_ARGS="--reps 100 --self-rows contiguous" timeout -k 10 300 bash tools/prof_mb.sh > /dev/null
+GS_LIN_FWD=sk TAG=lsk MB_ARGS="--reps 100" timeout -k 10 300 bash tools/prof_mb.sh > /dev/null
