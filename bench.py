@@ -124,6 +124,13 @@ def agg1_bytes(n_dst, n_pos, F, elem):
     return n_pos * (F * elem + 8) + n_dst * (F * elem + 16)
 
 
+def agg1_ids_bytes(n_dst, n_pos, F, elem, k):
+    """Algorithmic HBM bytes of one launch of the runner's layer-1 gather over
+    resolved ids (agg_ids_kernel): one feature row per sampled edge, the
+    destination's k padded neighbour ids (4 B each), one output row."""
+    return n_pos * F * elem + n_dst * (k * 4 + F * elem)
+
+
 def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
     """Oracle train step (CPU restatement of the reference) on this host."""
     import random as pyrandom
@@ -246,9 +253,9 @@ def main():
     if fused1:
         agg_bytes = layer1_fused_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], 128, elem)
         kname = "sage1_fwd_kernel (layer-1 gather-mean + concat-linear-relu, fused)"
-    else:
-        agg_bytes = agg1_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem)
-        kname = "agg_fwd_kernel (layer-1 expand gather-mean)"
+    else:  # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
+        agg_bytes = agg1_ids_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem, cfg["fanouts"][-1])
+        kname = "agg_ids_kernel (layer-1 gather-mean over resolved neighbour ids)"
 
     if rank == 0:
         achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9

@@ -1,7 +1,151 @@
-// C-ABI launchers of the gather-aggregate kernels (kernels/agg_dev.hpp).
+// C-ABI launchers of the gather-aggregate kernels (kernels/agg_dev.hpp), and
+// the runner's two-step layer-1 gather: resolve the sampled positions into
+// padded neighbour ids, then gather rows through them.
 #include "agg_dev.hpp"
+#include "internal.hpp"
 
 namespace gs {
+
+// ids[r·k + j] = node of destination r's j-th sampled position
+// (col[ent[ptr[r] + j]]), or -1 past its count and, unless gcn, for r's own
+// node (models.py:297-298: the aggregate skips self).  One thread per slot;
+// this is the gather's dependent index chain, run ahead of it.
+__global__ __launch_bounds__(kBlock) void resolve_ids_kernel(int n_dst, int k, const int* __restrict__ ptr,
+                                                             const int* __restrict__ ent,
+                                                             const int* __restrict__ col,
+                                                             const int* __restrict__ dst_ids, int gcn,
+                                                             int* __restrict__ ids) {
+    const int64_t t = blockIdx.x * int64_t(kBlock) + threadIdx.x;
+    if (t >= static_cast<int64_t>(n_dst) * k) return;
+    const int r = static_cast<int>(t / k), j = static_cast<int>(t - static_cast<int64_t>(r) * k);
+    const int e = ptr[r] + j;
+    int nb = -1;
+    if (e < ptr[r + 1]) nb = col[ent[e]];
+    if (!gcn && nb == dst_ids[r]) nb = -1;
+    ids[t] = nb;
+}
+
+// The layer-1 gather over resolved ids (k slots per destination, -1 = skip).
+// Same lane groups, chunking and accumulation order as agg_fwd_kernel's
+// expand mode (empty slots add +0 / never win a max), so the output is
+// bitwise that kernel's; the only index load is the destination's k ids.
+template <int OP, typename T, int VEC, int G>
+__global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X, int64_t ldx, int F, int n_dst, int k,
+                                                         const int* __restrict__ ids, const int* __restrict__ dst_ids,
+                                                         int gcn, T* __restrict__ out, int64_t ldo) {
+    const int gl = threadIdx.x % G;
+    const int r = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+    if (r >= n_dst) return;
+    const int node = gcn ? dst_ids[r] : 0;
+    const int* rid = ids + static_cast<int64_t>(r) * k;
+    constexpr int NR = VEC > 4 ? kRows / 2 : kRows;
+    const int nf = (F + G * VEC - 1) / (G * VEC);
+    for (int fi = 0; fi < nf; ++fi) {
+        const int f0 = fi * G * VEC + gl * VEC;
+        const bool act = f0 < F;
+        const int f0c = act ? f0 : 0;
+        float acc[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
+        int cnt = 0;
+        bool self_seen = false;
+        for (int base = 0; base < k; base += G) {
+            const int m = min(G, k - base);
+            const bool mine = gl < m;
+            const int nb = rid[mine ? base + gl : base];
+            if (gcn) self_seen |= group_bits<G>(mine && nb == node) != 0;
+            const int my = mine ? nb : -1;
+            for (int j = 0; j < m; j += NR) {
+                int rows[NR];
+                bool ok[NR];
+#pragma unroll
+                for (int u = 0; u < NR; ++u) {
+                    rows[u] = __shfl(my, j + u < m ? j + u : j, G);
+                    ok[u] = (j + u < m) && rows[u] >= 0;
+                }
+                const int fallback = rows[0] >= 0 ? rows[0] : node;
+                float x[NR][VEC];
+#pragma unroll
+                for (int u = 0; u < NR; ++u)
+                    RowIO<T, VEC>::load(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0c, x[u]);
+#pragma unroll
+                for (int u = 0; u < NR; ++u) {
+                    cnt += ok[u];
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) {
+                        if (OP == GS_AGG_MEAN) {
+                            acc[v] += ok[u] ? x[u][v] : 0.f;
+                        } else {
+                            const bool take = ok[u] && x[u][v] > acc[v];
+                            acc[v] = take ? x[u][v] : acc[v];
+                        }
+                    }
+                }
+            }
+        }
+        if (gcn && !self_seen) {  // gcn keeps self exactly once (set semantics)
+            ++cnt;
+            float x[VEC];
+            RowIO<T, VEC>::load(X + static_cast<int64_t>(node) * ldx + f0c, x);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+                if (OP == GS_AGG_MEAN) acc[v] += x[v];
+                else acc[v] = x[v] > acc[v] ? x[v] : acc[v];
+            }
+        }
+        if (!act) continue;
+        if (OP == GS_AGG_MEAN) {
+            const float inv = 1.0f / static_cast<float>(cnt);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v] *= inv;
+        }
+        RowIO<T, VEC>::store(out + static_cast<int64_t>(r) * ldo + f0, acc);
+    }
+}
+
+void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
+                        const int32_t* dst_ids, int gcn, int32_t* ids, hipStream_t st) {
+    GS_REQUIRE(n_dst >= 0 && k >= 1 && n_dst * k < (int64_t(1) << 31), GS_EINVAL, "bad sizes");
+    if (n_dst == 0) return;
+    const int64_t total = n_dst * k;
+    resolve_ids_kernel<<<dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
+        static_cast<int>(n_dst), k, ptr, ent, col, dst_ids, gcn, ids);
+    check_launch("resolve_ids");
+}
+
+void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
+                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st) {
+    GS_REQUIRE(op == GS_AGG_MEAN || op == GS_AGG_MAX, GS_EINVAL, "agg_func must be MEAN or MAX");
+    GS_REQUIRE(F >= 1 && n_dst >= 0 && k >= 1 && ldx >= F && ldo >= F, GS_EINVAL, "bad sizes");
+    if (n_dst == 0) return;
+    const int V = dt == GS_F32 ? 4 : 8;
+    const bool vec = F % V == 0 && ldx % V == 0 && ldo % V == 0 && aligned16(X) && aligned16(out);
+    const int f = static_cast<int>(F), n = static_cast<int>(n_dst);
+#define GS_IDS(OPV, TT, VV, GG)                                                                                  \
+    launch_k(agg_ids_kernel<OPV, TT, VV, GG>, dim3((n + (kBlock / GG) - 1) / (kBlock / GG)), dim3(kBlock), 0, st, \
+             static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo)
+#define GS_IDS_T(OPV, TT)                                                     \
+    do {                                                                      \
+        constexpr int VV = sizeof(TT) == 4 ? 4 : 8;                           \
+        if (!vec) GS_IDS(OPV, TT, 1, 64);                                     \
+        else {                                                                \
+            const int G = pick_group(f, VV);                                  \
+            if (G == 16) GS_IDS(OPV, TT, VV, 16);                             \
+            else if (G == 32) GS_IDS(OPV, TT, VV, 32);                        \
+            else GS_IDS(OPV, TT, VV, 64);                                     \
+        }                                                                     \
+    } while (0)
+    if (op == GS_AGG_MEAN) {
+        if (dt == GS_F32) GS_IDS_T(GS_AGG_MEAN, float);
+        else GS_IDS_T(GS_AGG_MEAN, bf16_t);
+    } else {
+        if (dt == GS_F32) GS_IDS_T(GS_AGG_MAX, float);
+        else GS_IDS_T(GS_AGG_MAX, bf16_t);
+    }
+#undef GS_IDS_T
+#undef GS_IDS
+    check_launch("agg_ids");
+}
 
 template <int OP, typename T, bool EXPAND>
 static void launch_fwd(int vec, const T* X, int64_t ldx, int F, int n_dst, const int* ptr,

@@ -13,6 +13,12 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
 void sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 int sum_slabs_grid(int64_t len);
 
+// agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)
+void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
+                        const int32_t* dst_ids, int gcn, int32_t* ids, hipStream_t st);
+void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
+                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st);
+
 // misc.hip
 int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,
                     const int32_t* labels, const int32_t* roots, int32_t mask_relu, float* dE, float* ws,

@@ -25,6 +25,10 @@ struct gs_trainer {
     static constexpr int kSlots = 3;
     void* a1_slot[kSlots] = {};
     int64_t a1_rows = 0;
+    // per slot, the layer-1 neighbour ids resolved ahead of the gather
+    // (k_ids slots per destination), when reserved with a fanout
+    int32_t* ids_slot[kSlots] = {};
+    int k_ids = 0;
     // clip-norm partials produced by the fused backward's reduce launches
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
@@ -38,6 +42,8 @@ struct gs_trainer {
         for (auto e : ev0) (void)hipEventDestroy(e);
         for (auto e : ev1) (void)hipEventDestroy(e);
         for (void* p : a1_slot)
+            if (p) (void)hipFree(p);
+        for (int32_t* p : ids_slot)
             if (p) (void)hipFree(p);
     }
 };
@@ -82,6 +88,31 @@ static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes
     ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F,
                   hop_sizes[4 * (L - 1)], fld(GS_PK_POS_PTR), fld(GS_PK_POS), nullptr, c.col, fld(GS_PK_DST_IDS),
                   c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+    if (timed) {
+        GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
+        ++T.n_timed;
+    }
+}
+
+// The same aggregate in two launches on `st`: resolve the sampled positions
+// into padded neighbour ids, then gather rows through them (the timed launch;
+// bitwise the expand-mode result).
+static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+                        int slot, hipStream_t st) {
+    const gs_trainer_config& c = T.cfg;
+    const int L = c.n_layers;
+    auto fld = [&](int f) -> const int32_t* {
+        const int64_t o = offsets[(L - 1) * GS_PK_NFIELDS + f];
+        GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
+        return pack + o;
+    };
+    const int64_t n_dst = hop_sizes[4 * (L - 1)];
+    int32_t* ids = T.ids_slot[slot];
+    resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids, st);
+    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
+    if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
+    agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim, n_dst,
+                   T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, T.a1_slot[slot], c.feat_dim, st);
     if (timed) {
         GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
         ++T.n_timed;
@@ -354,15 +385,28 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_
     GS_API_END
 }
 
-int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows) {
+int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout) {
     GS_API_BEGIN
-    GS_REQUIRE(t && max_rows >= 0, GS_EINVAL, "bad arguments");
-    if (max_rows <= t->a1_rows) return GS_OK;
+    GS_REQUIRE(t && max_rows >= 0 && max_fanout >= 0, GS_EINVAL, "bad arguments");
+    if (max_rows <= t->a1_rows && max_fanout <= t->k_ids) return GS_OK;
+    max_rows = std::max(max_rows, t->a1_rows);
     const int64_t bytes = max_rows * t->cfg.feat_dim * (t->cfg.feat_dtype == GS_BF16 ? 2 : 4);
     for (void*& p : t->a1_slot) {
         if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
         p = nullptr;
         GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(bytes, 256)) == hipSuccess, GS_ENOMEM, "hipMalloc(gather slot)");
+    }
+    for (int32_t*& p : t->ids_slot) {
+        if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
+        p = nullptr;
+    }
+    t->k_ids = 0;
+    if (max_fanout > 0) {
+        GS_REQUIRE(max_rows * max_fanout < (int64_t(1) << 31), GS_EINVAL, "gather slot too large for int32 ids");
+        for (int32_t*& p : t->ids_slot)
+            GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(max_rows * max_fanout * 4, 256)) == hipSuccess, GS_ENOMEM,
+                       "hipMalloc(gather ids)");
+        t->k_ids = max_fanout;
     }
     t->a1_rows = max_rows;
     GS_API_END
@@ -376,7 +420,11 @@ int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_siz
     const int L = t->cfg.n_layers;
     GS_REQUIRE(hop_sizes[4 * (L - 1)] <= t->a1_rows && t->a1_slot[slot], GS_EINVAL,
                "gather slot too small (gs_trainer_gather_reserve)");
-    gs::gather1(*t, pack, hop_sizes, offsets, t->a1_slot[slot], gs::as_stream(stream));
+    const int64_t n_dst = hop_sizes[4 * (L - 1)], n_pos = hop_sizes[4 * (L - 1) + 1];
+    if (t->k_ids > 0 && n_pos <= n_dst * t->k_ids)  // every neighbourhood fits k_ids slots
+        gs::gather1_ids(*t, pack, hop_sizes, offsets, slot, gs::as_stream(stream));
+    else
+        gs::gather1(*t, pack, hop_sizes, offsets, t->a1_slot[slot], gs::as_stream(stream));
     GS_API_END
 }
 

@@ -312,7 +312,8 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             const int64_t per = k > 0 ? std::min<int64_t>(k, md) : md;
             nd = std::min<int64_t>(nn, nd + nd * per);
         }
-        const int rc = gs_trainer_gather_reserve(cfg->trainer, nd);
+        const int32_t k_last = r->fanouts[cfg->n_hops - 1];  // bounds every last-hop neighbourhood
+        const int rc = gs_trainer_gather_reserve(cfg->trainer, nd, k_last > 0 ? k_last : 0);
         if (rc != GS_OK) fail(rc, gs_last_error());
     }
     const int32_t S = cfg->n_streams;

@@ -345,8 +345,12 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
  * trainer slot 0..2 on any stream, then the rest of the step reading that
  * slot.  The caller orders them (event) and keeps a slot until the step that
  * reads it has finished its backward.  gs_trainer_gather_reserve allocates
- * the three slots for up to max_rows layer-1 destinations. */
-int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows);
+ * the three slots for up to max_rows layer-1 destinations; with max_fanout
+ * > 0 (the last hop's fanout, which bounds every sampled neighbourhood)
+ * gs_trainer_gather runs as two launches: the positions resolved into
+ * padded neighbour ids, then the row gather through them (bitwise the same
+ * aggregate, without the index chain in the gather). */
+int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout);
 int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
                       const int64_t* offsets, int32_t slot, void* stream);
 int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack,

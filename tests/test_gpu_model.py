@@ -219,25 +219,26 @@ def test_prefetcher_streams_each_bit_exact(gs):
         assert roots_dev.cpu().tolist() == roots.tolist()
 
 
-@pytest.mark.parametrize("S", [1, 3])
-@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
-def test_native_runner_matches_python_loop(gs, S, agg):
-    """gs_runner (native sampler threads + pinned ring + copy stream + fused
-    step) leaves exactly the parameters of the Python loop over the same
-    sampler streams (same kernels, same order: bitwise equal)."""
+@pytest.mark.parametrize("S,agg,gcn", [(1, "MEAN", False), (3, "MEAN", False), (1, "MAX", False),
+                                       (3, "MAX", False), (3, "MEAN", True)])
+def test_native_runner_matches_python_loop(gs, S, agg, gcn):
+    """gs_runner (native sampler threads + pinned ring + side-stream pull,
+    resolved-id layer-1 gather, fused step) leaves exactly the parameters of
+    the Python loop over the same sampler streams, whose layer-1 gather is the
+    expand-mode kernel (same accumulation order: bitwise equal)."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:7]
-    a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
-    b = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, seed=824)
-    pf = train.Prefetcher(graph, None, batches, [25, 10], False, DEV,
+    a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, gcn=gcn, seed=824)
+    b = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, gcn=gcn, seed=824)
+    pf = train.Prefetcher(graph, None, batches, [25, 10], gcn, DEV,
                           rngs=[train.make_rng(11, 0, w) for w in range(S)], fail_empty=agg == "MAX")
     for _ in batches:
         ds, roots_dev, _info = pf.next()
         a.step(ds, roots_dev)
     pf.close()
-    runner = train.Runner(b, graph, batches, [train.make_rng(11, 0, w) for w in range(S)], [25, 10],
+    runner = train.Runner(b, graph, batches, [train.make_rng(11, 0, w) for w in range(S)], [25, 10], gcn=gcn,
                           fail_empty=agg == "MAX", depth=2)
     runner.run(3)
     runner.run(len(batches) - 3)

@@ -31,7 +31,7 @@ def main():
         w = write.get(k, (0.0, 0))[0] * 1024.0
         kernels[k] = {"fetch_bytes_raw": round(f), "read_bytes": round(2 * f), "write_bytes": round(w),
                       "hbm_bytes": round(2 * f + w), "dispatches": fetch.get(k, write.get(k, (0, 0)))[1]}
-    agg = [k for k in kernels if "sage1_fwd_kernel" in k] or \
+    agg = [k for k in kernels if "sage1_fwd_kernel" in k] or [k for k in kernels if "agg_ids_kernel" in k] or \
         [k for k in kernels if "agg_fwd_kernel" in k and k.endswith("true>")]
     bench = {}
     for line in open(f"{out_dir}/bench_FETCH_SIZE.log"):
