@@ -16,6 +16,7 @@
 // one, with a single workgroup barrier per chunk.
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kcommon.hpp"
 
@@ -568,9 +569,15 @@ __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
 // fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
 constexpr int kDwTargetBlocks = 256;
 
+inline int dw_target_blocks() {  // GS_DW_BLOCKS: measurement override
+    static const int v = std::getenv("GS_DW_BLOCKS") ? std::max(1, std::atoi(std::getenv("GS_DW_BLOCKS")))
+                                                       : kDwTargetBlocks;
+    return v;
+}
+
 inline int dw_rows_per_split(int64_t n, int64_t K, int64_t H) {
     const int64_t tiles = ((K + 63) / 64) * ((H + 63) / 64);
-    const int64_t want = std::max<int64_t>(1, (kDwTargetBlocks + tiles - 1) / tiles);
+    const int64_t want = std::max<int64_t>(1, (dw_target_blocks() + tiles - 1) / tiles);
     const int64_t cap = std::max<int64_t>(1, n / 64);
     const int64_t S = std::max(std::min(want, cap), (n + kDwMaxSlab - 1) / kDwMaxSlab);
     const int64_t rows = (n + S - 1) / S;

@@ -296,7 +296,11 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(bound > 0, GS_EINVAL, "pack bound failed");
     r->cap = bound + cfg->batch;
     hip_ok(hipGetDevice(&r->device), "hipGetDevice");
-    hip_ok(hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking), "hipStreamCreate");
+    {  // high priority: the side stream's pull + gather dispatch ahead of the step they overlap
+        int lo = 0, hi = 0;
+        hip_ok(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+        hip_ok(hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
+    }
     for (int d = 0; d < gs_runner::kDev; ++d) {
         hip_ok(hipEventCreateWithFlags(&r->dev_done[d], hipEventDisableTiming), "hipEventCreate");
         hip_ok(hipEventCreateWithFlags(&r->gathered[d], hipEventDisableTiming), "hipEventCreate");

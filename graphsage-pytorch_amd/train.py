@@ -304,7 +304,8 @@ class Communicator:
 
 class Runner:
     """The training loop as one native pipeline (gs_runner): S sampler
-    threads, pinned pack rings, H2D copies on a copy stream and the fused
+    threads, pinned pack rings, the next batch's device pull and layer-1
+    gather on a high-priority side stream, and the fused
     step, all without Python per step.  `batches`: iterable of equal-size
     int64 root arrays consumed in order; `rngs`: one RNG per sampler stream
     (stream w samples batches w, w+S, ...)."""

@@ -10,7 +10,7 @@ for tag in sys.argv[1:]:
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        if "gs::" not in n or "sum_slabs" in n:
+        if "gs::" not in n:
             continue
         k = n.split("(")[0][-34:] + f" grid=({r['Grid_Size_X']},{r['Grid_Size_Y']},{r['Grid_Size_Z']})"
         d[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
