@@ -408,9 +408,10 @@ __device__ __forceinline__ void linear_dw_body(
     __syncthreads();
 
     // Rows past the slab read a valid row and are zeroed at the LDS store
-    // (both operands: 0 · NaN would not vanish).
+    // (both operands: 0 · NaN would not vanish).  Chunks past the end re-read
+    // the last one (their data is never stashed).
     auto load = [&](int c, float4& z, float4& o, float4& x) {
-        const int t = min(16 * c + lr, i_end - i_beg - 1);
+        const int t = min(16 * min(c, nC - 1) + lr, i_end - i_beg - 1);
         const int ic = i_beg + t;
         z = row_quad_raw<ZVEC>(dout + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
         if (RELU) o = row_quad_raw<ZVEC>(out + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
@@ -418,25 +419,20 @@ __device__ __forceinline__ void linear_dw_body(
         const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sIdx[t]) * ldxs : nullptr;
         x = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
     };
-    auto stash = [&](int c, int buf, float4 z, float4 o, float4 x) {
+    auto stash = [&](int c, float4 z, float4 o, float4 x) {
         z = mask_quad(z, h0 + lq, H);
         if (RELU) z = relu_mask(z, o);
         x = mask_quad(x, k0 + lq, K);
         if (16 * c + lr >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(&sZ[buf][lr * kDwPitch + lq]) = z;
-        *reinterpret_cast<float4*>(&sI[buf][lr * kDwPitch + lq]) = x;
+        *reinterpret_cast<float4*>(&sZ[c & 1][lr * kDwPitch + lq]) = z;
+        *reinterpret_cast<float4*>(&sI[c & 1][lr * kDwPitch + lq]) = x;
     };
-    float4 z, o, x;
-    load(0, z, o, x);
-    stash(0, 0, z, o, x);
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nC; ++c) {
-        __syncthreads();
-        const int cn = min(c + 1, nC - 1);
-        load(cn, z, o, x);
-        __builtin_amdgcn_sched_barrier(0);  // loads issue before the chunk's LDS reads and MFMAs
+    // One chunk: its 20 LDS operands are all read before its first MFMA (one
+    // wait instead of one per MFMA pair), then 16 MFMAs on 4 accumulators.
+    auto compute = [&](int c) {
         const float* tz = sZ[c & 1];
         const float* ti = sI[c & 1];
         float a[4], b[4][4];
@@ -447,12 +443,36 @@ __device__ __forceinline__ void linear_dw_body(
 #pragma unroll
             for (int t = 0; t < 4; ++t) b[s][t] = ti[row * kDwPitch + t * 16 + r];
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+    };
+    // Global loads run two chunks ahead of the MFMAs (two named register sets,
+    // loop unrolled by two); LDS stays double-buffered.
+    float4 z0, o0, x0, z1, o1, x1;
+    load(0, z0, o0, x0);
+    stash(0, z0, o0, x0);
+    load(1, z1, o1, x1);
+    int c = 0;
+    for (; c + 1 < nC; c += 2) {
+        __syncthreads();
+        load(c + 2, z0, o0, x0);
         __builtin_amdgcn_sched_barrier(0);
-        stash(cn, (c + 1) & 1, z, o, x);
+        compute(c);
+        __builtin_amdgcn_sched_barrier(0);
+        stash(c + 1, z1, o1, x1);
+        __syncthreads();
+        load(c + 3, z1, o1, x1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(c + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (c + 2 < nC) stash(c + 2, z0, o0, x0);
+    }
+    if (c < nC) {
+        __syncthreads();
+        compute(c);
     }
     float* slab = dst + static_cast<int64_t>(bz) * split_stride;
 #pragma unroll
@@ -567,7 +587,7 @@ __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
 
 // Row slabs of the weight gradient: enough (64 h x 64 k) x slab workgroups to
 // fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
-constexpr int kDwTargetBlocks = 256;
+constexpr int kDwTargetBlocks = 512;  // two blocks per CU (measured best of 256 / 512 / 1024 in the step)
 
 inline int dw_target_blocks() {  // GS_DW_BLOCKS: measurement override
     static const int v = std::getenv("GS_DW_BLOCKS") ? std::max(1, std::atoi(std::getenv("GS_DW_BLOCKS")))
