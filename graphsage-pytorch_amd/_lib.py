@@ -94,6 +94,15 @@ _SIGS = {
     "gs_cls_nll_fwd_bwd": (_i32, [_i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                                   _vp, _vp, _vp]),
     "gs_clip_sgd": (_i32, [_i32, _vp, _vp, _vp, _f32, _f32, _f32, _vp, _vp]),
+    "gs_unsup_create": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _p(_vp)]),
+    "gs_unsup_destroy": (None, [_vp]),
+    "gs_unsup_extend": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _vp]),
+    "gs_unsup_fetch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gs_unsup_loss_plan": (_i32, [_vp, _vp, _i64, _vp, _p(_i64)]),
+    "gs_unsup_loss_ws_floats": (_i64, [_i64, _i64, _i64]),
+    "gs_unsup_loss_fwd": (_i32, [_i32, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _f32, _f32, _vp, _vp,
+                                 _vp]),
+    "gs_unsup_loss_bwd": (_i32, [_i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gs_cast_f32_bf16": (_i32, [_vp, _vp, _i64, _vp]),
     "gs_trainer_create": (_i32, [_vp, _p(_vp)]),
     "gs_trainer_destroy": (None, [_vp]),

@@ -18,10 +18,7 @@
 #include "graph.hpp"
 #include "mt19937.hpp"
 #include "pyset.hpp"
-
-struct gs_rng {
-    gs::MT19937 mt;
-};
+#include "rng.hpp"
 
 #ifndef GS_PHASE  // phase marks for tools/sampler_prof.cpp; no-ops in the library
 #define GS_PHASE(i)

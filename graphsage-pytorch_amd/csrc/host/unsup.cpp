@@ -1,0 +1,388 @@
+// UnsupervisedLoss.extend_nodes (models.py:135-147) on the host, bit-exact
+// with the reference's CPython `random` stream and set iteration orders, and
+// the index plan the device loss kernels (kernels/unsup.hip) read.
+//
+// extend_nodes(nodes, num_neg):
+//   positives  models.py:166-186  for each node with a non-empty row: N_WALKS
+//              walks of WALK_LEN steps, each step random.choice(list(adj[cur]))
+//              = randbelow(deg) over the CSR row (the row IS list(set)); the
+//              pair (node, next) is kept when next != node and next is a
+//              training node.                                   (sequential rng)
+//   negatives  models.py:152-164  the N_WALK_LEN-hop ball of each node, then
+//              far = set(train) - ball and random.sample(far, num_neg) unless
+//              num_neg >= len(far) (then far itself).  The ball only matters
+//              through membership; far's iteration order follows CPython's
+//              set_difference:
+//                (len(train) >> 2) > len(ball): copy(set(train)), then discard
+//                    -> the copy's slot order, ball members skipped;
+//                otherwise: a fresh set filled in set(train)'s slot order
+//                    with the non-members -> that set's slot order.
+//              Balls and far lists are built in parallel (no rng); the draws
+//              then run in node order on the one stream.
+//   unique     models.py:146  list(set(flat positives) | set(flat negatives)).
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "graph.hpp"
+#include "pyset.hpp"
+#include "rng.hpp"
+
+namespace gs {
+namespace {
+
+struct Ball {
+    std::vector<uint32_t> stamp;  // [n_nodes] == epoch -> in the ball
+    uint32_t epoch = 0;
+    std::vector<int32_t> edge, next;
+
+    // The frontier expansion of models.py:154-162 (membership only).  Returns
+    // len(neighbors).
+    int64_t grow(const Graph& g, int32_t v, int hops) {
+        if (stamp.empty()) stamp.assign(g.n_nodes, 0);
+        if (++epoch == 0) {  // wrapped: clear
+            std::fill(stamp.begin(), stamp.end(), 0);
+            epoch = 1;
+        }
+        stamp[v] = epoch;
+        int64_t size = 1;
+        edge.assign(1, v);
+        for (int h = 0; h < hops && !edge.empty(); ++h) {
+            next.clear();
+            for (int32_t u : edge) {
+                const int32_t* c = g.col.data() + g.row_ptr[u];
+                const int64_t d = g.degree(u);
+                for (int64_t e = 0; e < d; ++e) {
+                    const int32_t w = c[e];
+                    if (stamp[w] != epoch) {
+                        stamp[w] = epoch;
+                        next.push_back(w);
+                    }
+                }
+            }
+            size += static_cast<int64_t>(next.size());
+            edge.swap(next);
+        }
+        return size;
+    }
+    bool has(int32_t w) const { return stamp[w] == epoch; }
+};
+
+}  // namespace
+}  // namespace gs
+
+struct gs_unsup {
+    const gs::Graph* g = nullptr;
+    int32_t n_walks = 6, walk_len = 1, n_walk_len = 5;
+    std::vector<uint8_t> is_train;      // [n_nodes]
+    std::vector<int32_t> train_order;   // list(set(train_nodes))
+    std::vector<int32_t> copy_order;    // list(set(train_nodes).copy())
+    int64_t n_train_set = 0;
+    std::vector<gs::Ball> balls;        // one per worker thread
+    // last extend_nodes
+    std::vector<int64_t> nodes, unique, pos, neg;  // pairs flattened (a, b)
+    std::vector<int64_t> pos_cnt, neg_cnt;
+    std::vector<uint8_t> has_pos;
+    int32_t subset_ok = 0;
+};
+
+namespace {
+
+using gs::PySet;
+
+template <class Fn>
+void run_workers(int32_t n_threads, int64_t n, Fn&& fn) {
+    const int32_t nt = static_cast<int32_t>(std::max<int64_t>(1, std::min<int64_t>(n_threads, n)));
+    if (nt <= 1) {
+        for (int64_t i = 0; i < n; ++i) fn(i, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t i = t; i < n; i += nt) fn(i, t);
+        });
+    for (auto& x : th) x.join();
+}
+
+// far = set(train) - ball, in CPython iteration order (see file header).
+void far_list(const gs_unsup& u, const gs::Ball& b, int64_t ball_size, std::vector<int32_t>& out) {
+    out.clear();
+    if ((u.n_train_set >> 2) > ball_size) {
+        for (int32_t x : u.copy_order)
+            if (!b.has(x)) out.push_back(x);
+        return;
+    }
+    PySet r;
+    for (int32_t x : u.train_order)
+        if (!b.has(x)) r.add(x);
+    r.for_each([&](int32_t x) { out.push_back(x); });
+}
+
+void walk_pairs(gs_unsup& u, gs_rng* rng) {
+    const gs::Graph& g = *u.g;
+    const int64_t n = static_cast<int64_t>(u.nodes.size());
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t v = u.nodes[i];
+        if (g.degree(v) == 0) continue;  // models.py:168
+        u.has_pos[i] = 1;
+        for (int32_t w = 0; w < u.n_walks; ++w) {
+            int64_t cur = v;
+            for (int32_t s = 0; s < u.walk_len; ++s) {
+                const int64_t d = g.degree(cur);
+                GS_REQUIRE(d > 0, GS_EEMPTY, "Cannot choose from an empty sequence (walk reached an isolated node)");
+                const int64_t nxt = g.col[g.row_ptr[cur] + rng->mt.randbelow(static_cast<uint64_t>(d))];
+                if (nxt != v && u.is_train[nxt]) {
+                    u.pos.push_back(v);
+                    u.pos.push_back(nxt);
+                    ++u.pos_cnt[i];
+                }
+                cur = nxt;
+            }
+        }
+    }
+}
+
+void negative_pairs(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_threads) {
+    const int64_t n = static_cast<int64_t>(u.nodes.size());
+    const int32_t nt = std::max<int32_t>(1, n_threads);
+    if (static_cast<int32_t>(u.balls.size()) < nt) u.balls.resize(nt);
+    const int64_t chunk = std::max<int64_t>(nt, std::min<int64_t>(n, 4 * nt));
+    std::vector<std::vector<int32_t>> far(static_cast<size_t>(chunk));
+    const int64_t setsize = gs::sample_setsize(num_neg);
+    std::vector<int32_t> pool;
+    std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
+    for (int64_t c0 = 0; c0 < n; c0 += chunk) {
+        const int64_t cn = std::min(chunk, n - c0);
+        run_workers(nt, cn, [&](int64_t j, int32_t t) {
+            gs::Ball& b = u.balls[t];
+            const int64_t s = b.grow(*u.g, static_cast<int32_t>(u.nodes[c0 + j]), u.n_walk_len);
+            far_list(u, b, s, far[j]);
+        });
+        for (int64_t j = 0; j < cn; ++j) {  // the draws, in node order
+            const int64_t i = c0 + j, v = u.nodes[i];
+            const std::vector<int32_t>& f = far[j];
+            const int64_t len = static_cast<int64_t>(f.size());
+            if (num_neg < len) {
+                if (len <= setsize) pool.resize(static_cast<size_t>(len));
+                gs::sample_positions(rng->mt, len, num_neg, setsize, picks.data(), pool.data());
+                for (int64_t t = 0; t < num_neg; ++t) {
+                    u.neg.push_back(v);
+                    u.neg.push_back(f[picks[t]]);
+                }
+                u.neg_cnt[i] = num_neg;
+            } else {
+                for (int32_t x : f) {
+                    u.neg.push_back(v);
+                    u.neg.push_back(x);
+                }
+                u.neg_cnt[i] = len;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_unsup_create(const gs_graph* graph, const int64_t* train_nodes, int64_t n_train, int32_t n_walks,
+                    int32_t walk_len, int32_t n_walk_len, gs_unsup** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(graph && out && (train_nodes || n_train == 0) && n_train >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(n_walks >= 0 && walk_len >= 0 && n_walk_len >= 0, GS_EINVAL, "walk parameters must be >= 0");
+    const auto* g = reinterpret_cast<const gs::Graph*>(graph);
+    auto u = std::make_unique<gs_unsup>();
+    u->g = g;
+    u->n_walks = n_walks;
+    u->walk_len = walk_len;
+    u->n_walk_len = n_walk_len;
+    u->is_train.assign(g->n_nodes, 0);
+    PySet ts;  // set(self.train_nodes), models.py:163
+    for (int64_t i = 0; i < n_train; ++i) {
+        GS_REQUIRE(train_nodes[i] >= 0 && train_nodes[i] < g->n_nodes, GS_ERANGE, "train node id out of range");
+        u->is_train[train_nodes[i]] = 1;
+        ts.add(static_cast<int32_t>(train_nodes[i]));
+    }
+    u->n_train_set = ts.used;
+    ts.for_each([&](int32_t x) { u->train_order.push_back(x); });
+    gs::copy_of(ts).for_each([&](int32_t x) { u->copy_order.push_back(x); });
+    *out = u.release();
+    GS_API_END
+}
+
+void gs_unsup_destroy(gs_unsup* u) { delete u; }
+
+int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, int64_t num_neg,
+                    int32_t parts, int32_t n_threads, int64_t* sizes) {
+    GS_API_BEGIN
+    GS_REQUIRE(u && rng && sizes && (nodes || n == 0) && n >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(num_neg >= 0, GS_ERANGE, "Sample larger than population or is negative");
+    GS_REQUIRE(parts >= 1 && parts <= 3, GS_EINVAL, "parts: 1 walks, 2 negatives, 3 both");
+    const gs::Graph& g = *u->g;
+    for (int64_t i = 0; i < n; ++i) GS_REQUIRE(nodes[i] >= 0 && nodes[i] < g.n_nodes, GS_ERANGE, "node id out of range");
+    u->nodes.assign(nodes, nodes + n);
+    u->pos.clear();
+    u->neg.clear();
+    u->unique.clear();
+    u->pos_cnt.assign(n, 0);
+    u->neg_cnt.assign(n, 0);
+    u->has_pos.assign(n, 0);
+    u->subset_ok = 0;
+    if (parts & 1) walk_pairs(*u, rng);
+    if (parts & 2) negative_pairs(*u, rng, num_neg, n_threads);
+
+    PySet a, b;  // models.py:146
+    for (int64_t x : u->pos) a.add(static_cast<int32_t>(x));
+    for (int64_t x : u->neg) b.add(static_cast<int32_t>(x));
+    PySet r = gs::copy_of(a);
+    r.merge(b);
+    r.for_each([&](int32_t x) { u->unique.push_back(x); });
+
+    // set(target) < set(unique) (models.py:147): every target present and the
+    // union strictly larger than the distinct targets.
+    PySet tgt;
+    for (int64_t x : u->nodes) tgt.add(static_cast<int32_t>(x));
+    bool ok = r.used > tgt.used;
+    for (int64_t x : u->nodes) ok = ok && r.find_slot(static_cast<int32_t>(x)) >= 0;
+    u->subset_ok = ok ? 1 : 0;
+
+    sizes[0] = static_cast<int64_t>(u->unique.size());
+    sizes[1] = static_cast<int64_t>(u->pos.size() / 2);
+    sizes[2] = static_cast<int64_t>(u->neg.size() / 2);
+    sizes[3] = u->subset_ok;
+    GS_API_END
+}
+
+int gs_unsup_fetch(const gs_unsup* u, int64_t* unique, int64_t* pos_pairs, int64_t* neg_pairs, int64_t* pos_cnt,
+                   int64_t* neg_cnt, uint8_t* has_pos) {
+    GS_API_BEGIN
+    GS_REQUIRE(u, GS_EINVAL, "bad arguments");
+    auto put = [](auto* dst, const auto& v) {
+        if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(v[0]));
+    };
+    put(unique, u->unique);
+    put(pos_pairs, u->pos);
+    put(neg_pairs, u->neg);
+    put(pos_cnt, u->pos_cnt);
+    put(neg_cnt, u->neg_cnt);
+    put(has_pos, u->has_pos);
+    GS_API_END
+}
+
+// The loss loops of models.py:65-96 / :98-132 as index lists.  Dict semantics
+// of node_positive_pairs / node_negtive_pairs: a key's position is its first
+// occurrence in `nodes`, its value the last occurrence's pairs.  Scored nodes
+// (both lists non-empty) in key order; rows are positions in unique
+// (node2index, models.py:69).  Layout (int32):
+//   pos_ptr[M+1] | neg_ptr[M+1] | pos_a[P] | pos_b[P] | neg_a[Nn] | neg_b[Nn]
+//   | tptr[U+1] | tidx[2(P+Nn)]
+// tidx lists, per embedding row, 2*g + side for every pair g it belongs to
+// (g < P: positive pair g, else negative pair g-P; side 0 = first element),
+// ascending: the fixed summation order of the row gradient.
+int gs_unsup_loss_plan(const gs_unsup* u, int32_t* buf, int64_t cap, int64_t* dims, int64_t* used) {
+    GS_API_BEGIN
+    GS_REQUIRE(u && dims && used, GS_EINVAL, "bad arguments");
+    const int64_t n = static_cast<int64_t>(u->nodes.size());
+    const int64_t U = static_cast<int64_t>(u->unique.size());
+    std::vector<int64_t> pofs(n + 1, 0), nofs(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        pofs[i + 1] = pofs[i] + u->pos_cnt[i];
+        nofs[i + 1] = nofs[i] + u->neg_cnt[i];
+    }
+    // last occurrence per node id, key order = first occurrence
+    PySet seen;
+    std::vector<int64_t> keys;  // index of first occurrence
+    std::vector<int64_t> last_of(n);
+    {
+        std::vector<int64_t> ids(u->nodes);
+        std::vector<int64_t> order(n);
+        for (int64_t i = 0; i < n; ++i) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return ids[a] < ids[b]; });
+        for (int64_t s = 0; s < n;) {
+            int64_t e = s;
+            while (e < n && ids[order[e]] == ids[order[s]]) ++e;
+            for (int64_t t = s; t < e; ++t) last_of[order[t]] = order[e - 1];
+            s = e;
+        }
+    }
+    int64_t n_pos_keys = 0, n_neg_keys = 0;
+    std::vector<int64_t> scored;  // occurrence whose lists are scored
+    for (int64_t i = 0; i < n; ++i) {
+        if (!seen.add(static_cast<int32_t>(u->nodes[i]))) continue;
+        ++n_neg_keys;
+        if (!u->has_pos[i]) continue;
+        ++n_pos_keys;
+        const int64_t li = last_of[i];
+        if (u->pos_cnt[li] > 0 && u->neg_cnt[li] > 0) scored.push_back(li);
+    }
+    const int64_t M = static_cast<int64_t>(scored.size());
+    int64_t P = 0, N = 0;
+    for (int64_t li : scored) {
+        P += u->pos_cnt[li];
+        N += u->neg_cnt[li];
+    }
+    const int64_t need = 2 * (M + 1) + 2 * P + 2 * N + (U + 1) + 2 * (P + N);
+    dims[0] = M;
+    dims[1] = P;
+    dims[2] = N;
+    dims[3] = U;
+    dims[4] = n_pos_keys;
+    dims[5] = n_neg_keys;
+    *used = need;
+    if (!buf) return GS_OK;
+    GS_REQUIRE(cap >= need, GS_EINVAL, "plan buffer too small");
+    GS_REQUIRE(U < (int64_t(1) << 31) && P + N < (int64_t(1) << 30), GS_ERANGE, "batch too large for int32 plan");
+    std::vector<int32_t> where(u->g->n_nodes, -1);
+    for (int64_t r = 0; r < U; ++r) where[u->unique[r]] = static_cast<int32_t>(r);
+    int32_t* pos_ptr = buf;
+    int32_t* neg_ptr = pos_ptr + (M + 1);
+    int32_t* pa = neg_ptr + (M + 1);
+    int32_t* pb = pa + P;
+    int32_t* na = pb + P;
+    int32_t* nb = na + N;
+    int32_t* tptr = nb + N;
+    int32_t* tidx = tptr + (U + 1);
+    int64_t p = 0, q = 0;
+    auto row = [&](int64_t id) {
+        const int32_t r = where[id];
+        GS_REQUIRE(r >= 0, GS_EINVAL, "pair node missing from unique_nodes_batch");
+        return r;
+    };
+    for (int64_t m = 0; m < M; ++m) {
+        const int64_t li = scored[m];
+        pos_ptr[m] = static_cast<int32_t>(p);
+        neg_ptr[m] = static_cast<int32_t>(q);
+        for (int64_t t = pofs[li]; t < pofs[li + 1]; ++t, ++p) {
+            pa[p] = row(u->pos[2 * t]);
+            pb[p] = row(u->pos[2 * t + 1]);
+        }
+        for (int64_t t = nofs[li]; t < nofs[li + 1]; ++t, ++q) {
+            na[q] = row(u->neg[2 * t]);
+            nb[q] = row(u->neg[2 * t + 1]);
+        }
+    }
+    pos_ptr[M] = static_cast<int32_t>(P);
+    neg_ptr[M] = static_cast<int32_t>(N);
+    // transposed contribution lists (counting sort keeps 2g+side ascending)
+    std::fill_n(tptr, U + 1, 0);
+    auto each = [&](auto&& f) {
+        for (int64_t g = 0; g < P; ++g) {
+            f(pa[g], 2 * g);
+            f(pb[g], 2 * g + 1);
+        }
+        for (int64_t g = 0; g < N; ++g) {
+            f(na[g], 2 * (P + g));
+            f(nb[g], 2 * (P + g) + 1);
+        }
+    };
+    each([&](int32_t r, int64_t) { ++tptr[r + 1]; });
+    for (int64_t r = 0; r < U; ++r) tptr[r + 1] += tptr[r];
+    std::vector<int32_t> fillp(tptr, tptr + U);
+    each([&](int32_t r, int64_t code) { tidx[fillp[r]++] = static_cast<int32_t>(code); });
+    GS_API_END
+}
+
+}  // extern "C"

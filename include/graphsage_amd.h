@@ -184,6 +184,48 @@ int gs_sample_pack_run(const gs_graph* g, gs_rng* rng, const int64_t* roots,
                        int32_t flags, int32_t* buf, int64_t cap,
                        int64_t* hop_sizes, int64_t* offsets, int64_t* used);
 
+/* ------------------------------------------------- unsupervised-loss batch
+ * UnsupervisedLoss (models.py:30-186) over the same graph and rng:
+ * extend_nodes (models.py:135-147, called by apply_model at utils.py:149)
+ * consumes the stream exactly as the reference — random walks
+ * (random.choice, models.py:178) in node order, then per node the
+ * n_walk_len-hop ball and random.sample(set(train) - ball, num_neg)
+ * (models.py:152-164) — and returns list(set(pos) | set(neg))
+ * (models.py:146) in CPython set order.  Balls are grown on n_threads
+ * threads; the draws stay in node order.  Reference constants: n_walks 6,
+ * walk_len 1, n_walk_len 5 (models.py:36-39). */
+typedef struct gs_unsup gs_unsup;
+
+int gs_unsup_create(const gs_graph* g, const int64_t* train_nodes, int64_t n_train,
+                    int32_t n_walks, int32_t walk_len, int32_t n_walk_len,
+                    gs_unsup** out);
+void gs_unsup_destroy(gs_unsup* u);
+/* parts: 1 = the walks only (get_positive_nodes, models.py:149), 2 = the
+ * negatives only (get_negtive_nodes, :152), 3 = both (extend_nodes).
+ * sizes[4] = (len(unique_nodes_batch), len(positive_pairs),
+ * len(negtive_pairs), set(nodes) < set(unique) ? 1 : 0 — the assertion at
+ * models.py:147, which the Python host raises). */
+int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n,
+                    int64_t num_neg, int32_t parts, int32_t n_threads,
+                    int64_t* sizes);
+/* Copy out the last extend: unique[sizes0], pos_pairs[2*sizes1] and
+ * neg_pairs[2*sizes2] as (node, other) in append order, per input node its
+ * positive / negative pair counts and has_pos (node is a key of
+ * node_positive_pairs, i.e. its adjacency set is non-empty).  NULL skips. */
+int gs_unsup_fetch(const gs_unsup* u, int64_t* unique, int64_t* pos_pairs,
+                   int64_t* neg_pairs, int64_t* pos_cnt, int64_t* neg_cnt,
+                   uint8_t* has_pos);
+/* Index plan of get_loss_sage / get_loss_margin (models.py:65-132) for the
+ * last extend, int32, rows = positions in unique (node2index, :69):
+ *   pos_ptr[M+1] | neg_ptr[M+1] | pos_a[P] | pos_b[P] | neg_a[N] | neg_b[N]
+ *   | tptr[U+1] | tidx[2(P+N)]
+ * M scored nodes (both pair lists non-empty, dict order), tidx = 2*pair +
+ * side per embedding row, ascending.  dims[6] = (M, P, N, U,
+ * len(node_positive_pairs), len(node_negtive_pairs)); *used = elements.
+ * buf == NULL only reports dims / used. */
+int gs_unsup_loss_plan(const gs_unsup* u, int32_t* buf, int64_t cap,
+                       int64_t* dims, int64_t* used);
+
 /* --------------------------------------------------------- device kernels */
 typedef enum { GS_F32 = 0, GS_BF16 = 1 } gs_dtype;
 typedef enum { GS_AGG_MEAN = 0, GS_AGG_MAX = 1 } gs_agg;
@@ -289,6 +331,26 @@ int gs_cls_nll_fwd_bwd(int64_t B, int64_t D, int64_t C, const float* E,
                        const int32_t* roots, int32_t mask_relu, float* loss,
                        float* dE, float* dWc, float* dbc, float* ws,
                        void* stream);
+
+/* get_loss_sage (kind 0, models.py:65-96) / get_loss_margin (kind 1,
+ * models.py:98-132) over a device copy of gs_unsup_loss_plan:
+ *   sage  : mean_m [ -mean_p log σ(cos⁺) - q · mean_n log σ(-cos⁻) ]
+ *   margin: mean_m max(0, max_n log σ(cos⁻) - min_p log σ(cos⁺) + margin)
+ * with cos = F.cosine_similarity (eps 1e-8) of embedding rows emb[U, D]
+ * (D % 4 == 0, <= 1024, 16-byte aligned rows).  The forward (two launches)
+ * writes loss[0] and keeps per-pair state in ws
+ * (gs_unsup_loss_ws_floats floats, 16-byte aligned); the backward (one
+ * launch) writes dE[U, D] = dloss[0] · ∂loss/∂emb, every row overwritten,
+ * in a fixed summation order (no atomics).  Reference constants: q = 10,
+ * margin = 3 (models.py:35, :40). */
+int64_t gs_unsup_loss_ws_floats(int64_t M, int64_t P, int64_t N);
+int gs_unsup_loss_fwd(int32_t kind, int64_t M, int64_t P, int64_t N, int64_t U,
+                      int64_t D, const float* emb, int64_t lde, const int32_t* plan,
+                      float q, float margin, float* loss, float* ws, void* stream);
+int gs_unsup_loss_bwd(int64_t M, int64_t P, int64_t N, int64_t U, int64_t D,
+                      const float* emb, int64_t lde, const int32_t* plan,
+                      const float* ws, const float* dloss, float* dE, int64_t ldd,
+                      void* stream);
 
 /* clip_grad_norm_(params, max_norm) per group (utils.py:185-186) then SGD
  * (utils.py:136,187): p -= lr * g * min(1, max_norm / (||g_group|| + 1e-6)).

@@ -13,3 +13,4 @@ per-hop frontiers/sampled sets, embeddings and weight gradients.
 from .reference_semantics import (  # noqa: F401
     Adjacency, sample_hop, sample_layers, forward_dense, train_step_dense, nll_loss,
 )
+from . import unsup_semantics  # noqa: F401
