@@ -17,10 +17,15 @@
 //                    -> the copy's slot order, ball members skipped;
 //                otherwise: a fresh set filled in set(train)'s slot order
 //                    with the non-members -> that set's slot order.
-//              Balls and far lists are built in parallel (no rng); the draws
-//              then run in node order on the one stream.
+//              The balls of a chunk of roots grow together (bit-parallel
+//              multi-source BFS, 64 roots per word); far lists are built in
+//              parallel (no rng); the draws then run in node order on the
+//              one stream.
 //   unique     models.py:146  list(set(flat positives) | set(flat negatives)).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -33,41 +38,70 @@
 namespace gs {
 namespace {
 
-struct Ball {
-    std::vector<uint32_t> stamp;  // [n_nodes] == epoch -> in the ball
-    uint32_t epoch = 0;
-    std::vector<int32_t> edge, next;
+// Bit-parallel multi-source BFS: bit b of word w stands for root 64*w + b.
+// The balls of models.py:154-162 are pure membership (set order never
+// reaches the result, see far_list), so all roots of a chunk expand together:
+// per level, every node with a frontier word pushes it to its neighbours.
+// Layout is word-major ([w][node]) so each worker thread owns whole words and
+// the level loop needs no synchronisation.
+struct BallSet {
+    int64_t n_nodes = 0, n_words = 0;
+    std::vector<uint64_t> seen, edge, next;  // [n_words][n_nodes]
 
-    // The frontier expansion of models.py:154-162 (membership only).  Returns
-    // len(neighbors).
-    int64_t grow(const Graph& g, int32_t v, int hops) {
-        if (stamp.empty()) stamp.assign(g.n_nodes, 0);
-        if (++epoch == 0) {  // wrapped: clear
-            std::fill(stamp.begin(), stamp.end(), 0);
-            epoch = 1;
+    void grow(const Graph& g, const int64_t* roots, int64_t n_roots, int hops, int32_t n_threads,
+              std::vector<int64_t>& sizes) {
+        n_nodes = g.n_nodes;
+        n_words = (n_roots + 63) / 64;
+        const size_t total = static_cast<size_t>(n_words * n_nodes);
+        seen.assign(total, 0);
+        edge.assign(total, 0);
+        next.resize(total);
+        for (int64_t r = 0; r < n_roots; ++r) {
+            const uint64_t bit = uint64_t(1) << (r & 63);
+            seen[(r >> 6) * n_nodes + roots[r]] |= bit;
+            edge[(r >> 6) * n_nodes + roots[r]] |= bit;
         }
-        stamp[v] = epoch;
-        int64_t size = 1;
-        edge.assign(1, v);
-        for (int h = 0; h < hops && !edge.empty(); ++h) {
-            next.clear();
-            for (int32_t u : edge) {
-                const int32_t* c = g.col.data() + g.row_ptr[u];
-                const int64_t d = g.degree(u);
-                for (int64_t e = 0; e < d; ++e) {
-                    const int32_t w = c[e];
-                    if (stamp[w] != epoch) {
-                        stamp[w] = epoch;
-                        next.push_back(w);
-                    }
+        auto body = [&](int64_t w) {
+            uint64_t* S = seen.data() + w * n_nodes;
+            uint64_t* E = edge.data() + w * n_nodes;
+            uint64_t* X = next.data() + w * n_nodes;
+            for (int h = 0; h < hops; ++h) {
+                std::fill_n(X, n_nodes, 0);
+                bool any = false;
+                for (int64_t u = 0; u < n_nodes; ++u) {
+                    const uint64_t f = E[u];
+                    if (!f) continue;
+                    const int32_t* c = g.col.data() + g.row_ptr[u];
+                    const int64_t d = g.row_ptr[u + 1] - g.row_ptr[u];
+                    for (int64_t e = 0; e < d; ++e) X[c[e]] |= f;
                 }
+                for (int64_t u = 0; u < n_nodes; ++u) {
+                    const uint64_t nw = X[u] & ~S[u];
+                    E[u] = nw;
+                    S[u] |= nw;
+                    any |= nw != 0;
+                }
+                if (!any) break;
             }
-            size += static_cast<int64_t>(next.size());
-            edge.swap(next);
+            int64_t cnt[64] = {0};  // len(neighbors) of this word's roots
+            for (int64_t u = 0; u < n_nodes; ++u)
+                for (uint64_t m = S[u]; m; m &= m - 1) ++cnt[__builtin_ctzll(m)];
+            for (int b = 0; b < 64 && 64 * w + b < n_roots; ++b) sizes[64 * w + b] = cnt[b];
+        };
+        sizes.assign(n_roots, 0);
+        const int32_t nt = static_cast<int32_t>(std::max<int64_t>(1, std::min<int64_t>(n_threads, n_words)));
+        if (nt == 1) {
+            for (int64_t w = 0; w < n_words; ++w) body(w);
+        } else {
+            std::vector<std::thread> th;
+            for (int32_t t = 0; t < nt; ++t)
+                th.emplace_back([&, t] {
+                    for (int64_t w = t; w < n_words; w += nt) body(w);
+                });
+            for (auto& x : th) x.join();
         }
-        return size;
     }
-    bool has(int32_t w) const { return stamp[w] == epoch; }
+    bool has(int64_t r, int32_t x) const { return (seen[(r >> 6) * n_nodes + x] >> (r & 63)) & 1; }
 };
 
 }  // namespace
@@ -80,7 +114,7 @@ struct gs_unsup {
     std::vector<int32_t> train_order;   // list(set(train_nodes))
     std::vector<int32_t> copy_order;    // list(set(train_nodes).copy())
     int64_t n_train_set = 0;
-    std::vector<gs::Ball> balls;        // one per worker thread
+    gs::BallSet balls;                  // the chunk's 5-hop balls
     // last extend_nodes
     std::vector<int64_t> nodes, unique, pos, neg;  // pairs flattened (a, b)
     std::vector<int64_t> pos_cnt, neg_cnt;
@@ -107,17 +141,74 @@ void run_workers(int32_t n_threads, int64_t n, Fn&& fn) {
     for (auto& x : th) x.join();
 }
 
-// far = set(train) - ball, in CPython iteration order (see file header).
-void far_list(const gs_unsup& u, const gs::Ball& b, int64_t ball_size, std::vector<int32_t>& out) {
-    out.clear();
-    if ((u.n_train_set >> 2) > ball_size) {
-        for (int32_t x : u.copy_order)
-            if (!b.has(x)) out.push_back(x);
+// far = set(train) - ball, in CPython iteration order (see file header), for
+// the roots r0 .. r0+nr-1 that live in ball word w: one pass over the train
+// order serves all 64 roots of the word (one load of the word per key).
+// far[r - r0] receives root r's list.
+void fresh_set_order(std::vector<int32_t>& out);
+
+void far_lists_word(const gs_unsup& u, int64_t w, int64_t r0, int64_t nr, const std::vector<int64_t>& ball_size,
+                    std::vector<std::vector<int32_t>>& far) {
+    const gs::BallSet& b = u.balls;
+    uint64_t copy_roots = 0, fresh_roots = 0;
+    for (int bit = 0; bit < 64; ++bit) {
+        const int64_t r = 64 * w + bit;
+        if (r < r0 || r >= r0 + nr) continue;
+        far[r - r0].clear();
+        if ((u.n_train_set >> 2) > ball_size[r])
+            copy_roots |= uint64_t(1) << bit;
+        else
+            fresh_roots |= uint64_t(1) << bit;
+    }
+    const uint64_t* S = b.seen.data() + w * b.n_nodes;
+    auto pass = [&](const std::vector<int32_t>& order, uint64_t roots) {
+        if (!roots) return;
+        for (int32_t x : order)
+            for (uint64_t m = ~S[x] & roots; m; m &= m - 1)
+                far[64 * w + __builtin_ctzll(m) - r0].push_back(x);
+    };
+    pass(u.copy_order, copy_roots);    // copy(set(train)) then discard the ball
+    pass(u.train_order, fresh_roots);  // a fresh set filled in set(train) order
+    for (uint64_t m = fresh_roots; m; m &= m - 1) fresh_set_order(far[64 * w + __builtin_ctzll(m) - r0]);
+}
+
+// The iteration order of a fresh set built by adding `out`'s keys in order.
+void fresh_set_order(std::vector<int32_t>& out) {
+    // A fresh set filled by adds in this order.  Its final table size follows
+    // from the count alone (no deletions: fill == used at every growth check).
+    // When every key owns its home slot key & mask in that table, each add
+    // (and the insert_clean of the last resize) lands at home whatever came
+    // before, so the iteration order is the home-slot order: place directly.
+    // Any shared home slot: replay the adds through the emulator.
+    const int64_t k = static_cast<int64_t>(out.size());
+    size_t mask = PySet::MINSIZE - 1;
+    for (int64_t used = 1; used <= k; ++used) {
+        if (static_cast<size_t>(used) * 5 < mask * 3) {
+            used = std::max<int64_t>(used, static_cast<int64_t>((mask * 3 + 4) / 5) - 1);  // skip to the next check
+            continue;
+        }
+        size_t ns = PySet::MINSIZE;
+        const size_t minused = static_cast<size_t>(used > 50000 ? used * 2 : used * 4);
+        while (ns <= minused) ns <<= 1;
+        mask = ns - 1;
+    }
+    thread_local std::vector<int32_t> home;
+    home.assign(mask + 1, -1);
+    bool clash = false;
+    for (int32_t x : out) {
+        int32_t& h = home[static_cast<size_t>(x) & mask];
+        clash |= h != -1;
+        h = x;
+    }
+    if (!clash) {
+        out.clear();
+        for (int32_t h : home)
+            if (h != -1) out.push_back(h);
         return;
     }
     PySet r;
-    for (int32_t x : u.train_order)
-        if (!b.has(x)) r.add(x);
+    for (int32_t x : out) r.add(x);
+    out.clear();
     r.for_each([&](int32_t x) { out.push_back(x); });
 }
 
@@ -148,40 +239,58 @@ void walk_pairs(gs_unsup& u, gs_rng* rng) {
 void negative_pairs(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_threads) {
     const int64_t n = static_cast<int64_t>(u.nodes.size());
     const int32_t nt = std::max<int32_t>(1, n_threads);
-    if (static_cast<int32_t>(u.balls.size()) < nt) u.balls.resize(nt);
-    const int64_t chunk = std::max<int64_t>(nt, std::min<int64_t>(n, 4 * nt));
-    std::vector<std::vector<int32_t>> far(static_cast<size_t>(chunk));
+    // roots per ball chunk: whole words, ~96 MiB of ball bitmaps at most
+    const int64_t words = std::max<int64_t>(1, std::min<int64_t>(16, (int64_t(96) << 20) / (24 * u.g->n_nodes + 1)));
+    const int64_t chunk = 64 * words;
+    // far lists held at once: the whole chunk unless that exceeds ~256 MiB
+    const int64_t sub = 64 * std::max<int64_t>(1, std::min<int64_t>(words, (int64_t(1) << 20) / (u.n_train_set + 1)));
+    std::vector<std::vector<int32_t>> far(static_cast<size_t>(sub));
+    std::vector<int64_t> ball_size;
     const int64_t setsize = gs::sample_setsize(num_neg);
     std::vector<int32_t> pool;
     std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
+    static const bool prof = std::getenv("GS_UNSUP_PROF") != nullptr;
+    using clk = std::chrono::steady_clock;
+    double t_ball = 0, t_far = 0, t_draw = 0;
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
         const int64_t cn = std::min(chunk, n - c0);
-        run_workers(nt, cn, [&](int64_t j, int32_t t) {
-            gs::Ball& b = u.balls[t];
-            const int64_t s = b.grow(*u.g, static_cast<int32_t>(u.nodes[c0 + j]), u.n_walk_len);
-            far_list(u, b, s, far[j]);
-        });
-        for (int64_t j = 0; j < cn; ++j) {  // the draws, in node order
-            const int64_t i = c0 + j, v = u.nodes[i];
-            const std::vector<int32_t>& f = far[j];
-            const int64_t len = static_cast<int64_t>(f.size());
-            if (num_neg < len) {
-                if (len <= setsize) pool.resize(static_cast<size_t>(len));
-                gs::sample_positions(rng->mt, len, num_neg, setsize, picks.data(), pool.data());
-                for (int64_t t = 0; t < num_neg; ++t) {
-                    u.neg.push_back(v);
-                    u.neg.push_back(f[picks[t]]);
+        auto t0 = clk::now();
+        u.balls.grow(*u.g, u.nodes.data() + c0, cn, u.n_walk_len, nt, ball_size);
+        t_ball += std::chrono::duration<double>(clk::now() - t0).count();
+        if (prof) std::fprintf(stderr, "[unsup] balls %.2f ms\n", t_ball * 1e3);
+        for (int64_t s0 = 0; s0 < cn; s0 += sub) {
+            const int64_t sn = std::min(sub, cn - s0);
+            auto t1 = clk::now();
+            run_workers(nt, (sn + 63) / 64, [&](int64_t j, int32_t) {
+                far_lists_word(u, s0 / 64 + j, s0, sn, ball_size, far);
+            });
+            auto t2 = clk::now();
+            t_far += std::chrono::duration<double>(t2 - t1).count();
+            for (int64_t j = 0; j < sn; ++j) {  // the draws, in node order
+                const int64_t i = c0 + s0 + j, v = u.nodes[i];
+                const std::vector<int32_t>& f = far[j];
+                const int64_t len = static_cast<int64_t>(f.size());
+                if (num_neg < len) {
+                    if (len <= setsize) pool.resize(static_cast<size_t>(len));
+                    gs::sample_positions(rng->mt, len, num_neg, setsize, picks.data(), pool.data());
+                    for (int64_t t = 0; t < num_neg; ++t) {
+                        u.neg.push_back(v);
+                        u.neg.push_back(f[picks[t]]);
+                    }
+                    u.neg_cnt[i] = num_neg;
+                } else {
+                    for (int32_t x : f) {
+                        u.neg.push_back(v);
+                        u.neg.push_back(x);
+                    }
+                    u.neg_cnt[i] = len;
                 }
-                u.neg_cnt[i] = num_neg;
-            } else {
-                for (int32_t x : f) {
-                    u.neg.push_back(v);
-                    u.neg.push_back(x);
-                }
-                u.neg_cnt[i] = len;
             }
+            t_draw += std::chrono::duration<double>(clk::now() - t2).count();
         }
+        (void)t0;
     }
+    if (prof) std::fprintf(stderr, "[unsup] far %.2f ms draw %.2f ms\n", t_far * 1e3, t_draw * 1e3);
 }
 
 }  // namespace
