@@ -45,6 +45,12 @@ CONFIGS = {
     # configs[3]
     "rmat2m-max-bf16": dict(scale=21, pairs=20_000_000, feat=256, fanouts=(25, 10), agg="MAX",
                             dtype="bf16", batch=512, classes=16),
+    # configs[1]: the reference's own loop (apply_model, utils.py:113-193) on the Pubmed citation
+    # graph (pairs from the reference's cites file, tests/golden/graphs.npz): every step
+    # extend_nodes(512 roots, num_neg=100) -> GraphSage forward over the extended batch
+    # (fanouts 10,10) -> supervised NLL -> backward -> clip -> SGD, through the drop-in modules
+    "pubmed": dict(graph="pubmed", feat=500, fanouts=(10, 10), agg="MEAN", dtype="fp32", batch=512, classes=3,
+                   loop="apply_model"),
     # configs[4] (per-GPU share of the 8-GPU job)
     "rmat16m": dict(scale=24, pairs=160_000_000, feat=128, fanouts=(25, 10), agg="MEAN", dtype="fp32",
                     batch=512, classes=16),
@@ -179,6 +185,102 @@ def load_traffic(config_name, kernel):
     return best
 
 
+def pubmed_workload(cfg, device, seed=824):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "graphs.npz"))
+    src, dst, n = g["pubmed_src"].astype(np.int64), g["pubmed_dst"].astype(np.int64), int(g["pubmed_n"][0])
+    graph = gs.CSRGraph.from_pairs(src, dst, n)
+    X = torch.empty(n, cfg["feat"], dtype=torch.float32, device=device)
+    ops.fill_uniform(X, seed)
+    np.random.seed(seed)  # dataCenter.py:100-111 split after main.py:41's seed
+    perm = np.random.permutation(n)
+    train = perm[n // 3 + n // 6:]
+    labels = (np.arange(n) % cfg["classes"]).astype(np.int64)
+    return dict(src=src, dst=dst, n=n, graph=graph, X=X, train=train, labels=labels)
+
+
+def cpu_baseline_loop(wl, cfg, batches, seconds_budget=25.0, seed=824):
+    """The oracle's restatement of one apply_model step (extend_nodes with
+    Python sets + dense-mask forward/backward + clip + SGD) on this host."""
+    import random as pyrandom
+    import oracle
+    from oracle import unsup_semantics as U
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    adj = oracle.Adjacency(wl["src"], wl["dst"], wl["n"])
+    st = U.UnsupState(adj, wl["train"])
+    sage_w, cls_w, cls_b = train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, seed)
+    W = [w.clone().requires_grad_(True) for w in sage_w]
+    cw, cb = cls_w.clone().requires_grad_(True), cls_b.clone().requires_grad_(True)
+    X = wl["X"].float().cpu()
+    labels = torch.from_numpy(wl["labels"])
+    pyrandom.seed(seed)
+    times = []
+    t_start = time.perf_counter()
+    for roots in batches:
+        t = time.perf_counter()
+        nodes, _ = U.extend_nodes(st, roots, 100)
+        oracle.train_step_dense(adj, nodes, list(cfg["fanouts"]), X, W, cw, cb,
+                                labels[torch.as_tensor(nodes)], agg=cfg["agg"])
+        times.append(time.perf_counter() - t)
+        if time.perf_counter() - t_start > seconds_budget and len(times) >= 3:
+            break
+    med = float(np.median(times[1:] if len(times) > 1 else times))
+    return {"value": cfg["batch"] / med, "unit": "root nodes/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle apply_model steps of B={cfg['batch']} roots (first untimed), median "
+                      f"{med * 1e3:.1f} ms/step: extend_nodes (Python sets, num_neg 100) + dense-mask forward/"
+                      f"backward on the extended batch, torch CPU {threads} threads"}
+
+
+def run_apply_model_loop(args, cfg):
+    """configs[1]: timed steps of the reference's training loop body through the
+    drop-in modules (UnsupervisedLoss / GraphSage / fused head, utils.train_step)."""
+    import random as pyrandom
+    unsup = import_module("graphsage-pytorch_amd.unsup")
+    utils = import_module("graphsage-pytorch_amd.utils")
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    wl = pubmed_workload(cfg, device, args.seed)
+    torch.manual_seed(args.seed)
+    gsage = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], device, agg_func=cfg["agg"],
+                             fanouts=list(cfg["fanouts"])).to(device)
+    cls = models.Classification(128, cfg["classes"]).to(device)
+    ul = unsup.UnsupervisedLoss(wl["graph"], wl["train"], device, n_threads=host_threads())
+    params = [p for m in (gsage, cls) for p in m.parameters()]
+    opt = torch.optim.SGD(params, lr=0.7)
+    order = np.random.RandomState(args.seed + 1).permutation(wl["train"])
+    nb = len(order) // cfg["batch"]
+    batches = [order[(i % nb) * cfg["batch"]:(i % nb + 1) * cfg["batch"]] for i in range(args.warmup + args.steps)]
+    pyrandom.seed(args.seed)
+    step = lambda b: utils.train_step(gsage, cls, ul, opt, b, wl["labels"], 100, "sup", None)  # noqa: E731
+    for b in batches[:args.warmup]:
+        step(b)
+    torch.cuda.synchronize()
+    ext = 0
+    t0 = time.perf_counter()
+    for b in batches[args.warmup:]:
+        loss, nodes = step(b)
+        ext += len(nodes)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_loop(wl, cfg, batches, args.cpu_budget, args.seed)
+    out = {
+        "metric": "sampled nodes/sec (2-layer, fanout 25,10) at 1/2/4/8 MI355X",
+        "value": round(cfg["batch"] * args.steps / elapsed, 1), "unit": "root nodes/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
+        "data": "Pubmed citation graph (reference cites file), synthetic U(-1,1) 500-d features, labels id%3",
+        "config": {"workload": "pubmed: apply_model step (extend_nodes num_neg 100 + GraphSage fanouts (10, 10) "
+                               "MEAN over the extended batch + sup NLL + backward + clip + SGD), B=512 roots",
+                   "global_batch": cfg["batch"], "parallelism": "dp1",
+                   "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5)},
+        "roofline": None,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,6 +303,10 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
+    if cfg.get("loop") == "apply_model":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("the pubmed (apply_model) config runs on one GPU")
+        return run_apply_model_loop(args, cfg)
     rank, world = train.init_distributed()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)

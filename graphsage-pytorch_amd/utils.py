@@ -61,6 +61,30 @@ def _trainable(models):
     return [p for m in models for p in m.parameters() if p.requires_grad]
 
 
+def train_step(graphSage, classification, unsupervised_loss, optimizer, batch, labels, num_neg, learn_method,
+               unsup):
+    """The body of one apply_model batch (utils.py:146-191): extend, forward,
+    losses, backward, clip per model, SGD.  Returns (loss, extended nodes);
+    the loss stays on the device (no host sync)."""
+    nodes = np.asarray(list(unsupervised_loss.extend_nodes(batch, num_neg=num_neg)))
+    embs = graphSage(nodes)
+    parts = []
+    if learn_method in ("sup", "plus_unsup"):
+        parts.append(supervised_loss(classification, embs, labels[nodes]))
+    if learn_method != "sup":
+        parts.append(unsup(embs, nodes))
+    loss = parts[0] if len(parts) == 1 else parts[0] + parts[1]
+    loss.backward()
+    models = [graphSage, classification]
+    for m in models:
+        nn.utils.clip_grad_norm_(m.parameters(), 5)
+    optimizer.step()
+    optimizer.zero_grad()
+    for m in models:
+        m.zero_grad()
+    return loss.detach(), nodes
+
+
 def apply_model(dataCenter, ds, graphSage, classification, unsupervised_loss, b_sz, unsup_loss, device,
                 learn_method, verbose=True):
     """One training epoch, utils.py:113-193.  Returns (graphSage, classification)."""
@@ -84,25 +108,12 @@ def apply_model(dataCenter, ds, graphSage, classification, unsupervised_loss, b_
     seen = set()
     for index in range(n_batches):
         batch = train_nodes[index * b_sz:(index + 1) * b_sz]
-        nodes = np.asarray(list(unsupervised_loss.extend_nodes(batch, num_neg=num_neg)))
+        loss, nodes = train_step(graphSage, classification, unsupervised_loss, optimizer, batch, labels, num_neg,
+                                 learn_method, unsup)
         seen.update(nodes.tolist())
-        embs = graphSage(nodes)
-        parts = []
-        if learn_method in ("sup", "plus_unsup"):
-            parts.append(supervised_loss(classification, embs, labels[nodes]))
-        if learn_method != "sup":
-            parts.append(unsup(embs, nodes))
-        loss = parts[0] if len(parts) == 1 else parts[0] + parts[1]
         if verbose:
             print(f"Step [{index + 1}/{n_batches}], Loss: {loss.item():.4f}, "
                   f"Dealed Nodes [{len(seen)}/{len(train_nodes)}] ")
-        loss.backward()
-        for m in models:
-            nn.utils.clip_grad_norm_(m.parameters(), 5)
-        optimizer.step()
-        optimizer.zero_grad()
-        for m in models:
-            m.zero_grad()
     return graphSage, classification
 
 
