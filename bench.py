@@ -56,6 +56,7 @@ CONFIGS = {
                     batch=512, classes=16),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_PEAK_TFS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense F32 / BF16 matrix peaks (spec)
 
 
 def host_cores():
@@ -91,14 +92,19 @@ def build_workload(cfg, device, seed=824):
                 t_graph=t_graph, deg=deg)
 
 
-def agg1_times_ms(trainer, n):
-    """HIP-event durations of the layer-1 K-agg launches recorded by the native
-    step on its own stream (gs_trainer_time_agg)."""
+def kernel_times_ms(trainer, n, site=0):
+    """Kernel-bound HIP-event durations recorded by the native step on its
+    launch stream (gs_trainer_time_agg arms them): site 0 the layer-1
+    gather-aggregate, 1 the layer-1 SageLayer GEMM, 2 its weight-gradient GEMM."""
     out = np.zeros(max(n, 1), np.float32)
-    got = int(gs._lib.lib().gs_trainer_agg_times(trainer._h, out.ctypes.data, n))
+    got = int(gs._lib.lib().gs_trainer_kernel_times(trainer._h, site, out.ctypes.data, n))
     if got < 0:
         raise RuntimeError("event timing failed")
     return out[:got]
+
+
+def agg1_times_ms(trainer, n):
+    return kernel_times_ms(trainer, n, 0)
 
 
 def cgroup_throttle():
@@ -318,7 +324,8 @@ def main():
     trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2,
                                   hidden=128, fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=args.seed)
     rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
-    total_steps = args.warmup + args.steps
+    calib = min(50, args.steps)  # untimed steps after the measured ones that time the layer-1 GEMMs
+    total_steps = args.warmup + args.steps + calib
     batches = []
     epoch = 0
     while len(batches) < total_steps:
@@ -345,12 +352,16 @@ def main():
     elapsed = time.perf_counter() - t0
     thr1 = cgroup_throttle()
     st = runner.stats()
+    agg_ms = float(np.mean(agg1_times_ms(trainer, args.steps)))
+    gs._lib.check(gs._lib.lib().gs_trainer_time_kernels(trainer._h, 0b110, calib))
+    runner.run(calib)
+    torch.cuda.synchronize()
+    gemm_ms = {site: kernel_times_ms(trainer, calib, site) for site in (1, 2)}
     loss = float(trainer.loss.item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    agg_ms = float(np.mean(agg1_times_ms(trainer, args.steps)))
     value = cfg["batch"] * args.steps * world / elapsed
     L = len(cfg["fanouts"])
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
@@ -361,7 +372,7 @@ def main():
         kname = "sage1_fwd_kernel (layer-1 gather-mean + concat-linear-relu, fused)"
     else:  # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
         agg_bytes = agg1_ids_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem, cfg["fanouts"][-1])
-        kname = "agg_ids_kernel (layer-1 gather-mean over resolved neighbour ids)"
+        kname = f"agg_ids_kernel (layer-1 gather-{cfg['agg'].lower()} over resolved neighbour ids)"
 
     if rank == 0:
         achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9
@@ -371,6 +382,20 @@ def main():
                 "traffic": (tr["layer1_hbm_bytes_per_launch"] if tr else None),
                 "kernel": kname, "avg_launch_us": round(agg_ms * 1e3, 2),
                 "algo_bytes_per_launch": int(agg_bytes)}
+        # the MFMA side: layer-1 SageLayer GEMMs, 2·n1·K·H flops each
+        K1 = 2 * cfg["feat"]
+        flops = 2.0 * float(sizes[L - 1, 0]) * K1 * 128
+        mfma = {}
+        for site, name in ((1, "linear_fwd_kernel (layer 1: relu([X[self] | agg]·W1ᵀ))"),
+                           (2, "linear_dw_kernel (layer 1: dW1 = dZ1ᵀ·[X[self] | agg] row slabs)")):
+            t = gemm_ms[site]
+            if len(t):
+                tf = flops / (float(np.mean(t)) * 1e-3) / 1e12
+                peak = MFMA_PEAK_TFS[cfg["dtype"]]
+                mfma["fwd" if site == 1 else "dw"] = {
+                    "bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(tf / peak, 4), "kernel": name, "avg_launch_us": round(float(np.mean(t)) * 1e3, 2),
+                    "algo_flops_per_launch": int(flops)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(wl, cfg, args.cpu_budget, args.seed)
@@ -399,6 +424,7 @@ def main():
                                             "max_step": round(1e3 * st["max_step_s"], 3)},
                        "cgroup_throttled_ms": (round((thr1 - thr0) / 1e3, 3) if thr0 is not None else None)},
             "roofline": roof,
+            "roofline_mfma": mfma or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -116,6 +116,8 @@ _SIGS = {
     "gs_trainer_forward_backward_gathered": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
+    "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
+    "gs_trainer_time_kernels": (_i32, [_vp, _i32, _i64]),
     "gs_trainer_grads": (_vp, [_vp]),
     "gs_trainer_layer1_fused": (_i32, [_vp]),
     "gs_comm_unique_id": (_i32, [_vp]),

@@ -25,6 +25,35 @@ __global__ __launch_bounds__(kBlock) void resolve_ids_kernel(int n_dst, int k, c
     ids[t] = nb;
 }
 
+// A row chunk as loaded (one 16-byte vector per lane, or a scalar), unpacked
+// to floats only when accumulated.
+template <typename T, int VEC>
+struct RawVec {
+    using type = T;
+    static __device__ __forceinline__ void unpack(const T& r, float (&v)[VEC]) {
+        RowIO<T, VEC>::load(&r, v);
+    }
+};
+template <>
+struct RawVec<float, 4> {
+    using type = float4;
+    static __device__ __forceinline__ void unpack(const float4& r, float (&v)[4]) {
+        v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w;
+    }
+};
+template <>
+struct RawVec<bf16_t, 8> {
+    using type = uint4;
+    static __device__ __forceinline__ void unpack(const uint4& r, float (&v)[8]) {
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v[2 * i] = __uint_as_float(w[i] << 16);
+            v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+        }
+    }
+};
+
 // The layer-1 gather over resolved ids (k slots per destination, -1 = skip).
 // Same lane groups, chunking and accumulation order as agg_fwd_kernel's
 // expand mode (empty slots add +0 / never win a max), so the output is
@@ -64,20 +93,23 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
                     ok[u] = (j + u < m) && rows[u] >= 0;
                 }
                 const int fallback = rows[0] >= 0 ? rows[0] : node;
-                float x[NR][VEC];
+                using Raw = typename RawVec<T, VEC>::type;
+                Raw x[NR];
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
-                    RowIO<T, VEC>::load(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0c, x[u]);
+                    x[u] = *reinterpret_cast<const Raw*>(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0c);
 #pragma unroll
                 for (int u = 0; u < NR; ++u) {
                     cnt += ok[u];
+                    float xv[VEC];
+                    RawVec<T, VEC>::unpack(x[u], xv);
 #pragma unroll
                     for (int v = 0; v < VEC; ++v) {
                         if (OP == GS_AGG_MEAN) {
-                            acc[v] += ok[u] ? x[u][v] : 0.f;
+                            acc[v] += ok[u] ? xv[v] : 0.f;
                         } else {
-                            const bool take = ok[u] && x[u][v] > acc[v];
-                            acc[v] = take ? x[u][v] : acc[v];
+                            const bool take = ok[u] && xv[v] > acc[v];
+                            acc[v] = take ? xv[v] : acc[v];
                         }
                     }
                 }

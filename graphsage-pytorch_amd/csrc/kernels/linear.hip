@@ -69,7 +69,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     }
     const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 63) / 64));
 #define GS_LFWD1(TT, SELF, RELU, VL)                                                                     \
-    linear_fwd_kernel<TT, SELF, RELU, VL><<<grid, kThreads, 0, st>>>(                                   \
+    launch_k(linear_fwd_kernel<TT, SELF, RELU, VL>, grid, dim3(kThreads), 0, st,                        \
         nn, ff, hh, K, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,          \
         static_cast<const TT*>(Wd), out, ldo)
 #define GS_LFWD_V(TT, SELF, RELU) \
@@ -127,7 +127,7 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
                     static_cast<unsigned>(S));
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
 #define GS_LDW1(TT, SELF, RELU, VL, ZV)                                                                  \
-    linear_dw_kernel<TT, SELF, RELU, VL, ZV><<<grid, kThreads, 0, st>>>(                                \
+    launch_k(linear_dw_kernel<TT, SELF, RELU, VL, ZV>, grid, dim3(kThreads), 0, st,                     \
         nn, ff, hh, kk, rps, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,    \
         dout, out, ldo, target, H * K)
 #define GS_LDW_Z(TT, SELF, RELU, VL) \

@@ -17,9 +17,17 @@ struct gs_trainer {
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
     bool fused1 = false;  // layer 1 through gs_sage1_fwd (gather + linear in one launch)
     bool fused2 = false;  // layers >= 2 likewise (explicit lists; MEAN)
-    // optional HIP-event timing of the layer-1 gather-aggregate (bench roofline)
-    std::vector<hipEvent_t> ev0, ev1;
-    int64_t n_timed = 0;
+    // optional kernel-bound HIP-event timing (bench roofline): site 0 the
+    // layer-1 gather-aggregate, 1 the layer-1 linear forward, 2 its weight
+    // gradient (the MFMA kernels)
+    static constexpr int kSites = 3;
+    struct Timer {
+        std::vector<hipEvent_t> ev0, ev1;
+        int64_t n = 0;
+    } timer[kSites];
+    std::vector<hipEvent_t>& ev0 = timer[0].ev0;
+    std::vector<hipEvent_t>& ev1 = timer[0].ev1;
+    int64_t& n_timed = timer[0].n;
     // layer-1 aggregate slots for gathers issued ahead of their step
     // (gs_trainer_gather), so the next batch's gather overlaps this backward
     static constexpr int kSlots = 3;
@@ -39,8 +47,10 @@ struct gs_trainer {
     bool norm_ready = false;
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
-        for (auto e : ev0) (void)hipEventDestroy(e);
-        for (auto e : ev1) (void)hipEventDestroy(e);
+        for (auto& tm : timer) {
+            for (auto e : tm.ev0) (void)hipEventDestroy(e);
+            for (auto e : tm.ev1) (void)hipEventDestroy(e);
+        }
         for (void* p : a1_slot)
             if (p) (void)hipFree(p);
         for (int32_t* p : ids_slot)
@@ -69,6 +79,20 @@ struct HopSz {
 
 static inline void ok(int rc) {
     if (rc != GS_OK) fail(rc, gs_last_error());
+}
+
+// Bind the next launch_k launch to timer site `site` when it has capacity
+// left; returns whether it did (pass the result to timed_done).
+static inline bool timed_arm(gs_trainer& T, int site) {
+    auto& tm = T.timer[site];
+    if (tm.n >= static_cast<int64_t>(tm.ev0.size())) return false;
+    g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
+    return true;
+}
+static inline void timed_done(gs_trainer& T, int site, bool armed) {
+    if (!armed) return;
+    GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
+    ++T.timer[site].n;
 }
 
 // The layer-1 gather-aggregate of one packed sample (models.py:291-330 at
@@ -196,9 +220,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     } else if (a1_slot < 0) {
         gather1(T, pack, hop_sizes, offsets, agg[0], st);
     }
-    if (!fused1)
+    if (!fused1) {
+        const bool armed = timed_arm(T, 1);
         ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
                               dst_L, agg[0], F, W1, h[0], H, 1, st));
+        g_launch_events = {};  // an alternative kernel that does not time leaves it armed
+        timed_done(T, 1, armed);
+    }
     for (int l = 2; l <= L; ++l) {
         const int j = L - l + 1;
         if (T.fused2 && c.agg == GS_AGG_MEAN) {  // MAX needs the argmax the fused kernel does not keep
@@ -260,9 +288,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 np += n;
             }
             const int64_t K1 = T.w_cols[0];
+            const bool armed = timed_arm(T, 2);
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
                                            c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0],
                                            dw_ws, dw_need, st);
+            g_launch_events = {};
+            timed_done(T, 2, armed);
             if (S1 > 1) {
                 sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0], T.norm_part + np,
                                  st);
@@ -439,30 +470,38 @@ int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack, con
     GS_API_END
 }
 
-int gs_trainer_time_agg(gs_trainer* t, int64_t capacity) {
+int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity) {
     GS_API_BEGIN
     GS_REQUIRE(t && capacity >= 0, GS_EINVAL, "bad arguments");
-    for (auto e : t->ev0) (void)hipEventDestroy(e);
-    for (auto e : t->ev1) (void)hipEventDestroy(e);
-    t->ev0.assign(capacity, nullptr);
-    t->ev1.assign(capacity, nullptr);
-    for (int64_t i = 0; i < capacity; ++i)
-        GS_REQUIRE(hipEventCreate(&t->ev0[i]) == hipSuccess && hipEventCreate(&t->ev1[i]) == hipSuccess, GS_EHIP,
-                   "hipEventCreate");
-    t->n_timed = 0;
+    for (int s = 0; s < gs_trainer::kSites; ++s) {
+        auto& tm = t->timer[s];
+        for (auto e : tm.ev0) (void)hipEventDestroy(e);
+        for (auto e : tm.ev1) (void)hipEventDestroy(e);
+        const int64_t cap = (site_mask >> s) & 1 ? capacity : 0;
+        tm.ev0.assign(cap, nullptr);
+        tm.ev1.assign(cap, nullptr);
+        for (int64_t i = 0; i < cap; ++i)
+            GS_REQUIRE(hipEventCreate(&tm.ev0[i]) == hipSuccess && hipEventCreate(&tm.ev1[i]) == hipSuccess, GS_EHIP,
+                       "hipEventCreate");
+        tm.n = 0;
+    }
     GS_API_END
 }
 
-int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap) {
-    if (!t || !ms) return -1;
-    const int64_t n = std::min(cap, t->n_timed);
+int gs_trainer_time_agg(gs_trainer* t, int64_t capacity) { return gs_trainer_time_kernels(t, 1, capacity); }
+
+int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap) {
+    if (!t || !ms || site < 0 || site >= gs_trainer::kSites) return -1;
+    auto& tm = t->timer[site];
+    const int64_t n = std::min(cap, tm.n);
     for (int64_t i = 0; i < n; ++i) {
-        if (hipEventSynchronize(t->ev1[i]) != hipSuccess ||
-            hipEventElapsedTime(&ms[i], t->ev0[i], t->ev1[i]) != hipSuccess)
+        if (hipEventSynchronize(tm.ev1[i]) != hipSuccess || hipEventElapsedTime(&ms[i], tm.ev0[i], tm.ev1[i]) != hipSuccess)
             return -1;
     }
     return n;
 }
+
+int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap) { return gs_trainer_kernel_times(t, 0, ms, cap); }
 
 int gs_trainer_update_local(gs_trainer* t, void* stream) {
     GS_API_BEGIN

@@ -432,6 +432,16 @@ int gs_trainer_update_local(gs_trainer* t, void* stream);
  * synchronises and returns their durations (ms). */
 int gs_trainer_time_agg(gs_trainer* t, int64_t capacity);
 int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
+/* The same timers per site: 0 the layer-1 gather as above, 1 the layer-1
+ * SageLayer forward GEMM (gs_sage_linear_fwd, unfused path), 2 the layer-1
+ * weight-gradient GEMM of the fused backward (linear_dw slabs, before their
+ * sum).  gs_trainer_time_kernels arms the sites in site_mask (bit s = site
+ * s) for their next `capacity` launches and disarms the others;
+ * gs_trainer_time_agg(t, n) == gs_trainer_time_kernels(t, 1, n).  Every
+ * armed launch is an event-bound hipExtLaunchKernel, which costs the stream
+ * a little: time the GEMM sites in their own steps, not the measured ones. */
+int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity);
+int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap);
 /* The flat gradient buffer (cfg.grads), gs_trainer_n_params floats. */
 float* gs_trainer_grads(const gs_trainer* t);
 /* 1 when layer 1 runs through gs_sage1_fwd (opt-in: GS_FUSED1 set at create). */
