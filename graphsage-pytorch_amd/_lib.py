@@ -114,6 +114,8 @@ _SIGS = {
     "gs_trainer_gather_reserve": (_i32, [_vp, _i64, _i32]),
     "gs_trainer_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),
     "gs_trainer_forward_backward_gathered": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    "gs_trainer_forward": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "gs_trainer_forward_gathered": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]),
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
@@ -145,7 +147,7 @@ class RunnerConfig(ctypes.Structure):
     _fields_ = [
         ("graph", _vp), ("trainer", _vp), ("batches", _vp), ("n_batches", _i64), ("batch", _i64),
         ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
-        ("depth", _i32), ("comm", _vp), ("world", _i32),
+        ("depth", _i32), ("comm", _vp), ("world", _i32), ("embed_out", _vp), ("embed_ld", _i64),
     ]
 
 

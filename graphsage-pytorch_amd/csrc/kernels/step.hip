@@ -144,10 +144,13 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
 }
 
 // Runs (or, with ws == nullptr, only sizes) one forward + backward.  With
-// a1_slot >= 0 the layer-1 aggregate was produced by gs_trainer_gather.
+// a1_slot >= 0 the layer-1 aggregate was produced by gs_trainer_gather.  With
+// embed_out the step is the forward alone (models.py:241-269 as called by
+// get_gnn_embeddings, utils.py:59-78): the last layer writes its [B, H]
+// embeddings straight into embed_out and nothing after the forward runs.
 static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
                         const int32_t* roots, int64_t B, char* ws, int64_t ws_bytes, float* loss,
-                        hipStream_t st, int a1_slot = -1) {
+                        hipStream_t st, int a1_slot = -1, float* embed_out = nullptr) {
     const gs_trainer_config& c = T.cfg;
     const int L = c.n_layers;
     const int64_t H = c.hidden, F = c.feat_dim;
@@ -180,7 +183,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
         }
         else agg[l - 1] = cv.take<float>(rows[l - 1] * H);
-        h[l - 1] = cv.take<float>(rows[l - 1] * H);
+        h[l - 1] = (embed_out && l == L) ? embed_out : cv.take<float>(rows[l - 1] * H);
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
     }
     void* w1lp = lowp ? cv.take<uint16_t>(T.w_rows[0] * T.w_cols[0]) : nullptr;
@@ -240,6 +243,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
                               agg[l - 1], H, P + T.w_off[l - 1], h[l - 1], H, 1, st));
     }
+    if (embed_out) return cv.at;  // inference: no loss head, no backward
     T.norm_ready = false;
     // ---- fused backward (bwd.hip): same kernels and summation order as the
     // sequence below, two launches per layer >= 2 instead of five
@@ -467,6 +471,26 @@ int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack, con
                GS_EINVAL, "bad arguments");
     gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
                  gs::as_stream(stream), slot);
+    GS_API_END
+}
+
+int gs_trainer_forward(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+                       void* ws, int64_t ws_bytes, float* out, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && pack && hop_sizes && offsets && ws && out, GS_EINVAL, "NULL argument");
+    gs::run_step(*t, pack, hop_sizes, offsets, nullptr, hop_sizes[0], static_cast<char*>(ws), ws_bytes, nullptr,
+                 gs::as_stream(stream), -1, out);
+    GS_API_END
+}
+
+int gs_trainer_forward_gathered(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                                const int64_t* offsets, int32_t slot, void* ws, int64_t ws_bytes, float* out,
+                                void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && pack && hop_sizes && offsets && ws && out && slot >= 0 && slot < gs_trainer::kSlots, GS_EINVAL,
+               "bad arguments");
+    gs::run_step(*t, pack, hop_sizes, offsets, nullptr, hop_sizes[0], static_cast<char*>(ws), ws_bytes, nullptr,
+                 gs::as_stream(stream), slot, out);
     GS_API_END
 }
 

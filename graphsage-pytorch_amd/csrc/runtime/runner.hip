@@ -284,6 +284,8 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(cfg->n_streams >= 1 && cfg->n_streams <= 64 && cfg->depth >= 1 && cfg->depth <= 64, GS_EINVAL,
                "n_streams / depth out of range");
     GS_REQUIRE(cfg->world >= 1 && (cfg->world == 1 || cfg->comm), GS_EINVAL, "world > 1 needs a communicator");
+    GS_REQUIRE(!cfg->embed_out || (cfg->embed_ld >= 1 && !cfg->comm), GS_EINVAL,
+               "embed_out needs embed_ld >= 1 and no communicator");
     for (int32_t w = 0; w < cfg->n_streams; ++w) GS_REQUIRE(cfg->rngs[w], GS_EINVAL, "NULL rng");
     std::unique_ptr<gs_runner> r(new gs_runner());
     r->cfg = *cfg;
@@ -347,7 +349,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
 int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     GS_API_BEGIN
     using namespace gs;
-    GS_REQUIRE(r && loss && n_steps >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(r && (loss || r->cfg.embed_out) && n_steps >= 0, GS_EINVAL, "bad arguments");
     GS_REQUIRE(r->next_batch + n_steps <= r->cfg.n_batches, GS_ERANGE, "runner has fewer batches left");
     hipStream_t st = as_stream(stream);
     const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
@@ -383,21 +385,31 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         const int64_t pack_total = slot.used - r->cfg.batch;
         int32_t* pk = r->dev[k];
-        int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets,
-                                                      pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss, st);
-        if (rc != GS_OK) fail(rc, gs_last_error());
-        const auto t3 = Clock::now();
-        // with a communicator (any world size, so one rank exercises the same
-        // path): sum the gradients, then clip the averaged sum; without one
-        // the clip uses the norm partials of the step's own reductions
-        if (r->cfg.comm) {
-            rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
+        auto t3 = Clock::now();
+        if (r->cfg.embed_out) {  // inference: the forward into this batch's output rows
+            const int rc = gs_trainer_forward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets, k, r->ws,
+                                                       r->ws_bytes, r->cfg.embed_out + b * r->cfg.batch * r->cfg.embed_ld,
+                                                       st);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            t3 = Clock::now();
+        } else {
+            int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets,
+                                                          pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
+                                                          st);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            t3 = Clock::now();
+            // with a communicator (any world size, so one rank exercises the same
+            // path): sum the gradients, then clip the averaged sum; without one
+            // the clip uses the norm partials of the step's own reductions
+            if (r->cfg.comm) {
+                rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
+                if (rc != GS_OK) fail(rc, gs_last_error());
+            }
+            rc = r->cfg.comm
+                     ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
+                     : gs_trainer_update_local(r->cfg.trainer, st);
             if (rc != GS_OK) fail(rc, gs_last_error());
         }
-        rc = r->cfg.comm
-                 ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
-                 : gs_trainer_update_local(r->cfg.trainer, st);
-        if (rc != GS_OK) fail(rc, gs_last_error());
         hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
         r->dev_busy[k] = true;
         for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);

@@ -265,6 +265,16 @@ class GraphSage(nn.Module):
             layer_size = out_size if index != 1 else input_size
             setattr(self, 'sage_layer' + str(index), SageLayer(layer_size, out_size, gcn=self.gcn))
 
+    def __getstate__(self):
+        """Pickle support for torch.save(models) (utils.py:52): the native CSR
+        is a derived cache and is rebuilt from adj_lists after loading."""
+        if isinstance(self.adj_lists, CSRGraph) or self.rng is not None:
+            raise TypeError("GraphSage built on a native CSRGraph / RNG handle cannot be pickled; "
+                            "save its state_dict() instead")
+        state = self.__dict__.copy()
+        state["_graph"] = None
+        return state
+
     # -------------------------------------------------------------- helpers
     @property
     def graph(self):

@@ -100,16 +100,33 @@ class NativeTrainer:
         """Loss (device scalar) and gradients into self.p.grads for one batch:
         one native call that issues every kernel of the step on the stream."""
         sizes, offs = ds.native_sizes()
-        need = int(lib().gs_trainer_ws_bytes(self._h, sizes.ctypes.data))
-        if need < 0:
-            check(_lib.GS_EINVAL)
-        if self._ws.numel() < need:
-            self._ws = torch.empty(int(need * 1.25) + (1 << 20), dtype=torch.uint8, device=self.device)
+        self._reserve_ws(sizes)
         check(lib().gs_trainer_forward_backward(
             self._h, ds.buf.data_ptr(), sizes.ctypes.data, offs.ctypes.data, roots_dev.data_ptr(),
             roots_dev.numel(), self._ws.data_ptr(), self._ws.numel(), self.loss.data_ptr(),
             _lib.stream_ptr(self.device)))
         return self.loss
+
+    def _reserve_ws(self, sizes):
+        need = int(lib().gs_trainer_ws_bytes(self._h, sizes.ctypes.data))
+        if need < 0:
+            check(_lib.GS_EINVAL)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(int(need * 1.25) + (1 << 20), dtype=torch.uint8, device=self.device)
+
+    def forward(self, ds, out):
+        """GraphSage forward alone (models.py:241-269): the batch's embeddings
+        into `out` ([n_roots, hidden] fp32, contiguous); no loss or backward."""
+        if not (out.is_contiguous() and out.dtype == torch.float32 and out.shape[1] == self.H):
+            raise ValueError("out must be a contiguous fp32 [n_roots, hidden] tensor")
+        sizes, offs = ds.native_sizes()
+        if out.shape[0] != sizes[0]:
+            raise ValueError("out rows != batch roots")
+        self._reserve_ws(sizes)
+        check(lib().gs_trainer_forward(self._h, ds.buf.data_ptr(), sizes.ctypes.data, offs.ctypes.data,
+                                       self._ws.data_ptr(), self._ws.numel(), out.data_ptr(),
+                                       _lib.stream_ptr(self.device)))
+        return out
 
     def apply_update(self, world_size=1, group=None):
         """All-reduce (sum) the flat gradients over ranks, then clip + SGD with 1/world."""
@@ -311,8 +328,9 @@ class Runner:
     (stream w samples batches w, w+S, ...)."""
 
     def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
-                 comm=None):
+                 comm=None, embed_out=None):
         self.trainer, self.graph = trainer, graph
+        self.embed_out = embed_out
         self.rngs = list(rngs)
         self.batches = np.ascontiguousarray(np.stack([np.asarray(b, np.int64) for b in batches]))
         self.fanouts = np.ascontiguousarray(fanouts, dtype=np.int32)
@@ -325,15 +343,24 @@ class Runner:
             n_hops=len(self.fanouts), flags=flags, n_streams=len(self.rngs),
             rngs=ctypes.cast(self._rng_ptrs, ctypes.c_void_p), depth=depth,
             comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1)
+        if embed_out is not None:
+            n_rows = self.batches.shape[0] * self.batches.shape[1]
+            if not (embed_out.is_contiguous() and embed_out.dtype == torch.float32
+                    and embed_out.device == trainer.device and embed_out.dim() == 2
+                    and embed_out.shape[0] >= n_rows and embed_out.shape[1] == trainer.H):
+                raise ValueError("embed_out must be a contiguous fp32 [n_batches * batch, hidden] device tensor")
+            cfg.embed_out = embed_out.data_ptr()
+            cfg.embed_ld = trainer.H
         h = ctypes.c_void_p()
         check(lib().gs_runner_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
 
     def run(self, n_steps):
-        """Issue the next n_steps training steps (asynchronous on the device)."""
+        """Issue the next n_steps steps (asynchronous on the device): training
+        steps, or forward-only steps into embed_out."""
         check(lib().gs_runner_run(self._h, int(n_steps), self.trainer.loss.data_ptr(),
                                   _lib.stream_ptr(self.trainer.device)))
-        return self.trainer.loss
+        return self.embed_out if self.embed_out is not None else self.trainer.loss
 
     def stats(self, reset=False):
         st = _lib.RunnerStats()
@@ -354,3 +381,50 @@ class Runner:
 
     def __del__(self):
         self.close()
+
+
+# ------------------------------------------------------- full-graph inference
+class Embedder:
+    """get_gnn_embeddings (utils.py:59-78) as one native pipeline: the
+    training runner in forward-only mode (gs_runner_config.embed_out) over
+    batches of `batch` ids, S sampler streams, the next batch's pull + layer-1
+    gather under the current forward, embeddings written in place.
+
+    Stream w of `rngs` samples batches w, w+S, ...; a trailing partial batch
+    is sampled afterwards by the stream whose turn it is and run through
+    NativeTrainer.forward.  With one stream that is exactly the reference's
+    sequence of GraphSage calls on one `random` stream."""
+
+    def __init__(self, graph, features, weights, fanouts, agg_func="MEAN", gcn=False, depth=4):
+        weights = [w.detach() for w in weights]
+        H = weights[0].shape[0]
+        dev = features.device
+        dummy_cls = (torch.zeros(1, H, device=dev), torch.zeros(1, device=dev))
+        self.trainer = NativeTrainer(graph, features, torch.zeros(1, dtype=torch.int32), 1,
+                                     num_layers=len(weights), hidden=H, fanouts=fanouts, agg_func=agg_func,
+                                     gcn=gcn, weights=(weights, *dummy_cls))
+        self.graph, self.fanouts, self.gcn, self.agg = graph, list(fanouts), gcn, agg_func
+        self.depth = depth
+        self.last_stats = None
+
+    def embed(self, nodes, batch, rngs):
+        """[len(nodes), hidden] fp32 embeddings on the device, row i = nodes[i]."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.int64).reshape(-1)
+        rngs = list(rngs)
+        n_full = len(nodes) // batch
+        out = torch.empty(len(nodes), self.trainer.H, dtype=torch.float32, device=self.trainer.device)
+        if n_full:
+            r = Runner(self.trainer, self.graph, nodes[:n_full * batch].reshape(n_full, batch), rngs, self.fanouts,
+                       gcn=self.gcn, fail_empty=self.agg == "MAX", depth=self.depth, embed_out=out)
+            try:
+                r.run(n_full)
+                self.last_stats = r.stats()
+            finally:
+                r.close()  # joins the sampler threads: every rng has advanced past its batches
+        rest = nodes[n_full * batch:]
+        if len(rest):
+            s = sample(self.graph, rngs[n_full % len(rngs)], rest, self.fanouts, gcn=self.gcn)
+            if self.agg == "MAX" and any(s.n_empty(j) for j in range(1, s.n_hops + 1)):
+                raise IndexError("MAX aggregation over an empty neighbourhood (reference: models.py:321-325)")
+            self.trainer.forward(DeviceSample(s, self.trainer.device), out[n_full * batch:])
+        return out

@@ -419,6 +419,17 @@ int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack,
                                          const int64_t* hop_sizes, const int64_t* offsets,
                                          const int32_t* roots, int64_t n_roots, int32_t slot,
                                          void* ws, int64_t ws_bytes, float* loss, void* stream);
+/* Forward alone — GraphSage.forward (models.py:241-269) as get_gnn_embeddings
+ * (utils.py:59-78) and evaluate (utils.py:27, :39) call it: the batch's
+ * [n_roots, hidden] embeddings (row i = root i) are written to out
+ * (contiguous rows).  No loss head, backward or gradient writes.  The
+ * _gathered form reads the layer-1 aggregate from gather slot `slot`. */
+int gs_trainer_forward(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                       const int64_t* offsets, void* ws, int64_t ws_bytes, float* out,
+                       void* stream);
+int gs_trainer_forward_gathered(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
+                                const int64_t* offsets, int32_t slot, void* ws,
+                                int64_t ws_bytes, float* out, void* stream);
 /* grads *= grad_scale, clip per model, SGD.  ws: >= 130 floats. */
 int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
 /* Single-process update (no all-reduce between the step and the update):
@@ -481,6 +492,12 @@ typedef struct {
     int32_t depth;          /* pinned slots per stream (>= 1) */
     void* comm;             /* gs_comm_create handle or NULL */
     int32_t world;          /* gradient scale 1/world after the all-reduce */
+    /* Inference (get_gnn_embeddings, utils.py:59-78): when non-NULL every step
+     * is gs_trainer_forward_gathered into embed_out + b * batch * embed_ld
+     * ([n_batches * batch, embed_ld] fp32, embed_ld = hidden): no loss,
+     * backward, all-reduce or update. */
+    float* embed_out;
+    int64_t embed_ld;
 } gs_runner_config;
 
 typedef struct {
