@@ -54,6 +54,10 @@ CONFIGS = {
     # configs[4] (per-GPU share of the 8-GPU job)
     "rmat16m": dict(scale=24, pairs=160_000_000, feat=128, fanouts=(25, 10), agg="MEAN", dtype="fp32",
                     batch=512, classes=16),
+    # get_gnn_embeddings (utils.py:59-78) over the rmat2m graph — batches of 500 node ids
+    # in id order, batch i on rank i % W, forward-only runner, one all-gather of the [N, 128] result
+    "rmat2m-embed": dict(scale=21, pairs=20_000_000, feat=256, fanouts=(25, 10), agg="MEAN", dtype="fp32",
+                         batch=500, classes=16, loop="embed"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_PEAK_TFS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense F32 / BF16 matrix peaks (spec)
@@ -287,6 +291,106 @@ def run_apply_model_loop(args, cfg):
     print(json.dumps(out), flush=True)
 
 
+def cpu_baseline_embed(wl, cfg, seconds_budget=25.0, seed=824):
+    """The oracle's forward (sampling + dense-mask layers) over batches of
+    embedded node ids, as get_gnn_embeddings runs it, on this host."""
+    import random as pyrandom
+    import oracle
+    threads = host_threads()
+    torch.set_num_threads(threads)
+    adj = oracle.Adjacency(wl["src"], wl["dst"], wl["n"])
+    W = train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, seed)[0]
+    X = wl["X"].float().cpu()
+    pyrandom.seed(seed)
+    times, B = [], cfg["batch"]
+    t_start = time.perf_counter()
+    with torch.no_grad():
+        for i in range(wl["n"] // B):
+            t = time.perf_counter()
+            hops = oracle.sample_layers(adj, list(range(i * B, (i + 1) * B)), list(cfg["fanouts"]))
+            oracle.forward_dense(hops, X, W, cfg["agg"], False)
+            times.append(time.perf_counter() - t)
+            if time.perf_counter() - t_start > seconds_budget and len(times) >= 3:
+                break
+    med = float(np.median(times[1:] if len(times) > 1 else times))
+    return {"value": B / med, "unit": "embedded nodes/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} oracle forward batches of {B} ids in id order (first untimed), median "
+                      f"{med * 1e3:.1f} ms/batch; torch CPU {threads} threads"}
+
+
+def run_embed(args, cfg):
+    """full-graph inference throughput (utils.get_gnn_embeddings'
+    native path): this rank's batches through train.Embedder, then the
+    all-gather of [N, 128].  Times the first --steps batches per rank (all of
+    them with --full-graph)."""
+    utils = import_module("graphsage-pytorch_amd.utils")
+    rank, world = train.init_distributed()
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(device)
+    wl = build_workload(cfg, device, args.seed)
+    n, B = wl["n"], cfg["batch"]
+    n_used = n if args.full_graph else min(n, args.steps * world * B)
+    weights = [w.to(device) for w in train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, args.seed)[0]]
+    emb = train.Embedder(wl["graph"], wl["X"], weights, cfg["fanouts"], cfg["agg"])
+    mine = utils.shard_ids(n_used, B, rank, world)
+    warm = utils.shard_ids(min(n, args.warmup * world * B), B, rank, world)
+    if len(warm):
+        emb.embed(warm, B, [train.make_rng(args.seed + 1, rank, w) for w in range(args.sampler_streams)])
+    rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
+    gs._lib.check(gs._lib.lib().gs_trainer_time_agg(emb.trainer._h, len(mine) // B))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    E = emb.embed(mine, B, rngs)
+    if world > 1:  # the assembly get_gnn_embeddings does
+        lens = [len(utils.shard_ids(n_used, B, r, world)) for r in range(world)]
+        buf = torch.zeros(max(lens), E.shape[1], device=device)
+        buf[:len(mine)].copy_(E)
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    st = emb.last_stats
+    n_b = len(mine) // B
+    agg_ms = float(np.mean(agg1_times_ms(emb.trainer, n_b))) if n_b else float("nan")
+    if rank == 0:
+        L = len(cfg["fanouts"])
+        sizes = st["hop_sizes_sum"] / max(1, st["steps"])
+        agg_bytes = agg1_ids_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], 4, cfg["fanouts"][-1])
+        achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_embed(wl, cfg, args.cpu_budget, args.seed)
+        out = {
+            "metric": "embedded nodes/sec (get_gnn_embeddings, 2-layer, fanout 25,10)",
+            "value": round(n_used / elapsed, 1), "unit": "embedded nodes/s", "n_gpus": world,
+            "steps": n_b, "warmup": len(warm) // B, "ms_per_step": round(elapsed / max(1, n_b) * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong" if args.full_graph else "weak", "vs_baseline": None,
+            "dtype": cfg["dtype"], "data": "synthetic (R-MAT graph, hashed U(-1,1) features), reference-init weights",
+            "config": {"workload": f"rmat2m-embed: {n_used} of {n} node ids in batches of {B} (id order), "
+                                   f"fanout {tuple(cfg['fanouts'])}, MEAN, forward only + all-gather",
+                       "global_batch": B * world, "parallelism": f"dp{world}",
+                       "sampler_streams_per_gpu": args.sampler_streams,
+                       "host_sampler_ms_per_batch": round(1e3 * st["sample_s"] / max(1, st["steps"]), 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "agg_ids_kernel (layer-1 gather-mean over resolved neighbour ids)",
+                         "avg_launch_us": round(agg_ms * 1e3, 2), "algo_bytes_per_launch": int(agg_bytes)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -297,6 +401,7 @@ def main():
     ap.add_argument("--seed", type=int, default=824)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0)
+    ap.add_argument("--full-graph", action="store_true", help="rmat2m-embed: embed every node id")
     ap.add_argument("--sampler-streams", type=int, default=None,
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
@@ -313,6 +418,8 @@ def main():
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("the pubmed (apply_model) config runs on one GPU")
         return run_apply_model_loop(args, cfg)
+    if cfg.get("loop") == "embed":
+        return run_embed(args, cfg)
     rank, world = train.init_distributed()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
