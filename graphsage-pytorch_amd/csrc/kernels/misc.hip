@@ -39,7 +39,7 @@ __global__ __launch_bounds__(kTb) void cast_bf16_kernel(const float* in, bf16_t*
 
 
 // ------------------------------------------------------- classifier + NLL
-// One block of 16 waves per R rows, one wave per row.  Wc is staged in LDS
+// One block of 16 waves per R <= kClsRowsMax rows, one wave per row.  Wc is staged in LDS
 // (row pitch D + 1) when it fits.  Per row, lane (cl, dq) = (lane & 15,
 // lane >> 4) computes the dot product of class c0 + cl over one quarter of D
 // and two xor-shuffles add the quarters, so a group of 16 classes costs one
@@ -53,6 +53,11 @@ __global__ __launch_bounds__(kTb) void cast_bf16_kernel(const float* in, bf16_t*
 constexpr int kClsThreads = 1024;
 constexpr int64_t kClsLdsFloats = 16 * 1024;  // 64 KiB
 constexpr int64_t kClsWcLds = 8 * 1024;
+// Rows per block.  Fewer rows per block means more blocks in flight and a
+// shorter per-block partial-slab phase: at B = 512 the kernel took 12.1 us
+// with 16 rows (32 blocks), 8.3 us with 8 or 4 (rocprof, in-step); the step
+// ran 81.5-82.3 us with 4 against 86.9-89.1 us with 16.
+constexpr int kClsRowsMax = 4;
 
 struct ClsPlan {
     int rows;
@@ -65,7 +70,7 @@ inline ClsPlan cls_plan(int64_t C, int64_t D) {
     p.wc_lds = C * (D + 1) <= kClsWcLds;
     const int64_t fixed = p.wc_lds ? C * (D + 1) : 0;
     p.rows = 1;
-    for (int r = kClsThreads / 64; r > 1; r >>= 1)
+    for (int r = kClsRowsMax; r > 1; r >>= 1)
         if (fixed + r * (C + D + 1) <= kClsLdsFloats) {
             p.rows = r;
             break;
