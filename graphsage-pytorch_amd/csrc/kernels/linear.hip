@@ -43,11 +43,11 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         const float* a = static_cast<const float*>(A);
         const float* w = static_cast<const float*>(Wd);
         if (self) {
-            if (relu) linear_fwd_sk_kernel<true, true><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else linear_fwd_sk_kernel<true, false><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            if (relu) launch_k(linear_fwd_sk_kernel<true, true>, gs2, dim3(kThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else launch_k(linear_fwd_sk_kernel<true, false>, gs2, dim3(kThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
         } else {
-            if (relu) linear_fwd_sk_kernel<false, true><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else linear_fwd_sk_kernel<false, false><<<gs2, kThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            if (relu) launch_k(linear_fwd_sk_kernel<false, true>, gs2, dim3(kThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else launch_k(linear_fwd_sk_kernel<false, false>, gs2, dim3(kThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
         }
         check_launch("gs_sage_linear_fwd(sk)");
         return GS_OK;
@@ -58,11 +58,11 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         const float* a = static_cast<const float*>(A);
         const float* w = static_cast<const float*>(Wd);
         if (self) {
-            if (relu) linear_fwd_wide_kernel<true, true><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else linear_fwd_wide_kernel<true, false><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            if (relu) launch_k(linear_fwd_wide_kernel<true, true>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else launch_k(linear_fwd_wide_kernel<true, false>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
         } else {
-            if (relu) linear_fwd_wide_kernel<false, true><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else linear_fwd_wide_kernel<false, false><<<gw, kWideThreads, 0, st>>>(nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            if (relu) launch_k(linear_fwd_wide_kernel<false, true>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
+            else launch_k(linear_fwd_wide_kernel<false, false>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
         }
         check_launch("gs_sage_linear_fwd(wide)");
         return GS_OK;
