@@ -50,7 +50,9 @@ __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
         node = dst_ids[r];
         if (row_ptr) rs = row_ptr[node];
     }
-    constexpr int NR = VEC > 4 ? kRows / 2 : kRows;
+    // explicit lists (layers >= 2: fanout up to 25-30 per destination) keep
+    // twice the rows in flight, so a whole neighbourhood is one memory round
+    constexpr int NR = (VEC > 4 ? kRows / 2 : kRows) * (EXPAND ? 1 : 2);
     const bool want_am = (OP == GS_AGG_MAX) && (argmax != nullptr);
     const int nf = (F + G * VEC - 1) / (G * VEC);
     for (int fi = 0; fi < nf; ++fi) {
