@@ -493,7 +493,7 @@ def main():
         K1 = 2 * cfg["feat"]
         flops = 2.0 * float(sizes[L - 1, 0]) * K1 * 128
         mfma = {}
-        for site, name in ((1, "linear_fwd_kernel (layer 1: relu([X[self] | agg]·W1ᵀ))"),
+        for site, name in ((1, "linear_fwd_wide_kernel<32> (layer 1: relu([X[self] | agg]·W1ᵀ))"),
                            (2, "linear_dw_kernel (layer 1: dW1 = dZ1ᵀ·[X[self] | agg] row slabs)")):
             t = gemm_ms[site]
             if len(t):

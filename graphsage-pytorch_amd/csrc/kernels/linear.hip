@@ -36,7 +36,12 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
     static const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
+    // fp32 default: 32-row W-in-LDS tiles (bitwise the chunked kernel's sums:
+    // same MFMA operands in the same order).  In-step at rmat2m the step ran
+    // 80.2-80.7 us against 82.3-82.4 us with the 16-row chunked kernel, which
+    // GS_LIN_FWD=chunked (and bf16) still select; "wide" = 64-row tiles.
     static const bool wide_on = fwd_mode == "wide";
+    static const bool wide32_on = fwd_mode != "wide" && fwd_mode != "sk" && fwd_mode != "chunked";
     if (fwd_mode == "sk" && dt == GS_F32 && vload) {
         const dim3 gs2(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 31) / 32));
         const float* xs = static_cast<const float*>(Xs);
@@ -52,18 +57,21 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         check_launch("gs_sage_linear_fwd(sk)");
         return GS_OK;
     }
-    if (wide_on && dt == GS_F32 && vload) {
-        const dim3 gw(static_cast<unsigned>((n + kWideRows - 1) / kWideRows), static_cast<unsigned>((H + 63) / 64));
+    if ((wide_on || wide32_on) && dt == GS_F32 && vload) {
+        const int R = wide32_on ? 32 : kWideRows;
+        const dim3 gw(static_cast<unsigned>((n + R - 1) / R), static_cast<unsigned>((H + 63) / 64));
         const float* xs = static_cast<const float*>(Xs);
         const float* a = static_cast<const float*>(A);
         const float* w = static_cast<const float*>(Wd);
-        if (self) {
-            if (relu) launch_k(linear_fwd_wide_kernel<true, true>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else launch_k(linear_fwd_wide_kernel<true, false>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-        } else {
-            if (relu) launch_k(linear_fwd_wide_kernel<false, true>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-            else launch_k(linear_fwd_wide_kernel<false, false>, gw, dim3(kWideThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
-        }
+#define GS_LFWDW(RR, SELF, RELU_) \
+        launch_k(linear_fwd_wide_kernel<RR, SELF, RELU_>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo)
+#define GS_LFWDW_R(RR) \
+        do { if (self) { if (relu) GS_LFWDW(RR, true, true); else GS_LFWDW(RR, true, false); } \
+             else { if (relu) GS_LFWDW(RR, false, true); else GS_LFWDW(RR, false, false); } } while (0)
+        if (R == 32) GS_LFWDW_R(32);
+        else GS_LFWDW_R(64);
+#undef GS_LFWDW_R
+#undef GS_LFWDW
         check_launch("gs_sage_linear_fwd(wide)");
         return GS_OK;
     }

@@ -241,42 +241,50 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
     }
 }
 
-// Forward, fp32, W staged in LDS ("wide" tiles).  Block = 64 rows x 64
-// output columns, 16 waves: wave (wr, wc) = (w & 3, w >> 2) owns the 16 x 16
-// tile at rows 16·wr, cols 16·wc.  Per K chunk of 64 every thread loads one
-// 16-byte slot of the A tile and one of the W tile into a two-buffer LDS ring,
-// one chunk ahead.  Against the 16-row kernel this reads each W chunk once per
-// 64 rows instead of once per 16 (the W re-reads from L2/MALL bound that
-// kernel's K loop) while keeping ~2 waves per SIMD at n ~ 4k rows.
-constexpr int kWideThreads = 1024;
+// Forward, fp32, W staged in LDS ("wide" tiles).  Block = ROWS rows x 64
+// output columns, ROWS/4 waves: wave (wr, wc) = (w % (ROWS/16), w / (ROWS/16))
+// owns the 16 x 16 tile at rows 16·wr, cols 16·wc.  Per K chunk of 64 every
+// thread loads one 16-byte slot of the A tile and 64/ROWS slots of the W tile
+// into a two-buffer LDS ring, one chunk ahead.  Against the 16-row kernel
+// this reads each W chunk once per ROWS rows instead of once per 16.  ROWS =
+// 32 (8 waves, ~270 blocks at the rmat2m layer-1 shape) is the fp32 default:
+// W traffic from L2 halves while the grid still covers the chip.
 constexpr int kWideRows = 64;
-template <bool HAS_SELF, bool RELU>
-__global__ __launch_bounds__(kWideThreads) void linear_fwd_wide_kernel(
+template <int ROWS, bool HAS_SELF, bool RELU>
+__global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const float* __restrict__ A, int64_t lda, const float* __restrict__ W, float* __restrict__ out, int64_t ldo) {
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
-    __shared__ uint4 sA[2][kWideRows * SP];
+    constexpr int RT = ROWS / 16;   // row tiles
+    constexpr int WQ = 64 / ROWS;   // W slots per thread
+    __shared__ uint4 sA[2][ROWS * SP];
     __shared__ uint4 sW[2][64 * SP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, kq = lane >> 4;
-    const int wr = wave & 3, wc = wave >> 2;
-    const int m0 = blockIdx.x * kWideRows, c0 = blockIdx.y * 64;
-    const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr of both tiles, slot ls
+    const int wr = wave % RT, wc = wave / RT;
+    const int m0 = blockIdx.x * ROWS, c0 = blockIdx.y * 64;
+    const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
     const int arow_i = min(m0 + lr, n - 1);
     const float* arow = A + static_cast<int64_t>(arow_i) * lda;
     const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
-    const float* wrow = W + static_cast<int64_t>(min(c0 + lr, H - 1)) * K;
+    const float* wrow[WQ];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) wrow[q] = W + static_cast<int64_t>(min(c0 + lr + ROWS * q, H - 1)) * K;
     const int nC = (K + 63) / 64;
     uint4 a_nx = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, ls * 4);
-    uint4 w_nx = concat_slot<float, false, true>(nullptr, wrow, K, K, ls * 4);
+    uint4 w_nx[WQ];
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) w_nx[q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, ls * 4);
     sA[0][lr * SP + ls] = a_nx;
-    sW[0][lr * SP + ls] = w_nx;
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) sW[0][(lr + ROWS * q) * SP + ls] = w_nx[q];
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nC; ++c) {
         __syncthreads();
         const int kn = min(c + 1, nC - 1) * 64;
         a_nx = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + ls * 4);
-        w_nx = concat_slot<float, false, true>(nullptr, wrow, K, K, kn + ls * 4);
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) w_nx[q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, kn + ls * 4);
         __builtin_amdgcn_sched_barrier(0);
         const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
         const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
@@ -290,7 +298,8 @@ __global__ __launch_bounds__(kWideThreads) void linear_fwd_wide_kernel(
         for (int g = 0; g < 4; ++g) acc = mfma_slot<float>(av[g], wv[g], acc);
         __builtin_amdgcn_sched_barrier(0);
         sA[(c + 1) & 1][lr * SP + ls] = a_nx;
-        sW[(c + 1) & 1][lr * SP + ls] = w_nx;
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) sW[(c + 1) & 1][(lr + ROWS * q) * SP + ls] = w_nx[q];
     }
     const int col = c0 + 16 * wc + r;
     if (col >= H) return;
