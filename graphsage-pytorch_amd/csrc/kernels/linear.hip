@@ -134,10 +134,20 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
     const dim3 grid(static_cast<unsigned>((K + 63) / 64), static_cast<unsigned>((H + 63) / 64),
                     static_cast<unsigned>(S));
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
+    static const bool xcd_map = std::getenv("GS_DW_GRID3") == nullptr;
+    const int gx = static_cast<int>(grid.x), tiles = static_cast<int>(grid.x * grid.y);
+    const dim3 grid_x(static_cast<unsigned>(kXcds * tiles * ((S + kXcds - 1) / kXcds)));
 #define GS_LDW1(TT, SELF, RELU, VL, ZV)                                                                  \
-    launch_k(linear_dw_kernel<TT, SELF, RELU, VL, ZV>, grid, dim3(kThreads), 0, st,                     \
-        nn, ff, hh, kk, rps, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,    \
-        dout, out, ldo, target, H * K)
+    do {                                                                                                 \
+        if (xcd_map)                                                                                     \
+            launch_k(linear_dw_xcd_kernel<TT, SELF, RELU, VL, ZV>, grid_x, dim3(kThreads), 0, st,        \
+                nn, ff, hh, kk, rps, gx, tiles, S, static_cast<const TT*>(Xs), ldxs, sidx,               \
+                static_cast<const TT*>(A), lda, dout, out, ldo, target, H * K);                          \
+        else                                                                                             \
+            launch_k(linear_dw_kernel<TT, SELF, RELU, VL, ZV>, grid, dim3(kThreads), 0, st,              \
+                nn, ff, hh, kk, rps, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A),  \
+                lda, dout, out, ldo, target, H * K);                                                     \
+    } while (0)
 #define GS_LDW_Z(TT, SELF, RELU, VL) \
     do { if (zvec) GS_LDW1(TT, SELF, RELU, VL, true); else GS_LDW1(TT, SELF, RELU, VL, false); } while (0)
 #define GS_LDW_V(TT, SELF, RELU) \

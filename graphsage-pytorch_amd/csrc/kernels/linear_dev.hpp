@@ -396,6 +396,10 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_sk_kernel(
 // write fp32 partials that sum_slabs_kernel adds in a fixed order.
 constexpr int kDwPitch = 64 + 16;  // rows 16 banks apart: (kq, r) reads of a column hit distinct banks
 constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are staged in LDS)
+#ifndef GS_DW_AHEAD
+#define GS_DW_AHEAD 4
+#endif
+constexpr int kDwAhead = GS_DW_AHEAD;  // row chunks whose global loads are in flight ahead of the MFMAs
 
 template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
 __device__ __forceinline__ void linear_dw_body(
@@ -458,30 +462,27 @@ __device__ __forceinline__ void linear_dw_body(
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
     };
-    // Global loads run two chunks ahead of the MFMAs (two named register sets,
-    // loop unrolled by two); LDS stays double-buffered.
-    float4 z0, o0, x0, z1, o1, x1;
-    load(0, z0, o0, x0);
-    stash(0, z0, o0, x0);
-    load(1, z1, o1, x1);
-    int c = 0;
-    for (; c + 1 < nC; c += 2) {
-        __syncthreads();
-        load(c + 2, z0, o0, x0);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(c);
-        __builtin_amdgcn_sched_barrier(0);
-        stash(c + 1, z1, o1, x1);
-        __syncthreads();
-        load(c + 3, z1, o1, x1);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(c + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        if (c + 2 < nC) stash(c + 2, z0, o0, x0);
-    }
-    if (c < nC) {
-        __syncthreads();
-        compute(c);
+    // Global loads run kDwAhead chunks ahead of the MFMAs (a ring of register
+    // sets, loop unrolled by its length); LDS stays double-buffered.  Slot u
+    // holds chunk c (stashed one iteration earlier) when chunk c = u (mod
+    // kDwAhead) is computed, and is refilled with chunk c + kDwAhead then.
+    float4 zr[kDwAhead], orr[kDwAhead], xr[kDwAhead];
+#pragma unroll
+    for (int u = 0; u < kDwAhead; ++u) load(u, zr[u], orr[u], xr[u]);
+    stash(0, zr[0], orr[0], xr[0]);
+    for (int c0 = 0; c0 < nC; c0 += kDwAhead) {
+#pragma unroll
+        for (int u = 0; u < kDwAhead; ++u) {
+            const int c = c0 + u;
+            if (c >= nC) break;
+            __syncthreads();
+            load(c + kDwAhead, zr[u], orr[u], xr[u]);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(c);
+            __builtin_amdgcn_sched_barrier(0);
+            const int un = (u + 1) % kDwAhead;
+            if (c + 1 < nC) stash(c + 1, zr[un], orr[un], xr[un]);
+        }
     }
     float* slab = dst + static_cast<int64_t>(bz) * split_stride;
 #pragma unroll
@@ -503,6 +504,28 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
     linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(blockIdx.x, blockIdx.y, blockIdx.z, n, F, H, K, rows_per_split,
                                                    Xs, ldxs, sidx, A, lda, dout, out, ldo, dst, split_stride);
+}
+
+// The same tiles on a 1-D grid mapped XCD by XCD: workgroup w runs on XCD
+// w % 8, and every tile of slab z is given to XCD z % 8, so a slab's dZ and
+// input rows are fetched into one XCD's L2 once and re-read there by its
+// other tiles (on the (k, h, slab) grid the k tile sets the XCD, and every
+// XCD fetched every dZ row).  Grid: 8 · tiles · ceil(S / 8); spare
+// workgroups exit.
+constexpr int kXcds = 8;
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
+__global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
+    int n, int F, int H, int K, int rows_per_split, int gx, int tiles, int S, const T* __restrict__ Xs,
+    int64_t ldxs, const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda,
+    const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo, float* __restrict__ dst,
+    int64_t split_stride) {
+    const int w = blockIdx.x;
+    const int j = w / kXcds;
+    const int z = w % kXcds + kXcds * (j / tiles);
+    if (z >= S) return;
+    const int t = j % tiles;
+    linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx, A,
+                                                   lda, dout, out, ldo, dst, split_stride);
 }
 
 // out[i] = Σ_s slabs[s][i], fixed order; 4 elements per thread.  With
