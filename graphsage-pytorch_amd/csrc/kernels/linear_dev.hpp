@@ -250,6 +250,10 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
 // 32 (8 waves, ~270 blocks at the rmat2m layer-1 shape) is the fp32 default:
 // W traffic from L2 halves while the grid still covers the chip.
 constexpr int kWideRows = 64;
+#ifndef GS_FWD_AHEAD
+#define GS_FWD_AHEAD 2
+#endif
+constexpr int kFwdAhead = GS_FWD_AHEAD;  // K chunks in flight ahead of the MFMAs (wide kernels)
 template <int ROWS, bool HAS_SELF, bool RELU>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
@@ -271,35 +275,45 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
 #pragma unroll
     for (int q = 0; q < WQ; ++q) wrow[q] = W + static_cast<int64_t>(min(c0 + lr + ROWS * q, H - 1)) * K;
     const int nC = (K + 63) / 64;
-    uint4 a_nx = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, ls * 4);
-    uint4 w_nx[WQ];
+    // register ring of kFwdAhead chunks: slot u holds chunk c (c = u mod
+    // kFwdAhead) once it is in LDS and is then refilled with chunk c + kFwdAhead
+    uint4 ar[kFwdAhead], wr_[kFwdAhead][WQ];
+    auto load = [&](int c, int u) {
+        const int kn = min(c, nC - 1) * 64;  // past the end: re-read the last chunk (never stored)
+        ar[u] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + ls * 4);
 #pragma unroll
-    for (int q = 0; q < WQ; ++q) w_nx[q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, ls * 4);
-    sA[0][lr * SP + ls] = a_nx;
+        for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, kn + ls * 4);
+    };
+    auto stash = [&](int c, int u) {
+        sA[c & 1][lr * SP + ls] = ar[u];
 #pragma unroll
-    for (int q = 0; q < WQ; ++q) sW[0][(lr + ROWS * q) * SP + ls] = w_nx[q];
+        for (int q = 0; q < WQ; ++q) sW[c & 1][(lr + ROWS * q) * SP + ls] = wr_[u][q];
+    };
+#pragma unroll
+    for (int u = 0; u < kFwdAhead; ++u) load(u, u);
+    stash(0, 0);
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nC; ++c) {
-        __syncthreads();
-        const int kn = min(c + 1, nC - 1) * 64;
-        a_nx = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + ls * 4);
+    for (int c0 = 0; c0 < nC; c0 += kFwdAhead) {
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) w_nx[q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, kn + ls * 4);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
-        const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
-        uint4 av[4], wv[4];
+        for (int u = 0; u < kFwdAhead; ++u) {
+            const int c = c0 + u;
+            if (c >= nC) break;
+            __syncthreads();
+            load(c + kFwdAhead, u);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
+            const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
+            uint4 av[4], wv[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            av[g] = ta[4 * g + kq];
-            wv[g] = tw[4 * g + kq];
+            for (int g = 0; g < 4; ++g) {
+                av[g] = ta[4 * g + kq];
+                wv[g] = tw[4 * g + kq];
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc = mfma_slot<float>(av[g], wv[g], acc);
+            __builtin_amdgcn_sched_barrier(0);
+            if (c + 1 < nC) stash(c + 1, (u + 1) % kFwdAhead);
         }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc = mfma_slot<float>(av[g], wv[g], acc);
-        __builtin_amdgcn_sched_barrier(0);
-        sA[(c + 1) & 1][lr * SP + ls] = a_nx;
-#pragma unroll
-        for (int q = 0; q < WQ; ++q) sW[(c + 1) & 1][(lr + ROWS * q) * SP + ls] = w_nx[q];
     }
     const int col = c0 + 16 * wc + r;
     if (col >= H) return;
