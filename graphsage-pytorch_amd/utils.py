@@ -159,7 +159,8 @@ def get_gnn_embeddings(gnn_model, dataCenter, ds, b_sz=500, *, sampler_streams=N
     runs its batches through the forward-only runner (train.Embedder) with S
     sampler streams, then one all-gather assembles [N, H] on every rank.  At
     W = 1, S = 1 the stream is the global `random` state (same result and
-    same state afterwards as the default loop); otherwise stream (r, w) is
+    same state afterwards as the default loop), or the module's own `rng`
+    when it was given one; otherwise stream (r, w) is
     seeded train.rank_seed(seed, r, w) (seed defaults to 824), each one a
     reference stream on its own."""
     n = len(getattr(dataCenter, ds + "_labels"))
@@ -180,9 +181,12 @@ def get_gnn_embeddings(gnn_model, dataCenter, ds, b_sz=500, *, sampler_streams=N
     from .train import rank_seed
     S = int(sampler_streams or 1)
     ids = shard_ids(n, b_sz, rank, world)
-    exact = world == 1 and S == 1 and getattr(gnn_model, "rng", None) is None
+    own = getattr(gnn_model, "rng", None)
+    exact = world == 1 and S == 1 and own is None
     if exact:
         rngs = [RNG.from_python(_pyrandom)]
+    elif world == 1 and S == 1:  # the module's own stream, as its forward would draw
+        rngs = [own]
     else:
         base = 824 if seed is None else int(seed)
         rngs = [RNG(rank_seed(base, rank, w)) for w in range(S)]
