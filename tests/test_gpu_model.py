@@ -92,6 +92,33 @@ def test_graphsage_vs_oracle_bench_fanouts(gs, agg, fanouts):
                                    atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_graphsage_duplicate_roots_vs_oracle(gs, agg):
+    """Repeated ids in nodes_batch: every occurrence is sampled on its own
+    (models.py:282) and gets its own output row (row i = nodes_batch[i])."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(4, n, 64))
+    torch.manual_seed(2)
+    model = models.GraphSage(2, 64, 128, X.to(DEV), graph, DEV, agg_func=agg, fanouts=[6, 4]).to(DEV)
+    base = np.nonzero(graph.degrees())[0][::7][:30].tolist()
+    roots = base + base[:9] + [base[2]] * 4
+    random.seed(13)
+    emb = model(roots)
+    state = random.getstate()
+    W = [getattr(model, f"sage_layer{i}").weight.detach().cpu().clone().requires_grad_(True) for i in (1, 2)]
+    random.seed(13)
+    hops = oracle.sample_layers(oracle.Adjacency(g["rmat_src"], g["rmat_dst"], n), roots, [6, 4])
+    assert random.getstate() == state
+    ref = oracle.forward_dense(hops, X, W, agg, False)
+    torch.testing.assert_close(emb.detach().cpu(), ref.detach(), atol=1e-5, rtol=1e-5)
+    up = torch.from_numpy(uniform_features(6, len(roots), 128))
+    (emb * up.to(DEV)).sum().backward()
+    (ref * up).sum().backward()
+    for i in (1, 2):
+        torch.testing.assert_close(getattr(model, f"sage_layer{i}").weight.grad.cpu(), W[i - 1].grad,
+                                   atol=1e-4, rtol=1e-4)
+
+
 def test_graphsage_bf16_max_vs_oracle(gs):
     """configs[3] numerics: bf16 feature table, fp32 accumulate; oracle on the
     same bf16-rounded features, bf16-rounded W1 (tolerance stated: 2e-2)."""

@@ -150,6 +150,32 @@ def test_sampler_vs_oracle_random_graphs(gs):
             assert r2.getstate()[0].tolist() + [r2.getstate()[1]] == list(random.getstate()[1])
 
 
+def test_sampler_duplicate_roots_vs_oracle(gs):
+    """nodes_batch with repeated ids: the reference samples every occurrence
+    (drawing from `random` each time, models.py:282) and unions the results;
+    the same per occurrence here, and the same words consumed."""
+    rs = np.random.RandomState(5)
+    n = 300
+    src = rs.randint(0, n, 3000)
+    dst = (src + 1 + rs.randint(0, n - 1, 3000)) % n
+    Gn = gs.CSRGraph.from_pairs(src, dst, n)
+    adj = Adjacency(src, dst, n)
+    base = [int(v) for v in rs.permutation(np.nonzero(Gn.degrees())[0])[:20]]
+    roots = base + base[:7] + [base[3]] * 3
+    for fan in ([25, 10], [4, 3], [None, 5]):
+        random.seed(9)
+        want = sample_layers(adj, roots, fan)
+        s = gs.sample(Gn, gs.RNG(9), roots, fan, full=True)
+        for j, (_, samp, _, union) in enumerate(want, start=1):
+            h = s.hop(j)
+            assert h.dst_ids.tolist() == (roots if j == 1 else want[j - 2][3])
+            assert h.src_ids.tolist() == union
+            assert h.sets() == [list(x) for x in samp]
+        r2 = gs.RNG(9)
+        gs.sample(Gn, r2, roots, fan)
+        assert r2.getstate()[0].tolist() + [r2.getstate()[1]] == list(random.getstate()[1])
+
+
 def test_sample_pack_layout(gs):
     G_, _ = _graph(gs, "cora")
     s = gs.sample(G_, gs.RNG(824), list(range(0, 200, 7)), [10, 10])
