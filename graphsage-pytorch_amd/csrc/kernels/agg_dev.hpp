@@ -12,6 +12,9 @@
 namespace gs {
 
 constexpr int kBlock = 256;
+#ifndef GS_AGG_BWD_BATCH
+#define GS_AGG_BWD_BATCH 1
+#endif
 constexpr int kRows = 16;  // neighbour rows in flight per lane group (8 for 8-element bf16 vectors)
 
 // Lanes [lo, lo + G) of the wave's ballot.
@@ -151,6 +154,53 @@ __device__ __forceinline__ void agg_bwd_body(
         float g[VEC];
 #pragma unroll
         for (int v = 0; v < VEC; ++v) g[v] = 0.f;
+#if GS_AGG_BWD_BATCH
+        // Entries in groups of 8: the group's transposed indices in one load
+        // round, then every row (and MEAN count / MAX argmax) of the group in
+        // one more, then the adds in entry order (the same sums as one entry
+        // at a time).  Addresses are clamped, values selected at use.
+        const int f0c = act ? f0 : 0;
+        for (int t0 = beg; t0 < end; t0 += 8) {
+            int e[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) e[u] = tidx[min(t0 + u, end - 1)];
+            float x[8][VEC], w[8];
+            int am[8][VEC];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int eu = e[u];
+                const bool self_e = eu < 0;
+                const int row = self_e ? -eu - 1 : eu;
+                const float* src = (self_e && dSelf) ? dSelf : dA;
+                RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
+                if (OP == GS_AGG_MEAN) {
+                    const int re = self_e ? 0 : eu;
+                    w[u] = 1.0f / static_cast<float>(ptr[re + 1] - ptr[re]);
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v)
+                        am[u][v] = argmax[static_cast<int64_t>(self_e ? 0 : eu) * F + f0c + v];
+                }
+            }
+            if (!act) continue;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (t0 + u >= end) break;
+                if (e[u] < 0) {
+                    if (!dSelf) continue;  // gcn: self rows feed no linear input
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) g[v] += x[u][v];
+                } else if (OP == GS_AGG_MEAN) {
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) g[v] += x[u][v] * w[u];
+                } else {
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v)
+                        if (am[u][v] == c) g[v] += x[u][v];
+                }
+            }
+        }
+#else
         for (int t = beg; t < end; ++t) {
             const int e = tidx[t];
             if (!act) continue;
@@ -172,6 +222,7 @@ __device__ __forceinline__ void agg_bwd_body(
                     if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += x[v];
             }
         }
+#endif
         if (!act) continue;
         if (Hprev) {
             float h[VEC];
