@@ -496,4 +496,130 @@ int gs_sample_pack(const gs_sample* sp, int32_t* buf, int64_t cap) {
     GS_API_END
 }
 
+
+int64_t gs_sample_pack_bound_multi(const gs_graph* gp, int64_t n_roots, int64_t group, const int32_t* fanouts,
+                                   int32_t n_hops) {
+    if (group < 1 || n_roots < 1) return -1;
+    if (n_roots <= group) return gs_sample_pack_bound(gp, n_roots, fanouts, n_hops);
+    // every field of the merged image is at most the sum of the groups' (one
+    // pointer terminator and one alignment pad instead of one per group)
+    const int64_t full = gs_sample_pack_bound(gp, group, fanouts, n_hops);
+    const int64_t rest = n_roots % group;
+    const int64_t tail = rest ? gs_sample_pack_bound(gp, rest, fanouts, n_hops) : 0;
+    if (full < 0 || tail < 0) return -1;
+    return (n_roots / group) * full + tail;
+}
+
+int gs_sample_pack_run_multi(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots, int64_t group,
+                             const int32_t* fanouts, int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
+                             int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    if (group >= 1 && n_roots <= group)
+        return gs_sample_pack_run(gp, rng, roots, n_roots, fanouts, n_hops, flags, buf, cap, hop_sizes, offsets, used);
+    GS_API_BEGIN
+    GS_REQUIRE(gp && rng && roots && buf && hop_sizes && offsets && used, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(group >= 1 && n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "bad group / n_hops");
+    const int64_t bound = gs_sample_pack_bound_multi(gp, n_roots, group, fanouts, n_hops);
+    GS_REQUIRE(bound >= 0 && cap >= bound, GS_EINVAL, "buffer below gs_sample_pack_bound_multi");
+    const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
+    // the groups in order on one stream; an empty neighbourhood fails right
+    // after its own group, as the reference raises inside that batch
+    std::vector<std::unique_ptr<Sample>> parts;
+    for (int64_t lo = 0; lo < n_roots; lo += group) {
+        parts.emplace_back(gs::run_sample(g, rng->mt, roots + lo, std::min(group, n_roots - lo), fanouts, n_hops,
+                                          flags));
+        if (flags & GS_SAMPLE_FAIL_EMPTY)
+            for (int32_t j = 0; j < n_hops; ++j)
+                if (parts.back()->hops[j].n_empty) gs::fail(GS_EEMPTY, "empty neighbourhood");
+    }
+    // merged layout: the field order and alignment of layout_of
+    gs_pack_layout L;
+    for (auto& row : L.off)
+        for (auto& o : row) o = -1;
+    int64_t at = 0;
+    auto put = [&](int32_t j, int f, int64_t n) {
+        L.off[j][f] = at;
+        at += (n + 3) & ~int64_t(3);
+    };
+    for (int32_t j = 0; j < n_hops; ++j) {
+        int64_t nd = 0, n1 = 0, ns = 0, nt = 0;
+        for (const auto& p : parts) {
+            const Hop& h = p->hops[j];
+            nd += static_cast<int64_t>(h.dst_ids.size());
+            GS_REQUIRE(j < n_hops - 1 || h.ent.size() == h.pos.size(), GS_EINVAL, "pack entries mismatch");
+            n1 += static_cast<int64_t>(j == n_hops - 1 ? h.pos.size() : h.nbr.size());
+            ns += static_cast<int64_t>(h.src_ids.size());
+            nt += static_cast<int64_t>(h.tidx.size());
+        }
+        hop_sizes[4 * j] = nd;
+        if (j == n_hops - 1) {
+            put(j, GS_PK_POS_PTR, nd + 1);
+            put(j, GS_PK_POS, n1);
+            put(j, GS_PK_DST_IDS, nd);
+            hop_sizes[4 * j + 1] = n1;
+            hop_sizes[4 * j + 2] = hop_sizes[4 * j + 3] = -1;
+        } else {
+            put(j, GS_PK_NBR_PTR, nd + 1);
+            put(j, GS_PK_NBR, n1);
+            put(j, GS_PK_SELF, nd);
+            put(j, GS_PK_TPTR, ns + 1);
+            put(j, GS_PK_TIDX, nt);
+            int64_t np = 0;
+            for (const auto& p : parts) np += static_cast<int64_t>(p->hops[j].pos.size());
+            hop_sizes[4 * j + 1] = np;
+            hop_sizes[4 * j + 2] = ns;
+            hop_sizes[4 * j + 3] = n1;
+        }
+    }
+    L.total = at;
+    GS_REQUIRE(L.total + n_roots <= cap, GS_EINVAL, "merged pack exceeds its bound");
+    // fields, group by group, indices rebased on the groups before
+    for (int32_t j = 0; j < n_hops; ++j) {
+        int32_t* o[GS_PK_NFIELDS];
+        for (int f = 0; f < GS_PK_NFIELDS; ++f) o[f] = L.off[j][f] >= 0 ? buf + L.off[j][f] : nullptr;
+        int64_t bd = 0, b1 = 0, bs = 0, bt = 0;  // dst, pos / nbr, src, tidx bases
+        for (const auto& p : parts) {
+            const Hop& h = p->hops[j];
+            const int64_t nd = static_cast<int64_t>(h.dst_ids.size());
+            if (j == n_hops - 1) {
+                for (int64_t r = 0; r < nd; ++r) {
+                    o[GS_PK_POS_PTR][bd + r] = static_cast<int32_t>(h.pos_ptr[r] + b1);
+                    o[GS_PK_DST_IDS][bd + r] = static_cast<int32_t>(h.dst_ids[r]);
+                }
+                if (!h.ent.empty()) std::memcpy(o[GS_PK_POS] + b1, h.ent.data(), h.ent.size() * sizeof(int32_t));
+                b1 += static_cast<int64_t>(h.ent.size());
+            } else {
+                const int64_t ns = static_cast<int64_t>(h.src_ids.size());
+                GS_REQUIRE(ns == static_cast<int64_t>(p->hops[j + 1].dst_ids.size()), GS_EINVAL,
+                           "hop frontier mismatch");
+                for (int64_t r = 0; r < nd; ++r) {
+                    o[GS_PK_NBR_PTR][bd + r] = static_cast<int32_t>(h.nbr_ptr[r] + b1);
+                    o[GS_PK_SELF][bd + r] = static_cast<int32_t>(h.self_local[r] + bs);
+                }
+                for (size_t e = 0; e < h.nbr.size(); ++e) o[GS_PK_NBR][b1 + e] = static_cast<int32_t>(h.nbr[e] + bs);
+                for (int64_t c = 0; c < ns; ++c) o[GS_PK_TPTR][bs + c] = static_cast<int32_t>(h.tptr[c] + bt);
+                for (size_t t = 0; t < h.tidx.size(); ++t) {  // r -> r + bd; -(r+1) -> -(r+bd+1)
+                    const int32_t v = h.tidx[t];
+                    o[GS_PK_TIDX][bt + t] = static_cast<int32_t>(v >= 0 ? v + bd : v - bd);
+                }
+                b1 += static_cast<int64_t>(h.nbr.size());
+                bs += ns;
+                bt += static_cast<int64_t>(h.tidx.size());
+            }
+            bd += nd;
+        }
+        if (j == n_hops - 1) {
+            o[GS_PK_POS_PTR][bd] = static_cast<int32_t>(b1);
+        } else {
+            o[GS_PK_NBR_PTR][bd] = static_cast<int32_t>(b1);
+            o[GS_PK_TPTR][bs] = static_cast<int32_t>(bt);
+        }
+    }
+    for (int32_t j = 0; j < GS_MAX_HOPS; ++j)
+        for (int f = 0; f < GS_PK_NFIELDS; ++f) offsets[j * GS_PK_NFIELDS + f] = L.off[j][f];
+    int32_t* r = buf + L.total;
+    for (int64_t i = 0; i < n_roots; ++i) r[i] = static_cast<int32_t>(roots[i]);
+    *used = L.total + n_roots;
+    GS_API_END
+}
+
 }  // extern "C"

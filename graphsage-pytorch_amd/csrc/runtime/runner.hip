@@ -84,6 +84,8 @@ struct gs_runner {
     std::vector<int32_t> fanouts;
     std::vector<int64_t> roots;  // n_batches x batch
     int64_t cap = 0;             // int32 words per pack slot (pack bound + roots)
+    int64_t merge = 1;           // reference batches per step (inference only)
+    int64_t n_units = 0;         // steps: ceil(n_batches / merge)
     std::vector<std::unique_ptr<gs::SamplerStream>> streams;
     bool stop = false;
     int64_t next_batch = 0;
@@ -149,9 +151,10 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
         gs::PackSlot& slot = s.slots[slot_id];
         const auto t0 = gs::Clock::now();
         slot.batch = b;
-        slot.status = gs_sample_pack_run(cfg.graph, s.rng, roots.data() + b * cfg.batch, cfg.batch, fanouts.data(),
-                                         cfg.n_hops, cfg.flags, slot.host, cap, slot.hop_sizes, slot.offsets,
-                                         &slot.used);
+        const int64_t nb = std::min(merge, cfg.n_batches - b * merge);  // reference batches of step b
+        slot.status = gs_sample_pack_run_multi(cfg.graph, s.rng, roots.data() + b * merge * cfg.batch,
+                                               nb * cfg.batch, cfg.batch, fanouts.data(), cfg.n_hops, cfg.flags,
+                                               slot.host, cap, slot.hop_sizes, slot.offsets, &slot.used);
         if (slot.status != GS_OK) slot.error = gs_last_error();
         slot.sample_s = gs::secs(t0, gs::Clock::now());
         {
@@ -286,6 +289,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(cfg->world >= 1 && (cfg->world == 1 || cfg->comm), GS_EINVAL, "world > 1 needs a communicator");
     GS_REQUIRE(!cfg->embed_out || (cfg->embed_ld >= 1 && !cfg->comm), GS_EINVAL,
                "embed_out needs embed_ld >= 1 and no communicator");
+    GS_REQUIRE(cfg->merge <= 1 || cfg->embed_out, GS_EINVAL, "merge > 1 is inference only (embed_out)");
     for (int32_t w = 0; w < cfg->n_streams; ++w) GS_REQUIRE(cfg->rngs[w], GS_EINVAL, "NULL rng");
     std::unique_ptr<gs_runner> r(new gs_runner());
     r->cfg = *cfg;
@@ -294,9 +298,12 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     r->cfg.fanouts = r->fanouts.data();
     r->roots.assign(cfg->batches, cfg->batches + cfg->n_batches * cfg->batch);
     r->cfg.batches = r->roots.data();
-    const int64_t bound = gs_sample_pack_bound(cfg->graph, cfg->batch, r->fanouts.data(), cfg->n_hops);
+    r->merge = std::max<int64_t>(1, std::min<int64_t>(cfg->merge, cfg->n_batches));
+    r->n_units = (cfg->n_batches + r->merge - 1) / r->merge;
+    const int64_t mb = r->merge * cfg->batch;  // roots per step
+    const int64_t bound = gs_sample_pack_bound_multi(cfg->graph, mb, cfg->batch, r->fanouts.data(), cfg->n_hops);
     GS_REQUIRE(bound > 0, GS_EINVAL, "pack bound failed");
-    r->cap = bound + cfg->batch;
+    r->cap = bound + mb;
     hip_ok(hipGetDevice(&r->device), "hipGetDevice");
     {  // high priority: the side stream's pull + gather dispatch ahead of the step they overlap
         int lo = 0, hi = 0;
@@ -319,14 +326,14 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             nd = std::min<int64_t>(nn, nd + nd * per);
         }
         const int32_t k_last = r->fanouts[cfg->n_hops - 1];  // bounds every last-hop neighbourhood
-        const int rc = gs_trainer_gather_reserve(cfg->trainer, nd, k_last > 0 ? k_last : 0);
+        const int rc = gs_trainer_gather_reserve(cfg->trainer, nd * r->merge, k_last > 0 ? k_last : 0);
         if (rc != GS_OK) fail(rc, gs_last_error());
     }
     const int32_t S = cfg->n_streams;
     for (int32_t w = 0; w < S; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
-        for (int64_t b = w; b < cfg->n_batches; b += S) s->batches.push_back(b);
+        for (int64_t b = w; b < r->n_units; b += S) s->batches.push_back(b);
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {
             hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s->slots[q].host), r->cap * sizeof(int32_t),
@@ -350,7 +357,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     GS_API_BEGIN
     using namespace gs;
     GS_REQUIRE(r && (loss || r->cfg.embed_out) && n_steps >= 0, GS_EINVAL, "bad arguments");
-    GS_REQUIRE(r->next_batch + n_steps <= r->cfg.n_batches, GS_ERANGE, "runner has fewer batches left");
+    GS_REQUIRE(r->next_batch + n_steps <= r->n_units, GS_ERANGE, "runner has fewer batches left");
     hipStream_t st = as_stream(stream);
     const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
     float* grads = gs_trainer_grads(r->cfg.trainer);
@@ -364,7 +371,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         // look ahead: batch b+1's pull + gather run on the side stream under
         // this step (never block here: with a slow sampler that would idle the GPU)
-        if (b + 1 < r->cfg.n_batches && r->issued == b + 1) r->issue(b + 1, false);
+        if (b + 1 < r->n_units && r->issued == b + 1) r->issue(b + 1, false);
         const int k = static_cast<int>(b % gs_runner::kDev);
         const auto tg = Clock::now();
         hip_ok(hipEventSynchronize(r->gathered[k]), "hipEventSynchronize");  // normally long done
@@ -388,7 +395,8 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         auto t3 = Clock::now();
         if (r->cfg.embed_out) {  // inference: the forward into this batch's output rows
             const int rc = gs_trainer_forward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets, k, r->ws,
-                                                       r->ws_bytes, r->cfg.embed_out + b * r->cfg.batch * r->cfg.embed_ld,
+                                                       r->ws_bytes,
+                                                       r->cfg.embed_out + b * r->merge * r->cfg.batch * r->cfg.embed_ld,
                                                        st);
             if (rc != GS_OK) fail(rc, gs_last_error());
             t3 = Clock::now();

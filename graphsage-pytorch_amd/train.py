@@ -325,10 +325,12 @@ class Runner:
     gather on a high-priority side stream, and the fused
     step, all without Python per step.  `batches`: iterable of equal-size
     int64 root arrays consumed in order; `rngs`: one RNG per sampler stream
-    (stream w samples batches w, w+S, ...)."""
+    (stream w samples batches w, w+S, ...).  Forward-only (`embed_out`) with
+    `merge` = m > 1: each step is m consecutive batches in one pack and one
+    forward; step u (batches u·m .. u·m+m-1) is sampled by stream u % S."""
 
     def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
-                 comm=None, embed_out=None):
+                 comm=None, embed_out=None, merge=1):
         self.trainer, self.graph = trainer, graph
         self.embed_out = embed_out
         self.rngs = list(rngs)
@@ -351,13 +353,17 @@ class Runner:
                 raise ValueError("embed_out must be a contiguous fp32 [n_batches * batch, hidden] device tensor")
             cfg.embed_out = embed_out.data_ptr()
             cfg.embed_ld = trainer.H
+            cfg.merge = max(1, int(merge))
+        elif merge > 1:
+            raise ValueError("merge > 1 needs embed_out (forward-only)")
+        self.merge = max(1, int(merge)) if embed_out is not None else 1
         h = ctypes.c_void_p()
         check(lib().gs_runner_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
 
     def run(self, n_steps):
         """Issue the next n_steps steps (asynchronous on the device): training
-        steps, or forward-only steps into embed_out."""
+        steps, or forward-only steps (of `merge` batches each) into embed_out."""
         check(lib().gs_runner_run(self._h, int(n_steps), self.trainer.loss.data_ptr(),
                                   _lib.stream_ptr(self.trainer.device)))
         return self.embed_out if self.embed_out is not None else self.trainer.loss
@@ -390,12 +396,16 @@ class Embedder:
     batches of `batch` ids, S sampler streams, the next batch's pull + layer-1
     gather under the current forward, embeddings written in place.
 
-    Stream w of `rngs` samples batches w, w+S, ...; a trailing partial batch
-    is sampled afterwards by the stream whose turn it is and run through
-    NativeTrainer.forward.  With one stream that is exactly the reference's
-    sequence of GraphSage calls on one `random` stream."""
+    `merge` = m consecutive batches share one pack and one forward launch
+    sequence (each still sampled on its own, so each row equals its own
+    batch's forward): the runner is host-issue bound at one 500-id batch per
+    launch.  Stream w of `rngs` samples the groups w, w+S, ... (batch i on
+    stream (i // m) % S); a trailing partial batch is sampled afterwards by
+    the stream whose turn it is and run through NativeTrainer.forward.  With
+    one stream that is exactly the reference's sequence of GraphSage calls on
+    one `random` stream, for any m."""
 
-    def __init__(self, graph, features, weights, fanouts, agg_func="MEAN", gcn=False, depth=4):
+    def __init__(self, graph, features, weights, fanouts, agg_func="MEAN", gcn=False, depth=4, merge=2):
         weights = [w.detach() for w in weights]
         H = weights[0].shape[0]
         dev = features.device
@@ -405,6 +415,7 @@ class Embedder:
                                      gcn=gcn, weights=(weights, *dummy_cls))
         self.graph, self.fanouts, self.gcn, self.agg = graph, list(fanouts), gcn, agg_func
         self.depth = depth
+        self.merge = max(1, int(merge))
         self.last_stats = None
 
     def embed(self, nodes, batch, rngs):
@@ -415,15 +426,16 @@ class Embedder:
         out = torch.empty(len(nodes), self.trainer.H, dtype=torch.float32, device=self.trainer.device)
         if n_full:
             r = Runner(self.trainer, self.graph, nodes[:n_full * batch].reshape(n_full, batch), rngs, self.fanouts,
-                       gcn=self.gcn, fail_empty=self.agg == "MAX", depth=self.depth, embed_out=out)
+                       gcn=self.gcn, fail_empty=self.agg == "MAX", depth=self.depth, embed_out=out,
+                       merge=self.merge)
             try:
-                r.run(n_full)
+                r.run(-(-n_full // self.merge))
                 self.last_stats = r.stats()
             finally:
                 r.close()  # joins the sampler threads: every rng has advanced past its batches
         rest = nodes[n_full * batch:]
         if len(rest):
-            s = sample(self.graph, rngs[n_full % len(rngs)], rest, self.fanouts, gcn=self.gcn)
+            s = sample(self.graph, rngs[(n_full // self.merge) % len(rngs)], rest, self.fanouts, gcn=self.gcn)
             if self.agg == "MAX" and any(s.n_empty(j) for j in range(1, s.n_hops + 1)):
                 raise IndexError("MAX aggregation over an empty neighbourhood (reference: models.py:321-325)")
             self.trainer.forward(DeviceSample(s, self.trainer.device), out[n_full * batch:])

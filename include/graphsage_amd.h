@@ -183,6 +183,19 @@ int gs_sample_pack_run(const gs_graph* g, gs_rng* rng, const int64_t* roots,
                        int64_t n_roots, const int32_t* fanouts, int32_t n_hops,
                        int32_t flags, int32_t* buf, int64_t cap,
                        int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+/* Several batches in one pack (the inference runner's merged launches): the
+ * roots split into consecutive groups of `group` ids (the last one may be
+ * shorter), each group sampled on its own, in order, from `rng` — exactly
+ * the draws of one gs_sample_pack_run per group — and the groups' images
+ * concatenated field by field with their indices rebased, so each row's
+ * neighbourhood and every kernel's result for it are those of its own batch.
+ * hop_sizes are the groups' sums.  n_roots <= group: gs_sample_pack_run. */
+int64_t gs_sample_pack_bound_multi(const gs_graph* g, int64_t n_roots, int64_t group,
+                                   const int32_t* fanouts, int32_t n_hops);
+int gs_sample_pack_run_multi(const gs_graph* g, gs_rng* rng, const int64_t* roots,
+                             int64_t n_roots, int64_t group, const int32_t* fanouts,
+                             int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
+                             int64_t* hop_sizes, int64_t* offsets, int64_t* used);
 
 /* ------------------------------------------------- unsupervised-loss batch
  * UnsupervisedLoss (models.py:30-186) over the same graph and rng:
@@ -498,6 +511,11 @@ typedef struct {
      * backward, all-reduce or update. */
     float* embed_out;
     int64_t embed_ld;
+    /* Inference only: reference batches per device launch (<= 1: one).  Step
+     * u then samples batches u*merge .. u*merge+merge-1 on stream u % S into
+     * one pack (gs_sample_pack_run_multi) and runs one forward over all of
+     * them; gs_runner_run counts these merged steps. */
+    int32_t merge;
 } gs_runner_config;
 
 typedef struct {

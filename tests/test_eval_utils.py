@@ -125,18 +125,20 @@ def test_get_gnn_embeddings_matches_reference(streams):
 @pytest.mark.gpu
 @pytest.mark.parametrize("b_sz", [500, 256])
 def test_embedder_streams_match_module_forward(b_sz):
-    """S = 3 sampler streams: batch i is sampled by stream i % 3 (and the
-    trailing partial batch by the stream whose turn it is); each batch equals
-    the drop-in module's forward drawing from that stream."""
+    """S = 3 sampler streams, merged steps of m batches: batch i is sampled by
+    stream (i // m) % 3 (the trailing partial batch too); each batch equals the
+    drop-in module's forward drawing from that stream."""
     dev = torch.device("cuda", 0)
     A, dc, gsage, cls = _setup(dev)
     S = 3
     E = utils.get_gnn_embeddings(gsage, dc, "g", b_sz=b_sz, sampler_streams=S, seed=11)
     n = len(dc.g_labels)
     rngs = [sampler.RNG(train.rank_seed(11, 0, w)) for w in range(S)]
+    m = train.Embedder.__init__.__defaults__[-1]  # the merge get_gnn_embeddings runs with
+    assert m > 1
     with torch.no_grad():
         for i, lo in enumerate(range(0, n, b_sz)):
-            gsage.rng = rngs[i % S]
+            gsage.rng = rngs[(i // m) % S]
             ref = gsage(np.arange(lo, min(n, lo + b_sz)))
             torch.testing.assert_close(E[lo:lo + len(ref)], ref, atol=1e-6, rtol=1e-6)
     gsage.rng = None

@@ -96,10 +96,12 @@ def test_fullsize_runner_is_deterministic(wl, native):
     np.testing.assert_array_equal(sizes, sizes2)
 
 
-def test_fullsize_embedder_matches_module_forward(wl):
+@pytest.mark.parametrize("merge", [1, 4])
+def test_fullsize_embedder_matches_module_forward(wl, merge):
     W = [w.to(DEV) for w in train.reference_init(2, F, H, C, False, SEED)[0]]
     nodes = np.arange(0, 6 * 500 + 123, dtype=np.int64) * 331 % wl["n"]  # 6 full batches + a partial one
-    emb = train.Embedder(wl["graph"], wl["X"], W, FAN).embed(nodes, 500, [sampler.RNG(7)])
+    # 6 full batches: merged steps of 4 + 2 batches, then the partial one
+    emb = train.Embedder(wl["graph"], wl["X"], W, FAN, merge=merge).embed(nodes, 500, [sampler.RNG(7)])
     gsage = models.GraphSage(2, F, H, wl["X"], wl["graph"], DEV, fanouts=FAN, rng=sampler.RNG(7)).to(DEV)
     with torch.no_grad():
         for i in (1, 2):

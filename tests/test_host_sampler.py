@@ -253,6 +253,97 @@ def test_pack_run_matches_sample_pack(gs):
                                            ctypes.byref(used)))
 
 
+def _pack_run(gs, G_, rng, roots, fan, group=None):
+    L = gs._lib
+    nh = len(fan)
+    if group is None:
+        bound = int(L.lib().gs_sample_pack_bound(G_.handle, len(roots), fan.ctypes.data, nh))
+    else:
+        bound = int(L.lib().gs_sample_pack_bound_multi(G_.handle, len(roots), group, fan.ctypes.data, nh))
+    buf = np.full(bound, -7, np.int32)
+    sizes = np.empty(4 * nh, np.int64)
+    offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+    used = ctypes.c_int64()
+    if group is None:
+        L.check(L.lib().gs_sample_pack_run(G_.handle, rng._h, roots.ctypes.data, len(roots), fan.ctypes.data, nh,
+                                           0, buf.ctypes.data, bound, sizes.ctypes.data, offs.ctypes.data,
+                                           ctypes.byref(used)))
+    else:
+        L.check(L.lib().gs_sample_pack_run_multi(G_.handle, rng._h, roots.ctypes.data, len(roots), group,
+                                                 fan.ctypes.data, nh, 0, buf.ctypes.data, bound, sizes.ctypes.data,
+                                                 offs.ctypes.data, ctypes.byref(used)))
+    offs = offs.reshape(L.GS_MAX_HOPS, L.GS_PK_NFIELDS)
+    return buf[:used.value], sizes.reshape(nh, 4), offs, used.value
+
+
+@pytest.mark.parametrize("n_roots,group", [(40, 15), (45, 15), (12, 15), (3, 1)])
+def test_pack_run_multi_rebases_groups(gs, n_roots, group):
+    """Several batches in one pack (the merged inference steps): the same
+    draws as one gs_sample_pack_run per group on one stream, and every field
+    the concatenation of the groups' fields with pointers and frontier
+    indices rebased (TIDX keeps its self encoding -(r+1))."""
+    G_, _ = _graph(gs, "rmat")
+    L = gs._lib
+    roots = np.nonzero(G_.degrees())[0][5:5 + n_roots].astype(np.int64)
+    fan = np.array([25, 10], np.int32)
+    r1, r2 = gs.RNG(9), gs.RNG(9)
+    parts = [_pack_run(gs, G_, r1, roots[lo:lo + group], fan) for lo in range(0, n_roots, group)]
+    buf, sizes, offs, used = _pack_run(gs, G_, r2, roots, fan, group)
+    assert r1.getstate()[0].tolist() == r2.getstate()[0].tolist() and r1.getstate()[1] == r2.getstate()[1]
+    if len(parts) == 1:
+        assert np.array_equal(buf, parts[0][0])
+        return
+    assert np.array_equal(sizes[:, :2], sum(p[1][:, :2] for p in parts))
+    assert np.array_equal(sizes[0, 2:], sum(p[1][0, 2:] for p in parts)) and (sizes[1, 2:] == -1).all()
+
+    def field(p, j, f, n):
+        o = p[2][j, f]
+        return p[0][o:o + n]
+
+    def cat_ptr(j, f, nd_col, n_col):
+        out, base = [], 0
+        for p in parts:
+            v = field(p, j, f, p[1][j, nd_col] + 1)
+            out.append(v[:-1] + base)
+            base += p[1][j, n_col]
+        return np.concatenate(out + [np.array([base])])
+
+    def cat_idx(j, f, n_col, base_col, neg=False):
+        out, base = [], 0
+        for p in parts:
+            v = field(p, j, f, p[1][j, n_col]).astype(np.int64)
+            out.append(np.where(v >= 0, v + base, v - base) if neg else v + base)
+            base += p[1][j, base_col]
+        return np.concatenate(out)
+
+    got = lambda j, f, n: field((buf, sizes, offs), j, f, n)
+    # hop 1 (roots -> F1): explicit lists into the src frontier, transposed lists over it
+    nd, nn, ns = sizes[0, 0], sizes[0, 3], sizes[0, 2]
+    assert np.array_equal(got(0, L.GS_PK_NBR_PTR, nd + 1), cat_ptr(0, L.GS_PK_NBR_PTR, 0, 3))
+    assert np.array_equal(got(0, L.GS_PK_NBR, nn), cat_idx(0, L.GS_PK_NBR, 3, 2))
+    assert np.array_equal(got(0, L.GS_PK_SELF, nd), cat_idx(0, L.GS_PK_SELF, 0, 2))
+    tptr, base = [], 0
+    for p in parts:
+        v = field(p, 0, L.GS_PK_TPTR, p[1][0, 2] + 1)
+        tptr.append(v[:-1] + base)
+        base += v[-1]
+    assert np.array_equal(got(0, L.GS_PK_TPTR, ns + 1), np.concatenate(tptr + [np.array([base])]))
+    tidx, base_d = [], 0
+    for p in parts:
+        v = field(p, 0, L.GS_PK_TIDX, p[1][0, 3] + p[1][0, 0]).astype(np.int64)
+        tidx.append(np.where(v >= 0, v + base_d, v - base_d))
+        base_d += p[1][0, 0]
+    assert np.array_equal(got(0, L.GS_PK_TIDX, nn + nd), np.concatenate(tidx))
+    # hop 2 (F1 -> F0, the layer-1 gather): absolute CSR entries and global ids need no rebasing
+    nd2, npos = sizes[1, 0], sizes[1, 1]
+    assert nd2 == ns
+    assert np.array_equal(got(1, L.GS_PK_POS_PTR, nd2 + 1), cat_ptr(1, L.GS_PK_POS_PTR, 0, 1))
+    assert np.array_equal(got(1, L.GS_PK_POS, npos), np.concatenate([field(p, 1, L.GS_PK_POS, p[1][1, 1]) for p in parts]))
+    assert np.array_equal(got(1, L.GS_PK_DST_IDS, nd2),
+                          np.concatenate([field(p, 1, L.GS_PK_DST_IDS, p[1][1, 0]) for p in parts]))
+    assert np.array_equal(buf[used - n_roots:], roots.astype(np.int32))
+
+
 def test_stream_seeds_are_reference_seeds(gs):
     """Stream (rank, w) draws exactly what random.seed(seed + rank + 64 w) would."""
     import importlib
