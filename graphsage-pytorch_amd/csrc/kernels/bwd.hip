@@ -91,7 +91,6 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_b_kernel(BwdB b) {
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
 
-int sum_slabs_grid(int64_t len) { return sum_slabs_blocks(len); }
 
 bool layer_bwd_fusable(const LayerBwd& a) {
     const int64_t K = a.Xs ? 2 * a.fin : a.fin;

@@ -10,7 +10,7 @@ namespace gs {
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st);
-void sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
+int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 int sum_slabs_grid(int64_t len);
 
 // agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)

@@ -299,9 +299,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             g_launch_events = {};
             timed_done(T, 2, armed);
             if (S1 > 1) {
-                sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0], T.norm_part + np,
-                                 st);
-                np += sum_slabs_grid(H * K1);
+                np += sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0],
+                                       T.norm_part + np, st);
             } else {
                 parts = false;
             }
