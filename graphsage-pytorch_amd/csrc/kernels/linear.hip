@@ -14,15 +14,15 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
 }
 
 // The slab sum with the slabs split over the block: 64 float4 columns per
-// block, wave q adds slabs [q·P, (q+1)·P) (P = ceil(S/4)) from zero, and wave
-// 0 adds the four part sums in wave order (fixed, no atomics).  Each thread
-// then waits on ceil(S/4) loads instead of S: at the layer-1 dW (31 slabs of
-// 64 Ki floats) two load rounds instead of eight, over 256 blocks instead of
-// 65.  len % 4 == 0.
-constexpr int kSlabParts = kThreads / 64;
-__global__ __launch_bounds__(kThreads) void sum_slabs_split_kernel(const float* __restrict__ slabs, int S,
-                                                                   int64_t len, float* __restrict__ out,
-                                                                   float* __restrict__ part) {
+// block, wave q of kSlabParts adds slabs [q·P, (q+1)·P) (P = ceil(S/parts))
+// from zero, and wave 0 adds the part sums in wave order (fixed, no atomics).
+// Each thread then waits on ceil(S/parts) loads instead of S: at the layer-1
+// dW (31 slabs of 64 Ki floats) and 8 waves, one round of 4 loads instead of
+// eight rounds, over 256 blocks instead of 65.  len % 4 == 0.
+template <int kSlabParts>
+__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const float* __restrict__ slabs, int S,
+                                                                          int64_t len, float* __restrict__ out,
+                                                                          float* __restrict__ part) {
     __shared__ float4 red[kSlabParts - 1][64];
     const int q = threadIdx.x >> 6, c = threadIdx.x & 63;
     const int64_t n4 = len / 4;
@@ -215,7 +215,13 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st) {
     if (slab_split_on(len)) {
         const int64_t nb = slab_split_blocks(len);
-        sum_slabs_split_kernel<<<dim3(static_cast<unsigned>(nb)), kThreads, 0, st>>>(slabs, S, len, out, part);
+        // 8 waves (one round of 4 loads per thread at 31 slabs): 4.8 against 5.3 us for 4 waves,
+        // step 75.8-77.2 against 77.9-78.5 us (rocprof / alternating runs, same box)
+        static const bool four = std::getenv("GS_SLAB_PARTS4") != nullptr;
+        if (!four)
+            sum_slabs_split_kernel<8><<<dim3(static_cast<unsigned>(nb)), 512, 0, st>>>(slabs, S, len, out, part);
+        else
+            sum_slabs_split_kernel<4><<<dim3(static_cast<unsigned>(nb)), 256, 0, st>>>(slabs, S, len, out, part);
         check_launch("sum_slabs");
         return static_cast<int>(nb);
     }
