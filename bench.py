@@ -60,6 +60,12 @@ CONFIGS = {
                          batch=500, classes=16, loop="embed"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# the trainer's kernel timer sites (gs_trainer_time_kernels)
+SITES = (0, 1, 2)
+SITE_NAMES = {0: "gather", 1: "fwd", 2: "dw"}
+SITE_ROLES = {0: "layer-1 gather-aggregate (models.py:291-330 at layer 1)",
+              1: "layer-1 SageLayer forward GEMM relu([X[self] | agg]·W1ᵀ) (models.py:216-219)",
+              2: "layer-1 weight-gradient GEMM dW1 = dZ1ᵀ·[X[self] | agg] row slabs (autograd of models.py:219)"}
 MFMA_PEAK_TFS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense F32 / BF16 matrix peaks (spec)
 
 
@@ -180,17 +186,19 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
                       f"pair-list indexing {t_adj:.1f} s excluded"}
 
 
-def load_traffic(config_name, kernel):
+def load_traffic(config_name, batch, kernel):
     """Per-launch HBM bytes of the timed layer-1 kernel from the newest
-    committed rocprofv3 --pmc summary for this config (profiles/*pmc*.json)."""
+    committed rocprofv3 --pmc summary (profiles/*pmc*.json) recorded for this
+    config, this batch size and this kernel (its short name), else None."""
+    short = kernel.split("<")[0].split("(")[0].split("::")[-1].strip()
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("config") == config_name and kernel in d.get("layer1_kernel", "") and \
-                "layer1_hbm_bytes_per_launch" in d:
+        if d.get("config") == config_name and int(d.get("batch", -1)) == int(batch) and short and \
+                short in d.get("layer1_kernel", "") and "layer1_hbm_bytes_per_launch" in d:
             best = d
     return best
 
@@ -409,6 +417,8 @@ def main():
     ap.add_argument("--full-graph", action="store_true", help="rmat2m-embed: embed every node id")
     ap.add_argument("--embed-merge", type=int, default=2,
                     help="rmat2m-embed: reference batches per device launch (1 = one batch per launch)")
+    ap.add_argument("--ar-buckets", type=int, default=1, choices=(1, 2),
+                    help="N > 1: gradient all-reduce buckets (2 = upper layers + classifier under the layer-1 dW GEMM)")
     ap.add_argument("--sampler-streams", type=int, default=None,
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
@@ -447,69 +457,90 @@ def main():
         epoch += 1
     batches = batches[:total_steps]
     comm = train.Communicator(rank, world, device) if world > 1 else None
+    # hold=True: the sampler threads start no batch past the release mark, so the
+    # timed steps' batches are sampled inside the timed region (presampled_at_t0)
     runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
-                          fail_empty=cfg["agg"] == "MAX", comm=comm)
+                          fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets)
     elem = 2 if cfg["dtype"] == "bf16" else 4
+    L = len(cfg["fanouts"])
+    lib = gs._lib.lib()
 
+    # warmup: every timer site armed; the site with the longest median launch
+    # is the dominant kernel, the one timed inside the measured steps
+    runner.release(args.warmup)
+    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 0b111, args.warmup))
     runner.run(args.warmup)
     torch.cuda.synchronize()
+    warm = {site: kernel_times_ms(trainer, args.warmup, site) for site in SITES}
+    names = {site: lib.gs_trainer_kernel_name(trainer._h, site).decode() for site in SITES}
+    dominant = max(SITES, key=lambda site: float(np.median(warm[site])) if len(warm[site]) else -1.0)
     if world > 1:
         dist.barrier()
     runner.stats(reset=True)
-    gs._lib.check(gs._lib.lib().gs_trainer_time_agg(trainer._h, args.steps))
+    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 1 << dominant, args.steps))
     thr0 = cgroup_throttle()
+    sampled0, consumed0 = runner.progress()
     t0 = time.perf_counter()
+    runner.release(args.warmup + args.steps)
     runner.run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sampled1, consumed1 = runner.progress()
     thr1 = cgroup_throttle()
     st = runner.stats()
-    agg_ms = float(np.mean(agg1_times_ms(trainer, args.steps)))
-    gs._lib.check(gs._lib.lib().gs_trainer_time_kernels(trainer._h, 0b110, calib))
+    times = {dominant: kernel_times_ms(trainer, args.steps, dominant)}
+    # calibration steps after the measured ones time the other sites (an
+    # event-bound launch costs the stream a little: never inside the timed steps)
+    runner.release(total_steps)
+    others = sum(1 << site for site in SITES if site != dominant)
+    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, others, calib))
     runner.run(calib)
     torch.cuda.synchronize()
-    gemm_ms = {site: kernel_times_ms(trainer, calib, site) for site in (1, 2)}
+    for site in SITES:
+        if site != dominant:
+            times[site] = kernel_times_ms(trainer, calib, site)
     loss = float(trainer.loss.item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     value = cfg["batch"] * args.steps * world / elapsed
-    L = len(cfg["fanouts"])
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
     n_edges = float(sizes[:L, 1].sum()) * args.steps
-    fused1 = bool(gs._lib.lib().gs_trainer_layer1_fused(trainer._h))
+    fused1 = bool(lib.gs_trainer_layer1_fused(trainer._h))
+    n1, e1 = float(sizes[L - 1, 0]), float(sizes[L - 1, 1])
     if fused1:
-        agg_bytes = layer1_fused_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], 128, elem)
-        kname = "sage1_fwd_kernel (layer-1 gather-mean + concat-linear-relu, fused)"
+        agg_bytes = layer1_fused_bytes(n1, e1, cfg["feat"], 128, elem)
     else:  # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
-        agg_bytes = agg1_ids_bytes(sizes[L - 1, 0], sizes[L - 1, 1], cfg["feat"], elem, cfg["fanouts"][-1])
-        kname = f"agg_ids_kernel (layer-1 gather-{cfg['agg'].lower()} over resolved neighbour ids)"
+        agg_bytes = agg1_ids_bytes(n1, e1, cfg["feat"], elem, cfg["fanouts"][-1])
+    gemm_flops = 2.0 * n1 * (2 * cfg["feat"]) * 128  # 2·|L1|·2F·H per layer-1 GEMM
 
     if rank == 0:
-        achieved = float(agg_bytes) / (agg_ms * 1e-3) / 1e9
-        tr = load_traffic(args.config, kname.split(" ")[0])
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": (tr["layer1_hbm_bytes_per_launch"] if tr else None),
-                "kernel": kname, "avg_launch_us": round(agg_ms * 1e3, 2),
-                "algo_bytes_per_launch": int(agg_bytes)}
-        # the MFMA side: layer-1 SageLayer GEMMs, 2·n1·K·H flops each
-        K1 = 2 * cfg["feat"]
-        flops = 2.0 * float(sizes[L - 1, 0]) * K1 * 128
-        mfma = {}
-        for site, name in ((1, "linear_fwd_wide_kernel<32> (layer 1: relu([X[self] | agg]·W1ᵀ))"),
-                           (2, "linear_dw_kernel (layer 1: dW1 = dZ1ᵀ·[X[self] | agg] row slabs)")):
-            t = gemm_ms[site]
-            if len(t):
-                tf = flops / (float(np.mean(t)) * 1e-3) / 1e12
+        rooflines = {}
+        for site in SITES:
+            tt = times.get(site)
+            if tt is None or not len(tt):
+                continue
+            us = float(np.mean(tt)) * 1e3
+            if site == 0:
+                achieved, peak, unit, bound = float(agg_bytes) / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+                work = {"algo_bytes_per_launch": int(agg_bytes)}
+            else:
                 peak = MFMA_PEAK_TFS[cfg["dtype"]]
-                mfma["fwd" if site == 1 else "dw"] = {
-                    "bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(tf / peak, 4), "kernel": name, "avg_launch_us": round(float(np.mean(t)) * 1e3, 2),
-                    "algo_flops_per_launch": int(flops)}
+                achieved, unit, bound = gemm_flops / (us * 1e-6) / 1e12, "TFLOP/s", "mfma"
+                work = {"algo_flops_per_launch": int(gemm_flops)}
+            tr = load_traffic(args.config, cfg["batch"], names[site]) if site == 0 else None
+            rooflines[SITE_NAMES[site]] = dict(
+                bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
+                traffic=(tr["layer1_hbm_bytes_per_launch"] if tr else None), kernel=names[site],
+                role=SITE_ROLES[site], avg_launch_us=round(us, 2),
+                timed_in=("measured steps" if site == dominant else f"{calib} calibration steps after them"),
+                warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
+                **work)
+        roof = dict(rooflines[SITE_NAMES[dominant]])
+        roof["dominant_by"] = "longest median launch (HIP events) over the warmup steps"
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(wl, cfg, args.cpu_budget, args.seed)
@@ -524,6 +555,10 @@ def main():
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
                        "sampler_streams_per_gpu": args.sampler_streams,
+                       "presampled_at_t0": sampled0 - consumed0,
+                       "sampled_in_timed_region": sampled1 - sampled0,
+                       "sampled_ahead_at_t1": sampled1 - consumed1,
+                       "allreduce_buckets": args.ar_buckets if world > 1 else 0,
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
                        "host_ms_per_step": {"sampler": round(1e3 * st["sample_s"] / max(1, st["steps"]), 3),
@@ -538,7 +573,7 @@ def main():
                                             "max_step": round(1e3 * st["max_step_s"], 3)},
                        "cgroup_throttled_ms": (round((thr1 - thr0) / 1e3, 3) if thr0 is not None else None)},
             "roofline": roof,
-            "roofline_mfma": mfma or None,
+            "roofline_kernels": rooflines,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -123,6 +123,7 @@ _SIGS = {
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
     "gs_trainer_time_kernels": (_i32, [_vp, _i32, _i64]),
+    "gs_trainer_kernel_name": (ctypes.c_char_p, [_vp, _i32]),
     "gs_trainer_grads": (_vp, [_vp]),
     "gs_trainer_layer1_fused": (_i32, [_vp]),
     "gs_comm_unique_id": (_i32, [_vp]),
@@ -134,6 +135,8 @@ _SIGS = {
     "gs_runner_stats_get": (_i32, [_vp, _vp]),
     "gs_runner_stats_reset": (None, [_vp]),
     "gs_runner_destroy": (None, [_vp]),
+    "gs_runner_release": (_i32, [_vp, _i64]),
+    "gs_runner_progress": (_i32, [_vp, _p(_i64), _p(_i64)]),
 }
 
 
@@ -151,7 +154,7 @@ class RunnerConfig(ctypes.Structure):
         ("graph", _vp), ("trainer", _vp), ("batches", _vp), ("n_batches", _i64), ("batch", _i64),
         ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
         ("depth", _i32), ("comm", _vp), ("world", _i32), ("embed_out", _vp), ("embed_ld", _i64),
-        ("merge", _i32),
+        ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32),
     ]
 
 

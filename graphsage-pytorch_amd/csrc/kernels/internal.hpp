@@ -2,9 +2,21 @@
 // Internal launchers shared between the kernel translation units and the
 // trainer (step.hip).  Not part of the C-ABI: they throw gs::Error and take
 // hipStream_t directly.
+#include <functional>
+
 #include "kcommon.hpp"
 
+struct gs_trainer;
+
 namespace gs {
+
+// step.hip: called (on the launching thread, with the step's stream) once
+// every gradient except layer 1's weight gradient has been issued — after the
+// layers >= 2 backward and the classifier reduce, before the layer-1 dW GEMM —
+// so a caller can all-reduce the finished gradients [w1_floats, n_params)
+// under that GEMM (the runner's bucketed all-reduce).  Empty: no hook.
+void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
+int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,

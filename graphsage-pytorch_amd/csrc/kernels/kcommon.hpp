@@ -113,12 +113,16 @@ struct LaunchEvents {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 inline thread_local LaunchEvents g_launch_events;
+// The (mangled) symbol of the last kernel launch_k bound to timing events, so
+// a timer site reports which kernel variant it actually timed.
+inline thread_local const char* g_launch_name = nullptr;
 
 template <typename... KArgs, typename... Args>
 inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
     LaunchEvents ev = g_launch_events;
     if (ev.start) {
         g_launch_events = {};
+        g_launch_name = hipKernelNameRefByPtr(reinterpret_cast<const void*>(kernel), st);
         hipExtLaunchKernelGGL(kernel, grid, block, smem, st, ev.start, ev.stop, 0, static_cast<KArgs>(args)...);
     } else {
         kernel<<<grid, block, smem, st>>>(static_cast<KArgs>(args)...);

@@ -15,11 +15,11 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
 
 // The slab sum with the slabs split over the block: 64 float4 columns per
 // block, wave q of kSlabParts adds slabs [q·P, (q+1)·P) (P = ceil(S/parts))
-// from zero, and wave 0 adds the part sums in wave order (fixed, no atomics).
-// Each thread then waits on ceil(S/parts) loads instead of S: at the layer-1
-// dW (31 slabs of 64 Ki floats) and 8 waves, one round of 4 loads instead of
-// eight rounds, over 256 blocks instead of 65.  len % 4 == 0.
-template <int kSlabParts>
+// from zero, and wave 0 adds the part sums in wave order (fixed, no atomics;
+// the order of sum_slabs_body).  Each thread then waits on ceil(S/parts)
+// loads instead of S: at the layer-1 dW (31 slabs of 64 Ki floats) and 8
+// waves, one round of 4 loads instead of eight rounds, over 256 blocks
+// instead of 65.  len % 4 == 0.
 __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const float* __restrict__ slabs, int S,
                                                                           int64_t len, float* __restrict__ out,
                                                                           float* __restrict__ part) {
@@ -217,11 +217,7 @@ int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* 
         const int64_t nb = slab_split_blocks(len);
         // 8 waves (one round of 4 loads per thread at 31 slabs): 4.8 against 5.3 us for 4 waves,
         // step 75.8-77.2 against 77.9-78.5 us (rocprof / alternating runs, same box)
-        static const bool four = std::getenv("GS_SLAB_PARTS4") != nullptr;
-        if (!four)
-            sum_slabs_split_kernel<8><<<dim3(static_cast<unsigned>(nb)), 512, 0, st>>>(slabs, S, len, out, part);
-        else
-            sum_slabs_split_kernel<4><<<dim3(static_cast<unsigned>(nb)), 256, 0, st>>>(slabs, S, len, out, part);
+        sum_slabs_split_kernel<<<dim3(static_cast<unsigned>(nb)), kSlabParts * 64, 0, st>>>(slabs, S, len, out, part);
         check_launch("sum_slabs");
         return static_cast<int>(nb);
     }

@@ -542,31 +542,46 @@ __global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
                                                    lda, dout, out, ldo, dst, split_stride);
 }
 
-// out[i] = Σ_s slabs[s][i], fixed order; 4 elements per thread.  With
-// `part`, block bx also writes Σ out[i]² over its elements to part[bx]
-// (the clip norm's partial for these gradients).
+// out[i] = Σ_s slabs[s][i] in one fixed order shared by every slab-sum
+// kernel: the S slabs fall into kSlabParts consecutive groups of
+// P = ceil(S / kSlabParts); each group is summed from zero in slab order, and
+// the group sums are added in group order (empty groups add +0).  This is the
+// order of sum_slabs_split_kernel (one wave per group), so the fused backward
+// (which runs this body) and the standalone launch give bitwise the same
+// gradients for any S.  4 elements per thread.  With `part`, block bx also
+// writes Σ out[i]² over its elements to part[bx] (the clip norm's partial).
+constexpr int kSlabParts = 8;
+
 __device__ __forceinline__ void sum_slabs_body(int bx, int nblk, const float* __restrict__ slabs, int S,
                                                int64_t len, float* __restrict__ out, float* __restrict__ part) {
     const int64_t n4 = len / 4;
+    const int per = (S + kSlabParts - 1) / kSlabParts;
     float sq = 0.f;
     for (int64_t i = bx * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(nblk) * kThreads) {
-        float4 s = *reinterpret_cast<const float4*>(slabs + 4 * i);
-// 4 slab loads per unrolled round: measured (rocprof, in-step, 31 slabs) 5.3-5.9 us against 6.2
-// with 8, 7-9.7 with 16, 12 with 32 and 6.8-7.8 with 2
-#ifndef GS_SLAB_UNROLL
-#define GS_SLAB_UNROLL 4
-#endif
-#pragma unroll GS_SLAB_UNROLL
-        for (int t = 1; t < S; ++t) {
-            const float4 v = *reinterpret_cast<const float4*>(slabs + t * len + 4 * i);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < kSlabParts; ++q) {
+            const int t0 = min(S, q * per), t1 = min(S, t0 + per);
+            float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+            for (int t = t0; t < t1; ++t) {
+                const float4 v = *reinterpret_cast<const float4*>(slabs + t * len + 4 * i);
+                g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+            }
+            if (q == 0) s = g;
+            else { s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w; }
         }
         *reinterpret_cast<float4*>(out + 4 * i) = s;
         sq = fmaf(s.x, s.x, sq); sq = fmaf(s.y, s.y, sq); sq = fmaf(s.z, s.z, sq); sq = fmaf(s.w, s.w, sq);
     }
     for (int64_t i = 4 * n4 + bx * int64_t(kThreads) + threadIdx.x; i < len; i += int64_t(nblk) * kThreads) {
         float s = 0.f;
-        for (int t = 0; t < S; ++t) s += slabs[t * len + i];
+        for (int q = 0; q < kSlabParts; ++q) {
+            const int t0 = min(S, q * per), t1 = min(S, t0 + per);
+            float g = 0.f;
+            for (int t = t0; t < t1; ++t) g += slabs[t * len + i];
+            s = q == 0 ? g : s + g;
+        }
         out[i] = s;
         sq = fmaf(s, s, sq);
     }

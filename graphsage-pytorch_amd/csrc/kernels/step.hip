@@ -4,8 +4,11 @@
 // library, with every intermediate carved from one caller-owned workspace.
 // The Python host makes two calls per step (forward_backward, update) and
 // puts the RCCL gradient all-reduce between them.
+#include <cxxabi.h>
+
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "internal.hpp"
@@ -24,6 +27,7 @@ struct gs_trainer {
     struct Timer {
         std::vector<hipEvent_t> ev0, ev1;
         int64_t n = 0;
+        std::string kernel;  // demangled name of the kernel the site last timed
     } timer[kSites];
     std::vector<hipEvent_t>& ev0 = timer[0].ev0;
     std::vector<hipEvent_t>& ev1 = timer[0].ev1;
@@ -45,6 +49,7 @@ struct gs_trainer {
     int pstride = 0;
     int npart[2] = {0, 0};
     bool norm_ready = false;
+    std::function<void(hipStream_t)> upper_hook;  // internal.hpp trainer_set_upper_hook
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
         for (auto& tm : timer) {
@@ -89,9 +94,19 @@ static inline bool timed_arm(gs_trainer& T, int site) {
     g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
     return true;
 }
+static std::string demangle(const char* sym) {
+    if (!sym) return "?";
+    int status = 0;
+    char* d = abi::__cxa_demangle(sym, nullptr, nullptr, &status);
+    std::string out = (status == 0 && d) ? d : sym;
+    std::free(d);
+    return out;
+}
+
 static inline void timed_done(gs_trainer& T, int site, bool armed) {
     if (!armed) return;
     GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
+    if (T.timer[site].kernel.empty()) T.timer[site].kernel = demangle(g_launch_name);
     ++T.timer[site].n;
 }
 
@@ -107,15 +122,11 @@ static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes
         GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
         return pack + o;
     };
-    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
-    if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
+    const bool timed = timed_arm(T, 0);
     ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F,
                   hop_sizes[4 * (L - 1)], fld(GS_PK_POS_PTR), fld(GS_PK_POS), nullptr, c.col, fld(GS_PK_DST_IDS),
                   c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
-    if (timed) {
-        GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
-        ++T.n_timed;
-    }
+    timed_done(T, 0, timed);
 }
 
 // The same aggregate in two launches on `st`: resolve the sampled positions
@@ -133,14 +144,10 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const int64_t n_dst = hop_sizes[4 * (L - 1)];
     int32_t* ids = T.ids_slot[slot];
     resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids, st);
-    const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
-    if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
+    const bool timed = timed_arm(T, 0);
     agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim, n_dst,
                    T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, T.a1_slot[slot], c.feat_dim, st);
-    if (timed) {
-        GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
-        ++T.n_timed;
-    }
+    timed_done(T, 0, timed);
 }
 
 // Runs (or, with ws == nullptr, only sizes) one forward + backward.  With
@@ -211,15 +218,11 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const void* W1 = lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
     if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
-        const bool timed = T.n_timed < static_cast<int64_t>(T.ev0.size());
-        if (timed) g_launch_events = {T.ev0[T.n_timed], T.ev1[T.n_timed]};
+        const bool timed = timed_arm(T, 0);
         ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
                         rows[0], fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.col, dst_L, c.gcn, W1, agg[0], F, h[0],
                         H, 1, st));
-        if (timed) {
-            GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
-            ++T.n_timed;
-        }
+        timed_done(T, 0, timed);
     } else if (a1_slot < 0) {
         gather1(T, pack, hop_sizes, offsets, agg[0], st);
     }
@@ -291,6 +294,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 parts = parts && n > 0;
                 np += n;
             }
+            if (T.upper_hook) T.upper_hook(st);
             const int64_t K1 = T.w_cols[0];
             const bool armed = timed_arm(T, 2);
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
@@ -324,6 +328,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         const void* x_in = first ? c.X : h[l - 2];
         const int32_t* sidx = first ? dst_L : fld(j, GS_PK_SELF);
         const int64_t fin = in_dim[l - 1], ldx = first ? c.feat_ld : H;
+        if (first && L >= 2 && T.upper_hook) T.upper_hook(st);
         ok(gs_sage_linear_bwd_weight(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H,
                                      c.gcn ? nullptr : x_in, ldx, sidx, agg[l - 1], fin, dH, h[l - 1], H, relu,
                                      G + T.w_off[l - 1], dw_ws, dw_need, st));
@@ -341,6 +346,10 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     }
     return cv.at;
 }
+
+void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->upper_hook = std::move(hook); }
+
+int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols[0]; }
 
 }  // namespace gs
 
@@ -507,6 +516,7 @@ int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity) 
             GS_REQUIRE(hipEventCreate(&tm.ev0[i]) == hipSuccess && hipEventCreate(&tm.ev1[i]) == hipSuccess, GS_EHIP,
                        "hipEventCreate");
         tm.n = 0;
+        tm.kernel.clear();
     }
     GS_API_END
 }
@@ -525,6 +535,11 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
 }
 
 int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap) { return gs_trainer_kernel_times(t, 0, ms, cap); }
+
+const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site) {
+    if (!t || site < 0 || site >= gs_trainer::kSites) return "";
+    return t->timer[site].kernel.c_str();
+}
 
 int gs_trainer_update_local(gs_trainer* t, void* stream) {
     GS_API_BEGIN

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -29,7 +30,7 @@
 #include <thread>
 #include <vector>
 
-#include "../kernels/kcommon.hpp"
+#include "../kernels/internal.hpp"
 
 namespace gs {
 
@@ -87,8 +88,14 @@ struct gs_runner {
     int64_t merge = 1;           // reference batches per step (inference only)
     int64_t n_units = 0;         // steps: ceil(n_batches / merge)
     std::vector<std::unique_ptr<gs::SamplerStream>> streams;
-    bool stop = false;
+    std::atomic<bool> stop{false};
+    // cfg.hold: sampler threads start no batch >= mark until gs_runner_release
+    std::atomic<int64_t> release_mark{INT64_MAX};
+    std::atomic<int64_t> sampled{0};      // batches whose sampling completed
     int64_t next_batch = 0;
+    // cfg.ar_buckets == 2: the upper gradients' all-reduce on its own stream
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t upper_ready = nullptr, upper_reduced = nullptr;
     // Ring of 3 per batch in flight (b % 3): device pack buffer, trainer
     // gather slot, events.  The side stream pulls batch b's pack and gathers
     // its layer 1 (reads only X and the pack) while the main stream runs
@@ -143,7 +150,7 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
         int slot_id;
         {
             std::unique_lock<std::mutex> lk(s.mu);
-            s.cv.wait(lk, [&] { return stop || !s.free.empty(); });
+            s.cv.wait(lk, [&] { return stop.load() || (!s.free.empty() && b < release_mark.load()); });
             if (stop) return;
             slot_id = s.free.front();
             s.free.pop_front();
@@ -161,6 +168,7 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
             std::lock_guard<std::mutex> lk(s.mu);
             s.ready.push_back(slot_id);
         }
+        sampled.fetch_add(1);
         s.cv.notify_all();
         if (slot.status != GS_OK) return;  // the driver reports it when it reaches this batch
     }
@@ -211,29 +219,38 @@ bool gs_runner::issue(int64_t b, bool block) {
 }
 
 gs_runner::~gs_runner() {
+    stop = true;
     for (auto& s : streams) {
-        {
-            std::lock_guard<std::mutex> lk(s->mu);
-            stop = true;
-        }
+        { std::lock_guard<std::mutex> lk(s->mu); }  // a sampler between its predicate check and its wait sees stop
         s->cv.notify_all();
     }
     for (auto& s : streams)
         if (s->th.joinable()) s->th.join();
-    for (auto& s : streams)
-        for (int q : s->copying) (void)hipEventSynchronize(s->slots[q].copied);
+    // Device work that may still read the pinned slots or the device rings:
+    // the side stream (pull kernels of consumed and of issued-but-unconsumed
+    // lookahead batches), the steps in flight and the comm stream.  Drain all
+    // of it before any buffer is freed.
+    if (side) (void)hipStreamSynchronize(side);
+    if (comm_stream) (void)hipStreamSynchronize(comm_stream);
+    for (int d = 0; d < kDev; ++d)
+        if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
     for (auto& s : streams)
         for (auto& slot : s->slots) {
-            if (slot.copied) (void)hipEventDestroy(slot.copied);
+            if (slot.copied) {
+                (void)hipEventSynchronize(slot.copied);
+                (void)hipEventDestroy(slot.copied);
+            }
             if (slot.host) (void)hipHostFree(slot.host);
         }
-    if (side) (void)hipStreamSynchronize(side);
     for (int d = 0; d < kDev; ++d) {
-        if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
         if (dev[d]) (void)hipFree(dev[d]);
     }
+    if (cfg.trainer && comm_stream) gs::trainer_set_upper_hook(cfg.trainer, {});
+    if (upper_ready) (void)hipEventDestroy(upper_ready);
+    if (upper_reduced) (void)hipEventDestroy(upper_reduced);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
     if (side) (void)hipStreamDestroy(side);
     if (ws) (void)hipFree(ws);
     if (clip_ws) (void)hipFree(clip_ws);
@@ -344,6 +361,23 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         }
         r->streams.push_back(std::move(s));
     }
+    r->release_mark = cfg->hold ? 0 : INT64_MAX;
+    if (cfg->comm && cfg->ar_buckets == 2 && !cfg->embed_out && cfg->n_hops >= 2) {
+        hip_ok(hipStreamCreateWithFlags(&r->comm_stream, hipStreamNonBlocking), "hipStreamCreate(comm)");
+        hip_ok(hipEventCreateWithFlags(&r->upper_ready, hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipEventCreateWithFlags(&r->upper_reduced, hipEventDisableTiming), "hipEventCreate");
+        gs_runner* rp = r.get();
+        trainer_set_upper_hook(cfg->trainer, [rp](hipStream_t st) {
+            const int64_t w1 = trainer_w1_floats(rp->cfg.trainer);
+            const int64_t n = gs_trainer_n_params(rp->cfg.trainer);
+            hip_ok(hipEventRecord(rp->upper_ready, st), "hipEventRecord");
+            hip_ok(hipStreamWaitEvent(rp->comm_stream, rp->upper_ready, 0), "hipStreamWaitEvent");
+            const int rc = gs_comm_allreduce_sum(rp->cfg.comm, gs_trainer_grads(rp->cfg.trainer) + w1, n - w1,
+                                                 rp->comm_stream);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            hip_ok(hipEventRecord(rp->upper_reduced, rp->comm_stream), "hipEventRecord");
+        });
+    }
     for (auto& s : r->streams) {
         SamplerStream* sp = s.get();
         gs_runner* rp = r.get();
@@ -358,6 +392,8 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     using namespace gs;
     GS_REQUIRE(r && (loss || r->cfg.embed_out) && n_steps >= 0, GS_EINVAL, "bad arguments");
     GS_REQUIRE(r->next_batch + n_steps <= r->n_units, GS_ERANGE, "runner has fewer batches left");
+    GS_REQUIRE(r->next_batch + n_steps <= r->release_mark, GS_EINVAL,
+               "steps past the release mark (gs_runner_release) would wait forever");
     hipStream_t st = as_stream(stream);
     const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
     float* grads = gs_trainer_grads(r->cfg.trainer);
@@ -409,7 +445,11 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             // with a communicator (any world size, so one rank exercises the same
             // path): sum the gradients, then clip the averaged sum; without one
             // the clip uses the norm partials of the step's own reductions
-            if (r->cfg.comm) {
+            if (r->cfg.comm && r->comm_stream) {  // bucketed: W1 here, the rest went out under its GEMM
+                rc = gs_comm_allreduce_sum(r->cfg.comm, grads, trainer_w1_floats(r->cfg.trainer), st);
+                if (rc != GS_OK) fail(rc, gs_last_error());
+                hip_ok(hipStreamWaitEvent(st, r->upper_reduced, 0), "hipStreamWaitEvent");
+            } else if (r->cfg.comm) {
                 rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
                 if (rc != GS_OK) fail(rc, gs_last_error());
             }
@@ -444,6 +484,25 @@ int gs_runner_stats_get(const gs_runner* r, gs_runner_stats* out) {
 
 void gs_runner_stats_reset(gs_runner* r) {
     if (r) r->stats = gs_runner_stats{};
+}
+
+int gs_runner_release(gs_runner* r, int64_t mark) {
+    GS_API_BEGIN
+    GS_REQUIRE(r && mark >= r->release_mark.load(), GS_EINVAL, "release mark may only grow");
+    r->release_mark = mark;
+    for (auto& s : r->streams) {
+        { std::lock_guard<std::mutex> lk(s->mu); }
+        s->cv.notify_all();
+    }
+    GS_API_END
+}
+
+int gs_runner_progress(const gs_runner* r, int64_t* sampled, int64_t* consumed) {
+    GS_API_BEGIN
+    GS_REQUIRE(r && sampled && consumed, GS_EINVAL, "NULL argument");
+    *sampled = r->sampled.load();
+    *consumed = r->next_batch;
+    GS_API_END
 }
 
 void gs_runner_destroy(gs_runner* r) { delete r; }

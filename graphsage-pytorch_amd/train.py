@@ -128,6 +128,12 @@ class NativeTrainer:
                                        _lib.stream_ptr(self.device)))
         return out
 
+    def update(self, grad_scale=1.0):
+        """gs_trainer_update: grads *= grad_scale, clip per model, SGD — what
+        every rank runs after the gradient all-reduce (grad_scale = 1/world)."""
+        check(lib().gs_trainer_update(self._h, float(grad_scale), self.clip_ws.data_ptr(),
+                                      _lib.stream_ptr(self.device)))
+
     def apply_update(self, world_size=1, group=None):
         """All-reduce (sum) the flat gradients over ranks, then clip + SGD with 1/world."""
         if world_size > 1:
@@ -327,10 +333,14 @@ class Runner:
     int64 root arrays consumed in order; `rngs`: one RNG per sampler stream
     (stream w samples batches w, w+S, ...).  Forward-only (`embed_out`) with
     `merge` = m > 1: each step is m consecutive batches in one pack and one
-    forward; step u (batches u·m .. u·m+m-1) is sampled by stream u % S."""
+    forward; step u (batches u·m .. u·m+m-1) is sampled by stream u % S.
+    `hold`: no batch is sampled before `release(mark)` allows it (measurement:
+    proves a timed region sampled its own batches).  `ar_buckets=2` (with a
+    communicator): the upper layers' + classifier gradients are all-reduced on
+    a comm stream under the layer-1 weight-gradient GEMM, W1's after it."""
 
     def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
-                 comm=None, embed_out=None, merge=1):
+                 comm=None, embed_out=None, merge=1, hold=False, ar_buckets=1):
         self.trainer, self.graph = trainer, graph
         self.embed_out = embed_out
         self.rngs = list(rngs)
@@ -344,7 +354,8 @@ class Runner:
             n_batches=self.batches.shape[0], batch=self.batches.shape[1], fanouts=self.fanouts.ctypes.data,
             n_hops=len(self.fanouts), flags=flags, n_streams=len(self.rngs),
             rngs=ctypes.cast(self._rng_ptrs, ctypes.c_void_p), depth=depth,
-            comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1)
+            comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1,
+            hold=int(bool(hold)), ar_buckets=int(ar_buckets))
         if embed_out is not None:
             n_rows = self.batches.shape[0] * self.batches.shape[1]
             if not (embed_out.is_contiguous() and embed_out.dtype == torch.float32
@@ -367,6 +378,16 @@ class Runner:
         check(lib().gs_runner_run(self._h, int(n_steps), self.trainer.loss.data_ptr(),
                                   _lib.stream_ptr(self.trainer.device)))
         return self.embed_out if self.embed_out is not None else self.trainer.loss
+
+    def release(self, mark):
+        """hold=True runners: let the sampler threads start batches < mark."""
+        check(lib().gs_runner_release(self._h, int(mark)))
+
+    def progress(self):
+        """(batches sampled so far, steps issued so far)."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().gs_runner_progress(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def stats(self, reset=False):
         st = _lib.RunnerStats()

@@ -466,6 +466,9 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
  * a little: time the GEMM sites in their own steps, not the measured ones. */
 int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity);
 int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap);
+/* Demangled name of the kernel timer site `site` timed since it was last
+ * armed ("" before its first timed launch) — the variant actually launched. */
+const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site);
 /* The flat gradient buffer (cfg.grads), gs_trainer_n_params floats. */
 float* gs_trainer_grads(const gs_trainer* t);
 /* 1 when layer 1 runs through gs_sage1_fwd (opt-in: GS_FUSED1 set at create). */
@@ -516,6 +519,18 @@ typedef struct {
      * one pack (gs_sample_pack_run_multi) and runs one forward over all of
      * them; gs_runner_run counts these merged steps. */
     int32_t merge;
+    /* hold != 0: the sampler threads start no batch at or past the release
+     * mark (initially 0) until gs_runner_release raises it, so a measurement
+     * can prove that none of its batches was sampled before its clock
+     * started.  hold == 0: the mark is unbounded (sampling starts at create). */
+    int32_t hold;
+    /* Gradient all-reduce buckets with a communicator (training only): 1 (or
+     * 0) = one in-place all-reduce of the flat gradient after the backward;
+     * 2 = the upper layers' and classifier's gradients [W2 .. | Wc | bc]
+     * (final once the layers >= 2 backward has run) all-reduced on a comm
+     * stream under the layer-1 weight-gradient GEMM, then W1 on the main
+     * stream.  Same sums either way (the buckets are disjoint ranges). */
+    int32_t ar_buckets;
 } gs_runner_config;
 
 typedef struct {
@@ -539,6 +554,13 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out);
 int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream);
 int gs_runner_stats_get(const gs_runner* r, gs_runner_stats* out);
 void gs_runner_stats_reset(gs_runner* r);
+/* Raise the release mark (cfg.hold): batches < mark may now be sampled.
+ * Returns GS_EINVAL when mark is lower than the current one. */
+int gs_runner_release(gs_runner* r, int64_t mark);
+/* Progress counters: *sampled = batches (steps) whose sampling has
+ * completed, *consumed = steps issued by gs_runner_run; sampled - consumed
+ * is the number of batches sampled ahead of the device at this instant. */
+int gs_runner_progress(const gs_runner* r, int64_t* sampled, int64_t* consumed);
 void gs_runner_destroy(gs_runner* r);
 
 #ifdef __cplusplus

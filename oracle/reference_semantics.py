@@ -102,20 +102,34 @@ def _dense_aggregate(dst_nodes, samp, index, union, X, agg, gcn):
     raise ValueError(agg)
 
 
-def forward_dense(hops, X, weights, agg="MEAN", gcn=False):
-    """Bottom-up forward over sample_layers() output (models.py:255-267)."""
+def _bf16_value(t):
+    """t rounded to bf16 (round-to-nearest-even) in value only: the gradient
+    passes straight through to t (the fp32 master copy a bf16 GEMM reads)."""
+    return t + (t.detach().to(torch.bfloat16).float() - t.detach())
+
+
+def forward_dense(hops, X, weights, agg="MEAN", gcn=False, bf16_layer1=False):
+    """Bottom-up forward over sample_layers() output (models.py:255-267).
+
+    bf16_layer1 (BASELINE configs[3], not a reference mode): X holds
+    bf16-representable values; layer 1's aggregate and weight enter its GEMM
+    rounded to bf16 (fp32 accumulate), as the HIP path computes with a bf16
+    feature table — the reference algorithm on bf16 inputs."""
     L = len(hops)
     h = X
     for layer in range(1, L + 1):
         frontier, samp, index, union = hops[L - layer]
         a = _dense_aggregate(frontier, samp, index, union, h, agg, gcn)
+        w = weights[layer - 1]
+        if bf16_layer1 and layer == 1:
+            a, w = _bf16_value(a), _bf16_value(w)
         if layer == 1:
             self_rows = h[torch.as_tensor(list(frontier), dtype=torch.long)]
         else:
             # _nodes_map (models.py:271-275): rows of the previous hidden state
             self_rows = h[torch.as_tensor([index[x] for x in frontier], dtype=torch.long)]
         combined = a if gcn else torch.cat([self_rows, a], 1)
-        h = F.relu(weights[layer - 1].mm(combined.t())).t()
+        h = F.relu(w.mm(combined.t())).t()
     return h
 
 
@@ -124,10 +138,10 @@ def nll_loss(logp, labels):
 
 
 def train_step_dense(adj, roots, fanouts, X, weights, cls_w, cls_b, labels, agg="MEAN", gcn=False,
-                     lr=0.7, max_norm=5.0, rng=random):
+                     lr=0.7, max_norm=5.0, rng=random, bf16_layer1=False):
     """One supervised step of utils.py:144-191 (without extend_nodes)."""
     hops = sample_layers(adj, roots, fanouts, rng)
-    emb = forward_dense(hops, X, weights, agg, gcn)
+    emb = forward_dense(hops, X, weights, agg, gcn, bf16_layer1)
     logp = torch.log_softmax(emb.mm(cls_w.t()) + cls_b, 1)
     loss = nll_loss(logp, labels)
     loss.backward()

@@ -9,8 +9,22 @@ fp32 features, fanouts (25, 10), MEAN, B = 512 roots per step.
 * determinism: a second runner over the same batches leaves bitwise the same
   parameters and losses;
 * the forward-only inference runner (train.Embedder, get_gnn_embeddings'
-  native path) equals the drop-in module's forward batch by batch.
+  native path) equals the drop-in module's forward batch by batch;
+* the two other benchmarked training paths on the same graph, each through
+  NativeTrainer + Runner (sampler threads held until release) against the
+  oracle's train step over 3 steps:
+  - configs[3]: MAX over a bf16 feature table (bf16 agg_ids gather, bf16
+    layer-1 MFMA GEMM, dW1 from bf16 inputs, argmax backward at layer 2);
+    the oracle runs on the same bf16 values with W1 and the layer-1
+    aggregate rounded to bf16 in the GEMM (oracle.forward_dense
+    bf16_layer1).  bf16·bf16 products are exact in fp32 and the MAX aggregate
+    is exact, so only fp32 summation order differs — plus, rarely, a bf16
+    rounding of W1 that flips between two fp32 values 1 ulp apart, one bf16
+    ulp (2^-8 relative) on that weight: tolerance 1e-3 on loss and weights;
+  - configs[4]'s feature width F = 128 (rmat16m): MEAN through the 32-lane
+    agg_ids variant (512-byte rows), tolerance 1e-4 as the fp32 test.
 """
+import time
 import importlib
 import random
 
@@ -43,6 +57,11 @@ def wl(gs):
     return dict(src=src, dst=dst, n=n, graph=graph, X=X, labels=labels, batches=batches)
 
 
+@pytest.fixture(scope="module")
+def adj(wl):
+    return oracle.Adjacency(wl["src"], wl["dst"], wl["n"])
+
+
 def _run(wl):
     tr = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], C, fanouts=FAN, seed=SEED)
     r = train.Runner(tr, wl["graph"], wl["batches"], [train.make_rng(SEED, 0, w) for w in range(S)], FAN, depth=2)
@@ -60,9 +79,8 @@ def native(wl):
     return _run(wl)
 
 
-def test_fullsize_runner_vs_oracle_train_steps(wl, native):
+def test_fullsize_runner_vs_oracle_train_steps(wl, adj, native):
     tr, losses, sizes = native
-    adj = oracle.Adjacency(wl["src"], wl["dst"], wl["n"])
     X = wl["X"].cpu()
     labels = wl["labels"].cpu().long()
     sage_w, cw, cb = train.reference_init(2, F, H, C, False, SEED)
@@ -109,3 +127,64 @@ def test_fullsize_embedder_matches_module_forward(wl, merge):
         for lo in range(0, len(nodes), 500):
             ref = gsage(nodes[lo:lo + 500])
             torch.testing.assert_close(emb[lo:lo + len(ref)], ref, atol=1e-6, rtol=1e-6, equal_nan=True)
+
+
+def _oracle_steps(wl, adj, X_cpu, agg, feat, bf16, tol, tr, losses, sizes):
+    labels = wl["labels"].cpu().long()
+    sage_w, cw, cb = train.reference_init(2, feat, H, C, False, SEED)
+    W = [w.clone().requires_grad_(True) for w in sage_w]
+    cw, cb = cw.clone().requires_grad_(True), cb.clone().requires_grad_(True)
+    rngs = [random.Random(train.rank_seed(SEED, 0, w)) for w in range(S)]
+    n_dst = np.zeros(2)
+    for i, roots in enumerate(wl["batches"]):
+        rng = rngs[i % S]
+        probe = random.Random()
+        probe.setstate(rng.getstate())
+        hops = oracle.sample_layers(adj, roots.tolist(), FAN, probe)
+        n_dst += [len(hops[0][0]), len(hops[1][0])]
+        ref = oracle.train_step_dense(adj, roots.tolist(), FAN, X_cpu, W, cw, cb, labels[torch.from_numpy(roots)],
+                                      agg=agg, rng=rng, bf16_layer1=bf16)
+        assert abs(losses[i] - ref) < tol, (i, losses[i], ref)
+    np.testing.assert_array_equal(sizes[:2, 0], n_dst)
+    sd = tr.p.state_dict()
+    for i in (1, 2):
+        torch.testing.assert_close(sd[f"sage_layer{i}.weight"].cpu(), W[i - 1].detach(), atol=tol, rtol=tol)
+    torch.testing.assert_close(sd["layer.0.weight"].cpu(), cw.detach(), atol=tol, rtol=tol)
+    torch.testing.assert_close(sd["layer.0.bias"].cpu(), cb.detach(), atol=tol, rtol=tol)
+
+
+def _held_runner(wl, X, agg):
+    """NativeTrainer + Runner over the 3 batches with the sampler threads held
+    until release (the bench's measurement mode): nothing is sampled before."""
+    tr = train.NativeTrainer(wl["graph"], X, wl["labels"], C, fanouts=FAN, agg_func=agg, seed=SEED)
+    r = train.Runner(tr, wl["graph"], wl["batches"], [train.make_rng(SEED, 0, w) for w in range(S)], FAN,
+                     fail_empty=agg == "MAX", depth=2, hold=True)
+    time.sleep(0.2)
+    assert r.progress() == (0, 0)  # held: no batch sampled
+    r.release(len(wl["batches"]))
+    losses = []
+    for _ in wl["batches"]:
+        r.run(1)
+        losses.append(float(tr.loss.item()))
+    sizes = r.stats()["hop_sizes_sum"]
+    assert r.progress() == (len(wl["batches"]), len(wl["batches"]))
+    r.close()
+    return tr, losses, sizes
+
+
+def test_fullsize_bf16_max_runner_vs_oracle(wl, adj):
+    """configs[3]: rmat2m, MAX, bf16 feature table (tolerance 1e-3, see the module doc)."""
+    Xb = torch.empty(wl["n"], F, dtype=torch.bfloat16, device=DEV)
+    ops.fill_uniform(Xb, SEED)  # RNE of the fp32 table's values
+    tr, losses, sizes = _held_runner(wl, Xb, "MAX")
+    Xc = Xb.float().cpu()
+    del Xb
+    _oracle_steps(wl, adj, Xc, "MAX", F, True, 1e-3, tr, losses, sizes)
+
+
+def test_fullsize_f128_mean_runner_vs_oracle(wl, adj):
+    """configs[4]'s F = 128 on the rmat2m graph: the 32-lane agg_ids gather (tolerance 1e-4)."""
+    X128 = torch.empty(wl["n"], 128, dtype=torch.float32, device=DEV)
+    ops.fill_uniform(X128, SEED)
+    tr, losses, sizes = _held_runner(wl, X128, "MEAN")
+    _oracle_steps(wl, adj, X128.cpu(), "MEAN", 128, False, 1e-4, tr, losses, sizes)

@@ -279,15 +279,20 @@ def test_native_runner_matches_python_loop(gs, S, agg, gcn):
     runner.close()
 
 
-@pytest.mark.parametrize("agg,gcn,layers", [("MEAN", False, 2), ("MAX", False, 2), ("MEAN", True, 2),
-                                            ("MEAN", False, 3)])
-def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers):
+@pytest.mark.parametrize("agg,gcn,layers,name,B", [
+    ("MEAN", False, 2, "rmat", 96), ("MAX", False, 2, "rmat", 96), ("MEAN", True, 2, "rmat", 96),
+    ("MEAN", False, 3, "rmat", 96),
+    # B >= 1024: the layer-2 weight gradient spans more than 8 row slabs, so the
+    # fused launch's slab sum and the standalone split kernel both group slabs
+    ("MEAN", False, 2, "pubmed", 1536), ("MAX", False, 2, "pubmed", 1536)])
+def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name, B):
     """The horizontally fused backward launches (kernels/bwd.hip) run the same
-    per-role kernels and summation orders as the five-launch sequence: loss
-    and every gradient bitwise equal.  The single-process update then clips
-    with the norm partials those launches left (another summation order of
-    the same squares): parameters within fp32 rounding."""
-    graph, g, n = _graph(gs, "rmat")
+    per-role kernels and summation orders as the five-launch sequence (the
+    slab sums in one shared grouped order, linear_dev.hpp sum_slabs_body):
+    loss and every gradient bitwise equal.  The single-process update then
+    clips with the norm partials those launches left (another summation order
+    of the same squares): parameters within fp32 rounding."""
+    graph, g, n = _graph(gs, name)
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     fan = [25, 10, 5][:layers]
@@ -296,8 +301,9 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers):
     b = train.NativeTrainer(graph, X, labels, 16, num_layers=layers, fanouts=fan, agg_func=agg, gcn=gcn, seed=824)
     monkeypatch.delenv("GS_NO_FUSED_BWD")
     rng = gs.RNG(21)
-    for step, roots in enumerate(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 13)):
-        if step == 3:
+    done = 0
+    for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 13):
+        if done == 3:
             break
         s = gs.sample(graph, rng, roots, fan)
         if agg == "MAX" and any(s.n_empty(j) for j in range(1, layers + 1)):
@@ -313,6 +319,8 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers):
         b.apply_update()
         torch.testing.assert_close(a.p.params, b.p.params, atol=2e-6, rtol=1e-5)
         b.p.params.copy_(a.p.params)  # keep both on one trajectory
+        done += 1
+    assert done >= 1
 
 
 def test_rccl_communicator_single_rank(gs):
