@@ -417,6 +417,8 @@ def main():
     ap.add_argument("--full-graph", action="store_true", help="rmat2m-embed: embed every node id")
     ap.add_argument("--embed-merge", type=int, default=2,
                     help="rmat2m-embed: reference batches per device launch (1 = one batch per launch)")
+    ap.add_argument("--sustain", type=int, default=200,
+                    help="steady-state steps after the measured ones (samplers running ahead), reported as `sustained`")
     ap.add_argument("--ar-buckets", type=int, default=1, choices=(1, 2),
                     help="N > 1: gradient all-reduce buckets (2 = upper layers + classifier under the layer-1 dW GEMM)")
     ap.add_argument("--sampler-streams", type=int, default=None,
@@ -448,8 +450,9 @@ def main():
     trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2,
                                   hidden=128, fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=args.seed)
     rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
-    calib = min(50, args.steps)  # untimed steps after the measured ones that time the layer-1 GEMMs
-    total_steps = args.warmup + args.steps + calib
+    calib = min(50, args.steps)  # untimed steps after the measured ones that time the other kernels
+    sustain = max(0, args.sustain)  # then a steady-state window (sampler threads running ahead)
+    total_steps = args.warmup + args.steps + calib + sustain
     batches = []
     epoch = 0
     while len(batches) < total_steps:
@@ -502,6 +505,28 @@ def main():
         if site != dominant:
             times[site] = kernel_times_ms(trainer, calib, site)
     loss = float(trainer.loss.item())
+    # steady state: the remaining batches, with the sampler threads free to run
+    # ahead (released since the calibration steps); reported beside `value`
+    # with its proof that the window sampled at least the batches it consumed
+    sus = None
+    if sustain:
+        if world > 1:
+            dist.barrier()
+        ss0, sc0 = runner.progress()
+        ts = time.perf_counter()
+        runner.run(sustain)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        te = time.perf_counter() - ts
+        ss1, sc1 = runner.progress()
+        tt = torch.tensor([te], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        te = float(tt.item())
+        sus = {"value": round(cfg["batch"] * sustain * world / te, 1), "unit": "root nodes/s", "steps": sustain,
+               "ms_per_step": round(te / sustain * 1e3, 4), "sampled_ahead_at_start": ss0 - sc0,
+               "sampled_in_window": ss1 - ss0, "sampled_ahead_at_end": ss1 - sc1}
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -574,6 +599,7 @@ def main():
                        "cgroup_throttled_ms": (round((thr1 - thr0) / 1e3, 3) if thr0 is not None else None)},
             "roofline": roof,
             "roofline_kernels": rooflines,
+            "sustained": sus,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -94,6 +94,15 @@ static inline bool timed_arm(gs_trainer& T, int site) {
     g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
     return true;
 }
+// Timer events only measure: no system-scope release when they complete (a
+// system-scope release writes back and invalidates the caches under the work
+// that follows, which is what made event-bound launches cost the step
+// time).  GS_TIMER_SYSFENCE=1 restores the default events for A/B runs.
+static unsigned timer_event_flags() {
+    static const bool sysfence = std::getenv("GS_TIMER_SYSFENCE") != nullptr;
+    return sysfence ? hipEventDefault : hipEventDisableSystemFence;
+}
+
 static std::string demangle(const char* sym) {
     if (!sym) return "?";
     int status = 0;
@@ -513,8 +522,9 @@ int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity) 
         tm.ev0.assign(cap, nullptr);
         tm.ev1.assign(cap, nullptr);
         for (int64_t i = 0; i < cap; ++i)
-            GS_REQUIRE(hipEventCreate(&tm.ev0[i]) == hipSuccess && hipEventCreate(&tm.ev1[i]) == hipSuccess, GS_EHIP,
-                       "hipEventCreate");
+            GS_REQUIRE(hipEventCreateWithFlags(&tm.ev0[i], gs::timer_event_flags()) == hipSuccess &&
+                           hipEventCreateWithFlags(&tm.ev1[i], gs::timer_event_flags()) == hipSuccess,
+                       GS_EHIP, "hipEventCreate");
         tm.n = 0;
         tm.kernel.clear();
     }

@@ -44,6 +44,17 @@ static void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// The runner's events only order work: the host never reads device memory
+// through them (it waits on them before reusing a pinned slot the device has
+// read, or a device buffer whose readers have finished), and cross-stream
+// consumers are ordered by them on one device.  So they skip the system-scope
+// release that a default event performs (a cache writeback + invalidate at
+// every step boundary).  GS_RUNNER_SYSFENCE=1 restores default events (A/B).
+static unsigned sync_event_flags() {
+    static const bool sysfence = std::getenv("GS_RUNNER_SYSFENCE") != nullptr;
+    return hipEventDisableTiming | (sysfence ? 0u : static_cast<unsigned>(hipEventDisableSystemFence));
+}
+
 // Device-side pull of a pinned host pack (hipHostMalloc memory is mapped into
 // the device address space): the host pays one kernel launch instead of
 // hipMemcpyAsync's host-side cost (measured ~50 us per 0.3 MB pack).
@@ -328,8 +339,8 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         hip_ok(hipStreamCreateWithPriority(&r->side, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
     }
     for (int d = 0; d < gs_runner::kDev; ++d) {
-        hip_ok(hipEventCreateWithFlags(&r->dev_done[d], hipEventDisableTiming), "hipEventCreate");
-        hip_ok(hipEventCreateWithFlags(&r->gathered[d], hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipEventCreateWithFlags(&r->dev_done[d], sync_event_flags()), "hipEventCreate");
+        hip_ok(hipEventCreateWithFlags(&r->gathered[d], sync_event_flags()), "hipEventCreate");
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     }
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
@@ -356,7 +367,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s->slots[q].host), r->cap * sizeof(int32_t),
                                  hipHostMallocDefault),
                    "hipHostMalloc");
-            hip_ok(hipEventCreateWithFlags(&s->slots[q].copied, hipEventDisableTiming), "hipEventCreate");
+            hip_ok(hipEventCreateWithFlags(&s->slots[q].copied, sync_event_flags()), "hipEventCreate");
             s->free.push_back(q);
         }
         r->streams.push_back(std::move(s));
