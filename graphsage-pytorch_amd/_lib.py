@@ -15,7 +15,11 @@ import os
 import torch  # noqa: F401  (must load first: shares its HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgraphsage_amd.so")
+# GS_HOST_ASAN_LIB (sanitizer runs only, tools/asan_host_tests.sh): load the
+# host-only ASan/UBSan build of the library (host/*.cpp, no HIP) instead; the
+# device entry points are then absent and raise if called.
+_ASAN_LIB = os.environ.get("GS_HOST_ASAN_LIB")
+LIB_PATH = _ASAN_LIB or os.path.join(_HERE, "libgraphsage_amd.so")
 
 GS_OK, GS_EINVAL, GS_ENOMEM, GS_EHIP, GS_ERANGE, GS_EEMPTY = range(6)
 GS_F32, GS_BF16 = 0, 1
@@ -185,6 +189,8 @@ def lib():
                 "`make -C graphsage-pytorch_amd/csrc` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)  # CDLL releases the GIL around every call
         for name, (res, args) in _SIGS.items():
+            if _ASAN_LIB and not hasattr(L, name):
+                continue  # device entry point: not in the host-only sanitizer build
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
