@@ -153,6 +153,19 @@ def agg1_ids_bytes(n_dst, n_pos, F, elem, k):
     return n_pos * F * elem + n_dst * (k * 4 + F * elem)
 
 
+def port_calibration():
+    """The oracle port's speed relative to the reference itself on identical
+    rmat2m inputs, measured in the build container (tools/calibrate_oracle.py;
+    the reference never travels to the GPU box)."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "r02_oracle_calibration_rmat2m.json")))
+        return {"port_over_reference": d["port_over_reference"], "reference_ms_per_step": d["reference_ms_per_step"],
+                "port_ms_per_step": d["port_ms_per_step"], "host": d["host"], "losses_equal": d["max_loss_diff"] == 0.0,
+                "source": "profiles/r02_oracle_calibration_rmat2m.json"}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
     """Oracle train step (CPU restatement of the reference) on this host."""
     import random as pyrandom
@@ -179,11 +192,16 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
         if time.perf_counter() - t_start > seconds_budget and len(times) >= 3:
             break
     med = float(np.median(times[1:] if len(times) > 1 else times))
-    return {"value": cfg["batch"] / med, "unit": "root nodes/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} oracle train steps of B={cfg['batch']} roots (first untimed), "
-                      f"median {med * 1e3:.1f} ms/step; lazy dict-of-sets adjacency (built "
-                      f"per touched node), dense-mask mean, torch CPU {threads} threads; "
-                      f"pair-list indexing {t_adj:.1f} s excluded"}
+    cal = port_calibration() if cfg.get("scale") == 21 and cfg["agg"] == "MEAN" and cfg["dtype"] == "fp32" else None
+    out = {"value": cfg["batch"] / med, "unit": "root nodes/s", "cores": threads, "kind": "port",
+           "sample": f"{len(times)} oracle train steps of B={cfg['batch']} roots (first untimed), "
+                     f"median {med * 1e3:.1f} ms/step; lazy dict-of-sets adjacency (built "
+                     f"per touched node), dense-mask mean, torch CPU {threads} threads; "
+                     f"pair-list indexing {t_adj:.1f} s excluded"}
+    if cal:
+        out["calibration"] = cal
+        out["reference_estimate"] = round(out["value"] / cal["port_over_reference"], 1)
+    return out
 
 
 def load_traffic(config_name, batch, kernel):
