@@ -443,6 +443,8 @@ def main():
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
                          "each for the issuing thread, the HIP runtime and RCCL's proxy)")
+    ap.add_argument("--sampler-helpers", type=int, default=0,
+                    help="helper threads per sampler stream (same draws; lower per-batch latency)")
     args = ap.parse_args()
     if args.sampler_streams is None:
         per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
@@ -481,7 +483,8 @@ def main():
     # hold=True: the sampler threads start no batch past the release mark, so the
     # timed steps' batches are sampled inside the timed region (presampled_at_t0)
     runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
-                          fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets)
+                          fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets,
+                          helpers=args.sampler_helpers)
     elem = 2 if cfg["dtype"] == "bf16" else 4
     L = len(cfg["fanouts"])
     lib = gs._lib.lib()
@@ -598,6 +601,7 @@ def main():
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
                        "sampler_streams_per_gpu": args.sampler_streams,
+                       "sampler_helpers_per_stream": args.sampler_helpers,
                        "presampled_at_t0": sampled0 - consumed0,
                        "sampled_in_timed_region": sampled1 - sampled0,
                        "sampled_ahead_at_t1": sampled1 - consumed1,

@@ -81,6 +81,10 @@ _SIGS = {
     "gs_sample_pack_bound_multi": (_i64, [_vp, _i64, _i64, _vp, _i32]),
     "gs_sample_pack_run_multi": (_i32, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp,
                                         _p(_i64)]),
+    "gs_team_create": (_i32, [_i32, _p(_vp)]),
+    "gs_team_destroy": (None, [_vp]),
+    "gs_sample_pack_run_multi_team": (_i32, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp,
+                                             _vp, _p(_i64), _vp]),
     "gs_fill_uniform": (_i32, [_vp, _i32, _i64, _i64, _i64, _u64, _vp]),
     "gs_uniform_host": (_i32, [_u64, _i64, _i64, _i64, _vp]),
     "gs_agg_fwd": (_i32, [_i32, _i32, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i32,
@@ -158,7 +162,7 @@ class RunnerConfig(ctypes.Structure):
         ("graph", _vp), ("trainer", _vp), ("batches", _vp), ("n_batches", _i64), ("batch", _i64),
         ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
         ("depth", _i32), ("comm", _vp), ("world", _i32), ("embed_out", _vp), ("embed_ld", _i64),
-        ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32),
+        ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32), ("helpers", _i32),
     ]
 
 

@@ -8,6 +8,7 @@
 
 #include <immintrin.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -193,6 +194,104 @@ inline void select_chunked(MT19937& rng, int64_t n, int64_t k, OutT* out) {
     }
 }
 
+// Selected-set branch, common case for k <= 16: the k selected values are
+// the first k in-range words of the next 32 whenever those k values are
+// pairwise distinct (no word of the call is then a repeat).  The in-range
+// test is one vector compare per 8 words, the k values are compacted in
+// stream order and checked for a repeat with in-register rotations.  Returns
+// false, having consumed nothing, when fewer than k of the 32 words are in
+// range, a repeat occurs, or the block has fewer than 32 words left; the
+// caller then runs the general scan from the same stream position.
+template <class OutT>
+inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
+    if (rng.index + 32 > MT19937::N) return false;
+    const int sh = 32 - (64 - __builtin_clzll(static_cast<uint64_t>(n)));
+    const __m128i shv = _mm_cvtsi32_si128(sh);
+    const __m256i nv = _mm256_set1_epi32(static_cast<int32_t>(n));
+    const __m256i* src = reinterpret_cast<const __m256i*>(rng.out + rng.index);
+    alignas(32) int32_t w[32];
+    uint32_t inr = 0;
+#pragma GCC unroll 4
+    for (int q = 0; q < 4; ++q) {
+        const __m256i v = _mm256_srl_epi32(_mm256_loadu_si256(src + q), shv);
+        _mm256_store_si256(reinterpret_cast<__m256i*>(w) + q, v);
+        inr |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(nv, v)))) << (8 * q);
+    }
+    if (__builtin_popcount(inr) < k) return false;
+    // compacted values, padded with distinct negatives (never equal to a value)
+    alignas(32) int32_t c[16] = {-1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -16};
+    uint32_t m = inr;
+    int last = 0;
+    for (int i = 0; i < k; ++i) {
+        last = __builtin_ctz(m);
+        c[i] = w[last];
+        m &= m - 1;
+    }
+    const __m256i a = _mm256_load_si256(reinterpret_cast<const __m256i*>(c));
+    const __m256i b = _mm256_load_si256(reinterpret_cast<const __m256i*>(c) + 1);
+    __m256i dup = _mm256_setzero_si256();
+#pragma GCC unroll 4
+    for (int r = 1; r <= 4; ++r) {  // rotations 1..4 cover every pair inside a vector
+        const __m256i rot = _mm256_setr_epi32(r & 7, (r + 1) & 7, (r + 2) & 7, (r + 3) & 7, (r + 4) & 7,
+                                              (r + 5) & 7, (r + 6) & 7, (r + 7) & 7);
+        dup = _mm256_or_si256(dup, _mm256_cmpeq_epi32(a, _mm256_permutevar8x32_epi32(a, rot)));
+        if (k > 8) dup = _mm256_or_si256(dup, _mm256_cmpeq_epi32(b, _mm256_permutevar8x32_epi32(b, rot)));
+    }
+    if (k > 8) {
+#pragma GCC unroll 8
+        for (int r = 0; r < 8; ++r) {  // every pair across the two vectors
+            const __m256i rot = _mm256_setr_epi32(r & 7, (r + 1) & 7, (r + 2) & 7, (r + 3) & 7, (r + 4) & 7,
+                                                  (r + 5) & 7, (r + 6) & 7, (r + 7) & 7);
+            dup = _mm256_or_si256(dup, _mm256_cmpeq_epi32(a, _mm256_permutevar8x32_epi32(b, rot)));
+        }
+    }
+    if (!_mm256_testz_si256(dup, dup)) return false;
+    for (int i = 0; i < k; ++i) out[i] = static_cast<OutT>(c[i]);
+    rng.index += last + 1;
+    return true;
+}
+
+// Pool branch: the draws' word consumption first (each randbelow(n - i)
+// takes words until one is below n - i; a rejected word just advances the
+// stream), as one loop over words whose only unpredictable decision is a
+// counter increment, then the pool swaps (result[i] = pool[j];
+// pool[j] = pool[n-i-1]).  Requires k <= 32 and the draws to fit in the
+// current block (checked: otherwise false, nothing consumed).
+template <class OutT>
+inline bool pool_fast(MT19937& rng, int64_t n, int64_t k, OutT* out, int32_t* pool) {
+    constexpr int kMaxWords = 96;  // enough for k <= 32 at rejection rates < 1/2, else fall back
+    int idx = rng.index;
+    const int end = std::min(MT19937::N, idx + kMaxWords);
+    uint32_t r[32];
+    int i = 0;
+    const uint32_t nn = static_cast<uint32_t>(n);
+    const int sh0 = __builtin_clz(nn);  // 32 - bit_length(n)
+    if (__builtin_clz(nn - static_cast<uint32_t>(k - 1)) == sh0) {
+        // every n - i has n's bit length: one shift for all words
+        while (i < k && idx < end) {
+            const uint32_t v = rng.out[idx++] >> sh0;
+            r[i] = v;
+            i += v < nn - static_cast<uint32_t>(i);
+        }
+    } else {
+        while (i < k && idx < end) {
+            const uint32_t mlim = nn - static_cast<uint32_t>(i);
+            const uint32_t v = rng.out[idx++] >> __builtin_clz(mlim);
+            r[i] = v;
+            i += v < mlim;
+        }
+    }
+    if (i < k) return false;
+    rng.index = idx;
+    for (int64_t t = 0; t < n; ++t) pool[t] = static_cast<int32_t>(t);
+    for (int64_t q = 0; q < k; ++q) {
+        const uint32_t j = r[q];
+        out[q] = static_cast<OutT>(pool[j]);
+        pool[j] = pool[n - q - 1];
+    }
+    return true;
+}
+
 // random.sample(population, k) expressed on positions 0..n-1 of the
 // population: writes the k chosen positions in result order.  `pool` must
 // hold setsize entries.  Requires 0 <= k <= n.
@@ -200,6 +299,7 @@ template <class OutT>
 inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize, OutT* out,
                              int32_t* pool) {
     if (n <= setsize) {
+        if (GS_SELECT_SMALL && k <= 32 && pool_fast(rng, n, k, out, pool)) return;
         // pool branch: pool = list(population); j = randbelow(n-i);
         // result[i] = pool[j]; pool[j] = pool[n-i-1]   (positions stand in
         // for the population items).
@@ -210,6 +310,7 @@ inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize
             pool[j] = pool[n - i - 1];
         }
     } else if (GS_SELECT_SMALL && k <= 32 && n < (int64_t(1) << 31)) {
+        if (k <= 16 && select_fast16(rng, n, k, out)) return;
         select_chunked(rng, n, k, out);
     } else {
         // selected-set branch: j = randbelow(n), redrawn while j in selected.

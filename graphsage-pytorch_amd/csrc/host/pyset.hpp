@@ -119,8 +119,22 @@ struct PySet {
         fill = used;
     }
 
-    // set_add_entry.  Returns true when the key was new.
+    // set_add_entry.  Returns true when the key was new.  The home slot is
+    // settled without a data-dependent branch when it holds the key or is
+    // empty (the common cases of a union, whose keys repeat often).
     bool add(int32_t key) {
+        {
+            const size_t i0 = static_cast<size_t>(key) & mask;
+            const int32_t cur = tab[i0];
+            if (cur == key || cur == EMPTY) {
+                const bool fresh = cur == EMPTY;
+                tab[i0] = key;
+                fill += fresh;
+                used += fresh;
+                if (static_cast<size_t>(fill) * 5 >= mask * 3) resize(used > 50000 ? used * 2 : used * 4);
+                return fresh;
+            }
+        }
         size_t perturb = static_cast<size_t>(key);
         size_t i = static_cast<size_t>(key) & mask;
         int32_t* e;
@@ -177,6 +191,26 @@ struct PySet {
             return;
         }
         for (int64_t t = 0; t < n_used; ++t) add(keys[t]);
+    }
+
+    // merge_items over a run of key lists (set.union(first, *rest) after the
+    // copy of the first), prefetching each key's home slot kAhead keys early:
+    // the union table outgrows L1 and its probes are otherwise serial misses.
+    template <class K>
+    void merge_runs(const K* keys, const int32_t* ptr, int64_t n_runs) {
+        constexpr int64_t kAhead = 16;
+        const int64_t total = ptr[n_runs] - ptr[0];
+        const K* base = keys + ptr[0];
+        int64_t t = 0;
+        for (int64_t r = 0; r < n_runs; ++r) {
+            const int64_t n_used = ptr[r + 1] - ptr[r];
+            if (n_used == 0) continue;
+            if ((fill + n_used) * 5 >= static_cast<int64_t>(mask) * 3) resize((used + n_used) * 2);
+            for (int64_t e = t + n_used; t < e; ++t) {
+                if (t + kAhead < total) __builtin_prefetch(tab + (static_cast<size_t>(base[t + kAhead]) & mask));
+                add(base[t]);
+            }
+        }
     }
 
     // set_merge(this, other).

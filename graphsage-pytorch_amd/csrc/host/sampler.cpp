@@ -14,11 +14,14 @@
 #include <memory>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "common.hpp"
 #include "graph.hpp"
 #include "mt19937.hpp"
 #include "pyset.hpp"
 #include "rng.hpp"
+#include "team.hpp"
 
 #ifndef GS_PHASE  // phase marks for tools/sampler_prof.cpp; no-ops in the library
 #define GS_PHASE(i)
@@ -98,23 +101,29 @@ static int64_t count_empty(const Graph& g, const Hop& h, bool gcn) {
     return e;
 }
 
-// CPython-set replay of :282-288 for one hop: per-node sets, their union
-// (the next frontier, in iteration order), local neighbour lists, and the
-// transposed lists the backward pass gathers over.
-static void materialise(const Graph& g, Hop& h, bool gcn) {
-    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    // samp_neighs[r] = S_r | {v}: built in a scratch set, kept only as its
-    // iteration order (set_items) — all the union needs from r >= 1 — plus
-    // the full table of r == 0, which the union copies.
-    GS_PHASE(0);
-    PySet s, t, first;
-    h.set_ptr.assign(n + 1, 0);
-    h.set_items.clear();
-    h.set_items.reserve(h.pos.size() + n);
+// CPython-set replay of :282-288 for one hop, in three phases:
+//   sets_range    samp_neighs[r] = S_r | {v} for a range of r: kept only as
+//                 each set's iteration order (set_items) — all the union needs
+//                 from r >= 1 — plus the full table of r == 0, which the union
+//                 copies.  Independent per r (helper threads split it).
+//   union_map     list(set.union(*samp_neighs)) (:286): the next frontier in
+//                 iteration order, and each union slot's rank in it.
+//   lists         per-destination neighbour lists in union-local ids and the
+//                 transposed lists the backward pass gathers over.  Needs
+//                 nothing the next hop's draws produce, so it overlaps them.
+struct HopScratch {
+    PySet first, u;                   // samp_neighs[0]; the union
+    std::vector<int32_t> slot_local;  // union slot -> rank in iteration order
+};
+
+static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::vector<int64_t>& items,
+                       int32_t* counts, PySet* first) {
+    PySet s, t;
     // the rows read below are known ahead (positions are drawn): prefetch the
     // col / slot lines of the row kAhead destinations on (random row reads
-    // dominate this loop on large graphs)
-    constexpr int64_t kAhead = 4;
+    // dominate this loop on large graphs), and its row_ptr / table-size bytes
+    // further ahead still
+    constexpr int64_t kAhead = 4, kMeta = 16;
     auto prefetch_row = [&](int64_t q) {
         const int64_t v = h.dst_ids[q];
         const int64_t rs = g.row_ptr[v], d = g.row_ptr[v + 1] - rs;
@@ -127,9 +136,16 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
             }
         }
     };
-    for (int64_t q = 0; q < std::min(n, kAhead); ++q) prefetch_row(q);
-    for (int64_t r = 0; r < n; ++r) {
-        if (r + kAhead < n) prefetch_row(r + kAhead);
+    auto prefetch_meta = [&](int64_t q) {
+        const int64_t v = h.dst_ids[q];
+        __builtin_prefetch(g.row_ptr.data() + v);
+        __builtin_prefetch(g.log2size.data() + v);
+    };
+    for (int64_t q = a; q < std::min(b, a + kMeta); ++q) prefetch_meta(q);
+    for (int64_t q = a; q < std::min(b, a + kAhead); ++q) prefetch_row(q);
+    for (int64_t r = a; r < b; ++r) {
+        if (r + kMeta < b) prefetch_meta(r + kMeta);
+        if (r + kAhead < b) prefetch_row(r + kAhead);
         const int64_t v = h.dst_ids[r];
         const int64_t rs = g.row_ptr[v], d = g.degree(v);
         const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
@@ -144,34 +160,54 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
         }
         copy_into(t, s);  // samp_neigh | set([v])  (:285)
         t.merge_single(v);
-        if (r == 0) first = t;
-        t.for_each([&](int64_t key) { h.set_items.push_back(key); });
-        h.set_ptr[r + 1] = static_cast<int32_t>(h.set_items.size());
+        if (r == 0 && first) *first = t;
+        const size_t before = items.size();
+        t.for_each([&](int64_t key) { items.push_back(key); });
+        counts[r] = static_cast<int32_t>(items.size() - before);
     }
-    GS_PHASE(1);
-    // list(set.union(*samp_neighs))  (:286): copy of the first, then set_merge
-    // of each other set, which only walks that set's iteration order.
-    PySet u;
+}
+
+static void union_map(Hop& h, HopScratch& sc) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    PySet& u = sc.u;
+    u.reset();
     if (n > 0) {
-        copy_into(u, first);
-        for (int64_t r = 1; r < n; ++r)
-            u.merge_items(h.set_items.data() + h.set_ptr[r], h.set_ptr[r + 1] - h.set_ptr[r]);
+        copy_into(u, sc.first);  // non-empty: merge_runs never sees fill == 0
+        u.merge_runs(h.set_items.data(), h.set_ptr.data() + 1, n - 1);
     }
+    // The next frontier: the union's keys in slot order (a vector compaction
+    // of the table).  The slot -> rank map the lists need is built by lists().
+    GS_PHASE(2);
+    h.src_ids.resize(static_cast<size_t>(u.used));
+    int64_t* dst = h.src_ids.data();
+    const __m256i empty = _mm256_set1_epi32(PySet::EMPTY);
+    size_t sl = 0;
+    for (; sl + 8 <= u.mask + 1; sl += 8) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(u.tab + sl));
+        uint32_t m = ~static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpeq_epi32(v, empty)))) & 0xFFu;
+        while (m) {
+            *dst++ = u.tab[sl + __builtin_ctz(m)];
+            m &= m - 1;
+        }
+    }
+    for (; sl <= u.mask; ++sl)
+        if (u.tab[sl] != PySet::EMPTY) *dst++ = u.tab[sl];
+}
+
+static void lists(Hop& h, HopScratch& sc, bool gcn) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    const PySet& u = sc.u;
     // Union-local positions = rank of the key's slot in the union's table
     // (its iteration order): a probe of that cache-resident table instead of
     // a graph-sized node -> position array (random DRAM reads and writes).
-    GS_PHASE(2);
-    thread_local std::vector<int32_t> slot_local;
-    slot_local.resize(u.mask + 1);
-    h.src_ids.clear();
-    h.src_ids.reserve(u.used);
+    sc.slot_local.resize(u.mask + 1);
+    int32_t rank = 0;
     for (size_t sl = 0; sl <= u.mask; ++sl) {
-        const int32_t key = u.tab[sl];
-        slot_local[sl] = static_cast<int32_t>(h.src_ids.size());
-        if (key != PySet::EMPTY) h.src_ids.push_back(key);
+        sc.slot_local[sl] = rank;
+        rank += u.tab[sl] != PySet::EMPTY;
     }
     auto local_of = [&](int64_t key) -> int32_t {
-        return slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(key)))];
+        return sc.slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(key)))];
     };
     // Neighbourhoods in union-local ids, ascending (= the dense mask's column
     // order, :305-308); non-gcn removes self (:297-298).
@@ -180,10 +216,12 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     h.nbr.clear();
     h.self_local.resize(n);
     std::vector<int32_t> tmp;
+    const int64_t n_items = static_cast<int64_t>(h.set_items.size());
     for (int64_t r = 0; r < n; ++r) {
         const int64_t v = h.dst_ids[r];
         tmp.clear();
         for (int32_t q = h.set_ptr[r]; q < h.set_ptr[r + 1]; ++q) {
+            if (q + 16 < n_items) __builtin_prefetch(u.tab + (static_cast<size_t>(h.set_items[q + 16]) & u.mask));
             const int64_t key = h.set_items[q];
             if (!gcn && key == v) continue;
             tmp.push_back(local_of(key));
@@ -217,30 +255,77 @@ static void materialise(const Graph& g, Hop& h, bool gcn) {
     GS_PHASE(5);
 }
 
+// sets_range over the whole hop (split across the team's helpers when there
+// are any), then set_ptr and the concatenated set_items.
+static void build_sets(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    GS_PHASE(0);
+    h.set_ptr.assign(n + 1, 0);
+    h.set_items.clear();
+    const int parts = team ? static_cast<int>(std::min<int64_t>(team->helpers() + 1, std::max<int64_t>(n / 64, 1))) : 1;
+    if (parts <= 1) {
+        h.set_items.reserve(h.pos.size() + n);
+        sets_range(g, h, 0, n, h.set_items, h.set_ptr.data() + 1, &sc.first);
+    } else {
+        std::vector<std::vector<int64_t>> part_items(parts);
+        team->parallel_for(parts, [&](int p) {
+            const int64_t a = n * p / parts, b = n * (p + 1) / parts;
+            part_items[p].reserve(static_cast<size_t>(h.pos_ptr[b] - h.pos_ptr[a] + (b - a)));
+            sets_range(g, h, a, b, part_items[p], h.set_ptr.data() + 1, p == 0 ? &sc.first : nullptr);
+        });
+        size_t total = 0;
+        for (auto& v : part_items) total += v.size();
+        h.set_items.resize(total);
+        size_t at = 0;
+        for (auto& v : part_items) {
+            std::memcpy(h.set_items.data() + at, v.data(), v.size() * sizeof(int64_t));
+            at += v.size();
+        }
+    }
+    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] += h.set_ptr[r];
+    GS_PHASE(1);
+}
+
 static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
-                          const int32_t* fanouts, int32_t n_hops, int32_t flags) {
+                          const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team = nullptr) {
     GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
     GS_REQUIRE(n_roots >= 1 && roots, GS_EINVAL, "empty nodes_batch");
     GS_REQUIRE(g.n_entries < (int64_t(1) << 31), GS_ERANGE, "graph has >= 2^31 CSR entries (int32 pack entries)");
     for (int64_t i = 0; i < n_roots; ++i)
         GS_REQUIRE(roots[i] >= 0 && roots[i] < g.n_nodes, GS_ERANGE, "node id out of range");
+    if (team && team->helpers() == 0) team = nullptr;
     std::unique_ptr<Sample> s(new Sample());
     s->n_hops = n_hops;
     s->flags = flags;
     const bool gcn = flags & GS_SAMPLE_GCN;
     std::vector<int64_t> frontier(roots, roots + n_roots);
+    HopScratch scratch[2];  // hop j's lists may still run on a helper while hop j+1 builds its sets
+    bool pending = false;   // a lists job is outstanding on the team
     for (int32_t j = 0; j < n_hops; ++j) {
         Hop& h = s->hops[j];
         h.k = fanouts ? fanouts[j] : 10;
-        h.dst_ids = frontier;
+        h.dst_ids = std::move(frontier);
         draw_positions(g, rng, h);
         h.n_empty = count_empty(g, h, gcn);
         const bool last = (j == n_hops - 1);
         if (!last || (flags & GS_SAMPLE_FULL)) {
-            materialise(g, h, gcn);
+            HopScratch& sc = scratch[j & 1];
+            if (pending) {  // the team is needed for the sets below
+                team->wait();
+                pending = false;
+            }
+            build_sets(g, h, sc, team);
+            union_map(h, sc);
             frontier = h.src_ids;
+            if (team) {  // lists + transpose on a helper, under the next hop's draws
+                team->start(1, [&h, &sc, gcn](int) { lists(h, sc, gcn); });
+                pending = true;
+            } else {
+                lists(h, sc, gcn);
+            }
         }
     }
+    if (pending) team->wait();
     return s.release();
 }
 
@@ -438,15 +523,25 @@ int64_t gs_sample_pack_bound(const gs_graph* gp, int64_t n_roots, const int32_t*
     return total + al(n_roots);
 }
 
+static int pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots, const int32_t* fanouts,
+                    int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap, int64_t* hop_sizes, int64_t* offsets,
+                    int64_t* used, gs::Team* team);
+
 int gs_sample_pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots,
                        const int32_t* fanouts, int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
                        int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    return pack_run(gp, rng, roots, n_roots, fanouts, n_hops, flags, buf, cap, hop_sizes, offsets, used, nullptr);
+}
+
+static int pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots, const int32_t* fanouts,
+                    int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap, int64_t* hop_sizes, int64_t* offsets,
+                    int64_t* used, gs::Team* team) {
     GS_API_BEGIN
     GS_REQUIRE(gp && rng && buf && hop_sizes && offsets && used, GS_EINVAL, "NULL argument");
     const int64_t bound = gs_sample_pack_bound(gp, n_roots, fanouts, n_hops);
     GS_REQUIRE(bound >= 0 && cap >= bound, GS_EINVAL, "buffer below gs_sample_pack_bound");
     const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
-    std::unique_ptr<Sample> s(gs::run_sample(g, rng->mt, roots, n_roots, fanouts, n_hops, flags));
+    std::unique_ptr<Sample> s(gs::run_sample(g, rng->mt, roots, n_roots, fanouts, n_hops, flags, team));
     gs_pack_layout L;
     layout_of(*s, &L);
     gs_sample_pack(reinterpret_cast<const gs_sample*>(s.get()), buf, cap);
@@ -510,11 +605,28 @@ int64_t gs_sample_pack_bound_multi(const gs_graph* gp, int64_t n_roots, int64_t 
     return (n_roots / group) * full + tail;
 }
 
+int gs_team_create(int32_t helpers, gs_team** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(out && helpers >= 0 && helpers <= 64, GS_EINVAL, "helpers out of [0, 64]");
+    *out = reinterpret_cast<gs_team*>(new gs::Team(helpers));
+    GS_API_END
+}
+
+void gs_team_destroy(gs_team* team) { delete reinterpret_cast<gs::Team*>(team); }
+
 int gs_sample_pack_run_multi(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots, int64_t group,
                              const int32_t* fanouts, int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
                              int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    return gs_sample_pack_run_multi_team(gp, rng, roots, n_roots, group, fanouts, n_hops, flags, buf, cap, hop_sizes,
+                                         offsets, used, nullptr);
+}
+
+int gs_sample_pack_run_multi_team(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64_t n_roots,
+                                  int64_t group, const int32_t* fanouts, int32_t n_hops, int32_t flags, int32_t* buf,
+                                  int64_t cap, int64_t* hop_sizes, int64_t* offsets, int64_t* used, gs_team* tp) {
+    gs::Team* team = reinterpret_cast<gs::Team*>(tp);
     if (group >= 1 && n_roots <= group)
-        return gs_sample_pack_run(gp, rng, roots, n_roots, fanouts, n_hops, flags, buf, cap, hop_sizes, offsets, used);
+        return pack_run(gp, rng, roots, n_roots, fanouts, n_hops, flags, buf, cap, hop_sizes, offsets, used, team);
     GS_API_BEGIN
     GS_REQUIRE(gp && rng && roots && buf && hop_sizes && offsets && used, GS_EINVAL, "NULL argument");
     GS_REQUIRE(group >= 1 && n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "bad group / n_hops");
@@ -526,7 +638,7 @@ int gs_sample_pack_run_multi(const gs_graph* gp, gs_rng* rng, const int64_t* roo
     std::vector<std::unique_ptr<Sample>> parts;
     for (int64_t lo = 0; lo < n_roots; lo += group) {
         parts.emplace_back(gs::run_sample(g, rng->mt, roots + lo, std::min(group, n_roots - lo), fanouts, n_hops,
-                                          flags));
+                                          flags, team));
         if (flags & GS_SAMPLE_FAIL_EMPTY)
             for (int32_t j = 0; j < n_hops; ++j)
                 if (parts.back()->hops[j].n_empty) gs::fail(GS_EEMPTY, "empty neighbourhood");

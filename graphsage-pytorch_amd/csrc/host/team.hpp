@@ -1,0 +1,117 @@
+// Helper threads of one sampler stream.  A batch's sampling is sequential
+// where the reference's RNG stream and set-iteration order make it so (the
+// draws, the frontier union), but its per-node set builds and the
+// neighbour-list / transpose construction of a hop are independent of the
+// RNG: those run on the helpers, the latter concurrently with the next hop's
+// draws.  Only the owning sampler thread submits work.
+//
+// A job is a handful of coarse tasks, taken under the mutex (so a helper that
+// wakes late finds either the finished job or the next one fully set up).
+// Helpers spin briefly on a generation counter (a batch submits several jobs
+// tens of microseconds apart), then sleep on the condition variable.
+#pragma once
+
+#include <immintrin.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace gs {
+
+class Team {
+  public:
+    explicit Team(int helpers) {
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Team() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            gen_.fetch_add(1);
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    Team(const Team&) = delete;
+    Team& operator=(const Team&) = delete;
+
+    int helpers() const { return static_cast<int>(th_.size()); }
+
+    // Tasks 0..n-1 of fn start on the helpers; the caller continues.  At most
+    // one job is outstanding: wait() before the next start().
+    void start(int n, std::function<void(int)> fn) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = std::move(fn);
+            n_ = n;
+            next_ = 0;
+            done_.store(0, std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+    }
+
+    // The caller takes the job's remaining tasks too, then waits for the rest
+    // (all of them have returned when this does).
+    void wait() {
+        work();
+        while (done_.load(std::memory_order_acquire) < n_) _mm_pause();
+    }
+
+    // start() + wait(): the caller is one more worker.
+    void parallel_for(int n, std::function<void(int)> fn) {
+        start(n, std::move(fn));
+        wait();
+    }
+
+  private:
+    void work() {
+        for (;;) {
+            int i;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (next_ >= n_) return;
+                i = next_++;
+            }
+            fn_(i);  // fn_ is replaced only after every task has returned
+            done_.fetch_add(1, std::memory_order_release);
+        }
+    }
+
+    void loop() {
+        uint64_t seen = gen_.load();
+        for (;;) {
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            for (int spin = 0; g == seen && spin < 20000; ++spin) {
+                _mm_pause();
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_.load() != seen; });
+                g = gen_.load();
+            }
+            seen = g;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (stop_) return;
+            }
+            work();
+        }
+    }
+
+    std::vector<std::thread> th_;
+    std::function<void(int)> fn_;
+    int n_ = 0, next_ = 0;  // guarded by mu_
+    std::atomic<int> done_{0};
+    std::atomic<uint64_t> gen_{0};
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false;
+};
+
+}  // namespace gs

@@ -80,6 +80,7 @@ struct PackSlot {
 
 struct SamplerStream {
     gs_rng* rng = nullptr;
+    gs_team* team = nullptr;       // cfg.helpers threads (owned), or none
     std::vector<int64_t> batches;  // global batch indices, in order
     std::vector<PackSlot> slots;
     std::deque<int> free, ready;  // guarded by mu
@@ -170,9 +171,9 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
         const auto t0 = gs::Clock::now();
         slot.batch = b;
         const int64_t nb = std::min(merge, cfg.n_batches - b * merge);  // reference batches of step b
-        slot.status = gs_sample_pack_run_multi(cfg.graph, s.rng, roots.data() + b * merge * cfg.batch,
-                                               nb * cfg.batch, cfg.batch, fanouts.data(), cfg.n_hops, cfg.flags,
-                                               slot.host, cap, slot.hop_sizes, slot.offsets, &slot.used);
+        slot.status = gs_sample_pack_run_multi_team(cfg.graph, s.rng, roots.data() + b * merge * cfg.batch,
+                                                    nb * cfg.batch, cfg.batch, fanouts.data(), cfg.n_hops, cfg.flags,
+                                                    slot.host, cap, slot.hop_sizes, slot.offsets, &slot.used, s.team);
         if (slot.status != GS_OK) slot.error = gs_last_error();
         slot.sample_s = gs::secs(t0, gs::Clock::now());
         {
@@ -237,6 +238,7 @@ gs_runner::~gs_runner() {
     }
     for (auto& s : streams)
         if (s->th.joinable()) s->th.join();
+    for (auto& s : streams) gs_team_destroy(s->team);
     // Device work that may still read the pinned slots or the device rings:
     // the side stream (pull kernels of consumed and of issued-but-unconsumed
     // lookahead batches), the steps in flight and the comm stream.  Drain all
@@ -318,6 +320,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     GS_REQUIRE(!cfg->embed_out || (cfg->embed_ld >= 1 && !cfg->comm), GS_EINVAL,
                "embed_out needs embed_ld >= 1 and no communicator");
     GS_REQUIRE(cfg->merge <= 1 || cfg->embed_out, GS_EINVAL, "merge > 1 is inference only (embed_out)");
+    GS_REQUIRE(cfg->helpers >= 0 && cfg->helpers <= 64, GS_EINVAL, "helpers out of [0, 64]");
     for (int32_t w = 0; w < cfg->n_streams; ++w) GS_REQUIRE(cfg->rngs[w], GS_EINVAL, "NULL rng");
     std::unique_ptr<gs_runner> r(new gs_runner());
     r->cfg = *cfg;
@@ -361,6 +364,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     for (int32_t w = 0; w < S; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
+        if (cfg->helpers > 0 && gs_team_create(cfg->helpers, &s->team) != GS_OK) fail(GS_EINVAL, gs_last_error());
         for (int64_t b = w; b < r->n_units; b += S) s->batches.push_back(b);
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {

@@ -196,6 +196,21 @@ int gs_sample_pack_run_multi(const gs_graph* g, gs_rng* rng, const int64_t* root
                              int64_t n_roots, int64_t group, const int32_t* fanouts,
                              int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
                              int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+/* Helper threads for one sampling stream (not a reference interface: they
+ * split the RNG-independent parts of a batch — the per-node set builds of
+ * models.py:282-285 and the neighbour / transposed lists a hop's aggregate
+ * needs — while the calling thread keeps the sequential draws and union).
+ * The result is bit-identical to the team-less call.  A team serves one
+ * calling thread at a time. */
+typedef struct gs_team gs_team;
+int gs_team_create(int32_t helpers, gs_team** out);
+void gs_team_destroy(gs_team* team);
+/* gs_sample_pack_run_multi with a team (NULL: none). */
+int gs_sample_pack_run_multi_team(const gs_graph* g, gs_rng* rng, const int64_t* roots,
+                                  int64_t n_roots, int64_t group, const int32_t* fanouts,
+                                  int32_t n_hops, int32_t flags, int32_t* buf, int64_t cap,
+                                  int64_t* hop_sizes, int64_t* offsets, int64_t* used,
+                                  gs_team* team);
 
 /* ------------------------------------------------- unsupervised-loss batch
  * UnsupervisedLoss (models.py:30-186) over the same graph and rng:
@@ -531,6 +546,10 @@ typedef struct {
      * stream under the layer-1 weight-gradient GEMM, then W1 on the main
      * stream.  Same sums either way (the buckets are disjoint ranges). */
     int32_t ar_buckets;
+    /* Helper threads per sampler stream (gs_team): lower per-batch latency
+     * for the same draws — for few streams (the reference-sequence S = 1
+     * mode) or a cold pipeline.  0: none. */
+    int32_t helpers;
 } gs_runner_config;
 
 typedef struct {

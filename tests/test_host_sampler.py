@@ -382,3 +382,42 @@ def test_sample_positions_match_cpython_random_sample(gs):
         mt, pos = r.getstate()
         st = py.getstate()[1]
         assert mt.tolist() == list(st[:624]) and pos == st[624]
+
+
+@pytest.mark.parametrize("helpers", [1, 3])
+@pytest.mark.parametrize("fan,group", [((25, 10), None), ((10, 10, 5), None), ((25, 10), 150)])
+def test_team_pack_equals_single_thread(gs, helpers, fan, group):
+    """Helper threads (gs_team) split a batch's set builds and run each hop's
+    neighbour / transposed lists under the next hop's draws: the pack image,
+    sizes and rng state must equal the team-less call's bit for bit, batch
+    after batch on one stream (3 hops: two materialised hops, so a lists job
+    overlaps the next hop's set builds too)."""
+    L = gs._lib
+    G_, _ = _graph(gs, "rmat")
+    fan = np.array(fan, np.int32)
+    nh = len(fan)
+    team = ctypes.c_void_p()
+    L.check(L.lib().gs_team_create(helpers, ctypes.byref(team)))
+    try:
+        cand = np.nonzero(G_.degrees())[0]
+        rs = np.random.RandomState(5)
+        r1, r2 = gs.RNG(77), gs.RNG(77)
+        for _ in range(6):
+            roots = rs.choice(cand, 300).astype(np.int64)
+            want = _pack_run(gs, G_, r1, roots, fan, group)
+            g = group if group is not None else len(roots)
+            bound = int(L.lib().gs_sample_pack_bound_multi(G_.handle, len(roots), g, fan.ctypes.data, nh))
+            buf = np.full(bound, -7, np.int32)
+            sizes = np.empty(4 * nh, np.int64)
+            offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+            used = ctypes.c_int64()
+            L.check(L.lib().gs_sample_pack_run_multi_team(G_.handle, r2._h, roots.ctypes.data, len(roots), g,
+                                                          fan.ctypes.data, nh, 0, buf.ctypes.data, bound,
+                                                          sizes.ctypes.data, offs.ctypes.data, ctypes.byref(used),
+                                                          team))
+            assert used.value == want[3]
+            assert np.array_equal(buf[:used.value], want[0])
+            assert np.array_equal(sizes.reshape(nh, 4), want[1])
+            assert r1.getstate()[0].tolist() == r2.getstate()[0].tolist() and r1.getstate()[1] == r2.getstate()[1]
+    finally:
+        L.lib().gs_team_destroy(team)

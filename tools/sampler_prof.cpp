@@ -19,6 +19,15 @@ static clk::time_point g_last;
 
 #include "../graphsage-pytorch_amd/csrc/host/sampler.cpp"
 
+namespace gs {
+static void materialise(const Graph& g, Hop& h, bool gcn) {
+    HopScratch sc;
+    build_sets(g, h, sc, nullptr);
+    union_map(h, sc);
+    lists(h, sc, gcn);
+}
+}  // namespace gs
+
 static double us(clk::time_point a, clk::time_point b) {
     return std::chrono::duration<double, std::micro>(b - a).count();
 }
