@@ -101,7 +101,7 @@ Graph* build_graph(const int64_t* src, const int64_t* dst, int64_t n_pairs, int6
     g->n_entries = g->row_ptr[n_nodes];
     g->col.resize(g->n_entries);
     g->slot.resize(g->n_entries);
-    g->log2size = std::move(lg);
+    g->log2size.assign(lg.begin(), lg.end());
     g->max_degree = 0;
     for (int64_t v = 0; v < n_nodes; ++v) g->max_degree = std::max(g->max_degree, deg[v]);
     parallel_for(n_nodes, n_threads, [&](int64_t lo, int64_t hi, int32_t) {

@@ -3,19 +3,55 @@
 // frontier union as the adjacency set itself, models.py:282 `else to_neigh`).
 #pragma once
 
+#include <sys/mman.h>
+
+#include <cstddef>
 #include <cstdint>
+#include <new>
 #include <vector>
 
 namespace gs {
+
+// Allocator for the graph-sized arrays: anonymous mappings advised for
+// transparent huge pages.  The sampler reads these arrays at random (a row
+// per frontier node, hundreds of MB at the synthetic sizes); on 4-KiB pages
+// nearly every such read also misses the TLB, and a software prefetch that
+// misses the TLB is not guaranteed to be serviced.
+template <class T>
+struct HugeAlloc {
+    using value_type = T;
+    HugeAlloc() = default;
+    template <class U>
+    HugeAlloc(const HugeAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < (size_t(2) << 20)) return static_cast<T*>(::operator new(bytes));
+        void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(p, bytes, MADV_HUGEPAGE);
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < (size_t(2) << 20)) ::operator delete(p);
+        else munmap(p, bytes);
+    }
+    template <class U>
+    bool operator==(const HugeAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+template <class T>
+using hvec = std::vector<T, HugeAlloc<T>>;
 
 struct Graph {
     int64_t n_nodes = 0;
     int64_t n_entries = 0;
     int64_t max_degree = 0;
-    std::vector<int64_t> row_ptr;   // [n_nodes + 1]
-    std::vector<int32_t> col;       // [n_entries]
-    std::vector<uint32_t> slot;     // [n_entries] slot in the row's set table
-    std::vector<uint8_t> log2size;  // [n_nodes]  table size = 1 << log2size
+    hvec<int64_t> row_ptr;          // [n_nodes + 1]
+    hvec<int32_t> col;              // [n_entries]
+    hvec<uint32_t> slot;            // [n_entries] slot in the row's set table
+    hvec<uint8_t> log2size;         // [n_nodes]  table size = 1 << log2size
     std::vector<uint8_t> dirty;     // [n_nodes] or empty: row set holds dummy entries
     int64_t degree(int64_t v) const { return row_ptr[v + 1] - row_ptr[v]; }
 };

@@ -251,6 +251,25 @@ struct PySet {
         add(key);
     }
 
+    // copy_into(*this, o) for o = a set whose table is given verbatim (an
+    // adjacency row's own layout: keys in slot order, `slots` their slots in
+    // a table of m0 + 1), without building o: the copy's table is sized from
+    // o.used alone, then takes o's slots verbatim when the sizes agree and o
+    // has no dummies (set_merge's slot-copy path), else insert_clean in o's
+    // slot order.
+    void assign_copy_of_layout(size_t m0, const int32_t* keys, const uint32_t* slots, int64_t n, bool dummies) {
+        size_t newsize = MINSIZE;
+        if (n * 5 >= static_cast<int64_t>(MINSIZE - 1) * 3)
+            while (newsize <= static_cast<size_t>(2 * n)) newsize <<= 1;
+        alloc_table(newsize);
+        fill = used = n;
+        if (mask == m0 && !dummies) {
+            for (int64_t t = 0; t < n; ++t) tab[slots[t]] = keys[t];
+        } else {
+            for (int64_t t = 0; t < n; ++t) insert_clean(tab, mask, keys[t]);
+        }
+    }
+
     // A set whose table is given verbatim (an adjacency row's own layout).
     void assign_layout(size_t m, const int32_t* keys, const uint32_t* slots, int64_t n) {
         alloc_table(m + 1);

@@ -57,7 +57,7 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
     deg.resize(n);
     int64_t total = 0;
     const int64_t* rp = g.row_ptr.data();
-    constexpr int64_t kAhead = 16;  // frontier ids are known: prefetch their row_ptr
+    constexpr int64_t kAhead = 48;  // frontier ids are known: prefetch their row_ptr (DRAM misses)
     for (int64_t r = 0; r < std::min(n, kAhead); ++r) __builtin_prefetch(rp + h.dst_ids[r]);
     for (int64_t r = 0; r < n; ++r) {
         if (r + kAhead < n) __builtin_prefetch(rp + h.dst_ids[r + kAhead]);
@@ -114,6 +114,8 @@ static int64_t count_empty(const Graph& g, const Hop& h, bool gcn) {
 struct HopScratch {
     PySet first, u;                   // samp_neighs[0]; the union
     std::vector<int32_t> slot_local;  // union slot -> rank in iteration order
+    std::vector<std::vector<int64_t>> part_items;  // per helper part of build_sets
+    std::vector<int32_t> tmp, cur;    // lists()
 };
 
 static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::vector<int64_t>& items,
@@ -153,12 +155,13 @@ static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::
             // set(random.sample(adj, k)) : adds in result order
             s.reset();
             for (int64_t q = 0; q < cnt; ++q) s.add(g.col[rs + h.pos[h.pos_ptr[r] + q]]);
+            copy_into(t, s);  // samp_neigh | set([v])  (:285)
         } else {
-            // the adjacency set object itself, with its own table layout
-            s.assign_layout((size_t(1) << g.log2size[v]) - 1, g.col.data() + rs, g.slot.data() + rs, d);
-            if (!g.dirty.empty() && g.dirty[v]) s.fill = s.used + 1;  // dummies: no slot-copy fast path
+            // the adjacency set object itself (its own table layout; dummies
+            // disable the slot-copy fast path), copied by the `|`
+            t.assign_copy_of_layout((size_t(1) << g.log2size[v]) - 1, g.col.data() + rs, g.slot.data() + rs, d,
+                                    !g.dirty.empty() && g.dirty[v]);
         }
-        copy_into(t, s);  // samp_neigh | set([v])  (:285)
         t.merge_single(v);
         if (r == 0 && first) *first = t;
         const size_t before = items.size();
@@ -215,7 +218,7 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
     h.nbr_ptr.assign(n + 1, 0);
     h.nbr.clear();
     h.self_local.resize(n);
-    std::vector<int32_t> tmp;
+    std::vector<int32_t>& tmp = sc.tmp;
     const int64_t n_items = static_cast<int64_t>(h.set_items.size());
     for (int64_t r = 0; r < n; ++r) {
         const int64_t v = h.dst_ids[r];
@@ -245,7 +248,8 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
     for (int32_t c : h.self_local) ++h.tptr[c + 1];
     for (int64_t c = 0; c < ns; ++c) h.tptr[c + 1] += h.tptr[c];
     h.tidx.resize(h.tptr[ns]);
-    std::vector<int32_t> cur(h.tptr.begin(), h.tptr.end() - 1);
+    std::vector<int32_t>& cur = sc.cur;
+    cur.assign(h.tptr.begin(), h.tptr.end() - 1);
     for (int64_t r = 0; r < n; ++r) {
         h.tidx[cur[h.self_local[r]]++] = static_cast<int32_t>(-(r + 1));
         for (int32_t e = h.nbr_ptr[r]; e < h.nbr_ptr[r + 1]; ++e)
@@ -267,17 +271,20 @@ static void build_sets(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
         h.set_items.reserve(h.pos.size() + n);
         sets_range(g, h, 0, n, h.set_items, h.set_ptr.data() + 1, &sc.first);
     } else {
-        std::vector<std::vector<int64_t>> part_items(parts);
+        auto& part_items = sc.part_items;
+        if (static_cast<int>(part_items.size()) < parts) part_items.resize(parts);
+        for (int p = 0; p < parts; ++p) part_items[p].clear();
         team->parallel_for(parts, [&](int p) {
             const int64_t a = n * p / parts, b = n * (p + 1) / parts;
             part_items[p].reserve(static_cast<size_t>(h.pos_ptr[b] - h.pos_ptr[a] + (b - a)));
             sets_range(g, h, a, b, part_items[p], h.set_ptr.data() + 1, p == 0 ? &sc.first : nullptr);
         });
         size_t total = 0;
-        for (auto& v : part_items) total += v.size();
+        for (int p = 0; p < parts; ++p) total += part_items[p].size();
         h.set_items.resize(total);
         size_t at = 0;
-        for (auto& v : part_items) {
+        for (int p = 0; p < parts; ++p) {
+            const auto& v = part_items[p];
             std::memcpy(h.set_items.data() + at, v.data(), v.size() * sizeof(int64_t));
             at += v.size();
         }
@@ -286,37 +293,54 @@ static void build_sets(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     GS_PHASE(1);
 }
 
-static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
-                          const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team = nullptr) {
+// Sampling state reused from batch to batch by one thread (the runner's
+// sampler streams): every vector keeps its capacity, so a batch allocates
+// nothing once the first few have run.
+struct SampleCtx {
+    Sample s;
+    HopScratch scratch[2];  // hop j's lists may still run on a helper while hop j+1 builds its sets
+    std::vector<int64_t> frontier;
+};
+
+static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
+                            const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team) {
     GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
     GS_REQUIRE(n_roots >= 1 && roots, GS_EINVAL, "empty nodes_batch");
     GS_REQUIRE(g.n_entries < (int64_t(1) << 31), GS_ERANGE, "graph has >= 2^31 CSR entries (int32 pack entries)");
     for (int64_t i = 0; i < n_roots; ++i)
         GS_REQUIRE(roots[i] >= 0 && roots[i] < g.n_nodes, GS_ERANGE, "node id out of range");
     if (team && team->helpers() == 0) team = nullptr;
-    std::unique_ptr<Sample> s(new Sample());
+    Sample* s = &c.s;
     s->n_hops = n_hops;
     s->flags = flags;
+    for (int32_t j = 0; j < GS_MAX_HOPS; ++j) s->hops[j].materialised = false;
     const bool gcn = flags & GS_SAMPLE_GCN;
-    std::vector<int64_t> frontier(roots, roots + n_roots);
-    HopScratch scratch[2];  // hop j's lists may still run on a helper while hop j+1 builds its sets
-    bool pending = false;   // a lists job is outstanding on the team
+    std::vector<int64_t>& frontier = c.frontier;
+    frontier.assign(roots, roots + n_roots);
+    bool pending = false;  // a lists job is outstanding on the team
+    struct Join {           // never leave a helper job behind (an exception unwinds through here)
+        Team* t;
+        bool& p;
+        ~Join() {
+            if (p) t->wait();
+        }
+    } join{team, pending};
     for (int32_t j = 0; j < n_hops; ++j) {
         Hop& h = s->hops[j];
         h.k = fanouts ? fanouts[j] : 10;
-        h.dst_ids = std::move(frontier);
+        h.dst_ids.swap(frontier);
         draw_positions(g, rng, h);
         h.n_empty = count_empty(g, h, gcn);
         const bool last = (j == n_hops - 1);
         if (!last || (flags & GS_SAMPLE_FULL)) {
-            HopScratch& sc = scratch[j & 1];
+            HopScratch& sc = c.scratch[j & 1];
             if (pending) {  // the team is needed for the sets below
                 team->wait();
                 pending = false;
             }
             build_sets(g, h, sc, team);
             union_map(h, sc);
-            frontier = h.src_ids;
+            frontier.assign(h.src_ids.begin(), h.src_ids.end());
             if (team) {  // lists + transpose on a helper, under the next hop's draws
                 team->start(1, [&h, &sc, gcn](int) { lists(h, sc, gcn); });
                 pending = true;
@@ -325,8 +349,13 @@ static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, in
             }
         }
     }
-    if (pending) team->wait();
-    return s.release();
+}
+
+static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
+                          const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team = nullptr) {
+    std::unique_ptr<SampleCtx> c(new SampleCtx());
+    run_sample_into(*c, g, rng, roots, n_roots, fanouts, n_hops, flags, team);
+    return new Sample(std::move(c->s));
 }
 
 }  // namespace gs
@@ -541,10 +570,13 @@ static int pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64
     const int64_t bound = gs_sample_pack_bound(gp, n_roots, fanouts, n_hops);
     GS_REQUIRE(bound >= 0 && cap >= bound, GS_EINVAL, "buffer below gs_sample_pack_bound");
     const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
-    std::unique_ptr<Sample> s(gs::run_sample(g, rng->mt, roots, n_roots, fanouts, n_hops, flags, team));
+    thread_local std::unique_ptr<gs::SampleCtx> ctx;  // reused batch to batch by this thread
+    if (!ctx) ctx.reset(new gs::SampleCtx());
+    gs::run_sample_into(*ctx, g, rng->mt, roots, n_roots, fanouts, n_hops, flags, team);
+    const Sample* s = &ctx->s;
     gs_pack_layout L;
     layout_of(*s, &L);
-    gs_sample_pack(reinterpret_cast<const gs_sample*>(s.get()), buf, cap);
+    gs_sample_pack(reinterpret_cast<const gs_sample*>(s), buf, cap);
     for (int32_t j = 0; j < n_hops; ++j) {
         const Hop& h = s->hops[j];
         hop_sizes[4 * j] = static_cast<int64_t>(h.dst_ids.size());
