@@ -128,7 +128,7 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     A.dSelf = self ? a.dIn : nullptr;
     A.dA = self ? a.dIn + a.fin : a.dIn;
     A.dx_gx = static_cast<int>((a.n + 15) / 16);
-    A.dx_nb = A.dx_gx * static_cast<int>((K + 63) / 64);
+    A.dx_nb = a.din_ready ? 0 : A.dx_gx * static_cast<int>((K + 63) / 64);
     int cls_nb = 0;
     if (cls) {
         A.B = static_cast<int>(cls->B);

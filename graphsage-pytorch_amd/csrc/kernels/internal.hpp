@@ -64,6 +64,7 @@ struct LayerBwd {
     const int32_t* argmax;                // MAX routing, [n][H]
     const float* Hprev;                   // previous layer's output (relu mask), [n_src][H]
     float* dH;                            // [n_src][H] gradient of the previous layer's output (masked)
+    bool din_ready = false;               // dIn already written (top.hip): launch A skips its dIn role
 };
 
 struct ClsReduce {
@@ -81,5 +82,14 @@ int cls_reduce_grid(int64_t C, int64_t D);
 // Returns the number of norm partials written to `part` (0 when the weight
 // gradient fits one slab and was written directly: no partials).
 int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t st);
+
+// top.hip: a 2-layer model's layer 2 forward (aggregate + linear + relu), the
+// loss head and the layer's dIn in one launch (one block per 4 roots).
+// Returns the number of classifier partial slabs written (the loss head's).
+bool top_supported(int64_t H, int64_t C, bool gcn);
+int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
+                const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
+                const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
+                hipStream_t st);
 
 }  // namespace gs

@@ -45,6 +45,7 @@ struct gs_trainer {
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
     bool fuse_bwd = true;
+    bool use_top = true;  // GS_NO_TOP=1: layer 2 + loss head as separate launches (A/B)
     float* norm_part = nullptr;
     int pstride = 0;
     int npart[2] = {0, 0};
@@ -242,7 +243,11 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         g_launch_events = {};  // an alternative kernel that does not time leaves it armed
         timed_done(T, 1, armed);
     }
-    for (int l = 2; l <= L; ++l) {
+    // a 2-layer training step runs layer 2, the loss head and layer 2's dIn in
+    // one launch (top.hip) inside the fused backward below
+    const bool top = !embed_out && roots && T.fuse_bwd && T.use_top && L == 2 &&
+                     top_supported(H, c.n_classes, c.gcn != 0);
+    for (int l = 2; l <= L && !top; ++l) {
         const int j = L - l + 1;
         if (T.fused2 && c.agg == GS_AGG_MEAN) {  // MAX needs the argmax the fused kernel does not keep
             ok(gs_sage1_fwd(GS_AGG_MEAN, GS_F32, h[l - 2], H, H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
@@ -291,9 +296,18 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             fusable = fusable && layer_bwd_fusable(a);
             lb.push_back(a);
         }
+        GS_REQUIRE(!top || fusable, GS_EINVAL, "top launch needs the fused backward");
         if (fusable) {
-            const int cls_rows = cls_rows_launch(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off,
-                                                 c.labels, roots, 1, demb, cls_ws, st);
+            int cls_rows;
+            if (top) {
+                cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
+                                       fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
+                                       roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st);
+                lb[0].din_ready = true;
+            } else {
+                cls_rows = cls_rows_launch(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
+                                           roots, 1, demb, cls_ws, st);
+            }
             const ClsReduce cr{B, H, c.n_classes, cls_rows, cls_ws, G + T.cls_w_off, G + T.cls_b_off, loss,
                                T.norm_part + T.pstride};
             int np = 0;
@@ -398,6 +412,7 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
         }
     }
     T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
+    T->use_top = std::getenv("GS_NO_TOP") == nullptr;
     T->fused1 = gs_sage1_fwd_supported(static_cast<gs_dtype>(cfg->feat_dtype), cfg->feat_dim, cfg->hidden,
                                        cfg->gcn) != 0 &&
                 cfg->feat_ld % (cfg->feat_dtype == GS_F32 ? 4 : 8) == 0 && gs::aligned16(cfg->X) &&

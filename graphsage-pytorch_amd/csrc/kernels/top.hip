@@ -1,0 +1,413 @@
+// The top SageLayer and the loss head of a training step in one launch.
+//
+// In a 2-layer GraphSage the top layer's rows are the batch's roots, and
+// everything from its aggregate to the classifier's gradient is row-local:
+//   agg_r  = mean / max of h1 over r's sampled neighbours   (models.py:291-330)
+//   E_r    = relu([h1[self_r] | agg_r] · W2ᵀ)               (models.py:216-219)
+//   logits, log_softmax, NLL, dlogits = (softmax - onehot)/B  (models.py:8-27,
+//            utils.py:159-164), dZ_r = (dlogits · Wc) ⊙ (E_r > 0)
+//   dIn_r  = dZ_r · W2 = [dSelf_r | dA_r]                   (autograd of :219)
+// One block of 4 waves owns 4 rows (the loss head's row block, so its
+// classifier partial slab is the one cls_rows_kernel writes) and runs the
+// four stages back to back with the rows in LDS: the three launches this
+// replaces (layer-2 aggregate, layer-2 linear, loss head) and the dIn role of
+// the layer backward each paid a kernel boundary and a global round trip of
+// their inputs.
+//
+// Numerics are those of the launches it replaces, bit for bit: the aggregate
+// adds neighbours in list order as agg_fwd_kernel does; every product chain
+// is the fmaf chain the f32 MFMA kernels form (within each 16-wide k block
+// the order 0,4,8,12, 1,5,9,13, ... of four v_mfma_f32_16x16x4_f32 over the
+// four k-lane groups; blocks ascending); the head is cls_rows_kernel's code.
+// The two GEMMs run on the matrix cores with the linear kernels' own tiles
+// and operand order (the 4 rows padded to a 16-row tile), from a copy of W2 in
+// LDS that an LDS-DMA fills under the gather.  Measured alternatives: W2
+// streamed from L2 through registers took the kernel to 31 us (latency-bound
+// at ~25 GB/s per CU); VALU fmaf chains from LDS spent 3.4 + 3.7 us in the
+// two GEMMs, bound by the LDS broadcast reads of the rows.
+#include "cls_dev.hpp"
+#include "internal.hpp"
+#include "linear_dev.hpp"
+
+#ifndef GS_TOP_STAMP  // stage stamps for tools/lab/top_lab.hip; no-ops in the library
+#define GS_TOP_STAMP(i)
+#endif
+
+namespace gs {
+
+constexpr int kTopRows = 4;
+constexpr int kTopThreads = 256;
+constexpr int kTopH = 128;
+constexpr int kTopK = 2 * kTopH;
+constexpr int kTopMaxC = 32;
+
+struct TopArgs {
+    int B, C;
+    const float* Hprev;  // h1 [n1][H]
+    const int* ptr;      // hop-1 neighbour lists (GS_PK_NBR_PTR / NBR), union-local, ascending
+    const int* nbr;
+    const int* self;     // GS_PK_SELF
+    const float* W;      // W2 [H][2H]
+    const float* Wc;     // [C][H]
+    const float* bc;
+    const int* labels;
+    const int* roots;
+    float* agg;          // [B][H]
+    int* argmax;         // [B][H] (MAX)
+    float* E;            // h2 [B][H]
+    float* dZ;           // [B][H], masked by relu'(E)
+    float* dIn;          // [B][2H]
+    float* slab;         // classifier partials, one [C][H+1] + 1 slab per block
+};
+
+// k offset of step i (0..15) inside a 16-wide block: the MFMA kernels' order.
+__device__ __forceinline__ constexpr int mfma_k(int i) { return 4 * (i & 3) + (i >> 2); }
+
+template <int OP>
+__global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
+    constexpr int H = kTopH, K = kTopK, D = kTopH;
+    // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, Wc, dlogits, loss
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sW2 = smem;                                        // [H][K]
+    float (*sX)[K] = reinterpret_cast<float (*)[K]>(sW2 + H * K);
+    float (*sE)[H] = reinterpret_cast<float (*)[H]>(sX[kTopRows]);
+    float (*sZ)[H] = reinterpret_cast<float (*)[H]>(sE[kTopRows]);
+    float* sW = &sZ[kTopRows][0];                             // [C][D + 1]
+    float* sdl = sW + a.C * (D + 1);                          // [rows][C]
+    float* sloss = sdl + kTopRows * a.C;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int C = a.C;
+    const int r0 = blockIdx.x * kTopRows;
+    const int nr = min(kTopRows, a.B - r0);
+
+    GS_TOP_STAMP(0);
+    // ---- W2 -> LDS by DMA (no registers), issued before anything else so its
+    // latency hides under the gather.  Row c is one wave instruction of 64
+    // 16-byte quads; quad q of the row lands in slot q ^ (c & 15), which keeps
+    // both later access patterns free of bank conflicts: a column read by
+    // lanes = rows (ds_read_b128, 16 rows per quarter-wave on 16 distinct
+    // slots) and a row read by lanes = k.
+    // Waves 2 and 3 issue it: the gather below runs on waves 0 and 1, whose
+    // dependent load rounds would otherwise queue behind the DMA (vmcnt
+    // retires in order).
+    if (w >= 2)
+        for (int c = w - 2; c < H; c += 2)
+            __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
+                                             0, 0);
+
+    // ---- stage 0: loss-head operands (independent of the rest, issued first)
+    const int cl = lane & 15, dq = lane >> 4;
+    const int wr_ = min(w, nr - 1);
+    const int root = a.roots[r0 + wr_];
+    const float b_lane = a.bc[min(cl, C - 1)];
+    {
+        const int nW4 = C * D / 4;
+        for (int q = tid; q < nW4; q += kTopThreads) {
+            const float4 v = reinterpret_cast<const float4*>(a.Wc)[q];
+            const int t = 4 * q;
+            float* d = sW + t + t / D;  // row pitch D + 1 (D % 4 == 0: a quad stays in one row)
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    }
+    const int y_w = a.labels[root];
+
+    // ---- stage 1: the aggregate (agg_fwd_kernel<OP, float, 4, 32, explicit>)
+    // and the self row, one 32-lane group per row
+    {
+        constexpr int G = 32, NR = 32;
+        const int g = tid / G, gl = tid % G;
+        if (g < nr) {
+            const int r = r0 + g;
+            const int f0 = gl * 4;
+            const int srow = a.self[r];
+            const float4 xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+            const int beg = a.ptr[r], end = a.ptr[r + 1];
+            float acc[4];
+            int am[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
+                am[v] = -1;
+            }
+            int cnt = 0;
+            for (int base = beg; base < end; base += G) {
+                const int m = min(G, end - base);
+                const bool mine = gl < m;
+                const int e = a.nbr[mine ? base + gl : base];
+                const int my = mine ? e : -1;
+                for (int j = 0; j < m; j += NR) {
+                    int rows[NR];
+                    bool ok[NR];
+#pragma unroll
+                    for (int u = 0; u < NR; ++u) {
+                        rows[u] = __shfl(my, j + u < m ? j + u : j, G);
+                        ok[u] = (j + u < m) && rows[u] >= 0;
+                    }
+                    const int fallback = rows[0] >= 0 ? rows[0] : 0;
+                    float x[NR][4];
+#pragma unroll
+                    for (int u = 0; u < NR; ++u)
+                        RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * H + f0,
+                                              x[u]);
+#pragma unroll
+                    for (int u = 0; u < NR; ++u) {
+                        cnt += ok[u];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            if (OP == GS_AGG_MEAN) {
+                                acc[v] += ok[u] ? x[u][v] : 0.f;
+                            } else {
+                                const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
+                                acc[v] = take ? x[u][v] : acc[v];
+                                am[v] = take ? rows[u] : am[v];
+                            }
+                        }
+                    }
+                }
+            }
+            if (OP == GS_AGG_MEAN) {
+                const float inv = 1.0f / static_cast<float>(cnt);  // cnt == 0 -> NaN row, as 0/0 in :313
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[v] *= inv;
+            }
+            *reinterpret_cast<float4*>(&sX[g][f0]) = xs;
+            const float4 av = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            *reinterpret_cast<float4*>(&sX[g][H + f0]) = av;
+            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * H + f0) = av;
+            if (OP == GS_AGG_MAX)
+                *reinterpret_cast<int4*>(a.argmax + static_cast<int64_t>(r) * H + f0) = make_int4(am[0], am[1], am[2],
+                                                                                                   am[3]);
+        }
+    }
+    GS_TOP_STAMP(1);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's W2 DMA has landed (vmcnt); the barrier covers the others'
+    __syncthreads();
+    GS_TOP_STAMP(2);
+
+    // ---- stage 2: E = relu([self | agg] · W2ᵀ) on the matrix cores, as the
+    // linear kernel's tiles: wave w owns columns 32w .. 32w+31 (two 16x16
+    // tiles); the 4 rows ride in a 16-row A tile (rows >= nr are zero).
+    {
+        const int r = lane & 15, kq = lane >> 4;
+        const bool rowok = r < nr;
+        const uint4* xr = reinterpret_cast<const uint4*>(sX[min(r, nr - 1)]);
+        const uint4* wq = reinterpret_cast<const uint4*>(sW2);
+        const int c0 = 32 * w + r, c1 = c0 + 16;
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        // operands one k block ahead; the two tiles' MFMAs alternate so each
+        // accumulator's dependent latency (40 cycles) hides under the other's issue
+        auto ld = [&](int k0, uint4& av, uint4& b0, uint4& b1) {
+            const int q = (k0 >> 2) + kq;  // this lane's 4-k slot
+            av = xr[q];
+            b0 = wq[c0 * (K / 4) + (q ^ (c0 & 15))];
+            b1 = wq[c1 * (K / 4) + (q ^ (c1 & 15))];
+        };
+        uint4 an, bn0, bn1;
+        ld(0, an, bn0, bn1);
+#pragma unroll 2
+        for (int k0 = 0; k0 < K; k0 += 16) {
+            uint4 av = an;
+            const uint4 b0 = bn0, b1 = bn1;
+            ld(min(k0 + 16, K - 16), an, bn0, bn1);
+            if (!rowok) av = make_uint4(0, 0, 0, 0);
+            const float a4[4] = {__uint_as_float(av.x), __uint_as_float(av.y), __uint_as_float(av.z),
+                                 __uint_as_float(av.w)};
+            const float w0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
+                                 __uint_as_float(b0.w)};
+            const float w1[4] = {__uint_as_float(b1.x), __uint_as_float(b1.y), __uint_as_float(b1.z),
+                                 __uint_as_float(b1.w)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // = mfma_slot's order on each tile
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w0[j], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w1[j], acc1, 0, 0, 0);
+            }
+        }
+        if (kq == 0) {  // lanes 0..15 hold rows 0..3 of their column
+#pragma unroll
+            for (int j = 0; j < kTopRows; ++j) {
+                if (j >= nr) break;
+                const float v0 = (!(acc0[j] > 0.f) && acc0[j] == acc0[j]) ? 0.f : acc0[j];  // relu (NaN kept)
+                const float v1 = (!(acc1[j] > 0.f) && acc1[j] == acc1[j]) ? 0.f : acc1[j];
+                sE[j][c0] = v0;
+                sE[j][c1] = v1;
+                a.E[static_cast<int64_t>(r0 + j) * H + c0] = v0;
+                a.E[static_cast<int64_t>(r0 + j) * H + c1] = v1;
+            }
+        }
+    }
+    __syncthreads();
+    GS_TOP_STAMP(3);
+
+    // ---- stage 3: the loss head, one wave per row (cls_rows_kernel's code)
+    const float invB = 1.0f / static_cast<float>(a.B);
+    const int wp = D + 1;
+    if (w < nr) {
+        const int ii = w;
+        const float* e = sE[ii];
+        const int y = y_w;
+        const int DQ = (D + 3) / 4;
+        const int d_lo = min(D, dq * DQ), d_hi = min(D, d_lo + DQ);
+        float mx = -INFINITY;
+        for (int c0 = 0; c0 < C; c0 += 16) {
+            const int c = c0 + cl;
+            const float* wr = sW + static_cast<int64_t>(min(c, C - 1)) * wp;
+            float pz = 0.f;
+            for (int d = d_lo; d < d_hi; ++d) pz = fmaf(e[d], wr[d], pz);
+            pz += __shfl_xor(pz, 16, 64);
+            pz += __shfl_xor(pz, 32, 64);
+            const float z = pz + (c0 == 0 ? b_lane : a.bc[min(c, C - 1)]);
+            if (dq == 0 && c < C) sdl[ii * C + c] = z;
+            if (c < C) mx = fmaxf(mx, z);
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        __builtin_amdgcn_wave_barrier();
+        float se = 0.f;
+        for (int c = lane; c < C; c += 64) se += expf(sdl[ii * C + c] - mx);
+        const float lse = logf(wave_sum(se));
+        for (int c = lane; c < C; c += 64) {
+            const float lp = sdl[ii * C + c] - mx - lse;
+            if (c == y) sloss[ii] = -lp;
+            sdl[ii * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int d = lane; d < D; d += 64) {
+            float s = 0.f;
+            for (int c = 0; c < C; ++c) s = fmaf(sdl[ii * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
+            if (!(e[d] > 0.f)) s = 0.f;
+            sZ[ii][d] = s;
+            a.dZ[static_cast<int64_t>(r0 + ii) * D + d] = s;
+        }
+    }
+    __syncthreads();
+    GS_TOP_STAMP(4);
+
+    // ---- stage 4: this block's classifier partial slab (cls_rows_kernel's)
+    {
+        const int per = C * (D + 1);
+        float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
+        int c = tid / (D + 1), d = tid - c * (D + 1);  // advanced by kTopThreads per step, no divides
+        constexpr int dc = kTopThreads / (D + 1), dd = kTopThreads % (D + 1);
+        for (int t = tid; t < per; t += kTopThreads) {
+            float s = 0.f;
+#pragma unroll
+            for (int ii = 0; ii < kTopRows; ++ii)
+                if (ii < nr) s = fmaf(sdl[ii * C + c], d < D ? sE[ii][d] : 1.f, s);
+            out[t] = s;
+            c += dc;
+            d += dd;
+            if (d > D) {
+                d -= D + 1;
+                ++c;
+            }
+        }
+        if (tid < 64) {
+            float s = 0.f;
+            for (int ii = tid; ii < nr; ii += 64) s += sloss[ii];
+            s = wave_sum(s);
+            if (tid == 0) out[per] = s;
+        }
+    }
+
+    GS_TOP_STAMP(5);
+    // ---- stage 5: dIn = dZ · W2 on the matrix cores (linear_dx_body's
+    // tiles): wave w owns input columns 64w .. 64w+63 (four 16-wide tiles)
+    {
+        const int r = lane & 15, kq = lane >> 4;
+        const bool rowok = r < nr;
+        const float* zr = sZ[min(r, nr - 1)];
+        f32x4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // operands one h block ahead; the four tiles' MFMAs alternate (j-major)
+        auto ld = [&](int g, float4& z, float (&wv)[4][4]) {
+            const int hb = 16 * g + 4 * kq;
+            z = *reinterpret_cast<const float4*>(zr + hb);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int kc = 64 * w + 16 * t + r;  // this lane's input column
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int h = hb + j;
+                    wv[t][j] = sW2[h * K + 4 * ((kc >> 2) ^ (h & 15)) + (kc & 3)];
+                }
+            }
+        };
+        float4 zn;
+        float wn[4][4];
+        ld(0, zn, wn);
+#pragma unroll 2
+        for (int g = 0; g < H / 16; ++g) {
+            float4 z = zn;
+            float wv[4][4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) wv[t][j] = wn[t][j];
+            ld(min(g + 1, H / 16 - 1), zn, wn);
+            if (!rowok) z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float z4[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(z4[j], wv[t][j], acc[t], 0, 0, 0);
+        }
+        if (kq == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int j = 0; j < kTopRows; ++j)
+                    if (j < nr) a.dIn[static_cast<int64_t>(r0 + j) * K + 64 * w + 16 * t + r] = acc[t][j];
+        }
+    }
+    GS_TOP_STAMP(6);
+}
+
+static size_t top_smem_bytes(int64_t C) {
+    return sizeof(float) * (static_cast<size_t>(kTopH) * kTopK + kTopRows * (kTopK + 2 * kTopH) + C * (kTopH + 1) +
+                            kTopRows * C + kTopRows);
+}
+
+// The kernel keeps W2 in LDS (~146 KiB at 16 classes): raise the launch limit
+// once; where the runtime refuses, the caller keeps the separate launches.
+static bool top_lds_ready(int64_t C) {
+    static int ok_bytes = -1;
+    const size_t need = top_smem_bytes(C);
+    if (ok_bytes < 0) {
+        const size_t want = top_smem_bytes(kTopMaxC);
+        const bool a = hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) == hipSuccess;
+        const bool b = hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) == hipSuccess;
+        (void)hipGetLastError();
+        ok_bytes = (a && b) ? static_cast<int>(want) : 0;
+    }
+    return need <= static_cast<size_t>(ok_bytes);
+}
+
+bool top_supported(int64_t H, int64_t C, bool gcn) {
+    return H == kTopH && C >= 1 && C <= kTopMaxC && !gcn && top_lds_ready(C);
+}
+
+int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
+                const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
+                const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
+                hipStream_t st) {
+    GS_REQUIRE(B >= 1 && B < (int64_t(1) << 30) && C >= 1 && C <= kTopMaxC, GS_EINVAL, "top: bad sizes");
+    GS_REQUIRE(aligned16(Hprev) && aligned16(W) && aligned16(Wc) && aligned16(aggo) && aligned16(E) && aligned16(dZ) &&
+                   aligned16(dIn) && (agg == GS_AGG_MEAN || (argmax && aligned16(argmax))),
+               GS_EINVAL, "top: unaligned operand");
+    TopArgs a{static_cast<int>(B), static_cast<int>(C), Hprev, ptr, nbr, self, W, Wc, bc, labels, roots,
+              aggo, argmax, E, dZ, dIn, slab};
+    const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
+    const size_t smem = top_smem_bytes(C);
+    if (agg == GS_AGG_MEAN) sage_top_kernel<GS_AGG_MEAN><<<grid, kTopThreads, smem, st>>>(a);
+    else sage_top_kernel<GS_AGG_MAX><<<grid, kTopThreads, smem, st>>>(a);
+    check_launch("sage_top");
+    return static_cast<int>(grid.x);
+}
+
+}  // namespace gs

@@ -323,6 +323,46 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name,
     assert done >= 1
 
 
+@pytest.mark.parametrize("agg,name,B", [("MEAN", "pubmed", 512), ("MAX", "pubmed", 512), ("MEAN", "rmat", 97),
+                                         ("MAX", "pubmed", 1536)])
+def test_top_launch_matches_separate_launches(gs, monkeypatch, agg, name, B):
+    """The one-launch top layer + loss head (kernels/top.hip: layer-2
+    aggregate, linear, relu, NLL head, dZ and dIn on the VALU) against the
+    separate launches it replaces (agg_fwd, the MFMA linear, cls_rows, the
+    MFMA dIn role): it repeats their product chains in the f32 MFMA order, so
+    loss, every gradient and the updated parameters are bitwise equal,
+    including a batch that leaves its last 4-row block partial."""
+    graph, g, n = _graph(gs, name)
+    X = torch.from_numpy(uniform_features(7, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    fan = [25, 10]
+    a = train.NativeTrainer(graph, X, labels, 16, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
+    monkeypatch.setenv("GS_NO_TOP", "1")
+    b = train.NativeTrainer(graph, X, labels, 16, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
+    monkeypatch.delenv("GS_NO_TOP")
+    rng = gs.RNG(5)
+    done = 0
+    for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 17):
+        if done == 3:
+            break
+        s = gs.sample(graph, rng, roots, fan)
+        if agg == "MAX" and any(s.n_empty(j) for j in range(1, 3)):
+            continue
+        ds = models.DeviceSample(s, DEV)
+        r = torch.from_numpy(roots.astype(np.int32)).to(DEV)
+        la = a.forward_backward(ds, r).clone()
+        lb = b.forward_backward(ds, r).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb)
+        assert torch.equal(a.p.grads, b.p.grads)
+        a.apply_update()
+        b.apply_update()
+        torch.cuda.synchronize()
+        assert torch.equal(a.p.params, b.p.params)
+        done += 1
+    assert done >= 1
+
+
 def test_rccl_communicator_single_rank(gs):
     """The native RCCL communicator (gs_comm_*, torch's librccl) on one rank:
     unique id, init, an in-place sum all-reduce (identity at world 1)."""
