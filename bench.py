@@ -443,12 +443,21 @@ def main():
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
                          "each for the issuing thread, the HIP runtime and RCCL's proxy)")
-    ap.add_argument("--sampler-helpers", type=int, default=0,
-                    help="helper threads per sampler stream (same draws; lower per-batch latency)")
+    ap.add_argument("--sampler-helpers", type=int, default=None,
+                    help="helper threads per sampler stream (same draws; lower per-batch latency); "
+                         "default 1 with >= 8 host cores per GPU")
     args = ap.parse_args()
+    per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    if args.sampler_helpers is None:
+        # one helper per stream where the cores allow: a batch then samples in
+        # ~0.35-0.42 ms instead of ~0.5-0.57 (profiles/r02_ab_sampler_layouts.txt),
+        # which is what a cold pipeline waits for before its first step
+        args.sampler_helpers = 1 if per_gpu >= 8 and (args.sampler_streams or 2) > 1 else 0
     if args.sampler_streams is None:
-        per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-        args.sampler_streams = max(1, min(12, per_gpu - 3))
+        if args.sampler_helpers:  # two threads per stream, two cores for the issuing thread and the runtime
+            args.sampler_streams = max(1, min(8, (per_gpu - 2) // (1 + args.sampler_helpers)))
+        else:
+            args.sampler_streams = max(1, min(12, per_gpu - 3))
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:

@@ -67,7 +67,10 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
     if (r >= n_dst) return;
     const int node = gcn ? dst_ids[r] : 0;
     const int* rid = ids + static_cast<int64_t>(r) * k;
-    constexpr int NR = VEC > 4 ? kRows / 2 : kRows;
+    // 16 rows in flight for 16-byte fp32 and bf16 vectors alike, so a fanout
+    // <= 16 neighbourhood is one memory round (8 for bf16 split a 10-slot
+    // neighbourhood into two dependent rounds: 0.28 of HBM peak, round 1)
+    constexpr int NR = kRows;
     const int nf = (F + G * VEC - 1) / (G * VEC);
     for (int fi = 0; fi < nf; ++fi) {
         const int f0 = fi * G * VEC + gl * VEC;

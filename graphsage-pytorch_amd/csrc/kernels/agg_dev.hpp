@@ -15,7 +15,7 @@ constexpr int kBlock = 256;
 #ifndef GS_AGG_BWD_BATCH
 #define GS_AGG_BWD_BATCH 1
 #endif
-constexpr int kRows = 16;  // neighbour rows in flight per lane group (8 for 8-element bf16 vectors)
+constexpr int kRows = 16;  // neighbour rows in flight per lane group
 
 // Lanes [lo, lo + G) of the wave's ballot.
 template <int G>
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
     }
     // explicit lists (layers >= 2: fanout up to 25-30 per destination) keep
     // twice the rows in flight, so a whole neighbourhood is one memory round
-    constexpr int NR = (VEC > 4 ? kRows / 2 : kRows) * (EXPAND ? 1 : 2);
+    constexpr int NR = kRows * (EXPAND ? 1 : 2);
     const bool want_am = (OP == GS_AGG_MAX) && (argmax != nullptr);
     const int nf = (F + G * VEC - 1) / (G * VEC);
     for (int fi = 0; fi < nf; ++fi) {

@@ -58,6 +58,25 @@ static bool slab_split_on(int64_t len) {
 }
 static int64_t slab_split_blocks(int64_t len) { return (len / 4 + 63) / 64; }
 
+// 64 KiB of dynamic LDS per block for the W-resident forward: raise the
+// launch limit once (the default dynamic limit is lower); refused -> the
+// 32-row tiles.
+static bool wres_lds_ready(int K) {
+    static int ok = -1;
+    if (ok < 0) {
+        const int want = kWresCols * 512 * static_cast<int>(sizeof(float));
+        bool good = true;
+        const void* ks[4] = {reinterpret_cast<const void*>(linear_fwd_wres_kernel<true, true>),
+                             reinterpret_cast<const void*>(linear_fwd_wres_kernel<true, false>),
+                             reinterpret_cast<const void*>(linear_fwd_wres_kernel<false, true>),
+                             reinterpret_cast<const void*>(linear_fwd_wres_kernel<false, false>)};
+        for (const void* k : ks)
+            good = good && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, want) == hipSuccess;
+        (void)hipGetLastError();
+        ok = good ? 1 : 0;
+    }
+    return ok == 1 && K <= 512;
+}
 }  // namespace gs
 
 extern "C" {
@@ -80,13 +99,14 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                        aligned16(A) && aligned16(Wd);
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
-    static const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
+    // read per call (tests switch it between launches): wres | wide32 | wide | sk | chunked
+    const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
     // fp32 default: 32-row W-in-LDS tiles (bitwise the chunked kernel's sums:
     // same MFMA operands in the same order).  In-step at rmat2m the step ran
     // 80.2-80.7 us against 82.3-82.4 us with the 16-row chunked kernel, which
     // GS_LIN_FWD=chunked (and bf16) still select; "wide" = 64-row tiles.
-    static const bool wide_on = fwd_mode == "wide";
-    static const bool wide32_on = fwd_mode != "wide" && fwd_mode != "sk" && fwd_mode != "chunked";
+    const bool wide_on = fwd_mode == "wide";
+    const bool wide32_on = fwd_mode != "wide" && fwd_mode != "sk" && fwd_mode != "chunked";
     if (fwd_mode == "sk" && dt == GS_F32 && vload) {
         const dim3 gs2(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 31) / 32));
         const float* xs = static_cast<const float*>(Xs);
@@ -100,6 +120,30 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
             else launch_k(linear_fwd_sk_kernel<false, false>, gs2, dim3(kThreads), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo);
         }
         check_launch("gs_sage_linear_fwd(sk)");
+        return GS_OK;
+    }
+    // GS_LIN_FWD=wres: the W-resident kernel (a 32-column W slice per block
+    // in LDS, filled once by LDS-DMA).  Bitwise the same sums, but slower at
+    // the layer-1 shape (microbenchmark 14.5 against 10 us): each wave's
+    // 16-row tile runs its whole K chain (2 x 128 MFMAs), and 1.1k such waves
+    // on 1024 SIMDs leave a second round on some of them.  Opt-in.
+    const bool wres_on = fwd_mode == "wres";
+    if (wres_on && dt == GS_F32 && vload && K % 256 == 0 && K <= 512 && H % kWresCols == 0 &&
+        wres_lds_ready(K)) {
+        const int tiles = static_cast<int>((n + 15) / 16);
+        const int tx = (tiles + 3) / 4;  // row-tile groups (4 tiles per block)
+        const int nsl = hh / kWresCols;
+        const int gx = ((tx + 7) / 8) * 8 * nsl;  // remap padding: whole groups of 8
+        const size_t smem = static_cast<size_t>(kWresCols) * K * sizeof(float);
+        const float* xs = static_cast<const float*>(Xs);
+        const float* a = static_cast<const float*>(A);
+        const float* w = static_cast<const float*>(Wd);
+#define GS_LFWDR(SELF, RELU_) \
+        launch_k(linear_fwd_wres_kernel<SELF, RELU_>, dim3(gx), dim3(kThreads), static_cast<uint32_t>(smem), st, nn, ff, hh, K, tx, xs, ldxs, sidx, a, lda, w, out, ldo)
+        if (self) { if (relu) GS_LFWDR(true, true); else GS_LFWDR(true, false); }
+        else { if (relu) GS_LFWDR(false, true); else GS_LFWDR(false, false); }
+#undef GS_LFWDR
+        check_launch("gs_sage_linear_fwd(wres)");
         return GS_OK;
     }
     if ((wide_on || wide32_on) && dt == GS_F32 && vload) {

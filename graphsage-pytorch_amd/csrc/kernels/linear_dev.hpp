@@ -335,6 +335,108 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
 // atomics) and wave 0 applies relu and stores.  Many small blocks (n/16 ·
 // H/32) keep ~4 waves per SIMD to overlap those rounds.
 constexpr int kSkChunks = 2;  // chunks of 64 per wave issued at once (K <= 512 in one round)
+// W-resident forward (fp32, K a multiple of 256 up to 512: a row of the slice
+// is whole 64-quad DMA instructions): each block keeps one 32-column slice of W
+// ([32][K] fp32, <= 64 KiB) in LDS for its whole life, filled by
+// LDS-DMA (global_load_lds_dwordx4) with quad-swizzled rows (quad q of row c
+// in slot q ^ (c & 15): the per-MFMA b128 reads of 16 rows hit 16 distinct
+// slots), and each of its 4 waves runs one 16-row tile against both 16-column
+// halves of the slice (two interleaved accumulators), streaming its A rows
+// [X[sidx] | A] from global memory kWresAhead 64-k chunks ahead in registers.
+// No workgroup barrier after the fill: the K loop reads only its own
+// registers and the (read-only) W slice.  MFMA operands and order are the
+// chunked / wide kernels' (mfma_slot over slots 4g + kq, chunks ascending), so
+// the output is bitwise theirs.  Grid: (ceil(tiles / 4), H / 32); two blocks
+// fit a CU.  Blocks y (slices) of one x share an XCD (x-major dispatch of a
+// 2-D grid keeps them 1 apart in linear order; see the launcher's remap).
+constexpr int kWresAhead = 4;
+constexpr int kWresCols = 32;
+
+template <bool HAS_SELF, bool RELU>
+__global__ __launch_bounds__(kThreads) void linear_fwd_wres_kernel(
+    int n, int F, int H, int K, int n_tiles_x, const float* __restrict__ Xs, int64_t ldxs,
+    const int* __restrict__ sidx, const float* __restrict__ A, int64_t lda, const float* __restrict__ W,
+    float* __restrict__ out, int64_t ldo) {
+    extern __shared__ uint4 sWq[];  // [kWresCols][K / 4] quads, swizzled
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // linear block id -> (row-tile group, slice): the H/32 slices of one
+    // group are 8 apart in dispatch order, i.e. on one XCD (round-robin)
+    const int nsl = H / kWresCols;
+    const int b = blockIdx.x;
+    const int sl = (b >> 3) % nsl;
+    const int tg = (b & 7) + 8 * (b / (8 * nsl));
+    const int KQ = K >> 2;
+    const int r = lane & 15, kq = lane >> 4;
+    const int tile = tg * 4 + wave;
+    if (tg >= n_tiles_x) return;  // padding block of the remap (block-uniform: no barrier skipped)
+    const int row = min(tile * 16 + r, n - 1);
+    const int srow_i = HAS_SELF ? (sidx ? sidx[row] : row) : 0;
+    // fill the slice: row c is KQ / 64 wave instructions of 64 quads
+    const int per_row = KQ >> 6;
+    for (int i = wave; i < kWresCols * per_row; i += kThreads / 64) {
+        const int c = i / per_row, part = i - c * per_row;
+        const int qsrc = (part * 64 + lane) ^ (c & 15);
+        const int gc = min(sl * kWresCols + c, H - 1);
+        __builtin_amdgcn_global_load_lds(W + static_cast<int64_t>(gc) * K + 4 * qsrc, sWq + c * KQ + part * 64, 16,
+                                         0, 0);
+    }
+    const float* arow = A + static_cast<int64_t>(row) * lda;
+    const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(srow_i) * ldxs : nullptr;
+    const int nC = K >> 6;
+    uint4 ar[kWresAhead][4];
+    auto load = [&](int c, uint4 (&dst)[4]) {
+        const int kn = min(c, nC - 1) * 64;  // past the end: re-read the last chunk (unused)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) dst[g] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + 4 * (4 * g + kq));
+    };
+#pragma unroll
+    for (int u = 0; u < kWresAhead; ++u) load(u, ar[u]);
+    __builtin_amdgcn_s_waitcnt(0);  // the fill (and the first chunks) landed for this wave
+    __syncthreads();                // ... and for every wave
+    if (tile * 16 >= n) return;
+    const int c0 = r, c1 = 16 + r;  // this lane's W rows (output columns) within the slice
+    const uint4* w0 = sWq + c0 * KQ;
+    const uint4* w1 = sWq + c1 * KQ;
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int c = 0; c < nC; c += kWresAhead) {
+#pragma unroll
+        for (int u = 0; u < kWresAhead; ++u) {
+            const int cc = c + u;
+            if (cc >= nC) break;
+            uint4 av[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) av[g] = ar[u][g];
+            load(cc + kWresAhead, ar[u]);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q = cc * 16 + 4 * g + kq;
+                const uint4 b0 = w0[q ^ (c0 & 15)];
+                const uint4 b1 = w1[q ^ (c1 & 15)];
+                const float a4[4] = {__uint_as_float(av[g].x), __uint_as_float(av[g].y), __uint_as_float(av[g].z),
+                                     __uint_as_float(av[g].w)};
+                const float x0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
+                                     __uint_as_float(b0.w)};
+                const float x1[4] = {__uint_as_float(b1.x), __uint_as_float(b1.y), __uint_as_float(b1.z),
+                                     __uint_as_float(b1.w)};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {  // = mfma_slot's order on each accumulator
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], x0[j], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], x1[j], acc1, 0, 0, 0);
+                }
+            }
+        }
+    }
+    const int col0 = sl * kWresCols + r, col1 = col0 + 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int orow = tile * 16 + 4 * kq + j;
+        if (orow >= n) continue;
+        const float v0 = acc0[j], v1 = acc1[j];
+        if (col0 < H) out[static_cast<int64_t>(orow) * ldo + col0] = (RELU && !(v0 > 0.f) && v0 == v0) ? 0.f : v0;
+        if (col1 < H) out[static_cast<int64_t>(orow) * ldo + col1] = (RELU && !(v1 > 0.f) && v1 == v1) ? 0.f : v1;
+    }
+}
+
 template <bool HAS_SELF, bool RELU>
 __global__ __launch_bounds__(kThreads) void linear_fwd_sk_kernel(
     int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,

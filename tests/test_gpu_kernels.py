@@ -129,6 +129,32 @@ def test_sage_linear_fwd_bwd(n, F, H, gcn, dtype):
     torch.testing.assert_close(dIn, (dZ.double() @ W.double()).float(), atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("n,F,H", [(1, 256, 128), (37, 128, 128), (4321, 256, 128), (4400, 256, 128),
+                                   (513, 128, 64), (100, 64, 32), (2048, 256, 256)])
+@pytest.mark.parametrize("gcn", [False, True])
+def test_wres_forward_bitwise_equals_tiled_kernels(monkeypatch, n, F, H, gcn):
+    """The W-resident fp32 forward (linear_fwd_wres_kernel: a 32-column W
+    slice per block in LDS by LDS-DMA) feeds the same MFMA operands in the
+    same order as the 32-row and 16-row tiled kernels: outputs bitwise
+    equal, partial last tiles and the self-row gather included."""
+    torch.manual_seed(n + F + H)
+    n_src = n + 29
+    Xs = torch.randn(n_src, F, device=DEV)
+    A = torch.randn(n, F, device=DEV)
+    sidx = torch.randint(0, n_src, (n,), dtype=torch.int32, device=DEV)
+    K = F if gcn else 2 * F
+    W = torch.randn(H, K, device=DEV) * 0.05
+    outs = {}
+    for mode in ("wres", "wide32", "chunked"):
+        monkeypatch.setenv("GS_LIN_FWD", mode)
+        out = torch.full((n, H), float("nan"), device=DEV)
+        ops.sage_linear_fwd(A, W, out, Xs=None if gcn else Xs, sidx=None if gcn else sidx)
+        torch.cuda.synchronize()
+        outs[mode] = out
+    assert torch.equal(outs["wres"], outs["wide32"])
+    assert torch.equal(outs["wres"], outs["chunked"])
+
+
 @pytest.mark.parametrize("agg", ["MEAN", "MAX"])
 @pytest.mark.parametrize("F", [128, 36, 5])
 def test_agg_bwd_matches_autograd(agg, F):
