@@ -510,7 +510,8 @@ def main():
     if world > 1:
         dist.barrier()
     runner.stats(reset=True)
-    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 1 << dominant, args.steps))
+    no_timer = bool(os.environ.get("GS_BENCH_NO_TIMER"))  # A/B of the in-window timer's cost
+    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 0 if no_timer else 1 << dominant, args.steps))
     thr0 = cgroup_throttle()
     sampled0, consumed0 = runner.progress()
     t0 = time.perf_counter()
@@ -523,16 +524,16 @@ def main():
     sampled1, consumed1 = runner.progress()
     thr1 = cgroup_throttle()
     st = runner.stats()
-    times = {dominant: kernel_times_ms(trainer, args.steps, dominant)}
+    times = {} if no_timer else {dominant: kernel_times_ms(trainer, args.steps, dominant)}
     # calibration steps after the measured ones time the other sites (an
     # event-bound launch costs the stream a little: never inside the timed steps)
     runner.release(total_steps)
-    others = sum(1 << site for site in SITES if site != dominant)
+    others = sum(1 << site for site in SITES if site != dominant or no_timer)
     gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, others, calib))
     runner.run(calib)
     torch.cuda.synchronize()
     for site in SITES:
-        if site != dominant:
+        if site not in times:
             times[site] = kernel_times_ms(trainer, calib, site)
     loss = float(trainer.loss.item())
     # steady state: the remaining batches, with the sampler threads free to run
