@@ -2,6 +2,6 @@
 reference's src/models.py GraphSage / SageLayer / Classification)."""
 from . import _lib  # noqa: F401
 from .graph import CSRGraph, rmat_pairs  # noqa: F401
-from .sampler import RNG, Sample, pyset_union_of_lists, sample  # noqa: F401
+from .sampler import RNG, DeviceSampler, Sample, pyset_union_of_lists, sample  # noqa: F401
 
 __version__ = "0.1.0"

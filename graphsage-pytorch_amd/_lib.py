@@ -145,6 +145,14 @@ _SIGS = {
     "gs_runner_destroy": (None, [_vp]),
     "gs_runner_release": (_i32, [_vp, _i64]),
     "gs_runner_progress": (_i32, [_vp, _p(_i64), _p(_i64)]),
+    "gs_dsampler_create": (_i32, [_vp, _vp, _i32, _i64, _i32, _p(_vp)]),
+    "gs_dsampler_destroy": (None, [_vp]),
+    "gs_dsampler_set_rng": (_i32, [_vp, _vp, _i64, _vp]),
+    "gs_dsampler_get_rng": (_i32, [_vp, _vp, _p(_i64), _vp]),
+    "gs_dsampler_words": (_i32, [_vp, _i64, _vp, _vp]),
+    "gs_dsampler_pack_bound": (_i64, [_vp, _i64]),
+    "gs_dsampler_run": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "gs_dsampler_result": (_i32, [_vp, _vp, _vp, _p(_i64)]),
 }
 
 

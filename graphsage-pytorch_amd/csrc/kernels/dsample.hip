@@ -1,0 +1,873 @@
+// Device-resident neighbour sampler: GraphSage.forward's hop
+// loop over _get_unique_neighs_list (models.py:246-251, :277-289) run on the
+// GPU, bit-exact with the host sampler (host/sampler.cpp) and therefore with
+// the reference's CPython `random` stream and set iteration order.  It writes
+// the same device pack the host sampler writes (gs_sample_pack_run), straight
+// into device memory, so nothing downstream changes.
+//
+// Pieces (each one documented at its kernel):
+//   word stream   MT19937 (CPython's genrand_uint32, Modules/_randommodule.c)
+//                 regenerated on the device into a ring of tempered words,
+//                 indexed by absolute stream position.  x[A] = x[A-227] ^
+//                 twist(x[A-624], x[A-623]) is the whole recurrence, so one
+//                 wave produces 227 words per dependent step.
+//   draws         random.sample (Lib/random.py 3.10, both branches) for every
+//                 frontier node of a hop, in frontier order.  The only
+//                 sequential quantity is the stream position, and it is the
+//                 hop's draw count plus the rejections so far (j).  Frontier
+//                 nodes are cut into blocks; for every block and every entry
+//                 j in a window around the expected rejection count the exit
+//                 j' is computed in parallel (one lane per entry), the block
+//                 maps are composed group by group in LDS, one lane chains the
+//                 group maps, and every block then re-walks from its true
+//                 entry and emits its positions.  A true entry outside its
+//                 window is detected and reported (never silently wrong).
+//   sets/union    (hops before the last) samp_neigh | {node} per frontier node
+//                 and list(set.union(*samp_neighs)) — see dsample_union.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../host/graph.hpp"
+#include "../host/mt19937.hpp"
+#include "dsample.hpp"
+
+namespace gs {
+namespace ds {
+
+// ------------------------------------------------------------ word stream
+
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// One wave extends the stream from c->gen_end until it covers `need`
+// (absolute word index, exclusive): stages of 227 words, each word
+// x[A] = x[A-227] ^ ((y >> 1) ^ (y & 1 ? MATRIX_A : 0)), y = (x[A-624] & UPPER)
+// | (x[A-623] & LOWER) — CPython's twist loop written on absolute indices (its
+// three index ranges are this one recurrence).  The last 1024 raw words live
+// in LDS; every word goes to both rings (raw for the state, tempered for the
+// draws).
+__global__ __launch_bounds__(64) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr, Ctl* c,
+                                                    int64_t need_fixed, int need_hop) {
+    __shared__ uint32_t L[1024];
+    const int lane = threadIdx.x;
+    int64_t g = c->gen_end;
+    const int64_t need = need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
+    if (g >= need) return;
+    for (int i = lane; i < 624; i += 64) {
+        const int64_t A = g - 624 + i;
+        L[A & 1023] = xr[A & kRingMask];
+    }
+    __syncthreads();
+    while (g < need) {
+        uint32_t nx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = lane + 64 * q;
+            const int64_t A = g + i;
+            const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023], m = L[(A - 227) & 1023];
+            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+            nx[q] = m ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = lane + 64 * q;
+            if (i < 227) {
+                const int64_t A = g + i;
+                L[A & 1023] = nx[q];
+                xr[A & kRingMask] = nx[q];
+                wr[A & kRingMask] = temper(nx[q]);
+            }
+        }
+        __syncthreads();
+        g += 227;
+    }
+    if (lane == 0) c->gen_end = g;
+}
+
+// Seed the stream from random.setstate's (mt[624], pos): block 0 = mt, the
+// next word is at absolute index pos.
+__global__ void mt_seed_kernel(const uint32_t* __restrict__ mt, int64_t pos, uint32_t* __restrict__ xr,
+                               uint32_t* __restrict__ wr, Ctl* c) {
+    for (int i = threadIdx.x; i < 624; i += blockDim.x) {
+        xr[i] = mt[i];
+        wr[i] = temper(mt[i]);
+    }
+    if (threadIdx.x == 0) {
+        c->gen_end = 624;
+        c->pos_cur = pos;
+        c->status = 0;
+    }
+}
+
+// --------------------------------------------------------------- draws
+
+// Expected rejections (and their variance) before the k accepted draws of
+// one frontier node: geometric with acceptance m / 2^bitlen per word (pool
+// branch, m = d - i), (d - i) / 2^bitlen(d) in the selected-set branch.
+__device__ __forceinline__ void rejection_moments(uint32_t d, int k, int setsize, float& mean, float& var) {
+    mean = 0.f;
+    var = 0.f;
+    if (k <= 0 || d < static_cast<uint32_t>(k)) return;
+    const bool pool = d <= static_cast<uint32_t>(setsize);
+    for (int i = 0; i < k; ++i) {
+        const uint32_t m = d - i;
+        const uint32_t span = pool ? m : d;
+        const float full = ldexpf(1.f, 32 - __clz(span));
+        const float p = static_cast<float>(m) / full;
+        mean += (1.f - p) / p;
+        var += (1.f - p) / (p * p);
+    }
+}
+
+__device__ __forceinline__ int warp_incl_scan(int v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ float warp_incl_scan(float v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive scan over a 1024-thread block of one value per thread; returns
+// the thread's exclusive prefix, *total the block total.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh /* >= 17 */, T* total) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const T inc = warp_incl_scan(v);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = T(0);
+        for (int q = 0; q < 16; ++q) {
+            const T t = sh[q];
+            sh[q] = run;
+            run += t;
+        }
+        sh[16] = run;
+    }
+    __syncthreads();
+    const T out = sh[w] + inc - v;
+    *total = sh[16];
+    __syncthreads();
+    return out;
+}
+
+__device__ __forceinline__ int32_t al4(int32_t n) { return (n + 3) & ~3; }
+
+// Per hop, one 1024-thread block: degrees of the frontier, the scans of the
+// sampled counts (pos_ptr) and draw counts, the rejection-count windows of
+// the blocks, the word need of the hop, and (last hop) the pack offsets.
+__global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, HopBufs hb, int hop, int k, int setsize,
+                                                         int R, int last, int n_roots, int gcn) {
+    __shared__ int shi[17];
+    __shared__ float shf[17];
+    __shared__ int s_maxw, s_maxlo;
+    HopCtl& h = c->hop[hop];
+    const int n = hop == 0 ? n_roots : c->hop[hop - 1].n_src;
+    if (threadIdx.x == 0) {
+        s_maxw = 0;
+        s_maxlo = 0;
+    }
+    const int per = (n + 1023) / 1024;
+    const int r0 = min(n, static_cast<int>(threadIdx.x) * per), r1 = min(n, r0 + per);
+    int cnt_sum = 0, draw_sum = 0;
+    float mean_sum = 0.f, var_sum = 0.f;
+    for (int r = r0; r < r1; ++r) {
+        const int32_t v = hb.dst[r];
+        const int64_t d64 = g.row_ptr[v + 1] - g.row_ptr[v];
+        const int32_t d = static_cast<int32_t>(d64);
+        hb.deg[r] = d;
+        const bool sampled = k > 0 && d >= k;
+        cnt_sum += sampled ? k : d;
+        draw_sum += sampled ? k : 0;
+        float mu, va;
+        rejection_moments(static_cast<uint32_t>(d), k, setsize, mu, va);
+        hb.mv[r] = make_float2(mu, va);
+        mean_sum += mu;
+        var_sum += va;
+    }
+    int cnt_tot, draw_tot;
+    float mean_tot, var_tot;
+    int cnt_pre = block_excl_scan(cnt_sum, shi, &cnt_tot);
+    int draw_pre = block_excl_scan(draw_sum, shi, &draw_tot);
+    float mean_pre = block_excl_scan(mean_sum, shf, &mean_tot);
+    float var_pre = block_excl_scan(var_sum, shf, &var_tot);
+    for (int r = r0; r < r1; ++r) {
+        const int32_t d = hb.deg[r];
+        const bool sampled = k > 0 && d >= k;
+        hb.pos_ptr[r] = cnt_pre;
+        if (r % R == 0) {
+            const int b = r / R;
+            const float sd = sqrtf(var_pre);
+            const int lo = max(0, static_cast<int>(floorf(mean_pre - 6.f * sd)) - 16);
+            const int hi = static_cast<int>(ceilf(mean_pre + 6.f * sd)) + 16;
+            hb.blo[b] = lo;
+            hb.dbase[b] = draw_pre;
+            atomicMax(&s_maxw, hi - lo);
+            atomicMax(&s_maxlo, lo);
+        }
+        cnt_pre += sampled ? k : d;
+        draw_pre += sampled ? k : 0;
+        const float2 mv = hb.mv[r];
+        mean_pre += mv.x;
+        var_pre += mv.y;
+    }
+    if (threadIdx.x == 0) {
+        hb.pos_ptr[n] = cnt_tot;
+        const int nb = (n + R - 1) / R;
+        hb.dbase[nb] = draw_tot;
+        hb.blo[nb] = 0;  // never an entry window (the last group's exit is absolute)
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int W = 64;
+        while (W < s_maxw) W <<= 1;
+        if (W > kWMax) c->status |= kStWindow;
+        W = min(W, kWMax);
+        const int nb = (n + R - 1) / R;
+        const int G = max(1, kComposeEntries / W);
+        h.n_dst = n;
+        h.n_pos = cnt_tot;
+        h.n_draws = draw_tot;
+        h.n_blocks = nb;
+        h.W = W;
+        h.G = G;
+        h.n_groups = (nb + G - 1) / G;
+        h.P0 = c->pos_cur;
+        h.n_empty = 0;
+        h.need_end = h.P0 + draw_tot + s_maxlo + W + 3 * R * max(k, 1) + 256;
+        if (last) {
+            int at = c->total;
+            h.off[GS_PK_POS_PTR] = at;
+            at += al4(n + 1);
+            h.off[GS_PK_POS] = at;
+            at += al4(cnt_tot);
+            h.off[GS_PK_DST_IDS] = at;
+            at += al4(n);
+            c->total = at;
+        }
+    }
+}
+
+// Consumption of one block's draws from word index idx (into the block's LDS
+// words); returns the index after the block, or -1 past the loaded words.
+template <int KMAX>
+__device__ __forceinline__ int walk_block(const uint32_t* __restrict__ w, int nvalid, int idx,
+                                          const int32_t* __restrict__ bdeg, int nr, int k, int setsize) {
+    for (int q = 0; q < nr; ++q) {
+        const uint32_t d = static_cast<uint32_t>(bdeg[q]);
+        if (k <= 0 || d < static_cast<uint32_t>(k)) continue;
+        if (d <= static_cast<uint32_t>(setsize)) {
+            for (int i = 0; i < k; ++i) {
+                const uint32_t m = d - i;
+                const int sh = __clz(m);
+                for (;;) {
+                    if (idx >= nvalid) return -1;
+                    const uint32_t v = w[idx++] >> sh;
+                    if (v < m) break;
+                }
+            }
+        } else {
+            const int sh = __clz(d);
+            uint32_t sel[KMAX];
+            int cnt = 0;
+            while (cnt < k) {
+                if (idx >= nvalid) return -1;
+                const uint32_t v = w[idx++] >> sh;
+                bool fresh = v < d;
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == v);
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t)
+                    if (t == cnt) sel[t] = v;
+                cnt += fresh;
+            }
+        }
+    }
+    return idx;
+}
+
+// Words of block b's window into LDS: relative positions dbase + lo .. , as
+// many as are generated (the count is returned).
+__device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const Ctl* c, int64_t A0, int nw,
+                                          uint32_t* __restrict__ dst) {
+    const int64_t gen = c->gen_end;
+    const int nvalid = static_cast<int>(max<int64_t>(0, min<int64_t>(nw, gen - A0)));
+    for (int i = threadIdx.x; i < nvalid; i += blockDim.x) dst[i] = wr[(A0 + i) & kRingMask];
+    return nvalid;
+}
+
+// Block maps: E[b][e] = rejections inside block b when it is entered with
+// lo_b + e rejections so far (0xFFFF: ran past the loaded words).
+template <int KMAX>
+__global__ __launch_bounds__(256) void draw_tables_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, int hop,
+                                                          int k, int setsize, int R) {
+    extern __shared__ uint32_t smem[];
+    const HopCtl& h = c->hop[hop];
+    const int b = blockIdx.x;
+    if (b >= h.n_blocks) return;
+    const int W = h.W;
+    const int r0 = b * R, nr = min(R, h.n_dst - r0);
+    int32_t* bdeg = reinterpret_cast<int32_t*>(smem);
+    uint32_t* w = smem + R;
+    for (int q = threadIdx.x; q < nr; q += blockDim.x) bdeg[q] = hb.deg[r0 + q];
+    const int lo = hb.blo[b];
+    const int nw = W + 3 * R * max(k, 1) + 64;
+    const int nvalid = load_words(wr, c, h.P0 + hb.dbase[b] + lo, nw, w);
+    __syncthreads();
+    uint16_t* E = hb.tab + static_cast<int64_t>(b) * W;
+    for (int e = threadIdx.x; e < W; e += blockDim.x) {
+        const int end = walk_block<KMAX>(w, nvalid, e, bdeg, nr, k, setsize);
+        const int dr = end - e - (hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b]);
+        E[e] = (end < 0 || dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
+    }
+}
+
+// Group maps: for every entry of the group's first block, the entries of each
+// of its blocks (path) and the group's exit, relative to the next group's
+// window (uint16; 0xFFFF outside it), or absolute for the last group.  The
+// group's block maps are staged in LDS.
+__global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, int hop) {
+    extern __shared__ uint16_t tabs[];
+    __shared__ int los[kComposeEntries / 64 + 1];
+    const HopCtl& h = c->hop[hop];
+    const int gi = blockIdx.x;
+    if (gi >= h.n_groups) return;
+    const int W = h.W, G = h.G;
+    const int b0 = gi * G, nbk = min(G, h.n_blocks - b0);
+    const bool last_group = gi == h.n_groups - 1;
+    for (int i = threadIdx.x; i < nbk * W; i += blockDim.x) tabs[i] = hb.tab[static_cast<int64_t>(b0) * W + i];
+    for (int i = threadIdx.x; i <= nbk; i += blockDim.x) los[i] = hb.blo[b0 + i];  // blo[nb] exists (setup)
+    __syncthreads();
+    int32_t* path = hb.path + static_cast<int64_t>(b0) * W;
+    for (int e = threadIdx.x; e < W; e += blockDim.x) {
+        int j = los[0] + e;
+        for (int q = 0; q < nbk; ++q) {
+            path[q * W + e] = j;
+            if (j < 0) continue;
+            const int t = j - los[q];
+            if (t < 0 || t >= W) {
+                j = -1;
+                continue;
+            }
+            const uint16_t d = tabs[q * W + t];
+            j = d == 0xFFFF ? -1 : j + d;
+        }
+        if (last_group) {
+            hb.gexit_last[e] = j;
+        } else {
+            const int t = j - los[nbk];
+            hb.gexit[static_cast<int64_t>(gi) * W + e] = (j < 0 || t < 0 || t >= W) ? 0xFFFF : static_cast<uint16_t>(t);
+        }
+    }
+}
+
+// One block: chain the group maps from j = 0 (staged in LDS when they fit),
+// then every block's true entry (a lookup in its group's path) and the hop's
+// end position.
+__global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, int hop) {
+    extern __shared__ uint16_t gx[];
+    __shared__ int gentry[kMaxGroups + 1];
+    HopCtl& h = c->hop[hop];
+    const int W = h.W, G = h.G, ng = h.n_groups;
+    if (ng > kMaxGroups) {
+        if (threadIdx.x == 0) c->status |= kStWindow;
+        return;
+    }
+    const int64_t n16 = static_cast<int64_t>(ng - 1) * W;
+    const bool staged = n16 <= kChainEntries;
+    if (staged)
+        for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) gx[i] = hb.gexit[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int j = 0;
+        for (int gi = 0; gi < ng; ++gi) {
+            gentry[gi] = j;
+            const int lo = hb.blo[gi * G];
+            const int t = j - lo;
+            if (j < 0 || t < 0 || t >= W) {
+                j = -1;
+                for (int q = gi + 1; q < ng; ++q) gentry[q] = -1;
+                break;
+            }
+            if (gi == ng - 1) {
+                j = hb.gexit_last[t];
+            } else {
+                const uint16_t d = staged ? gx[static_cast<int64_t>(gi) * W + t] : hb.gexit[static_cast<int64_t>(gi) * W + t];
+                j = d == 0xFFFF ? -1 : hb.blo[(gi + 1) * G] + d;
+            }
+        }
+        gentry[ng] = j;
+        if (j < 0) c->status |= kStWindow;
+        h.j_end = j;
+        c->pos_cur = h.P0 + h.n_draws + max(j, 0);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < h.n_blocks; b += blockDim.x) {
+        const int gi = b / G;
+        const int jg = gentry[gi];
+        const int t = jg - hb.blo[gi * G];
+        hb.entry[b] = (jg < 0 || t < 0 || t >= W) ? -1 : hb.path[static_cast<int64_t>(b) * W + t];
+    }
+}
+
+// Every block from its true entry: lane 0 walks the block once to find each
+// frontier node's first word, then one lane per node replays its draws and
+// emits positions in random.sample's result order (the pool branch through a
+// sparse map of the swapped pool slots), as absolute CSR entries.
+template <int KMAX>
+__global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
+                                                       DevGraph g, int hop, int k, int setsize, int R, int last,
+                                                       int gcn, int32_t* __restrict__ pack) {
+    extern __shared__ uint32_t smem[];
+    HopCtl& h = c->hop[hop];
+    const int b = blockIdx.x;
+    if (b >= h.n_blocks) return;
+    const int r0 = b * R, nr = min(R, h.n_dst - r0);
+    int32_t* bdeg = reinterpret_cast<int32_t*>(smem);
+    int32_t* rstart = bdeg + R;
+    uint32_t* w = reinterpret_cast<uint32_t*>(rstart + R);
+    const int j = hb.entry[b];
+    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
+    const int nw = 4 * ndr + 64;
+    for (int q = threadIdx.x; q < nr; q += 64) bdeg[q] = hb.deg[r0 + q];
+    const int nvalid = j < 0 ? 0 : load_words(wr, c, h.P0 + hb.dbase[b] + j, nw, w);
+    __syncthreads();
+    if (j < 0) return;  // reported by the chain
+    if (threadIdx.x == 0) {
+        int idx = 0;
+        for (int q = 0; q < nr; ++q) {
+            rstart[q] = idx;
+            idx = idx < 0 ? -1 : walk_block<KMAX>(w, nvalid, idx, bdeg + q, 1, k, setsize);
+        }
+        if (idx < 0) atomicOr(&c->status, kStWords);
+    }
+    __syncthreads();
+    int32_t* ent = last ? pack + h.off[GS_PK_POS] : hb.ent;
+    for (int q = threadIdx.x; q < nr; q += 64) {
+        const int r = r0 + q;
+        const int32_t v = hb.dst[r];
+        const uint32_t d = static_cast<uint32_t>(bdeg[q]);
+        const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
+        int32_t* out = ent + hb.pos_ptr[r];
+        int idx = rstart[q];
+        const bool sampled = k > 0 && d >= static_cast<uint32_t>(k);
+        int cnt = sampled ? k : static_cast<int>(d);
+        if (idx < 0) {
+            for (int t = 0; t < cnt; ++t) out[t] = base;
+        } else if (!sampled) {
+            for (int t = 0; t < cnt; ++t) out[t] = base + t;
+        } else if (d <= static_cast<uint32_t>(setsize)) {
+            uint32_t mk[KMAX], mv[KMAX];
+            int nm = 0;
+            for (int i = 0; i < k; ++i) {
+                const uint32_t m = d - i;
+                const int sh = __clz(m);
+                uint32_t x = 0;
+                for (;;) {
+                    x = idx < nvalid ? w[idx] >> sh : 0u;
+                    ++idx;
+                    if (x < m || idx >= nvalid) break;
+                }
+                uint32_t val = x, lastv = m - 1;
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t) {
+                    if (t < nm && mk[t] == x) val = mv[t];
+                    if (t < nm && mk[t] == m - 1) lastv = mv[t];
+                }
+                bool found = false;
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t)
+                    if (t < nm && mk[t] == x) {
+                        mv[t] = lastv;
+                        found = true;
+                    }
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t)
+                    if (!found && t == nm) {
+                        mk[t] = x;
+                        mv[t] = lastv;
+                    }
+                nm += !found;
+                out[i] = base + static_cast<int32_t>(val);
+            }
+        } else {
+            const int sh = __clz(d);
+            uint32_t sel[KMAX];
+            int n_sel = 0;
+            while (n_sel < k && idx < nvalid) {
+                const uint32_t x = w[idx++] >> sh;
+                bool fresh = x < d;
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t) fresh &= !(t < n_sel && sel[t] == x);
+#pragma unroll
+                for (int t = 0; t < KMAX; ++t)
+                    if (t == n_sel) sel[t] = x;
+                if (fresh) out[n_sel] = base + static_cast<int32_t>(x);
+                n_sel += fresh;
+            }
+        }
+        // empty neighbourhood after the self rule (non-gcn): no entry, or a
+        // lone entry that is the node itself
+        if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
+        if (last) {
+            pack[h.off[GS_PK_DST_IDS] + r] = v;
+            pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
+            if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
+        }
+    }
+}
+
+// Roots after the pack (the host sampler's layout), totals for the host.
+__global__ void finish_kernel(Ctl* c, const int32_t* __restrict__ roots, int n_roots, int32_t* __restrict__ pack,
+                              int fail_empty, int n_hops) {
+    const int at = c->total;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_roots; i += gridDim.x * blockDim.x)
+        pack[at + i] = roots[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        c->used = at + n_roots;
+        if (fail_empty)
+            for (int j = 0; j < n_hops; ++j)
+                if (c->hop[j].n_empty) c->status |= kStEmpty;
+    }
+}
+
+__global__ void begin_kernel(Ctl* c, const int32_t* __restrict__ roots, int32_t* __restrict__ dst0, int n_roots) {
+    for (int i = threadIdx.x; i < n_roots; i += blockDim.x) dst0[i] = roots[i];
+    if (threadIdx.x == 0) {
+        c->total = 0;
+        c->used = 0;
+        c->pos_batch = c->pos_cur;
+    }
+}
+
+// Words [pos, pos + n) of the stream, for the known-answer helper.
+__global__ void copy_words_kernel(const uint32_t* __restrict__ wr, int64_t pos, int64_t n, uint32_t* __restrict__ out) {
+    for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        out[i] = wr[(pos + i) & kRingMask];
+}
+
+__global__ void copy_block_kernel(const uint32_t* __restrict__ xr, int64_t first, uint32_t* __restrict__ out) {
+    for (int i = threadIdx.x; i < 624; i += blockDim.x) out[i] = xr[(first + i) & kRingMask];
+}
+
+}  // namespace ds
+}  // namespace gs
+
+// --------------------------------------------------------------- host side
+
+using namespace gs::ds;
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) gs::fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int r_of(int k) { return k > 0 ? std::max(1, 256 / k) : 256; }
+
+}  // namespace
+
+struct gs_dsampler {
+    int32_t n_hops = 0;
+    int32_t fanouts[GS_MAX_HOPS] = {};
+    int32_t flags = 0;
+    int64_t max_roots = 0;
+    int64_t nd_max[GS_MAX_HOPS] = {};   // frontier bound per hop
+    int64_t npos_max[GS_MAX_HOPS] = {};
+    const gs_graph* host_graph = nullptr;
+    DevGraph g{};
+    std::vector<void*> owned;
+    uint32_t* xr = nullptr;   // raw words ring
+    uint32_t* wr = nullptr;   // tempered words ring
+    uint32_t* tmp = nullptr;  // small transfer buffer (state block, words)
+    int64_t tmp_n = 0;
+    Ctl* ctl = nullptr;       // device control block
+    Ctl* ctl_host = nullptr;  // pinned mirror, copied at the end of every run
+    HopBufs hb[GS_MAX_HOPS];
+    UnionBufs ub[GS_MAX_HOPS];
+    int32_t* pack_cur = nullptr;
+    hipEvent_t done = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool ran = false;
+
+    template <typename T>
+    T* alloc(int64_t n) {
+        void* p = nullptr;
+        hip_ok(hipMalloc(&p, std::max<int64_t>(n, 1) * sizeof(T)), "hipMalloc(dsampler)");
+        owned.push_back(p);
+        return static_cast<T*>(p);
+    }
+    ~gs_dsampler() {
+        if (done) (void)hipEventSynchronize(done);
+        for (void* p : owned) (void)hipFree(p);
+        if (ctl_host) (void)hipHostFree(ctl_host);
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+
+namespace {
+
+void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStream_t st) {
+    const int k = ds->fanouts[hop];
+    const int setsize = static_cast<int>(gs::sample_setsize(k));
+    const int R = r_of(k);
+    const int gcn = (ds->flags & GS_SAMPLE_GCN) ? 1 : 0;
+    const HopBufs& hb = ds->hb[hop];
+    hop_setup_kernel<<<1, 1024, 0, st>>>(ds->g, ds->ctl, hb, hop, k, setsize, R, last ? 1 : 0, n_roots, gcn);
+    gs::check_launch("hop_setup_kernel");
+    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
+    gs::check_launch("mt_gen_kernel");
+    const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
+    const size_t tab_lds = (R + kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
+    if (k <= 16)
+        draw_tables_kernel<16><<<nb_max, 256, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    else
+        draw_tables_kernel<32><<<nb_max, 256, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    gs::check_launch("draw_tables_kernel");
+    const int ng_max = (nb_max + kMinG - 1) / kMinG;
+    draw_compose_kernel<<<ng_max, 256, kComposeEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
+    gs::check_launch("draw_compose_kernel");
+    draw_chain_kernel<<<1, 1024, kChainEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
+    gs::check_launch("draw_chain_kernel");
+    const size_t emit_lds = (2 * R + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
+    if (k <= 16)
+        draw_emit_kernel<16><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R,
+                                                           last ? 1 : 0, gcn, ds->pack_cur);
+    else
+        draw_emit_kernel<32><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R,
+                                                           last ? 1 : 0, gcn, ds->pack_cur);
+    gs::check_launch("draw_emit_kernel");
+}
+
+void ensure_tmp(gs_dsampler* ds, int64_t n) {
+    if (ds->tmp_n >= n) return;
+    ds->tmp = ds->alloc<uint32_t>(n);
+    ds->tmp_n = n;
+}
+
+int64_t pos_now(gs_dsampler* ds, hipStream_t st) {
+    int64_t p = 0;
+    hip_ok(hipMemcpyAsync(&p, &ds->ctl->pos_cur, sizeof(p), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    return p;
+}
+
+void check_status(int status) {
+    if (!status) return;
+    if (status & kStEmpty) gs::fail(GS_EEMPTY, "empty neighbourhood");
+    if (status & kStWindow)
+        gs::fail(GS_ERANGE, "device sampler: a rejection count fell outside its block window (resample on the host)");
+    if (status & kStWords) gs::fail(GS_ERANGE, "device sampler: a walk ran past its loaded words");
+    if (status & kStTable) gs::fail(GS_ERANGE, "device sampler: frontier union outgrew the device table");
+    if (status & kStSize) gs::fail(GS_ERANGE, "device sampler: frontier outgrew its bound");
+    gs::fail(GS_EINVAL, "device sampler: status " + std::to_string(status));
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hops, int64_t max_roots, int32_t flags,
+                       gs_dsampler** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(gp && out, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
+    GS_REQUIRE(max_roots >= 1 && max_roots < (int64_t(1) << 24), GS_EINVAL, "max_roots out of range");
+    const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
+    GS_REQUIRE(g.n_entries < (int64_t(1) << 31) && g.n_nodes < (int64_t(1) << 31), GS_ERANGE,
+               "graph too large for int32 entries");
+    std::unique_ptr<gs_dsampler> ds(new gs_dsampler());
+    ds->n_hops = n_hops;
+    ds->flags = flags;
+    ds->max_roots = max_roots;
+    ds->host_graph = gp;
+    for (int32_t j = 0; j < n_hops; ++j) {
+        ds->fanouts[j] = fanouts ? fanouts[j] : 10;
+        GS_REQUIRE(ds->fanouts[j] <= 32, GS_EINVAL, "device sampler: fanouts above 32 are not supported");
+    }
+    int64_t nd = max_roots;
+    for (int32_t j = 0; j < n_hops; ++j) {
+        const int64_t k = ds->fanouts[j];
+        const int64_t per = k > 0 ? std::min<int64_t>(k, g.max_degree) : g.max_degree;
+        ds->nd_max[j] = nd;
+        ds->npos_max[j] = nd * per;
+        GS_REQUIRE(ds->npos_max[j] < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
+        nd = std::min<int64_t>(g.n_nodes, nd + nd * per);
+    }
+    // graph
+    auto up = [&](const void* src, size_t bytes) {
+        void* p = nullptr;
+        hip_ok(hipMalloc(&p, std::max<size_t>(bytes, 1)), "hipMalloc(graph)");
+        ds->owned.push_back(p);
+        if (bytes) hip_ok(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice), "hipMemcpy(graph)");
+        return p;
+    };
+    ds->g.n_nodes = g.n_nodes;
+    ds->g.row_ptr = static_cast<const int64_t*>(up(g.row_ptr.data(), g.row_ptr.size() * sizeof(int64_t)));
+    ds->g.col = static_cast<const int32_t*>(up(g.col.data(), g.col.size() * sizeof(int32_t)));
+    ds->g.slot = static_cast<const uint32_t*>(up(g.slot.data(), g.slot.size() * sizeof(uint32_t)));
+    ds->g.log2size = static_cast<const uint8_t*>(up(g.log2size.data(), g.log2size.size()));
+    ds->g.dirty = g.dirty.empty() ? nullptr : static_cast<const uint8_t*>(up(g.dirty.data(), g.dirty.size()));
+    ds->xr = ds->alloc<uint32_t>(kRing);
+    ds->wr = ds->alloc<uint32_t>(kRing);
+    ds->ctl = ds->alloc<Ctl>(1);
+    hip_ok(hipMemset(ds->ctl, 0, sizeof(Ctl)), "hipMemset");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&ds->ctl_host), sizeof(Ctl), hipHostMallocDefault), "hipHostMalloc");
+    std::memset(ds->ctl_host, 0, sizeof(Ctl));
+    for (int32_t j = 0; j < n_hops; ++j) {
+        const int k = ds->fanouts[j];
+        const int64_t ndj = ds->nd_max[j];
+        const int64_t nb = (ndj + r_of(k) - 1) / r_of(k);
+        const int64_t ng = (nb + kMinG - 1) / kMinG;
+        HopBufs& h = ds->hb[j];
+        h.dst = ds->alloc<int32_t>(ndj);
+        h.deg = ds->alloc<int32_t>(ndj);
+        h.mv = ds->alloc<float2>(ndj);
+        h.pos_ptr = ds->alloc<int32_t>(ndj + 1);
+        h.blo = ds->alloc<int32_t>(nb + 1);
+        h.dbase = ds->alloc<int32_t>(nb + 1);
+        h.tab = ds->alloc<uint16_t>(nb * kWMax);
+        h.path = ds->alloc<int32_t>(nb * kWMax);
+        h.gexit = ds->alloc<uint16_t>(ng * kWMax);
+        h.gexit_last = ds->alloc<int32_t>(kWMax);
+        h.entry = ds->alloc<int32_t>(nb);
+        h.ent = j + 1 < n_hops ? ds->alloc<int32_t>(ds->npos_max[j]) : nullptr;
+    }
+    hip_ok(hipEventCreateWithFlags(&ds->done, hipEventDisableTiming), "hipEventCreate");
+    // the stream starts as random.seed(0) would leave it; callers set it
+    gs::MT19937 mt;
+    const uint32_t zero = 0;
+    mt.init_by_array(&zero, 1);
+    *out = ds.release();
+    GS_REQUIRE(gs_dsampler_set_rng(*out, mt.mt, mt.index, nullptr) == GS_OK, GS_EHIP, gs_last_error());
+    GS_API_END
+}
+
+void gs_dsampler_destroy(gs_dsampler* ds) { delete ds; }
+
+int gs_dsampler_set_rng(gs_dsampler* ds, const uint32_t* mt624, int64_t pos, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && mt624, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(pos >= 0 && pos <= 624, GS_EINVAL, "state index out of range");
+    hipStream_t st = gs::as_stream(stream);
+    if (ds->ran) hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    ensure_tmp(ds, 624);
+    hip_ok(hipMemcpyAsync(ds->tmp, mt624, 624 * sizeof(uint32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    mt_seed_kernel<<<1, 256, 0, st>>>(ds->tmp, pos, ds->xr, ds->wr, ds->ctl);
+    gs::check_launch("mt_seed_kernel");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    GS_API_END
+}
+
+int gs_dsampler_get_rng(gs_dsampler* ds, uint32_t* mt624, int64_t* pos, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && mt624 && pos, GS_EINVAL, "NULL argument");
+    hipStream_t st = gs::as_stream(stream);
+    if (ds->ran) hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    const int64_t p = pos_now(ds, st);
+    int64_t blk = p / 624, idx = p % 624;
+    if (p > 0 && idx == 0) {
+        blk -= 1;
+        idx = 624;
+    }
+    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, 624 * (blk + 1), -1);
+    gs::check_launch("mt_gen_kernel");
+    ensure_tmp(ds, 624);
+    copy_block_kernel<<<1, 256, 0, st>>>(ds->xr, 624 * blk, ds->tmp);
+    gs::check_launch("copy_block_kernel");
+    hip_ok(hipMemcpyAsync(mt624, ds->tmp, 624 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    *pos = idx;
+    GS_API_END
+}
+
+int gs_dsampler_words(gs_dsampler* ds, int64_t n, uint32_t* out, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && out && n >= 0 && n < kRing / 2, GS_EINVAL, "bad arguments");
+    hipStream_t st = gs::as_stream(stream);
+    if (ds->ran) hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    const int64_t p = pos_now(ds, st);
+    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, p + n, -1);
+    gs::check_launch("mt_gen_kernel");
+    ensure_tmp(ds, n);
+    copy_words_kernel<<<64, 256, 0, st>>>(ds->wr, p, n, ds->tmp);
+    gs::check_launch("copy_words_kernel");
+    if (n) hip_ok(hipMemcpyAsync(out, ds->tmp, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    GS_API_END
+}
+
+int64_t gs_dsampler_pack_bound(const gs_dsampler* ds, int64_t n_roots) {
+    if (!ds || n_roots < 1 || n_roots > ds->max_roots) return -1;
+    return gs_sample_pack_bound(ds->host_graph, n_roots, ds->fanouts, ds->n_hops) + n_roots;
+}
+
+int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int32_t* pack, int64_t cap, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && roots && pack, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(n_roots >= 1 && n_roots <= ds->max_roots, GS_EINVAL, "n_roots out of [1, max_roots]");
+    GS_REQUIRE(cap >= gs_dsampler_pack_bound(ds, n_roots), GS_EINVAL, "pack buffer below gs_dsampler_pack_bound");
+    hipStream_t st = gs::as_stream(stream);
+    ds->pack_cur = pack;
+    begin_kernel<<<1, 256, 0, st>>>(ds->ctl, roots, ds->hb[0].dst, static_cast<int>(n_roots));
+    gs::check_launch("begin_kernel");
+    for (int32_t j = 0; j < ds->n_hops; ++j) {
+        const bool last = j == ds->n_hops - 1;
+        launch_hop_draws(ds, j, last, static_cast<int>(n_roots), st);
+        if (!last) gs::ds::launch_hop_union(ds->g, ds->ctl, ds->hb[j], ds->ub[j], ds->hb[j + 1], j, ds->fanouts[j],
+                                            ds->nd_max[j], ds->nd_max[j + 1], ds->flags, pack, st);
+    }
+    finish_kernel<<<8, 256, 0, st>>>(ds->ctl, roots, static_cast<int>(n_roots), pack,
+                                     (ds->flags & GS_SAMPLE_FAIL_EMPTY) ? 1 : 0, ds->n_hops);
+    gs::check_launch("finish_kernel");
+    hip_ok(hipMemcpyAsync(ds->ctl_host, ds->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st), "hipMemcpyAsync(ctl)");
+    hip_ok(hipEventRecord(ds->done, st), "hipEventRecord");
+    ds->ran = true;
+    GS_API_END
+}
+
+int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && ds->ran, GS_EINVAL, "no run to report");
+    hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    const Ctl& c = *ds->ctl_host;
+    check_status(c.status);
+    for (int32_t j = 0; j < GS_MAX_HOPS; ++j) {
+        const bool on = j < ds->n_hops;
+        const bool last = j == ds->n_hops - 1;
+        if (hop_sizes) {
+            hop_sizes[4 * j] = on ? c.hop[j].n_dst : 0;
+            hop_sizes[4 * j + 1] = on ? c.hop[j].n_pos : 0;
+            hop_sizes[4 * j + 2] = on && !last ? c.hop[j].n_src : -1;
+            hop_sizes[4 * j + 3] = on && !last ? c.hop[j].n_nbr : -1;
+        }
+        if (offsets)
+            for (int f = 0; f < GS_PK_NFIELDS; ++f) {
+                const bool lastf = f == GS_PK_POS_PTR || f == GS_PK_POS || f == GS_PK_DST_IDS;
+                offsets[j * GS_PK_NFIELDS + f] = on && (last == lastf) ? c.hop[j].off[f] : -1;
+            }
+    }
+    if (used) *used = c.used;
+    GS_API_END
+}
+
+}  // extern "C"

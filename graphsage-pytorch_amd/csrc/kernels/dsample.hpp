@@ -1,0 +1,92 @@
+// Device sampler internals shared by dsample.hip (stream, draws, C-ABI) and
+// dsample_union.hip (per-node sets, the frontier union and the lists).
+#pragma once
+
+#include "kcommon.hpp"
+
+namespace gs {
+namespace ds {
+
+constexpr int64_t kRing = int64_t(1) << 20;  // words kept per stream ring (tempered and raw)
+constexpr int64_t kRingMask = kRing - 1;
+constexpr int kWMax = 4096;                  // widest rejection-count window per block
+constexpr int kComposeEntries = 30720;       // G * W entries a compose block stages in LDS (60 KiB)
+constexpr int kMinG = kComposeEntries / kWMax;
+constexpr int kChainEntries = 30720;         // group exits the chain block stages in LDS (uint16)
+constexpr int kMaxGroups = 1024;
+
+// status bits (Ctl::status)
+constexpr int kStWindow = 1;   // a true entry fell outside its block window
+constexpr int kStWords = 2;    // a walk ran past the words loaded for it
+constexpr int kStTable = 4;    // a frontier union outgrew the device table
+constexpr int kStEmpty = 8;    // empty neighbourhood with GS_SAMPLE_FAIL_EMPTY
+constexpr int kStSize = 16;    // a frontier outgrew its preallocated bound
+
+struct DevGraph {
+    const int64_t* row_ptr;
+    const int32_t* col;
+    const uint32_t* slot;      // slot of each entry in its row's set table
+    const uint8_t* log2size;   // row table size = 1 << log2size
+    const uint8_t* dirty;      // row set has dummies (nullptr: none)
+    int64_t n_nodes;
+};
+
+struct HopCtl {
+    int32_t n_dst, n_pos, n_draws;
+    int32_t n_blocks, W, G, n_groups;
+    int32_t j_end;
+    int32_t n_empty;
+    int32_t n_src, n_nbr;      // hops before the last (union, lists)
+    int64_t P0;                // absolute stream position at the hop's first draw
+    int64_t need_end;          // words the hop may read (exclusive)
+    int32_t off[GS_PK_NFIELDS];
+};
+
+struct Ctl {
+    int64_t gen_end;           // raw/tempered words valid below this absolute index
+    int64_t pos_cur;           // next word of the stream
+    int64_t pos_batch;         // stream position at the start of the last run
+    int32_t status;
+    int32_t epoch;
+    int32_t total;             // pack elements before the roots
+    int32_t used;
+    HopCtl hop[GS_MAX_HOPS];
+};
+
+struct HopBufs {
+    int32_t* dst;              // frontier F(j-1) (ids), [nd_max]
+    int32_t* deg;              // [nd_max]
+    float2* mv;                // rejection moments per node
+    int32_t* pos_ptr;          // [nd_max + 1]
+    int32_t* blo;              // block windows' first entry, [nb_max + 1]
+    int32_t* dbase;            // draws before each block, [nb_max + 1]
+    uint16_t* tab;             // block maps [nb_max][kWMax]
+    int32_t* path;             // group paths [nb_max][kWMax]
+    uint16_t* gexit;           // group exits relative to the next group's window [ng_max][kWMax]
+    int32_t* gexit_last;       // the last group's absolute exits [kWMax]
+    int32_t* entry;            // true entry per block [nb_max]
+    int32_t* ent;              // absolute CSR entries of the hop's samples (hops before the last)
+};
+
+struct UnionBufs {
+    int32_t* set_cnt;          // |samp_neighs[r]| per node
+    int32_t* set_items;        // items in iteration order at [pos_ptr[r] + r]
+    int32_t* first_tab;        // samp_neighs[0]'s table
+    int32_t* first_mask;
+    int64_t* mark;             // [n_nodes] (epoch << 32 | ~t) first occurrence in the union
+    int32_t* keys;             // stage key lists
+    int32_t* tcnt;             // transposed counts / cursors
+};
+
+}  // namespace ds
+}  // namespace gs
+
+namespace gs {
+namespace ds {
+// dsample_union.hip: for hop `hop` (not the last): per-node sets, the frontier
+// union (next.dst, n_src), the neighbour / self / transposed lists into the
+// pack.  Buffers in `ub` are allocated on first use.
+void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& ub, const HopBufs& next, int hop,
+                      int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st);
+}  // namespace ds
+}  // namespace gs

@@ -205,3 +205,65 @@ def sample(graph, rng, roots, fanouts, gcn=False, full=False):
     check(lib().gs_sample_run(graph.handle, rng._h, ptr(roots), len(roots), ptr(fan), len(fan),
                               flags, ctypes.byref(h)))
     return Sample(h.value)
+
+
+class DeviceSampler:
+    """The hop loop of GraphSage.forward (models.py:246-251 over
+    _get_unique_neighs_list, :277-289) on the GPU: a device
+    copy of the graph and a device MT19937 stream produce the same int32 pack
+    as ``sample(...).pack()`` — bit for bit — directly in device memory, and
+    advance the stream exactly as the reference's ``random`` would.
+
+    ``rng`` moves between host and device with ``set_rng`` / ``get_rng``
+    (``RNG`` objects or ``random.getstate()``-style (mt, pos) pairs)."""
+
+    def __init__(self, graph, fanouts, max_roots, gcn=False, fail_empty=False):
+        from ._lib import GS_SAMPLE_GCN
+        self.fanouts = np.ascontiguousarray(fanouts, np.int32)
+        flags = (GS_SAMPLE_GCN if gcn else 0) | (4 if fail_empty else 0)
+        h = ctypes.c_void_p()
+        check(lib().gs_dsampler_create(graph._h, ptr(self.fanouts), len(self.fanouts), int(max_roots), flags,
+                                       ctypes.byref(h)))
+        self._h = h
+        self.graph = graph  # keep the host graph alive (pack bounds)
+        self.n_hops = len(self.fanouts)
+
+    def set_rng(self, rng):
+        mt, pos = rng.getstate() if isinstance(rng, RNG) else rng
+        mt = np.ascontiguousarray(mt, np.uint32)
+        check(lib().gs_dsampler_set_rng(self._h, ptr(mt), int(pos), _lib.stream_ptr()))
+
+    def get_rng(self):
+        mt = np.zeros(624, np.uint32)
+        pos = ctypes.c_int64()
+        check(lib().gs_dsampler_get_rng(self._h, ptr(mt), ctypes.byref(pos), _lib.stream_ptr()))
+        return mt, int(pos.value)
+
+    def words(self, n):
+        out = np.zeros(max(int(n), 1), np.uint32)
+        check(lib().gs_dsampler_words(self._h, int(n), ptr(out), _lib.stream_ptr()))
+        return out[:int(n)]
+
+    def pack_bound(self, n_roots):
+        return int(lib().gs_dsampler_pack_bound(self._h, int(n_roots)))
+
+    def run(self, roots, pack=None):
+        """Sample one batch; returns (pack, hop_sizes[n_hops, 4], offsets[8, 8], used)."""
+        roots = torch.as_tensor(np.asarray(roots, np.int64).astype(np.int32)).cuda() \
+            if not isinstance(roots, torch.Tensor) else roots.to(torch.int32)
+        n = int(roots.numel())
+        if pack is None:
+            pack = torch.zeros(self.pack_bound(n), dtype=torch.int32, device=roots.device)
+        check(lib().gs_dsampler_run(self._h, ptr(roots), n, ptr(pack), int(pack.numel()), _lib.stream_ptr()))
+        hs = np.zeros(4 * _lib.GS_MAX_HOPS, np.int64)
+        off = np.zeros(_lib.GS_MAX_HOPS * _lib.GS_PK_NFIELDS, np.int64)
+        used = ctypes.c_int64()
+        check(lib().gs_dsampler_result(self._h, ptr(hs), ptr(off), ctypes.byref(used)))
+        return pack, hs.reshape(-1, 4)[:self.n_hops], off.reshape(_lib.GS_MAX_HOPS, _lib.GS_PK_NFIELDS), \
+            int(used.value)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.gs_dsampler_destroy(h)
+            self._h = None

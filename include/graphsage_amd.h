@@ -212,6 +212,32 @@ int gs_sample_pack_run_multi_team(const gs_graph* g, gs_rng* rng, const int64_t*
                                   int64_t* hop_sizes, int64_t* offsets, int64_t* used,
                                   gs_team* team);
 
+/* ------------------------------------------------------- device sampler
+ * The same sampling as gs_sample_pack_run (models.py:246-251 over
+ * _get_unique_neighs_list, models.py:277-289), run on the GPU from a device
+ * copy of the graph and a device MT19937 stream: the pack lands in device
+ * memory, bit-identical to the host sampler's image, and the stream advances
+ * exactly as the reference's `random` would.  One handle is one
+ * stream; its calls are ordered on the caller's stream.  Fanouts <= 32. */
+typedef struct gs_dsampler gs_dsampler;
+int gs_dsampler_create(const gs_graph* g, const int32_t* fanouts, int32_t n_hops,
+                       int64_t max_roots, int32_t flags, gs_dsampler** out);
+void gs_dsampler_destroy(gs_dsampler* ds);
+/* random.setstate / getstate on the device stream (both synchronise). */
+int gs_dsampler_set_rng(gs_dsampler* ds, const uint32_t* mt624, int64_t pos, void* stream);
+int gs_dsampler_get_rng(gs_dsampler* ds, uint32_t* mt624, int64_t* pos, void* stream);
+/* Known answers: the next n words of the stream (genrand_uint32 outputs),
+ * without consuming them (synchronises). */
+int gs_dsampler_words(gs_dsampler* ds, int64_t n, uint32_t* out, void* stream);
+/* Elements a pack of n_roots roots may need (gs_sample_pack_bound + roots). */
+int64_t gs_dsampler_pack_bound(const gs_dsampler* ds, int64_t n_roots);
+/* Sample one batch (device int32 roots) into a device pack, asynchronously on
+ * `stream`; gs_dsampler_result waits for it and reports the layout exactly as
+ * gs_sample_pack_run does (hop_sizes, offsets, used), or its error. */
+int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int32_t* pack,
+                    int64_t cap, void* stream);
+int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+
 /* ------------------------------------------------- unsupervised-loss batch
  * UnsupervisedLoss (models.py:30-186) over the same graph and rng:
  * extend_nodes (models.py:135-147, called by apply_model at utils.py:149)

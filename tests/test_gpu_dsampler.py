@@ -1,0 +1,143 @@
+"""Device-resident sampler (graphsage-pytorch_amd/csrc/kernels/
+dsample.hip) against the host sampler, which is itself pinned to the
+reference (test_host_sampler.py, test_oracle_golden.py):
+
+* the device MT19937 stream: the next words equal CPython's genrand_uint32
+  outputs (host RNG, interchangeable with random.getstate()) from arbitrary
+  states, block boundaries included;
+* whole packs: the device pack, its layout (hop sizes, field offsets) and the
+  stream position afterwards are bit-identical to gs_sample_pack_run on the
+  same graph, roots and state, batch after batch on one stream.  Graphs mix
+  the three draw regimes of random.sample (whole row when deg < k, the pool
+  branch for deg <= setsize(k), the selected-set branch above it).
+"""
+import ctypes
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+gs = importlib.import_module("graphsage-pytorch_amd")
+L = importlib.import_module("graphsage-pytorch_amd._lib")
+
+
+def host_pack(G_, rng, roots, fan, flags=0):
+    nh = len(fan)
+    bound = int(L.lib().gs_sample_pack_bound(G_.handle, len(roots), fan.ctypes.data, nh))
+    buf = np.full(bound + len(roots), -7, np.int32)
+    sizes = np.empty(4 * nh, np.int64)
+    offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+    used = ctypes.c_int64()
+    L.check(L.lib().gs_sample_pack_run(G_.handle, rng._h, roots.ctypes.data, len(roots), fan.ctypes.data, nh,
+                                       flags, buf.ctypes.data, len(buf), sizes.ctypes.data, offs.ctypes.data,
+                                       ctypes.byref(used)))
+    return buf[:used.value], sizes.reshape(nh, 4), offs.reshape(L.GS_MAX_HOPS, L.GS_PK_NFIELDS), used.value
+
+
+def assert_packs_equal(got, ref, sizes, offs, n_roots, what=""):
+    """Field by field (the alignment padding between fields is unspecified)."""
+    nh = len(sizes)
+    for j in range(nh):
+        nd, npos, ns, nn = (int(x) for x in sizes[j])
+        if j == nh - 1:
+            fields = {L.GS_PK_POS_PTR: nd + 1, L.GS_PK_POS: npos, L.GS_PK_DST_IDS: nd}
+        else:
+            fields = {L.GS_PK_NBR_PTR: nd + 1, L.GS_PK_NBR: nn, L.GS_PK_SELF: nd, L.GS_PK_TPTR: ns + 1,
+                      L.GS_PK_TIDX: nn + nd}
+        for f, n in fields.items():
+            o = int(offs[j, f])
+            np.testing.assert_array_equal(got[o:o + n], ref[o:o + n], err_msg=f"{what} hop {j} field {f}")
+    np.testing.assert_array_equal(got[len(ref) - n_roots:len(ref)], ref[-n_roots:], err_msg=f"{what} roots")
+
+
+def mixed_graph(seed=0, n=3000, hubs=12, hub_deg=900, self_loops=5):
+    """R-MAT-like power law plus explicit hubs (selected-set branch for both
+    fanouts) and a few self loops (a node in its own adjacency set)."""
+    rs = np.random.RandomState(seed)
+    m = 12 * n
+    src = (rs.pareto(1.2, m) * 10).astype(np.int64) % n
+    dst = rs.randint(0, n, m)
+    hs, hd = [], []
+    for h in range(hubs):
+        hs.append(np.full(hub_deg, h * 7 + 1))
+        hd.append(rs.randint(0, n, hub_deg))
+    loops = rs.randint(0, n, self_loops)
+    src = np.concatenate([src] + hs + [loops])
+    dst = np.concatenate([dst] + hd + [loops])
+    keep = (src != dst) | np.isin(src, loops)
+    return gs.CSRGraph.from_pairs(src[keep], dst[keep], n)
+
+
+@pytest.fixture(scope="module")
+def graph():
+    return mixed_graph()
+
+
+@pytest.mark.parametrize("seed,pos", [(824, 624), (7, 0), (11, 5), (3, 623), (2 ** 40 + 3, 300)])
+def test_device_stream_words(graph, seed, pos):
+    rng = gs.RNG(seed)
+    mt, p0 = rng.getstate()
+    rng.setstate(mt, pos)
+    ds = gs.sampler.DeviceSampler(graph, [10], 8)
+    ds.set_rng(rng)
+    n = 5000
+    dev = ds.words(n)
+    host = rng.getrandbits(32, n)
+    np.testing.assert_array_equal(dev, host)
+    # words() does not consume: the device state is still the one set
+    mt2, pos2 = ds.get_rng()
+    np.testing.assert_array_equal(mt2, mt)
+    assert pos2 == pos
+
+
+@pytest.mark.parametrize("fan", [[25], [10], [3], [32]])
+def test_device_one_hop_matches_host(graph, fan):
+    fan = np.array(fan, np.int32)
+    rng_h = gs.RNG(824)
+    ds = gs.sampler.DeviceSampler(graph, fan, 512)
+    ds.set_rng(rng_h)
+    deg = graph.degrees()
+    rs = np.random.RandomState(1)
+    cand = np.arange(graph.n_nodes)
+    for b, B in enumerate([512, 200, 1, 512, 77]):
+        roots = rs.choice(cand, B, replace=b % 2 == 0).astype(np.int64)
+        if b == 3:  # hubs and isolated nodes first
+            roots[:12] = np.arange(12) * 7 + 1
+            roots[12:20] = np.nonzero(deg == 0)[0][:8] if (deg == 0).sum() >= 8 else roots[12:20]
+        ref, sizes, offs, used = host_pack(graph, rng_h, roots, fan)
+        pack, dsz, doff, dused = ds.run(roots)
+        torch.cuda.synchronize()
+        assert dused == used, (b, dused, used)
+        np.testing.assert_array_equal(dsz, sizes)
+        np.testing.assert_array_equal(doff, offs)
+        assert_packs_equal(pack[:used].cpu().numpy(), ref, sizes, offs, len(roots), f"batch {b}")
+        mt_h, pos_h = rng_h.getstate()
+        mt_d, pos_d = ds.get_rng()
+        assert pos_d == pos_h
+        np.testing.assert_array_equal(mt_d, mt_h)
+
+
+def test_device_one_hop_rmat_large():
+    """A scale-16 R-MAT graph (hub degrees in the thousands), 4096 roots:
+    wide rejection windows, many blocks and groups."""
+    src, dst = gs.rmat_pairs(16, 1_000_000, seed=5, n_threads=8)
+    G_ = gs.CSRGraph.from_pairs(src, dst, 1 << 16, n_threads=8)
+    cand = np.nonzero(G_.degrees() > 0)[0]
+    fan = np.array([10], np.int32)
+    rng_h = gs.RNG(3)
+    ds = gs.sampler.DeviceSampler(G_, fan, 4096)
+    ds.set_rng(rng_h)
+    rs = np.random.RandomState(2)
+    for b in range(3):
+        roots = rs.choice(cand, 4096, replace=False).astype(np.int64)
+        ref, sizes, offs, used = host_pack(G_, rng_h, roots, fan)
+        pack, dsz, doff, dused = ds.run(roots)
+        assert dused == used
+        assert_packs_equal(pack[:used].cpu().numpy(), ref, sizes, offs, len(roots), f"batch {b}")
+    mt_h, pos_h = rng_h.getstate()
+    mt_d, pos_d = ds.get_rng()
+    assert pos_d == pos_h
+    np.testing.assert_array_equal(mt_d, mt_h)
