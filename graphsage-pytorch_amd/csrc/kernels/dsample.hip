@@ -129,49 +129,6 @@ __device__ __forceinline__ void rejection_moments(uint32_t d, int k, int setsize
     }
 }
 
-__device__ __forceinline__ int warp_incl_scan(int v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if ((threadIdx.x & 63) >= o) v += t;
-    }
-    return v;
-}
-__device__ __forceinline__ float warp_incl_scan(float v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const float t = __shfl_up(v, o, 64);
-        if ((threadIdx.x & 63) >= o) v += t;
-    }
-    return v;
-}
-
-// Exclusive scan over a 1024-thread block of one value per thread; returns
-// the thread's exclusive prefix, *total the block total.
-template <typename T>
-__device__ __forceinline__ T block_excl_scan(T v, T* sh /* >= 17 */, T* total) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const T inc = warp_incl_scan(v);
-    if (lane == 63) sh[w] = inc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        T run = T(0);
-        for (int q = 0; q < 16; ++q) {
-            const T t = sh[q];
-            sh[q] = run;
-            run += t;
-        }
-        sh[16] = run;
-    }
-    __syncthreads();
-    const T out = sh[w] + inc - v;
-    *total = sh[16];
-    __syncthreads();
-    return out;
-}
-
-__device__ __forceinline__ int32_t al4(int32_t n) { return (n + 3) & ~3; }
-
 // Per hop, one 1024-thread block: degrees of the frontier, the scans of the
 // sampled counts (pos_ptr) and draw counts, the rejection-count windows of
 // the blocks, the word need of the hop, and (last hop) the pack offsets.
@@ -605,6 +562,7 @@ struct gs_dsampler {
     HopBufs hb[GS_MAX_HOPS];
     UnionBufs ub[GS_MAX_HOPS];
     int32_t* pack_cur = nullptr;
+    uint64_t* mark = nullptr;  // first-occurrence marks of the frontier unions (shared by the hops)
     hipEvent_t done = nullptr;
     hipStream_t last_stream = nullptr;
     bool ran = false;
@@ -751,6 +709,23 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
         h.gexit_last = ds->alloc<int32_t>(kWMax);
         h.entry = ds->alloc<int32_t>(nb);
         h.ent = j + 1 < n_hops ? ds->alloc<int32_t>(ds->npos_max[j]) : nullptr;
+        if (j + 1 < n_hops) {
+            GS_REQUIRE(k >= 1, GS_EINVAL, "device sampler: hops before the last need a fanout >= 1");
+            UnionBufs& u = ds->ub[j];
+            u.set_cnt = ds->alloc<int32_t>(ndj);
+            u.set_items = ds->alloc<int32_t>(ds->npos_max[j] + ndj);
+            u.first_tab = ds->alloc<int32_t>(kSmallSet);
+            u.first_meta = ds->alloc<int32_t>(2);
+            u.tpre = ds->alloc<int32_t>(ndj + 1);
+            u.ubef = ds->alloc<int32_t>(ndj + 1);
+            u.fresh = ds->alloc<int32_t>(ds->npos_max[j] + ndj);
+            u.tcnt = ds->alloc<int32_t>(ds->nd_max[j + 1] + 1);
+            if (!ds->mark) {
+                ds->mark = ds->alloc<uint64_t>(g.n_nodes);
+                hip_ok(hipMemset(ds->mark, 0, g.n_nodes * sizeof(uint64_t)), "hipMemset(mark)");
+            }
+            u.mark = ds->mark;
+        }
     }
     hip_ok(hipEventCreateWithFlags(&ds->done, hipEventDisableTiming), "hipEventCreate");
     // the stream starts as random.seed(0) would leave it; callers set it

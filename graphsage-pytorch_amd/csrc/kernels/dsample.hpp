@@ -69,14 +69,64 @@ struct HopBufs {
 };
 
 struct UnionBufs {
-    int32_t* set_cnt;          // |samp_neighs[r]| per node
-    int32_t* set_items;        // items in iteration order at [pos_ptr[r] + r]
-    int32_t* first_tab;        // samp_neighs[0]'s table
-    int32_t* first_mask;
-    int64_t* mark;             // [n_nodes] (epoch << 32 | ~t) first occurrence in the union
-    int32_t* keys;             // stage key lists
-    int32_t* tcnt;             // transposed counts / cursors
+    int32_t* set_cnt;          // |samp_neighs[r]| per frontier node, [nd_max]
+    int32_t* set_items;        // their items in iteration order at [pos_ptr[r] + r], [npos_max + nd_max]
+    int32_t* first_tab;        // samp_neighs[0]'s table, [kSmallSet]
+    int32_t* first_meta;       // its (mask, used)
+    uint64_t* mark;            // [n_nodes]: epoch << 32 | ~t, the first occurrence of a key in the union
+    int32_t* tpre;             // items of runs 1..r-1 (union order), [nd_max + 1]
+    int32_t* ubef;             // union size before run r, [nd_max]
+    int32_t* fresh;            // keys new to the union, in insertion order, [npos_max + nd_max]
+    int32_t* tcnt;             // transposed counts / cursors, [nd_next_max + 1]
 };
+
+constexpr int kSmallSet = 128;      // table slots of one samp_neighs set (k <= 32)
+constexpr int kUnionMax = 16384;    // table slots of a frontier union in LDS
+constexpr int kMaxStages = 24;
+
+
+__device__ __forceinline__ int warp_incl_scan(int v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ float warp_incl_scan(float v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(v, o, 64);
+        if ((threadIdx.x & 63) >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive scan over a 1024-thread block of one value per thread; returns
+// the thread's exclusive prefix, *total the block total.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh /* >= 17 */, T* total) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const T inc = warp_incl_scan(v);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = T(0);
+        for (int q = 0; q < 16; ++q) {
+            const T t = sh[q];
+            sh[q] = run;
+            run += t;
+        }
+        sh[16] = run;
+    }
+    __syncthreads();
+    const T out = sh[w] + inc - v;
+    *total = sh[16];
+    __syncthreads();
+    return out;
+}
+
+__device__ __forceinline__ int32_t al4(int32_t n) { return (n + 3) & ~3; }
 
 }  // namespace ds
 }  // namespace gs

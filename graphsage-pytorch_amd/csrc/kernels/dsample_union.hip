@@ -1,12 +1,563 @@
-// Device sampler, hops before the last: models.py:282-286 (see dsample.hip).
+// Device sampler, hops before the last (see dsample.hip): the CPython-set part
+// of _get_unique_neighs_list (models.py:282-288) and the lists the aggregate
+// kernels read, written into the pack exactly as host/sampler.cpp writes them.
+//
+//   sets_kernel   samp_neighs[r] = set(sample) | {node} (:282, :285), one
+//                 lane per frontier node on a lane-private 128-slot table in
+//                 LDS: Objects/setobject.c's add / resize / copy / merge rules
+//                 as host/pyset.hpp restates them.  Out: each set's iteration
+//                 order (all the union needs) and samp_neighs[0]'s table.
+//   union_kernel  list(set.union(*samp_neighs)) (:286), one block, table in
+//                 LDS.  The union is a copy of samp_neighs[0] followed by one
+//                 set_merge per other set; a merge can only resize before its
+//                 first add (its pre-resize leaves room for all of them), and
+//                 no key is ever deleted.  So the final table is a sequence of
+//                 stages — resize, re-insert the previous table in slot
+//                 order, insert the keys new to the union in merge order —
+//                 and each stage is "every key takes the first free slot of
+//                 its probe sequence, in priority order".  That assignment is
+//                 computed in parallel by priority displacement (a key claims
+//                 its current probe slot with an LDS atomicMin of its
+//                 priority; a key that loses, or is later displaced, moves to
+//                 its next probe slot), which converges to exactly the
+//                 sequential result: the highest-priority key always keeps its
+//                 first free slot, and by induction so does every key after
+//                 it.  Keys new to the union are found with one 64-bit
+//                 atomicMax per item on a per-node mark (epoch, first index).
+//                 Then: the frontier in slot order, each destination's
+//                 neighbourhood in frontier-local ids (ascending), its self id.
+//   t*_kernels    the transposed lists (per source, ascending destination;
+//                 self entries -(r+1) first), counted, scanned, scattered and
+//                 sorted per source.
 #include "dsample.hpp"
 
 namespace gs {
 namespace ds {
 
+namespace {
+
+constexpr int kLaneSet = kSmallSet + 40;  // table + resize scratch per lane (ints)
+constexpr int kMaxItems = 33;             // |samp_neighs[r]| <= k + 1 <= 33
+
+__device__ __forceinline__ void ps_clear(int32_t* T, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) T[i] = -1;
+}
+
+// set_insert_clean: key absent, room in the table.
+__device__ __forceinline__ void ps_insert_clean(int32_t* T, uint32_t mask, int32_t key) {
+    uint32_t perturb = static_cast<uint32_t>(key);
+    uint32_t i = static_cast<uint32_t>(key) & mask;
+    for (;;) {
+        if (T[i] == -1) {
+            T[i] = key;
+            return;
+        }
+        if (i + 9 <= mask) {
+            for (uint32_t j = 1; j <= 9; ++j)
+                if (T[i + j] == -1) {
+                    T[i + j] = key;
+                    return;
+                }
+        }
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+struct LSet {
+    int32_t* T;
+    int32_t* tmp;
+    uint32_t mask;
+    int used;
+};
+
+// set_table_resize: smallest power of two > minused, keys re-inserted in slot order.
+__device__ __forceinline__ void ls_resize(LSet& s, int minused) {
+    int n = 0;
+    for (uint32_t i = 0; i <= s.mask; ++i)
+        if (s.T[i] != -1) s.tmp[n++] = s.T[i];
+    uint32_t ns = 8;
+    while (ns <= static_cast<uint32_t>(minused)) ns <<= 1;
+    ps_clear(s.T, ns);
+    s.mask = ns - 1;
+    for (int q = 0; q < n; ++q) ps_insert_clean(s.T, s.mask, s.tmp[q]);
+}
+
+// set_add_entry.
+__device__ __forceinline__ void ls_add(LSet& s, int32_t key) {
+    uint32_t perturb = static_cast<uint32_t>(key);
+    uint32_t i = static_cast<uint32_t>(key) & s.mask;
+    uint32_t e;
+    for (;;) {
+        e = i;
+        uint32_t probes = (i + 9 <= s.mask) ? 9 : 0;
+        for (;;) {
+            if (s.T[e] == -1) goto found_unused;
+            if (s.T[e] == key) return;
+            if (probes-- == 0) break;
+            ++e;
+        }
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & s.mask;
+    }
+found_unused:
+    s.T[e] = key;
+    ++s.used;
+    if (static_cast<uint32_t>(s.used) * 5 >= s.mask * 3) ls_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4);
+}
+
+__device__ __forceinline__ uint32_t mask_for(int64_t minused) {
+    uint32_t ns = 8;
+    while (ns <= minused) ns <<= 1;
+    return ns - 1;
+}
+
+// ---- union probe state: slot i (14 bits), linear step (4 bits), perturb shifts (4 bits)
+__device__ __forceinline__ uint32_t pr_slot(uint32_t ps) { return (ps & 0xFFFFu) + ((ps >> 16) & 15u); }
+__device__ __forceinline__ uint32_t pr_init(int32_t key, uint32_t mask) { return static_cast<uint32_t>(key) & mask; }
+__device__ __forceinline__ uint32_t pr_next(uint32_t ps, int32_t key, uint32_t mask) {
+    uint32_t i = ps & 0xFFFFu, lin = (ps >> 16) & 15u, steps = ps >> 20;
+    if (lin < 9 && i + 9 <= mask) return i | ((lin + 1) << 16) | (steps << 20);
+    steps = min(steps + 1, 15u);
+    const uint32_t perturb = steps * 5 >= 32 ? 0u : static_cast<uint32_t>(key) >> (steps * 5);
+    i = (i * 5 + 1 + perturb) & mask;
+    return i | (steps << 20);
+}
+
+constexpr int kOldPT = kUnionMax / 2 / 1024;          // previous-table slots per thread
+constexpr int kFreshPT = (kUnionMax * 3 / 5) / 1024 + 1;  // new keys per thread per stage
+constexpr int kKPT = kOldPT + kFreshPT;
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb, UnionBufs ub, int hop, int k) {
+    extern __shared__ int32_t lds[];
+    const int r = blockIdx.x * 64 + threadIdx.x;
+    const int n = c->hop[hop].n_dst;
+    if (r >= n) return;
+    LSet s{lds + threadIdx.x * kLaneSet, lds + threadIdx.x * kLaneSet + kSmallSet, 7, 0};
+    ps_clear(s.T, 8);
+    const int32_t v = hb.dst[r];
+    const int d = hb.deg[r];
+    if (k > 0 && d >= k) {
+        // set(random.sample(...)) in result order, then the copy that `|` makes
+        const int32_t* ent = hb.ent + hb.pos_ptr[r];
+        for (int i = 0; i < k; ++i) ls_add(s, g.col[ent[i]]);
+        uint32_t nm = 7;
+        if (s.used * 5 >= 21) nm = mask_for(2 * s.used);
+        if (nm != s.mask) {
+            int m = 0;
+            for (uint32_t i = 0; i <= s.mask; ++i)
+                if (s.T[i] != -1) s.tmp[m++] = s.T[i];
+            ps_clear(s.T, nm + 1);
+            for (int q = 0; q < m; ++q) ps_insert_clean(s.T, nm, s.tmp[q]);
+            s.mask = nm;
+        }
+    } else {
+        // the adjacency set itself, copied by `|`: its own layout when the
+        // copy's table has its size and it holds no dummies
+        const int64_t rs = g.row_ptr[v];
+        const uint32_t m0 = (1u << g.log2size[v]) - 1;
+        const bool dirty = g.dirty && g.dirty[v];
+        uint32_t ns = 8;
+        if (d * 5 >= 21)
+            while (ns <= static_cast<uint32_t>(2 * d)) ns <<= 1;
+        ps_clear(s.T, ns);
+        s.mask = ns - 1;
+        s.used = d;
+        if (s.mask == m0 && !dirty)
+            for (int t = 0; t < d; ++t) s.T[g.slot[rs + t]] = g.col[rs + t];
+        else
+            for (int t = 0; t < d; ++t) ps_insert_clean(s.T, s.mask, g.col[rs + t]);
+    }
+    // | set([node]): set_merge with a one-element set
+    if ((s.used + 1) * 5 >= static_cast<int>(s.mask) * 3) ls_resize(s, (s.used + 1) * 2);
+    if (s.used == 0 && s.mask == 7) {
+        ps_clear(s.T, 8);
+        s.T[v & 7] = v;
+        s.used = 1;
+    } else if (s.used == 0) {
+        s.used = 1;
+        ps_insert_clean(s.T, s.mask, v);
+    } else {
+        ls_add(s, v);
+    }
+    int32_t* out = ub.set_items + hb.pos_ptr[r] + r;
+    int q = 0;
+    for (uint32_t i = 0; i <= s.mask; ++i)
+        if (s.T[i] != -1) out[q++] = s.T[i];
+    ub.set_cnt[r] = s.used;
+    if (r == 0) {
+        for (uint32_t i = 0; i <= s.mask; ++i) ub.first_tab[i] = s.T[i];
+        ub.first_meta[0] = static_cast<int32_t>(s.mask);
+        ub.first_meta[1] = s.used;
+    }
+}
+
+// Priority-displacement insertion of the keys this thread owns (on[q]) into
+// the LDS table T (all slots EMPTY or holding priorities); returns when every
+// key of the block sits in its final slot.
+__device__ __forceinline__ void settle(uint32_t* T, uint32_t mask, const int32_t (&key)[kKPT],
+                                       const uint32_t (&prio)[kKPT], uint32_t (&ps)[kKPT], const bool (&on)[kKPT]) {
+    bool placed[kKPT];
+#pragma unroll
+    for (int q = 0; q < kKPT; ++q) placed[q] = false;
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q)
+            if (on[q] && !placed[q]) atomicMin(&T[pr_slot(ps[q])], prio[q]);
+        __syncthreads();
+        int any = 0;
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q)
+            if (on[q]) {
+                placed[q] = T[pr_slot(ps[q])] == prio[q];
+                if (!placed[q]) {
+                    ps[q] = pr_next(ps[q], key[q], mask);
+                    any = 1;
+                }
+            }
+        if (!__syncthreads_or(any)) break;
+    }
+}
+
+__device__ __forceinline__ uint32_t find_slot(const uint32_t* T, uint32_t mask, int32_t key) {
+    uint32_t ps = pr_init(key, mask);
+    for (int guard = 0; guard < 4 * kUnionMax; ++guard) {
+        const uint32_t s = pr_slot(ps);
+        if (T[s] == static_cast<uint32_t>(key)) return s;
+        ps = pr_next(ps, key, mask);
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(1024) void union_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop,
+                                                     int gcn, int32_t* __restrict__ pack, int nd_next_max) {
+    extern __shared__ uint32_t T[];
+    uint16_t* rank = reinterpret_cast<uint16_t*>(T + kUnionMax);
+    __shared__ int shi[17];
+    __shared__ uint64_t s_epoch;
+    __shared__ int st_run[kMaxStages + 1];
+    __shared__ uint32_t st_mask[kMaxStages];
+    __shared__ int s_nst, s_best, s_bad;
+    HopCtl& h = c->hop[hop];
+    const int n = h.n_dst;
+    const int tid = threadIdx.x;
+    const int used0 = ub.set_cnt[0];
+    const uint32_t m_first = static_cast<uint32_t>(ub.first_meta[0]);
+    if (tid == 0) {
+        const int e = c->epoch + 1;
+        c->epoch = e;
+        s_epoch = static_cast<uint64_t>(static_cast<uint32_t>(e)) << 32;
+        s_bad = 0;
+    }
+    // runs 1..n-1 in contiguous chunks, one per thread
+    const int per = (n - 1 + 1023) / 1024;
+    const int ra = min(n, 1 + tid * per), rb = min(n, ra + per);
+    int my_items = 0;
+    for (int r = ra; r < rb; ++r) my_items += ub.set_cnt[r];
+    int items_tot;
+    int t0 = block_excl_scan(my_items, shi, &items_tot);  // also a barrier (s_epoch visible)
+    const uint64_t E = s_epoch;
+    {
+        int t = t0;
+        for (int r = ra; r < rb; ++r) {
+            ub.tpre[r] = t;
+            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
+            const int cn = ub.set_cnt[r];
+            for (int q = 0; q < cn; ++q, ++t)
+                atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[it[q]]),
+                          static_cast<unsigned long long>(E | (0xFFFFFFFEu - static_cast<uint32_t>(t))));
+        }
+        if (tid == 0) {
+            ub.tpre[0] = 0;
+            ub.tpre[n] = items_tot;
+        }
+        for (int q = tid; q < used0; q += 1024)
+            atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[ub.set_items[q]]),
+                      static_cast<unsigned long long>(E | 0xFFFFFFFFu));
+    }
+    __threadfence();
+    __syncthreads();
+    auto is_fresh = [&](int32_t key, int t) {
+        const uint64_t m = __hip_atomic_load(&ub.mark[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return m == (E | (0xFFFFFFFEu - static_cast<uint32_t>(t)));
+    };
+    int my_fresh = 0;
+    {
+        int t = t0;
+        for (int r = ra; r < rb; ++r) {
+            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
+            const int cn = ub.set_cnt[r];
+            for (int q = 0; q < cn; ++q, ++t) my_fresh += is_fresh(it[q], t);
+        }
+    }
+    int fresh_tot;
+    int f = block_excl_scan(my_fresh, shi, &fresh_tot);
+    {
+        int t = t0;
+        for (int r = ra; r < rb; ++r) {
+            ub.ubef[r] = used0 + f;
+            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
+            const int cn = ub.set_cnt[r];
+            for (int q = 0; q < cn; ++q, ++t)
+                if (is_fresh(it[q], t)) ub.fresh[f++] = it[q];
+        }
+        if (tid == 0) ub.ubef[n] = used0 + fresh_tot;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // resize schedule: stage 0 is the copy of samp_neighs[0] (resized to
+    // 2 * used when used * 5 >= 21) plus the runs up to the first merge whose
+    // pre-resize fires; every such merge starts a stage
+    if (tid == 0) {
+        const uint32_t mu = used0 * 5 >= 21 ? mask_for(2 * used0) : 7u;
+        st_run[0] = 1;
+        st_mask[0] = mu;
+        s_nst = 1;
+    }
+    __syncthreads();
+    for (;;) {
+        const int cur_r = st_run[s_nst - 1] + (s_nst > 1 ? 1 : 0);
+        const int64_t cur_m = st_mask[s_nst - 1];
+        if (tid == 0) s_best = INT_MAX;
+        __syncthreads();
+        for (int r = max(ra, cur_r); r < rb; ++r) {
+            if ((static_cast<int64_t>(ub.ubef[r]) + ub.set_cnt[r]) * 5 >= cur_m * 3) {
+                atomicMin(&s_best, r);
+                break;
+            }
+        }
+        __syncthreads();
+        const int best = s_best;
+        if (best == INT_MAX) break;
+        if (tid == 0) {
+            if (s_nst >= kMaxStages) {
+                s_bad = 1;
+            } else {
+                st_run[s_nst] = best;
+                st_mask[s_nst] = mask_for(2 * (static_cast<int64_t>(ub.ubef[best]) + ub.set_cnt[best]));
+                ++s_nst;
+            }
+        }
+        __syncthreads();
+        if (s_bad) break;
+    }
+    if (tid == 0) {
+        st_run[s_nst] = n;
+        if (st_mask[s_nst - 1] + 1 > static_cast<uint32_t>(kUnionMax)) s_bad = 1;
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (tid == 0) c->status |= kStTable;
+        return;
+    }
+    const int nst = s_nst;
+    // stages
+    int32_t key[kKPT];
+    uint32_t prio[kKPT], ps[kKPT];
+    bool on[kKPT];
+    uint32_t prev_mask = m_first;
+    for (int s = 0; s < nst; ++s) {
+        const uint32_t m = st_mask[s];
+        // previous table's keys (samp_neighs[0]'s own table for stage 0), priority = slot
+#pragma unroll
+        for (int q = 0; q < kOldPT; ++q) {
+            const uint32_t sl = tid + 1024u * q;
+            int32_t kk = -1;
+            if (sl <= prev_mask) kk = s == 0 ? ub.first_tab[sl] : static_cast<int32_t>(T[sl]);
+            key[q] = kk;
+            prio[q] = sl;
+            on[q] = kk != -1;
+            // stage 0 with the copy's table size equal to the set's: slot copy
+            ps[q] = (s == 0 && m == m_first) ? sl : pr_init(kk, m);
+        }
+        const int f0 = ub.ubef[st_run[s]] - used0, f1 = ub.ubef[st_run[s + 1]] - used0;
+#pragma unroll
+        for (int q = 0; q < kFreshPT; ++q) {
+            const int o = f0 + tid + 1024 * q;
+            const bool ok = o < f1;
+            const int32_t kk = ok ? ub.fresh[o] : -1;
+            key[kOldPT + q] = kk;
+            prio[kOldPT + q] = prev_mask + 1 + static_cast<uint32_t>(o - f0);
+            on[kOldPT + q] = ok;
+            ps[kOldPT + q] = pr_init(kk, m);
+        }
+        if (tid == 0 && f1 - f0 > 1024 * kFreshPT) s_bad = 1;
+        __syncthreads();
+        for (uint32_t i = tid; i <= m; i += 1024) T[i] = 0xFFFFFFFFu;
+        __syncthreads();
+        if (s_bad) break;
+        settle(T, m, key, prio, ps, on);
+        // priorities -> keys (every slot has one owner)
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q)
+            if (on[q]) T[pr_slot(ps[q])] = static_cast<uint32_t>(key[q]);
+        __syncthreads();
+        prev_mask = m;
+    }
+    if (s_bad) {
+        if (tid == 0) c->status |= kStTable;
+        return;
+    }
+    // the next frontier: keys in slot order, and each slot's rank
+    const uint32_t mf = prev_mask;
+    const int sper = static_cast<int>((mf + 1 + 1023) / 1024);
+    const uint32_t sa = min<uint32_t>(mf + 1, tid * sper), sb = min<uint32_t>(mf + 1, sa + sper);
+    int my_keys = 0;
+    for (uint32_t i = sa; i < sb; ++i) my_keys += T[i] != 0xFFFFFFFFu;
+    int n_src;
+    int rk = block_excl_scan(my_keys, shi, &n_src);
+    if (n_src > nd_next_max) {
+        if (tid == 0) c->status |= kStSize;
+        return;
+    }
+    for (uint32_t i = sa; i < sb; ++i)
+        if (T[i] != 0xFFFFFFFFu) {
+            rank[i] = static_cast<uint16_t>(rk);
+            next.dst[rk++] = static_cast<int32_t>(T[i]);
+        }
+    // pack layout of this hop
+    const int g1 = gcn ? 0 : 1;
+    const int n_nbr = used0 + items_tot - n * g1;
+    __shared__ int off[GS_PK_NFIELDS];
+    if (tid == 0) {
+        int at = c->total;
+        off[GS_PK_NBR_PTR] = at;
+        at += al4(n + 1);
+        off[GS_PK_NBR] = at;
+        at += al4(n_nbr);
+        off[GS_PK_SELF] = at;
+        at += al4(n);
+        off[GS_PK_TPTR] = at;
+        at += al4(n_src + 1);
+        off[GS_PK_TIDX] = at;
+        at += al4(n_nbr + n);
+        c->total = at;
+        for (int f = 0; f < GS_PK_NFIELDS; ++f) h.off[f] = (f >= GS_PK_NBR_PTR) ? off[f] : -1;
+        h.n_src = n_src;
+        h.n_nbr = n_nbr;
+        pack[off[GS_PK_NBR_PTR] + n] = n_nbr;
+    }
+    __syncthreads();
+    // neighbourhoods in frontier-local ids, ascending (the dense mask's
+    // column order, models.py:305-308); non-gcn drops self (:297-298)
+    for (int r = tid; r < n; r += 1024) {
+        const int32_t v = hb.dst[r];
+        const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
+        const int cn = ub.set_cnt[r];
+        const int base = r == 0 ? 0 : used0 + ub.tpre[r] - r * g1;
+        int loc[kMaxItems];
+#pragma unroll
+        for (int q = 0; q < kMaxItems; ++q) {
+            loc[q] = INT_MAX;
+            if (q < cn) {
+                const int32_t kk = it[q];
+                if (!(g1 && kk == v)) loc[q] = rank[find_slot(T, mf, kk)];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kMaxItems; ++q) {
+            if (loc[q] == INT_MAX) continue;
+            int pos = 0;
+#pragma unroll
+            for (int p = 0; p < kMaxItems; ++p) pos += loc[p] < loc[q];
+            pack[off[GS_PK_NBR] + base + pos] = loc[q];
+        }
+        pack[off[GS_PK_NBR_PTR] + r] = base;
+        pack[off[GS_PK_SELF] + r] = rank[find_slot(T, mf, v)];
+    }
+    for (int i = tid; i <= n_src; i += 1024) ub.tcnt[i] = 0;
+}
+
+// ---- transposed lists (GS_PK_TPTR / GS_PK_TIDX)
+
+__global__ void tcount_kernel(Ctl* c, int hop, const int32_t* __restrict__ pack, int32_t* tcnt) {
+    const HopCtl& h = c->hop[hop];
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= h.n_dst || h.n_src <= 0) return;
+    atomicAdd(&tcnt[pack[h.off[GS_PK_SELF] + r]], 1);
+    const int32_t* np = pack + h.off[GS_PK_NBR_PTR];
+    for (int e = np[r]; e < np[r + 1]; ++e) atomicAdd(&tcnt[pack[h.off[GS_PK_NBR] + e]], 1);
+}
+
+__global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
+    __shared__ int shi[17];
+    const HopCtl& h = c->hop[hop];
+    const int ns = h.n_src;
+    if (ns <= 0) return;
+    const int per = (ns + 1023) / 1024;
+    const int a = min(ns, static_cast<int>(threadIdx.x) * per), b = min(ns, a + per);
+    int mine = 0;
+    for (int i = a; i < b; ++i) mine += tcnt[i];
+    int tot;
+    int p = block_excl_scan(mine, shi, &tot);
+    int32_t* tp = pack + h.off[GS_PK_TPTR];
+    for (int i = a; i < b; ++i) {
+        const int cc = tcnt[i];
+        tp[i] = p;
+        tcnt[i] = p;
+        p += cc;
+    }
+    if (threadIdx.x == 0) tp[ns] = tot;
+}
+
+__global__ void tfill_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
+    const HopCtl& h = c->hop[hop];
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= h.n_dst || h.n_src <= 0) return;
+    int32_t* tidx = pack + h.off[GS_PK_TIDX];
+    tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_SELF] + r]], 1)] = -(r + 1);
+    const int32_t* np = pack + h.off[GS_PK_NBR_PTR];
+    for (int e = np[r]; e < np[r + 1]; ++e) tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_NBR] + e]], 1)] = r;
+}
+
+// per source: ascending destination, a destination's self entry before its
+// neighbour entry (host order: -(r+1) then r)
+__global__ void tsort_kernel(Ctl* c, int hop, int32_t* __restrict__ pack) {
+    const HopCtl& h = c->hop[hop];
+    const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cidx >= h.n_src) return;
+    const int32_t* tp = pack + h.off[GS_PK_TPTR];
+    int32_t* x = pack + h.off[GS_PK_TIDX];
+    const int lo = tp[cidx], hi = tp[cidx + 1];
+    auto kf = [](int32_t v) { return v >= 0 ? 2 * v + 1 : -2 * v - 2; };
+    for (int i = lo + 1; i < hi; ++i) {
+        const int32_t v = x[i];
+        const int kv = kf(v);
+        int j = i;
+        while (j > lo && kf(x[j - 1]) > kv) {
+            x[j] = x[j - 1];
+            --j;
+        }
+        x[j] = v;
+    }
+}
+
 void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& ub, const HopBufs& next, int hop,
                       int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st) {
-    fail(GS_EINVAL, "device sampler: multi-hop union not built yet");
+    static const bool attr = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(union_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kUnionMax * (sizeof(uint32_t) + sizeof(uint16_t))) == hipSuccess;
+    }();
+    if (!attr) fail(GS_EHIP, "union_kernel: cannot raise its LDS limit");
+    const int gcn = (flags & GS_SAMPLE_GCN) ? 1 : 0;
+    const unsigned nb64 = static_cast<unsigned>((nd_max + 63) / 64);
+    sets_kernel<<<nb64, 64, 64 * kLaneSet * sizeof(int32_t), st>>>(g, c, hb, ub, hop, k);
+    check_launch("sets_kernel");
+    union_kernel<<<1, 1024, kUnionMax * (sizeof(uint32_t) + sizeof(uint16_t)), st>>>(
+        c, hb, ub, next, hop, gcn, pack, static_cast<int>(nd_next_max));
+    check_launch("union_kernel");
+    const unsigned nb256 = static_cast<unsigned>((nd_max + 255) / 256);
+    tcount_kernel<<<nb256, 256, 0, st>>>(c, hop, pack, ub.tcnt);
+    check_launch("tcount_kernel");
+    tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt);
+    check_launch("tscan_kernel");
+    tfill_kernel<<<nb256, 256, 0, st>>>(c, hop, pack, ub.tcnt);
+    check_launch("tfill_kernel");
+    tsort_kernel<<<static_cast<unsigned>((nd_next_max + 255) / 256), 256, 0, st>>>(c, hop, pack);
+    check_launch("tsort_kernel");
 }
 
 }  // namespace ds

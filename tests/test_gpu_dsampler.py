@@ -141,3 +141,34 @@ def test_device_one_hop_rmat_large():
     mt_d, pos_d = ds.get_rng()
     assert pos_d == pos_h
     np.testing.assert_array_equal(mt_d, mt_h)
+
+
+@pytest.mark.parametrize("fan,gcn", [([25, 10], False), ([10, 10], False), ([3, 5], False), ([25, 10], True),
+                                     ([5, 4, 3], False), ([32, 2], False)])
+def test_device_multi_hop_matches_host(graph, fan, gcn):
+    """Hops before the last: samp_neighs sets, the CPython-order frontier
+    union (resize stages, slot-copy and re-insert copies), neighbourhoods in
+    frontier-local ids, self ids and transposed lists — the whole pack."""
+    fan = np.array(fan, np.int32)
+    flags = L.GS_SAMPLE_GCN if gcn else 0
+    rng_h = gs.RNG(99)
+    ds = gs.sampler.DeviceSampler(graph, fan, 512, gcn=gcn)
+    ds.set_rng(rng_h)
+    deg = graph.degrees()
+    rs = np.random.RandomState(4)
+    for b, B in enumerate([512, 1, 3, 300, 512]):
+        roots = rs.choice(graph.n_nodes, B, replace=True).astype(np.int64)
+        if b == 4:
+            roots[:12] = np.arange(12) * 7 + 1
+            iso = np.nonzero(deg == 0)[0]
+            roots[12:12 + min(8, len(iso))] = iso[:8]
+        ref, sizes, offs, used = host_pack(graph, rng_h, roots, fan, flags)
+        pack, dsz, doff, dused = ds.run(roots)
+        np.testing.assert_array_equal(dsz, sizes, err_msg=f"batch {b}")
+        np.testing.assert_array_equal(doff, offs, err_msg=f"batch {b}")
+        assert dused == used
+        assert_packs_equal(pack[:used].cpu().numpy(), ref, sizes, offs, len(roots), f"batch {b}")
+        mt_h, pos_h = rng_h.getstate()
+        mt_d, pos_d = ds.get_rng()
+        assert pos_d == pos_h
+        np.testing.assert_array_equal(mt_d, mt_h)
