@@ -52,43 +52,48 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 // (absolute word index, exclusive): stages of 227 words, each word
 // x[A] = x[A-227] ^ ((y >> 1) ^ (y & 1 ? MATRIX_A : 0)), y = (x[A-624] & UPPER)
 // | (x[A-623] & LOWER) — CPython's twist loop written on absolute indices (its
-// three index ranges are this one recurrence).  The last 1024 raw words live
-// in LDS; every word goes to both rings (raw for the state, tempered for the
-// draws).
+// three index ranges are this one recurrence).  Lane l owns the residues
+// l, l+64, l+128, l+192 (< 227) of A - g0 mod 227, so x[A-227] is the lane's
+// own previous value (a register) and x[A-624], x[A-623] were written to the
+// LDS ring three stages ago: no dependent LDS round trip per stage.  Every word
+// goes to both rings (raw for the state, tempered for the draws).
 __global__ __launch_bounds__(64) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr, Ctl* c,
                                                     int64_t need_fixed, int need_hop) {
     __shared__ uint32_t L[1024];
     const int lane = threadIdx.x;
-    int64_t g = c->gen_end;
+    const int64_t g0 = c->gen_end;
     const int64_t need = need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
-    if (g >= need) return;
+    if (g0 >= need) return;
     for (int i = lane; i < 624; i += 64) {
-        const int64_t A = g - 624 + i;
+        const int64_t A = g0 - 624 + i;
         L[A & 1023] = xr[A & kRingMask];
     }
     __syncthreads();
-    while (g < need) {
-        uint32_t nx[4];
+    uint32_t prev[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = lane + 64 * q;
-            const int64_t A = g + i;
-            const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023], m = L[(A - 227) & 1023];
-            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-            nx[q] = m ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-        }
-        __syncthreads();
+    for (int q = 0; q < 4; ++q) {
+        const int i = lane + 64 * q;
+        prev[q] = i < 227 ? L[(g0 - 227 + i) & 1023] : 0u;
+    }
+    int64_t g = g0;
+    while (g < need) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int i = lane + 64 * q;
             if (i < 227) {
                 const int64_t A = g + i;
-                L[A & 1023] = nx[q];
-                xr[A & kRingMask] = nx[q];
-                wr[A & kRingMask] = temper(nx[q]);
+                const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023];
+                const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+                const uint32_t x = prev[q] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+                prev[q] = x;
+                L[A & 1023] = x;
+                xr[A & kRingMask] = x;
+                wr[A & kRingMask] = temper(x);
             }
         }
-        __syncthreads();
+        // x[A-623] of the next stage's last word is this stage's first word (A-623
+        // = g+227+226-623 = g-170 <  g: written two stages ago) — every read is
+        // at least 170 words back, so one wave's in-order LDS traffic suffices
         g += 227;
     }
     if (lane == 0) c->gen_end = g;
@@ -272,29 +277,146 @@ __device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const
     return nvalid;
 }
 
-// Block maps: E[b][e] = rejections inside block b when it is entered with
-// lo_b + e rejections so far (0xFFFF: ran past the loaded words).
+// One frontier node's consumption from word u (a word per iteration, so the
+// lanes of a wave stay together apart from the last draw); -1 past the words.
 template <int KMAX>
-__global__ __launch_bounds__(256) void draw_tables_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, int hop,
-                                                          int k, int setsize, int R) {
+__device__ __forceinline__ int walk_root(const uint32_t* __restrict__ w, int nvalid, int u, uint32_t d, int k,
+                                         bool pool) {
+    if (u < 0) return -1;
+    if (pool) {
+        int i = 0;
+        uint32_t m = d;
+        int sh = __clz(m);
+        while (i < k) {
+            if (u >= nvalid) return -1;
+            const uint32_t v = w[u++] >> sh;
+            if (v < m) {
+                ++i;
+                m = d - i;
+                sh = __clz(m | 1u);
+            }
+        }
+        return u;
+    }
+    const int sh = __clz(d);
+    uint32_t sel[KMAX];
+    int cnt = 0;
+    while (cnt < k) {
+        if (u >= nvalid) return -1;
+        const uint32_t v = w[u++] >> sh;
+        bool fresh = v < d;
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == v);
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t)
+            if (t == cnt) sel[t] = v;
+        cnt += fresh;
+    }
+    return u;
+}
+
+// Block maps: E[b][e] = rejections inside block b when it is entered with
+// lo_b + e rejections so far (0xFFFF: ran past the loaded words).  The W
+// entry states are advanced node by node; two states at the same word at a
+// node boundary have the same future, so after every node the states are
+// deduplicated (they stay sorted: a later start never finishes a node
+// earlier; checked) and only the distinct ones are walked on.  Paths from
+// neighbouring entries coalesce slowly — a start one word later is one draw
+// behind on the same words, and the two draws' bounds accept nearly the same
+// words — so this saves ~40 % of the walks (507 against 878 us per hop-2
+// launch at rmat2m), not the W-fold that the window costs.
+template <int KMAX>
+__global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, int hop,
+                                                           int k, int setsize, int R) {
     extern __shared__ uint32_t smem[];
+    __shared__ int shi[17];
+    __shared__ int s_nsr, s_bad;
     const HopCtl& h = c->hop[hop];
     const int b = blockIdx.x;
     if (b >= h.n_blocks) return;
     const int W = h.W;
+    const int tid = threadIdx.x;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
-    int32_t* bdeg = reinterpret_cast<int32_t*>(smem);
-    uint32_t* w = smem + R;
-    for (int q = threadIdx.x; q < nr; q += blockDim.x) bdeg[q] = hb.deg[r0 + q];
+    int32_t* sdeg = reinterpret_cast<int32_t*>(smem);  // sampled nodes' degrees, in order
+    int32_t* U = sdeg + R;                              // distinct states (word index), ascending
+    int32_t* nx = U + kWMax;                            // their successors / the rank map
+    uint16_t* emap = reinterpret_cast<uint16_t*>(nx + kWMax);  // entry -> state index
+    uint32_t* w = reinterpret_cast<uint32_t*>(emap + kWMax);
     const int lo = hb.blo[b];
     const int nw = W + 3 * R * max(k, 1) + 64;
     const int nvalid = load_words(wr, c, h.P0 + hb.dbase[b] + lo, nw, w);
+    if (tid == 0) {
+        int m = 0;
+        for (int q = 0; q < nr; ++q) {
+            const int d = hb.deg[r0 + q];
+            if (k > 0 && d >= k) sdeg[m++] = d;
+        }
+        s_nsr = m;
+        s_bad = 0;
+    }
+    for (int e = tid; e < W; e += 1024) {
+        U[e] = e;
+        emap[e] = static_cast<uint16_t>(e);
+    }
     __syncthreads();
+    const int nsr = s_nsr;
+    int nU = W;
+    for (int q = 0; q < nsr; ++q) {
+        const uint32_t d = static_cast<uint32_t>(sdeg[q]);
+        const bool pool = d <= static_cast<uint32_t>(setsize);
+        const int per = (nU + 1023) / 1024;
+        const int ua = min(nU, tid * per), ub = min(nU, ua + per);
+        for (int u = ua; u < ub; ++u) {
+            const int x = walk_root<KMAX>(w, nvalid, U[u] == INT_MAX ? -1 : U[u], d, k, pool);
+            nx[u] = x < 0 ? INT_MAX : x;
+        }
+        __syncthreads();
+        int f = 0;
+        int prev = ua > 0 ? nx[ua - 1] : -1;
+        for (int u = ua; u < ub; ++u) {
+            const int x = nx[u];
+            if (x < prev) s_bad = 1;
+            f += (u == 0 || x != prev);
+            prev = x;
+        }
+        int tot;
+        int rk = block_excl_scan(f, shi, &tot) - 1;
+        int keep[4], rks[4];
+        prev = ua > 0 ? nx[ua - 1] : -1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int u = ua + t;
+            keep[t] = -1;
+            rks[t] = 0;
+            if (u < ub) {
+                const int x = nx[u];
+                if (u == 0 || x != prev) ++rk;
+                keep[t] = (u == 0 || x != prev) ? x : -1;
+                rks[t] = rk;
+                prev = x;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int u = ua + t;
+            if (u < ub) {
+                if (keep[t] >= 0) U[rks[t]] = keep[t];
+                nx[u] = rks[t];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < W; e += 1024) emap[e] = static_cast<uint16_t>(nx[emap[e]]);
+        nU = tot;
+        __syncthreads();
+    }
+    if (tid == 0 && s_bad) atomicOr(&c->status, kStOrder);
+    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
     uint16_t* E = hb.tab + static_cast<int64_t>(b) * W;
-    for (int e = threadIdx.x; e < W; e += blockDim.x) {
-        const int end = walk_block<KMAX>(w, nvalid, e, bdeg, nr, k, setsize);
-        const int dr = end - e - (hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b]);
-        E[e] = (end < 0 || dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
+    for (int e = tid; e < W; e += 1024) {
+        const int x = U[emap[e]];
+        const int dr = x == INT_MAX ? -1 : x - e - ndr;
+        E[e] = (dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
     }
 }
 
@@ -311,7 +433,11 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
     const int W = h.W, G = h.G;
     const int b0 = gi * G, nbk = min(G, h.n_blocks - b0);
     const bool last_group = gi == h.n_groups - 1;
-    for (int i = threadIdx.x; i < nbk * W; i += blockDim.x) tabs[i] = hb.tab[static_cast<int64_t>(b0) * W + i];
+    {  // W is a multiple of 64: 16-byte loads
+        const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0) * W);
+        uint4* dst = reinterpret_cast<uint4*>(tabs);
+        for (int i = threadIdx.x; i < nbk * W / 8; i += blockDim.x) dst[i] = src[i];
+    }
     for (int i = threadIdx.x; i <= nbk; i += blockDim.x) los[i] = hb.blo[b0 + i];  // blo[nb] exists (setup)
     __syncthreads();
     int32_t* path = hb.path + static_cast<int64_t>(b0) * W;
@@ -386,111 +512,112 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
     }
 }
 
-// Every block from its true entry: lane 0 walks the block once to find each
-// frontier node's first word, then one lane per node replays its draws and
-// emits positions in random.sample's result order (the pool branch through a
-// sparse map of the swapped pool slots), as absolute CSR entries.
-template <int KMAX>
-__global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
-                                                       DevGraph g, int hop, int k, int setsize, int R, int last,
-                                                       int gcn, int32_t* __restrict__ pack) {
-    extern __shared__ uint32_t smem[];
+// Every block from its true entry, one wave: the wave walks the block's
+// nodes in order, 64 words per step — a ballot of the words acceptable for the
+// current draw finds the next accepted one — and emits each node's positions
+// in random.sample's result order as absolute CSR entries.  Pool branch: the
+// swapped pool slots live in lanes (key, value), looked up by ballot;
+// selected-set branch: the node's selected values live in lanes.
+__global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, DevGraph g,
+                                                       int hop, int k, int setsize, int R, int last, int gcn,
+                                                       int32_t* __restrict__ pack) {
+    extern __shared__ uint32_t w[];
     HopCtl& h = c->hop[hop];
     const int b = blockIdx.x;
     if (b >= h.n_blocks) return;
+    const int lane = threadIdx.x;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
-    int32_t* bdeg = reinterpret_cast<int32_t*>(smem);
-    int32_t* rstart = bdeg + R;
-    uint32_t* w = reinterpret_cast<uint32_t*>(rstart + R);
     const int j = hb.entry[b];
     const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    const int nw = 4 * ndr + 64;
-    for (int q = threadIdx.x; q < nr; q += 64) bdeg[q] = hb.deg[r0 + q];
+    const int nw = 4 * ndr + 128;
     const int nvalid = j < 0 ? 0 : load_words(wr, c, h.P0 + hb.dbase[b] + j, nw, w);
     __syncthreads();
     if (j < 0) return;  // reported by the chain
-    if (threadIdx.x == 0) {
-        int idx = 0;
-        for (int q = 0; q < nr; ++q) {
-            rstart[q] = idx;
-            idx = idx < 0 ? -1 : walk_block<KMAX>(w, nvalid, idx, bdeg + q, 1, k, setsize);
-        }
-        if (idx < 0) atomicOr(&c->status, kStWords);
-    }
-    __syncthreads();
     int32_t* ent = last ? pack + h.off[GS_PK_POS] : hb.ent;
-    for (int q = threadIdx.x; q < nr; q += 64) {
+    int u = 0;
+    bool over = false;
+    for (int q = 0; q < nr; ++q) {
         const int r = r0 + q;
         const int32_t v = hb.dst[r];
-        const uint32_t d = static_cast<uint32_t>(bdeg[q]);
+        const uint32_t d = static_cast<uint32_t>(hb.deg[r]);
         const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
         int32_t* out = ent + hb.pos_ptr[r];
-        int idx = rstart[q];
         const bool sampled = k > 0 && d >= static_cast<uint32_t>(k);
-        int cnt = sampled ? k : static_cast<int>(d);
-        if (idx < 0) {
-            for (int t = 0; t < cnt; ++t) out[t] = base;
-        } else if (!sampled) {
-            for (int t = 0; t < cnt; ++t) out[t] = base + t;
+        const int cnt = sampled ? k : static_cast<int>(d);
+        if (!sampled) {
+            for (int t = lane; t < cnt; t += 64) out[t] = base + t;
         } else if (d <= static_cast<uint32_t>(setsize)) {
-            uint32_t mk[KMAX], mv[KMAX];
+            uint32_t mk = 0, mv = 0;  // lane t < nm: pool slot mk holds mv
             int nm = 0;
-            for (int i = 0; i < k; ++i) {
+            for (int i = 0; i < k && !over;) {
                 const uint32_t m = d - i;
                 const int sh = __clz(m);
-                uint32_t x = 0;
-                for (;;) {
-                    x = idx < nvalid ? w[idx] >> sh : 0u;
-                    ++idx;
-                    if (x < m || idx >= nvalid) break;
+                const int at = u + lane;
+                const uint32_t x = at < nvalid ? w[at] >> sh : 0xFFFFFFFFu;
+                const uint64_t acc = __ballot(x < m);
+                if (!acc) {
+                    u += 64;
+                    if (u >= nvalid) over = true;
+                    continue;
                 }
-                uint32_t val = x, lastv = m - 1;
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t) {
-                    if (t < nm && mk[t] == x) val = mv[t];
-                    if (t < nm && mk[t] == m - 1) lastv = mv[t];
+                const int p = __ffsll(static_cast<unsigned long long>(acc)) - 1;
+                const uint32_t xs = __shfl(x, p, 64);
+                u += p + 1;
+                const uint64_t hx = __ballot(lane < nm && mk == xs);
+                const uint64_t hl = __ballot(lane < nm && mk == m - 1);
+                const uint32_t val = hx ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hx)) - 1, 64) : xs;
+                const uint32_t lastv = hl ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hl)) - 1, 64) : m - 1;
+                if (hx) {
+                    if (lane == __ffsll(static_cast<unsigned long long>(hx)) - 1) mv = lastv;
+                } else {
+                    if (lane == nm) {
+                        mk = xs;
+                        mv = lastv;
+                    }
+                    ++nm;
                 }
-                bool found = false;
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t)
-                    if (t < nm && mk[t] == x) {
-                        mv[t] = lastv;
-                        found = true;
-                    }
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t)
-                    if (!found && t == nm) {
-                        mk[t] = x;
-                        mv[t] = lastv;
-                    }
-                nm += !found;
-                out[i] = base + static_cast<int32_t>(val);
+                if (lane == 0) out[i] = base + static_cast<int32_t>(val);
+                ++i;
             }
         } else {
             const int sh = __clz(d);
-            uint32_t sel[KMAX];
+            uint32_t selv = 0xFFFFFFFFu;  // lane t < n_sel: the t-th selected value
             int n_sel = 0;
-            while (n_sel < k && idx < nvalid) {
-                const uint32_t x = w[idx++] >> sh;
-                bool fresh = x < d;
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t) fresh &= !(t < n_sel && sel[t] == x);
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t)
-                    if (t == n_sel) sel[t] = x;
-                if (fresh) out[n_sel] = base + static_cast<int32_t>(x);
-                n_sel += fresh;
+            while (n_sel < k && !over) {
+                const int at = u + lane;
+                const uint32_t x = at < nvalid ? w[at] >> sh : 0xFFFFFFFFu;
+                uint64_t cand = __ballot(x < d);
+                int consumed = 64;
+                while (cand) {
+                    const int p = __ffsll(static_cast<unsigned long long>(cand)) - 1;
+                    cand &= cand - 1;
+                    const uint32_t xs = __shfl(x, p, 64);
+                    if (!__ballot(lane < n_sel && selv == xs)) {
+                        if (lane == n_sel) selv = xs;
+                        if (lane == 0) out[n_sel] = base + static_cast<int32_t>(xs);
+                        ++n_sel;
+                        if (n_sel == k) {
+                            consumed = p + 1;
+                            break;
+                        }
+                    }
+                }
+                u += consumed;
+                if (n_sel < k && u >= nvalid) over = true;
             }
         }
-        // empty neighbourhood after the self rule (non-gcn): no entry, or a
-        // lone entry that is the node itself
-        if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
-        if (last) {
+        if (lane == 0) {
+            // empty neighbourhood after the self rule (non-gcn): no entry, or
+            // a lone entry that is the node itself
+            if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
+        }
+        if (last && lane == 0) {
             pack[h.off[GS_PK_DST_IDS] + r] = v;
             pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
             if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
         }
     }
+    if (lane == 0 && over) atomicOr(&c->status, kStWords);
 }
 
 // Roots after the pack (the host sampler's layout), totals for the host.
@@ -595,24 +722,21 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
     gs::check_launch("mt_gen_kernel");
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
-    const size_t tab_lds = (R + kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
+    const size_t tab_lds = (R + 2 * kWMax) * sizeof(int32_t) + kWMax * sizeof(uint16_t) +
+                           (kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
     if (k <= 16)
-        draw_tables_kernel<16><<<nb_max, 256, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+        draw_tables_kernel<16><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else
-        draw_tables_kernel<32><<<nb_max, 256, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+        draw_tables_kernel<32><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     gs::check_launch("draw_tables_kernel");
     const int ng_max = (nb_max + kMinG - 1) / kMinG;
     draw_compose_kernel<<<ng_max, 256, kComposeEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
     gs::check_launch("draw_compose_kernel");
     draw_chain_kernel<<<1, 1024, kChainEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
     gs::check_launch("draw_chain_kernel");
-    const size_t emit_lds = (2 * R + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
-    if (k <= 16)
-        draw_emit_kernel<16><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R,
-                                                           last ? 1 : 0, gcn, ds->pack_cur);
-    else
-        draw_emit_kernel<32><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R,
-                                                           last ? 1 : 0, gcn, ds->pack_cur);
+    const size_t emit_lds = (4 * R * std::max(k, 1) + 128) * sizeof(uint32_t);
+    draw_emit_kernel<<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R, last ? 1 : 0, gcn,
+                                                   ds->pack_cur);
     gs::check_launch("draw_emit_kernel");
 }
 
@@ -636,6 +760,7 @@ void check_status(int status) {
         gs::fail(GS_ERANGE, "device sampler: a rejection count fell outside its block window (resample on the host)");
     if (status & kStWords) gs::fail(GS_ERANGE, "device sampler: a walk ran past its loaded words");
     if (status & kStTable) gs::fail(GS_ERANGE, "device sampler: frontier union outgrew the device table");
+    if (status & kStOrder) gs::fail(GS_ERANGE, "device sampler: block states out of order");
     if (status & kStSize) gs::fail(GS_ERANGE, "device sampler: frontier outgrew its bound");
     gs::fail(GS_EINVAL, "device sampler: status " + std::to_string(status));
 }

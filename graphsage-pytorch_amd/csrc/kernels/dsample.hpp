@@ -21,6 +21,7 @@ constexpr int kStWords = 2;    // a walk ran past the words loaded for it
 constexpr int kStTable = 4;    // a frontier union outgrew the device table
 constexpr int kStEmpty = 8;    // empty neighbourhood with GS_SAMPLE_FAIL_EMPTY
 constexpr int kStSize = 16;    // a frontier outgrew its preallocated bound
+constexpr int kStOrder = 32;   // block states lost their order (never expected)
 
 struct DevGraph {
     const int64_t* row_ptr;

@@ -196,16 +196,26 @@ __global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb
 
 // Priority-displacement insertion of the keys this thread owns (on[q]) into
 // the LDS table T (all slots EMPTY or holding priorities); returns when every
-// key of the block sits in its final slot.
+// key of the block sits in its final slot.  Rounds: every unplaced key walks
+// its probe sequence until it wins a slot; then every key checks it still
+// holds its slot (a higher-priority key may have taken it) and, if not,
+// steps past it — so rounds follow displacement chains, not probe lengths.
 __device__ __forceinline__ void settle(uint32_t* T, uint32_t mask, const int32_t (&key)[kKPT],
                                        const uint32_t (&prio)[kKPT], uint32_t (&ps)[kKPT], const bool (&on)[kKPT]) {
     bool placed[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) placed[q] = false;
     for (;;) {
+        // claim: walk the probe sequence until a slot is won (empty, or held
+        // by a lower-priority key, which notices below and moves on)
 #pragma unroll
         for (int q = 0; q < kKPT; ++q)
-            if (on[q] && !placed[q]) atomicMin(&T[pr_slot(ps[q])], prio[q]);
+            if (on[q] && !placed[q])
+                for (;;) {
+                    const uint32_t old = atomicMin(&T[pr_slot(ps[q])], prio[q]);
+                    if (old > prio[q]) break;
+                    ps[q] = pr_next(ps[q], key[q], mask);
+                }
         __syncthreads();
         int any = 0;
 #pragma unroll
