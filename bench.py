@@ -443,6 +443,8 @@ def main():
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
                          "each for the issuing thread, the HIP runtime and RCCL's proxy)")
+    ap.add_argument("--no-warm", action="store_true",
+                    help="skip the sampler threads' throwaway warm-up batch (A/B of the cold first batches)")
     ap.add_argument("--sampler-helpers", type=int, default=None,
                     help="helper threads per sampler stream (same draws; lower per-batch latency); "
                          "default 1 with >= 8 host cores per GPU")
@@ -493,7 +495,7 @@ def main():
     # timed steps' batches are sampled inside the timed region (presampled_at_t0)
     runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
                           fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets,
-                          helpers=args.sampler_helpers)
+                          helpers=args.sampler_helpers, warm=not args.no_warm)
     elem = 2 if cfg["dtype"] == "bf16" else 4
     L = len(cfg["fanouts"])
     lib = gs._lib.lib()
@@ -612,6 +614,7 @@ def main():
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
+                       "sampler_contexts_warmed": not args.no_warm,
                        "presampled_at_t0": sampled0 - consumed0,
                        "sampled_in_timed_region": sampled1 - sampled0,
                        "sampled_ahead_at_t1": sampled1 - consumed1,

@@ -170,7 +170,7 @@ class RunnerConfig(ctypes.Structure):
         ("graph", _vp), ("trainer", _vp), ("batches", _vp), ("n_batches", _i64), ("batch", _i64),
         ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
         ("depth", _i32), ("comm", _vp), ("world", _i32), ("embed_out", _vp), ("embed_ld", _i64),
-        ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32), ("helpers", _i32),
+        ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32), ("helpers", _i32), ("warm", _i32),
     ]
 
 

@@ -104,6 +104,9 @@ struct gs_runner {
     // cfg.hold: sampler threads start no batch >= mark until gs_runner_release
     std::atomic<int64_t> release_mark{INT64_MAX};
     std::atomic<int64_t> sampled{0};      // batches whose sampling completed
+    std::mutex warm_mu;                   // cfg.warm: threads done warming
+    std::condition_variable warm_cv;
+    int warmed = 0;
     int64_t next_batch = 0;
     // cfg.ar_buckets == 2: the upper gradients' all-reduce on its own stream
     hipStream_t comm_stream = nullptr;
@@ -158,6 +161,29 @@ void gs_runner::recycle(gs::SamplerStream& s, bool block) {
 }
 
 void gs_runner::sampler_loop(gs::SamplerStream& s) {
+    if (cfg.warm) {
+        // one throwaway batch from a copy of the stream's rng into a free
+        // slot: the context's buffers grow and fault in here, not inside a
+        // measured step; the stream itself does not advance
+        gs_rng* tmp = nullptr;
+        uint32_t mt[624];
+        int64_t pos = 0;
+        if (!s.batches.empty() && !s.free.empty() && gs_rng_create(&tmp) == GS_OK &&
+            gs_rng_get_state(s.rng, mt, &pos) == GS_OK && gs_rng_set_state(tmp, mt, pos) == GS_OK) {
+            gs::PackSlot& slot = s.slots[s.free.front()];
+            const int64_t b = s.batches.back();
+            const int64_t nb = std::min(merge, cfg.n_batches - b * merge);
+            (void)gs_sample_pack_run_multi_team(cfg.graph, tmp, roots.data() + b * merge * cfg.batch, nb * cfg.batch,
+                                                cfg.batch, fanouts.data(), cfg.n_hops, cfg.flags, slot.host, cap,
+                                                slot.hop_sizes, slot.offsets, &slot.used, s.team);
+        }
+        if (tmp) gs_rng_destroy(tmp);
+        {
+            std::lock_guard<std::mutex> lk(warm_mu);
+            ++warmed;
+        }
+        warm_cv.notify_all();
+    }
     for (int64_t b : s.batches) {
         int slot_id;
         {
@@ -416,6 +442,10 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         SamplerStream* sp = s.get();
         gs_runner* rp = r.get();
         s->th = std::thread([rp, sp] { rp->sampler_loop(*sp); });
+    }
+    if (cfg->warm) {
+        std::unique_lock<std::mutex> lk(r->warm_mu);
+        r->warm_cv.wait(lk, [&] { return r->warmed == static_cast<int>(r->streams.size()); });
     }
     *out = r.release();
     GS_API_END

@@ -339,10 +339,12 @@ class Runner:
     communicator): the upper layers' + classifier gradients are all-reduced on
     a comm stream under the layer-1 weight-gradient GEMM, W1's after it.
     `helpers`: helper threads per sampler stream (gs_team; same draws, lower
-    per-batch latency)."""
+    per-batch latency).  `warm`: every sampler thread samples one throwaway
+    batch (its last, from a copy of its rng) before the constructor returns,
+    so measured batches never pay a cold sampling context."""
 
     def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
-                 comm=None, embed_out=None, merge=1, hold=False, ar_buckets=1, helpers=0):
+                 comm=None, embed_out=None, merge=1, hold=False, ar_buckets=1, helpers=0, warm=False):
         self.trainer, self.graph = trainer, graph
         self.embed_out = embed_out
         self.rngs = list(rngs)
@@ -357,7 +359,7 @@ class Runner:
             n_hops=len(self.fanouts), flags=flags, n_streams=len(self.rngs),
             rngs=ctypes.cast(self._rng_ptrs, ctypes.c_void_p), depth=depth,
             comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1,
-            hold=int(bool(hold)), ar_buckets=int(ar_buckets), helpers=int(helpers))
+            hold=int(bool(hold)), ar_buckets=int(ar_buckets), helpers=int(helpers), warm=int(bool(warm)))
         if embed_out is not None:
             n_rows = self.batches.shape[0] * self.batches.shape[1]
             if not (embed_out.is_contiguous() and embed_out.dtype == torch.float32

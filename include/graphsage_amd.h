@@ -576,6 +576,12 @@ typedef struct {
      * for the same draws — for few streams (the reference-sequence S = 1
      * mode) or a cold pipeline.  0: none. */
     int32_t helpers;
+    /* warm != 0: before gs_runner_create returns, every sampler thread (and
+     * its helpers) samples one throwaway batch — the stream's last batch,
+     * drawn from a copy of its rng, so no stream advances and no batch is
+     * sampled ahead — so that no measured batch pays the first-use costs of
+     * the thread's sampling context (allocation, page faults). */
+    int32_t warm;
 } gs_runner_config;
 
 typedef struct {
