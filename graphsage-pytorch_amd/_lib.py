@@ -107,6 +107,7 @@ _SIGS = {
     "gs_clip_sgd": (_i32, [_i32, _vp, _vp, _vp, _f32, _f32, _f32, _vp, _vp]),
     "gs_unsup_create": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _p(_vp)]),
     "gs_unsup_destroy": (None, [_vp]),
+    "gs_unsup_attach_device": (_i32, [_vp, _vp]),
     "gs_unsup_extend": (_i32, [_vp, _vp, _vp, _i64, _i64, _i32, _i32, _vp]),
     "gs_unsup_fetch": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gs_unsup_loss_plan": (_i32, [_vp, _vp, _i64, _vp, _p(_i64)]),

@@ -34,6 +34,7 @@
 #include "graph.hpp"
 #include "pyset.hpp"
 #include "rng.hpp"
+#include "unsup_dev.hpp"
 
 namespace gs {
 namespace {
@@ -120,7 +121,15 @@ struct gs_unsup {
     std::vector<int64_t> pos_cnt, neg_cnt;
     std::vector<uint8_t> has_pos;
     int32_t subset_ok = 0;
+    gs::UnsupDev* dev = nullptr;        // gs_unsup_attach_device: balls + far picks on the GPU
+    ~gs_unsup();
 };
+
+#ifndef GS_HOST_ONLY
+gs_unsup::~gs_unsup() { gs::unsup_dev_destroy(dev); }
+#else
+gs_unsup::~gs_unsup() {}
+#endif
 
 namespace {
 
@@ -172,15 +181,9 @@ void far_lists_word(const gs_unsup& u, int64_t w, int64_t r0, int64_t nr, const 
     for (uint64_t m = fresh_roots; m; m &= m - 1) fresh_set_order(far[64 * w + __builtin_ctzll(m) - r0]);
 }
 
-// The iteration order of a fresh set built by adding `out`'s keys in order.
-void fresh_set_order(std::vector<int32_t>& out) {
-    // A fresh set filled by adds in this order.  Its final table size follows
-    // from the count alone (no deletions: fill == used at every growth check).
-    // When every key owns its home slot key & mask in that table, each add
-    // (and the insert_clean of the last resize) lands at home whatever came
-    // before, so the iteration order is the home-slot order: place directly.
-    // Any shared home slot: replay the adds through the emulator.
-    const int64_t k = static_cast<int64_t>(out.size());
+// Final table mask of a fresh set after k adds of distinct keys (no deletions:
+// fill == used at every growth check, so the size follows from k alone).
+size_t fresh_mask(int64_t k) {
     size_t mask = PySet::MINSIZE - 1;
     for (int64_t used = 1; used <= k; ++used) {
         if (static_cast<size_t>(used) * 5 < mask * 3) {
@@ -192,6 +195,17 @@ void fresh_set_order(std::vector<int32_t>& out) {
         while (ns <= minused) ns <<= 1;
         mask = ns - 1;
     }
+    return mask;
+}
+
+// The iteration order of a fresh set built by adding `out`'s keys in order.
+void fresh_set_order(std::vector<int32_t>& out) {
+    // A fresh set filled by adds in this order.  When every key owns its home
+    // slot key & mask in the final table, each add (and the insert_clean of
+    // the last resize) lands at home whatever came before, so the iteration
+    // order is the home-slot order: place directly.  Any shared home slot:
+    // replay the adds through the emulator.
+    const size_t mask = fresh_mask(static_cast<int64_t>(out.size()));
     thread_local std::vector<int32_t> home;
     home.assign(mask + 1, -1);
     bool clash = false;
@@ -293,9 +307,79 @@ void negative_pairs(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_threads
     if (prof) std::fprintf(stderr, "[unsup] far %.2f ms draw %.2f ms\n", t_far * 1e3, t_draw * 1e3);
 }
 
+#ifndef GS_HOST_ONLY
+// negative_pairs with the balls and the far-list picks on the device (the
+// draws unchanged, on this thread, in node order).  Far-list order per node
+// (see the file header): the copy order when (len(train) >> 2) > len(ball);
+// else a fresh set, whose order is ascending ids when its final table has a
+// home slot per id (mask + 1 >= n_nodes), and otherwise comes from the host
+// emulator on the node's ball bits.
+void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg) {
+    const int64_t n = static_cast<int64_t>(u.nodes.size());
+    std::vector<int64_t> bsize(n), tib(n);
+    gs::unsup_dev_balls(u.dev, u.nodes.data(), static_cast<int>(n), u.n_walk_len, bsize.data(), tib.data());
+    const int64_t setsize = gs::sample_setsize(num_neg);
+    std::vector<int32_t> pool;
+    std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
+    std::vector<int32_t> req_r, req_j, host_far;
+    std::vector<uint8_t> req_kind;
+    std::vector<int32_t> direct;      // ids picked on the host (fallback nodes), request order
+    std::vector<uint8_t> is_direct;   // per request
+    std::vector<uint64_t> bits;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = u.n_train_set - tib[i];
+        int kind = 0;
+        if (!((u.n_train_set >> 2) > bsize[i])) kind = fresh_mask(len) + 1 >= static_cast<size_t>(u.g->n_nodes) ? 1 : 2;
+        if (kind == 2) {  // the host emulator on this node's ball
+            if (bits.empty()) gs::unsup_dev_ball_bits(u.dev, static_cast<int>(n), bits);
+            const uint64_t* S = bits.data() + (i >> 6) * u.g->n_nodes;
+            host_far.clear();
+            for (int32_t x : u.train_order)
+                if (!((S[x] >> (i & 63)) & 1)) host_far.push_back(x);
+            fresh_set_order(host_far);
+        }
+        auto want = [&](int64_t j) {
+            req_r.push_back(static_cast<int32_t>(i));
+            req_j.push_back(static_cast<int32_t>(j));
+            req_kind.push_back(static_cast<uint8_t>(kind == 1));
+            is_direct.push_back(kind == 2);
+            if (kind == 2) direct.push_back(host_far[static_cast<size_t>(j)]);
+        };
+        if (num_neg < len) {
+            if (len <= setsize) pool.resize(static_cast<size_t>(len));
+            gs::sample_positions(rng->mt, len, num_neg, setsize, picks.data(), pool.data());
+            for (int64_t t = 0; t < num_neg; ++t) want(picks[t]);
+            u.neg_cnt[i] = num_neg;
+        } else {
+            for (int64_t t = 0; t < len; ++t) want(t);
+            u.neg_cnt[i] = len;
+        }
+    }
+    std::vector<int32_t> ids;
+    gs::unsup_dev_select(u.dev, req_r, req_j, req_kind, ids);
+    size_t dq = 0;
+    for (size_t q = 0; q < req_r.size(); ++q) {
+        u.neg.push_back(u.nodes[static_cast<size_t>(req_r[q])]);
+        u.neg.push_back(is_direct[q] ? direct[dq++] : ids[q]);
+    }
+}
+#endif
+
 }  // namespace
 
 extern "C" {
+
+int gs_unsup_attach_device(gs_unsup* u, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(u, GS_EINVAL, "NULL argument");
+#ifdef GS_HOST_ONLY
+    (void)stream;
+    gs::fail(GS_EINVAL, "host-only build: no device");
+#else
+    if (!u->dev) u->dev = gs::unsup_dev_create(*u->g, u->copy_order, stream);
+#endif
+    GS_API_END
+}
 
 int gs_unsup_create(const gs_graph* graph, const int64_t* train_nodes, int64_t n_train, int32_t n_walks,
                     int32_t walk_len, int32_t n_walk_len, gs_unsup** out) {
@@ -341,6 +425,10 @@ int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, i
     u->has_pos.assign(n, 0);
     u->subset_ok = 0;
     if (parts & 1) walk_pairs(*u, rng);
+#ifndef GS_HOST_ONLY
+    if ((parts & 2) && u->dev) negative_pairs_dev(*u, rng, num_neg);
+    else
+#endif
     if (parts & 2) negative_pairs(*u, rng, num_neg, n_threads);
 
     PySet a, b;  // models.py:146

@@ -1,0 +1,318 @@
+// extend_nodes' negatives on the device (models.py:152-164):
+// the N_WALK_LEN-hop balls of a batch's nodes as a bit-parallel multi-source
+// BFS (bit b of word w = node 64w+b, 64 balls per 64-bit word, word-major
+// [w][node]), and the far-list elements the host's draws pick.
+//
+// The far list of a node is set(train) - ball in CPython iteration order
+// (host/unsup.cpp, file header): either the train set's copy order with the
+// ball's members skipped, or — when the ball is large — a fresh set filled in
+// train order, whose iteration order is ascending ids whenever its final table
+// has a slot per id (mask + 1 >= n_nodes: every key at home).  Both are a
+// fixed order of the train nodes filtered by "not in this ball", so the j-th
+// element is a select query: per (ball word, 64 consecutive order entries) one
+// ballot per ball gives the 64-bit mask of far entries, a per-ball prefix over
+// the chunk counts finds the chunk, and the rank inside the chunk the entry.
+// The host keeps the sequential part (the draws, models.py:164, on the one
+// random stream) and reads back only the counts and the picked ids.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../host/graph.hpp"
+#include "../host/unsup_dev.hpp"
+#include "kcommon.hpp"
+
+namespace gs {
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+__global__ void ball_seed_kernel(const int32_t* __restrict__ roots, int n_roots, int64_t n_nodes,
+                                 unsigned long long* __restrict__ S, unsigned long long* __restrict__ E) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_roots) return;
+    const int64_t at = static_cast<int64_t>(r >> 6) * n_nodes + roots[r];
+    const unsigned long long bit = 1ull << (r & 63);
+    atomicOr(&S[at], bit);
+    atomicOr(&E[at], bit);
+}
+
+// One BFS level (models.py:156-161: current |= adj[outer] for outer in
+// frontier): every node with frontier bits pushes them to its neighbours.
+__global__ void ball_push_kernel(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+                                 int64_t n_nodes, int n_words, const unsigned long long* __restrict__ E,
+                                 unsigned long long* __restrict__ X) {
+    const int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    if (i >= n_nodes * n_words) return;
+    const unsigned long long f = E[i];
+    if (!f) return;
+    const int64_t w = i / n_nodes, u = i - w * n_nodes;
+    unsigned long long* Xw = X + w * n_nodes;
+    for (int64_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) atomicOr(&Xw[col[e]], f);
+}
+
+// frontier = current - neighbors; neighbors |= current (models.py:160-161)
+__global__ void ball_step_kernel(int64_t total, unsigned long long* __restrict__ S, unsigned long long* __restrict__ E,
+                                 unsigned long long* __restrict__ X) {
+    const int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    if (i >= total) return;
+    const unsigned long long nw = X[i] & ~S[i];
+    E[i] = nw;
+    S[i] |= nw;
+    X[i] = 0;
+}
+
+// Per ball (one block per word, lane b of every wave counting ball 64w+b):
+// len(neighbors) over all nodes and |train ∩ ball| over the train ids.
+__global__ __launch_bounds__(256) void ball_count_kernel(const unsigned long long* __restrict__ S, int64_t n_nodes,
+                                                          const int32_t* __restrict__ train, int n_train,
+                                                          int n_roots, int64_t* __restrict__ size,
+                                                          int64_t* __restrict__ in_train) {
+    __shared__ int64_t acc[2][4][64];
+    const int w = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long* Sw = S + static_cast<int64_t>(w) * n_nodes;
+    int64_t cs = 0, ct = 0;
+    for (int64_t base = 64 * wave; base < n_nodes; base += 256) {
+        const int64_t u = base + lane;
+        const unsigned long long x = u < n_nodes ? Sw[u] : 0ull;
+        for (int b = 0; b < 64; ++b) {
+            const int c = __popcll(__ballot((x >> b) & 1ull));
+            if (lane == b) cs += c;
+        }
+    }
+    for (int base = 64 * wave; base < n_train; base += 256) {
+        const int t = base + lane;
+        const unsigned long long x = t < n_train ? Sw[train[t]] : 0ull;
+        for (int b = 0; b < 64; ++b) {
+            const int c = __popcll(__ballot((x >> b) & 1ull));
+            if (lane == b) ct += c;
+        }
+    }
+    acc[0][wave][lane] = cs;
+    acc[1][wave][lane] = ct;
+    __syncthreads();
+    if (wave == 0) {
+        const int r = 64 * w + lane;
+        if (r < n_roots) {
+            size[r] = acc[0][0][lane] + acc[0][1][lane] + acc[0][2][lane] + acc[0][3][lane];
+            in_train[r] = acc[1][0][lane] + acc[1][1][lane] + acc[1][2][lane] + acc[1][3][lane];
+        }
+    }
+}
+
+// Far masks: for order entries 64c .. 64c+63 and the 64 balls of word w,
+// M[r][c] = entries NOT in ball r (one ballot per ball); cnt in pre[r][c].
+__global__ __launch_bounds__(64) void far_mask_kernel(const unsigned long long* __restrict__ S, int64_t n_nodes,
+                                                       const int32_t* __restrict__ order, int n_order, int n_chunks,
+                                                       int n_roots, unsigned long long* __restrict__ M,
+                                                       int32_t* __restrict__ cnt) {
+    const int c = blockIdx.x, w = blockIdx.y, lane = threadIdx.x;
+    const int t = 64 * c + lane;
+    const bool ok = t < n_order;
+    const unsigned long long x = ok ? S[static_cast<int64_t>(w) * n_nodes + order[t]] : ~0ull;
+    unsigned long long mine = 0;
+    for (int b = 0; b < 64; ++b) {
+        const unsigned long long m = __ballot(ok && !((x >> b) & 1ull));
+        if (lane == b) mine = m;
+    }
+    const int r = 64 * w + lane;
+    if (r < n_roots) {
+        M[static_cast<int64_t>(r) * n_chunks + c] = mine;
+        cnt[static_cast<int64_t>(r) * (n_chunks + 1) + c] = __popcll(mine);
+    }
+}
+
+// Exclusive prefix of the chunk counts, one wave per ball.
+__global__ __launch_bounds__(64) void far_prefix_kernel(int32_t* __restrict__ pre, int n_chunks) {
+    int32_t* p = pre + static_cast<int64_t>(blockIdx.x) * (n_chunks + 1);
+    const int lane = threadIdx.x;
+    int run = 0;
+    for (int base = 0; base < n_chunks; base += 64) {
+        const int c = base + lane;
+        const int v = c < n_chunks ? p[c] : 0;
+        int inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        if (c < n_chunks) p[c] = run + inc - v;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) p[n_chunks] = run;
+}
+
+// The picks: request q = (ball r, order kind, position j) -> order[entry].
+__global__ void far_select_kernel(const int32_t* __restrict__ req_r, const int32_t* __restrict__ req_j,
+                                  const uint8_t* __restrict__ req_kind, int n_req, int n_chunks,
+                                  const unsigned long long* __restrict__ M0, const int32_t* __restrict__ pre0,
+                                  const int32_t* __restrict__ order0, const unsigned long long* __restrict__ M1,
+                                  const int32_t* __restrict__ pre1, const int32_t* __restrict__ order1,
+                                  int32_t* __restrict__ out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_req) return;
+    const int r = req_r[q], j = req_j[q];
+    const bool k1 = req_kind[q] != 0;
+    const int32_t* p = (k1 ? pre1 : pre0) + static_cast<int64_t>(r) * (n_chunks + 1);
+    int lo = 0, hi = n_chunks - 1;  // last chunk with p[c] <= j
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (p[mid] <= j) lo = mid;
+        else hi = mid - 1;
+    }
+    unsigned long long m = (k1 ? M1 : M0)[static_cast<int64_t>(r) * n_chunks + lo];
+    for (int t = j - p[lo]; t > 0; --t) m &= m - 1;
+    out[q] = (k1 ? order1 : order0)[64 * lo + __ffsll(m) - 1];
+}
+
+}  // namespace
+
+struct UnsupDev {
+    int64_t n_nodes = 0;
+    int n_order = 0, n_chunks = 0;
+    std::vector<void*> owned;
+    const int64_t* row_ptr = nullptr;
+    const int32_t* col = nullptr;
+    int32_t* copy_order = nullptr;  // list(set(train).copy())
+    int32_t* asc_order = nullptr;   // sorted(set(train))
+    int cap_roots = 0;
+    unsigned long long *S = nullptr, *E = nullptr, *X = nullptr;
+    int32_t* roots = nullptr;
+    int64_t* counts = nullptr;  // [2][cap_roots]
+    unsigned long long *M0 = nullptr, *M1 = nullptr;
+    int32_t *pre0 = nullptr, *pre1 = nullptr;
+    int cap_req = 0;
+    int32_t *req_r = nullptr, *req_j = nullptr, *picks = nullptr;
+    uint8_t* req_kind = nullptr;
+    hipStream_t st = nullptr;
+
+    template <typename T>
+    T* alloc(int64_t n) {
+        void* p = nullptr;
+        hip_ok(hipMalloc(&p, std::max<int64_t>(n, 1) * sizeof(T)), "hipMalloc(unsup dev)");
+        owned.push_back(p);
+        return static_cast<T*>(p);
+    }
+    void free_all() {
+        for (void* p : owned) (void)hipFree(p);
+        owned.clear();
+    }
+};
+
+UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_order, void* stream) {
+    auto d = std::make_unique<UnsupDev>();
+    d->st = as_stream(stream);
+    d->n_nodes = g.n_nodes;
+    d->n_order = static_cast<int>(copy_order.size());
+    d->n_chunks = std::max(1, (d->n_order + 63) / 64);
+    auto up = [&](const void* src, size_t bytes) {
+        void* p = d->alloc<uint8_t>(static_cast<int64_t>(bytes));
+        if (bytes) hip_ok(hipMemcpy(p, src, bytes, hipMemcpyHostToDevice), "hipMemcpy(unsup dev)");
+        return p;
+    };
+    d->row_ptr = static_cast<const int64_t*>(up(g.row_ptr.data(), g.row_ptr.size() * sizeof(int64_t)));
+    d->col = static_cast<const int32_t*>(up(g.col.data(), g.col.size() * sizeof(int32_t)));
+    std::vector<int32_t> asc(copy_order);
+    std::sort(asc.begin(), asc.end());
+    d->copy_order = static_cast<int32_t*>(up(copy_order.data(), copy_order.size() * sizeof(int32_t)));
+    d->asc_order = static_cast<int32_t*>(up(asc.data(), asc.size() * sizeof(int32_t)));
+    return d.release();
+}
+
+void unsup_dev_destroy(UnsupDev* d) {
+    if (!d) return;
+    d->free_all();
+    delete d;
+}
+
+static void reserve_roots(UnsupDev* d, int n) {
+    if (n <= d->cap_roots) return;
+    const int cap = std::max(n, 64);
+    const int64_t words = (cap + 63) / 64;
+    d->S = d->alloc<unsigned long long>(words * d->n_nodes);
+    d->E = d->alloc<unsigned long long>(words * d->n_nodes);
+    d->X = d->alloc<unsigned long long>(words * d->n_nodes);
+    d->roots = d->alloc<int32_t>(cap);
+    d->counts = d->alloc<int64_t>(2 * cap);
+    d->M0 = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
+    d->M1 = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
+    d->pre0 = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
+    d->pre1 = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
+    d->cap_roots = cap;
+}
+
+void unsup_dev_balls(UnsupDev* d, const int64_t* nodes, int n, int hops, int64_t* ball_size, int64_t* train_in_ball) {
+    reserve_roots(d, n);
+    const int n_words = (n + 63) / 64;
+    const int64_t total = static_cast<int64_t>(n_words) * d->n_nodes;
+    std::vector<int32_t> r32(nodes, nodes + n);
+    hipStream_t st = d->st;
+    hip_ok(hipMemcpyAsync(d->roots, r32.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    hip_ok(hipMemsetAsync(d->S, 0, total * 8, st), "hipMemsetAsync");
+    hip_ok(hipMemsetAsync(d->E, 0, total * 8, st), "hipMemsetAsync");
+    hip_ok(hipMemsetAsync(d->X, 0, total * 8, st), "hipMemsetAsync");
+    ball_seed_kernel<<<(n + 255) / 256, 256, 0, st>>>(d->roots, n, d->n_nodes, d->S, d->E);
+    check_launch("ball_seed_kernel");
+    const unsigned nb = static_cast<unsigned>((total + 255) / 256);
+    for (int h = 0; h < hops; ++h) {
+        ball_push_kernel<<<nb, 256, 0, st>>>(d->row_ptr, d->col, d->n_nodes, n_words, d->E, d->X);
+        check_launch("ball_push_kernel");
+        ball_step_kernel<<<nb, 256, 0, st>>>(total, d->S, d->E, d->X);
+        check_launch("ball_step_kernel");
+    }
+    ball_count_kernel<<<n_words, 256, 0, st>>>(d->S, d->n_nodes, d->asc_order, d->n_order, n, d->counts,
+                                               d->counts + d->cap_roots);
+    check_launch("ball_count_kernel");
+    // far masks and their prefixes for both orders (needed by the picks)
+    const dim3 mg(static_cast<unsigned>(d->n_chunks), static_cast<unsigned>(n_words));
+    far_mask_kernel<<<mg, 64, 0, st>>>(d->S, d->n_nodes, d->copy_order, d->n_order, d->n_chunks, n, d->M0, d->pre0);
+    check_launch("far_mask_kernel");
+    far_mask_kernel<<<mg, 64, 0, st>>>(d->S, d->n_nodes, d->asc_order, d->n_order, d->n_chunks, n, d->M1, d->pre1);
+    check_launch("far_mask_kernel");
+    far_prefix_kernel<<<n, 64, 0, st>>>(d->pre0, d->n_chunks);
+    check_launch("far_prefix_kernel");
+    far_prefix_kernel<<<n, 64, 0, st>>>(d->pre1, d->n_chunks);
+    check_launch("far_prefix_kernel");
+    hip_ok(hipMemcpyAsync(ball_size, d->counts, n * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(train_in_ball, d->counts + d->cap_roots, n * sizeof(int64_t), hipMemcpyDeviceToHost, st),
+           "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
+void unsup_dev_ball_bits(UnsupDev* d, int n, std::vector<uint64_t>& bits) {
+    const int64_t total = static_cast<int64_t>((n + 63) / 64) * d->n_nodes;
+    bits.resize(static_cast<size_t>(total));
+    hip_ok(hipMemcpyAsync(bits.data(), d->S, total * 8, hipMemcpyDeviceToHost, d->st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(d->st), "hipStreamSynchronize");
+}
+
+void unsup_dev_select(UnsupDev* d, const std::vector<int32_t>& req_r, const std::vector<int32_t>& req_j,
+                      const std::vector<uint8_t>& req_kind, std::vector<int32_t>& out) {
+    const int n = static_cast<int>(req_r.size());
+    out.resize(n);
+    if (!n) return;
+    if (n > d->cap_req) {
+        const int cap = std::max(n, 1024);
+        d->req_r = d->alloc<int32_t>(cap);
+        d->req_j = d->alloc<int32_t>(cap);
+        d->picks = d->alloc<int32_t>(cap);
+        d->req_kind = d->alloc<uint8_t>(cap);
+        d->cap_req = cap;
+    }
+    hipStream_t st = d->st;
+    hip_ok(hipMemcpyAsync(d->req_r, req_r.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(d->req_j, req_j.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(d->req_kind, req_kind.data(), n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    far_select_kernel<<<(n + 255) / 256, 256, 0, st>>>(d->req_r, d->req_j, d->req_kind, n, d->n_chunks, d->M0,
+                                                        d->pre0, d->copy_order, d->M1, d->pre1, d->asc_order,
+                                                        d->picks);
+    check_launch("far_select_kernel");
+    hip_ok(hipMemcpyAsync(out.data(), d->picks, n * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
+}  // namespace gs

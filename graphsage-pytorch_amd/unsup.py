@@ -54,9 +54,12 @@ class UnsupervisedLoss:
 
     adj_lists may be the reference's dict of sets (adopted with its set
     layouts) or a CSRGraph.  ``rng``: a sampler.RNG to draw from instead of the
-    module-global ``random`` (the reference always uses the global stream)."""
+    module-global ``random`` (the reference always uses the global stream).
+    ``device_balls``: grow extend_nodes' 5-hop balls and pick the far-list
+    negatives on the GPU (gs_unsup_attach_device; same results and stream);
+    default: when ``device`` is a HIP device."""
 
-    def __init__(self, adj_lists, train_nodes, device, *, rng=None, n_threads=None):
+    def __init__(self, adj_lists, train_nodes, device, *, rng=None, n_threads=None, device_balls=None):
         self.Q = 10
         self.N_WALKS = 6
         self.WALK_LEN = 1
@@ -69,6 +72,8 @@ class UnsupervisedLoss:
         self.unique_nodes_batch = []
         self.rng = rng
         self.n_threads = n_threads or _threads()
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.device_balls = (dev.type == "cuda") if device_balls is None else bool(device_balls)
         self._reset_pairs()
         if isinstance(adj_lists, CSRGraph):
             self.graph = adj_lists
@@ -87,6 +92,8 @@ class UnsupervisedLoss:
         check(lib().gs_unsup_create(self.graph.handle, ptr(tr), len(tr), self.N_WALKS, self.WALK_LEN,
                                     self.N_WALK_LEN, ctypes.byref(h)))
         self._h = h
+        if self.device_balls:
+            check(lib().gs_unsup_attach_device(h, _lib.stream_ptr()))
         self._params = (self.N_WALKS, self.WALK_LEN, self.N_WALK_LEN)
 
     def _run(self, nodes, num_neg, parts):

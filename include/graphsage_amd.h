@@ -254,6 +254,14 @@ int gs_unsup_create(const gs_graph* g, const int64_t* train_nodes, int64_t n_tra
                     int32_t n_walks, int32_t walk_len, int32_t n_walk_len,
                     gs_unsup** out);
 void gs_unsup_destroy(gs_unsup* u);
+/* Grow the n_walk_len-hop balls (models.py:154-162) on the GPU — a
+ * bit-parallel multi-source BFS, 64 balls per 64-bit word — and pick the
+ * negatives' far-list elements there (select queries over set(train)'s order
+ * with the ball's members skipped); the draws of models.py:164 stay on the
+ * calling thread in node order, so every result and the rng stream are those
+ * of the host path.  Uploads the CSR once; `stream` orders
+ * the device work (each extend synchronises it). */
+int gs_unsup_attach_device(gs_unsup* u, void* stream);
 /* parts: 1 = the walks only (get_positive_nodes, models.py:149), 2 = the
  * negatives only (get_negtive_nodes, :152), 3 = both (extend_nodes).
  * sizes[4] = (len(unique_nodes_batch), len(positive_pairs),
