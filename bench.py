@@ -61,11 +61,13 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # the trainer's kernel timer sites (gs_trainer_time_kernels)
-SITES = (0, 1, 2)
-SITE_NAMES = {0: "gather", 1: "fwd", 2: "dw"}
+SITES = (0, 1, 2, 3)
+SITE_NAMES = {0: "gather", 1: "fwd", 2: "dw", 3: "top"}
 SITE_ROLES = {0: "layer-1 gather-aggregate (models.py:291-330 at layer 1)",
               1: "layer-1 SageLayer forward GEMM relu([X[self] | agg]·W1ᵀ) (models.py:216-219)",
-              2: "layer-1 weight-gradient GEMM dW1 = dZ1ᵀ·[X[self] | agg] row slabs (autograd of models.py:219)"}
+              2: "layer-1 weight-gradient GEMM dW1 = dZ1ᵀ·[X[self] | agg] row slabs (autograd of models.py:219)",
+              3: "top layer + loss head in one launch: layer-2 aggregate, linear + relu, log_softmax/NLL, dZ2, "
+                 "dIn2 = dZ2·W2 (models.py:291-330, :216-219, :8-27; utils.py:159-164)"}
 MFMA_PEAK_TFS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: dense F32 / BF16 matrix peaks (spec)
 
 
@@ -144,6 +146,13 @@ def agg1_bytes(n_dst, n_pos, F, elem):
     column entries (4 B each) + one output row per destination + per-destination
     metadata (dst id 4 B, row_ptr 8 B, pos_ptr 4 B)."""
     return n_pos * (F * elem + 8) + n_dst * (F * elem + 16)
+
+
+def top_bytes(B, n_nbr, H, C):
+    """Algorithmic HBM bytes of one fused top launch (kernels/top.hip): the
+    roots' neighbour and self rows of h1, their neighbour lists, W2 and the
+    classifier, and the rows it writes (agg, E, dZ: H each; dIn: 2H)."""
+    return (n_nbr + B) * H * 4 + n_nbr * 4 + H * 2 * H * 4 + C * (H + 1) * 4 + B * 5 * H * 4
 
 
 def agg1_ids_bytes(n_dst, n_pos, F, elem, k):
@@ -503,7 +512,7 @@ def main():
     # warmup: every timer site armed; the site with the longest median launch
     # is the dominant kernel, the one timed inside the measured steps
     runner.release(args.warmup)
-    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 0b111, args.warmup))
+    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, (1 << len(SITES)) - 1, args.warmup))
     runner.run(args.warmup)
     torch.cuda.synchronize()
     warm = {site: kernel_times_ms(trainer, args.warmup, site) for site in SITES}
@@ -582,9 +591,10 @@ def main():
             if tt is None or not len(tt):
                 continue
             us = float(np.mean(tt)) * 1e3
-            if site == 0:
-                achieved, peak, unit, bound = float(agg_bytes) / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
-                work = {"algo_bytes_per_launch": int(agg_bytes)}
+            if site in (0, 3):
+                nb = agg_bytes if site == 0 else top_bytes(cfg["batch"], float(sizes[0, 3]), 128, cfg["classes"])
+                achieved, peak, unit, bound = float(nb) / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+                work = {"algo_bytes_per_launch": int(nb)}
             else:
                 peak = MFMA_PEAK_TFS[cfg["dtype"]]
                 achieved, unit, bound = gemm_flops / (us * 1e-6) / 1e12, "TFLOP/s", "mfma"

@@ -22,8 +22,8 @@ struct gs_trainer {
     bool fused2 = false;  // layers >= 2 likewise (explicit lists; MEAN)
     // optional kernel-bound HIP-event timing (bench roofline): site 0 the
     // layer-1 gather-aggregate, 1 the layer-1 linear forward, 2 its weight
-    // gradient (the MFMA kernels)
-    static constexpr int kSites = 3;
+    // gradient (the MFMA kernels), 3 the fused top layer + loss head (top.hip)
+    static constexpr int kSites = 4;
     struct Timer {
         std::vector<hipEvent_t> ev0, ev1;
         int64_t n = 0;
@@ -300,9 +300,11 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         if (fusable) {
             int cls_rows;
             if (top) {
+                const bool armed = timed_arm(T, 3);
                 cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
                                        fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
                                        roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st);
+                timed_done(T, 3, armed);
                 lb[0].din_ready = true;
             } else {
                 cls_rows = cls_rows_launch(B, H, c.n_classes, h[L - 1], P + T.cls_w_off, P + T.cls_b_off, c.labels,

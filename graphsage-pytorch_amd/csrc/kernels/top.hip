@@ -404,8 +404,8 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
               aggo, argmax, E, dZ, dIn, slab};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
-    if (agg == GS_AGG_MEAN) sage_top_kernel<GS_AGG_MEAN><<<grid, kTopThreads, smem, st>>>(a);
-    else sage_top_kernel<GS_AGG_MAX><<<grid, kTopThreads, smem, st>>>(a);
+    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);
+    else launch_k(sage_top_kernel<GS_AGG_MAX>, grid, dim3(kTopThreads), smem, st, a);
     check_launch("sage_top");
     return static_cast<int>(grid.x);
 }

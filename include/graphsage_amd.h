@@ -508,7 +508,8 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 /* The same timers per site: 0 the layer-1 gather as above, 1 the layer-1
  * SageLayer forward GEMM (gs_sage_linear_fwd, unfused path), 2 the layer-1
  * weight-gradient GEMM of the fused backward (linear_dw slabs, before their
- * sum).  gs_trainer_time_kernels arms the sites in site_mask (bit s = site
+ * sum), 3 the fused top layer + loss head launch (2-layer models).
+ * gs_trainer_time_kernels arms the sites in site_mask (bit s = site
  * s) for their next `capacity` launches and disarms the others;
  * gs_trainer_time_agg(t, n) == gs_trainer_time_kernels(t, 1, n).  Every
  * armed launch is an event-bound hipExtLaunchKernel, which costs the stream

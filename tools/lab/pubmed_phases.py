@@ -1,0 +1,33 @@
+"""Phase times of the pubmed apply_model step (bench.py --config pubmed):
+extend_nodes (device balls) / GraphSage forward (host sampler + kernels) /
+head + backward + clip + SGD."""
+import sys, time, importlib, random
+sys.path.insert(0, '.')
+import numpy as np, torch
+bench = importlib.import_module("bench")
+models = importlib.import_module("graphsage-pytorch_amd.models")
+unsup = importlib.import_module("graphsage-pytorch_amd.unsup")
+utils = importlib.import_module("graphsage-pytorch_amd.utils")
+cfg = dict(bench.CONFIGS["pubmed"])
+dev = torch.device("cuda", 0)
+wl = bench.pubmed_workload(cfg, dev)
+torch.manual_seed(824)
+g = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], dev, agg_func="MEAN", fanouts=[10, 10]).to(dev)
+cls = models.Classification(128, cfg["classes"]).to(dev)
+for mode in (True, False):
+    ul = unsup.UnsupervisedLoss(wl["graph"], wl["train"], dev, n_threads=16, device_balls=mode)
+    opt = torch.optim.SGD([p for m in (g, cls) for p in m.parameters()], lr=0.7)
+    order = np.random.RandomState(1).permutation(wl["train"])
+    random.seed(824)
+    T = {"extend": [], "forward": [], "rest": []}
+    for i in range(12):
+        b = order[(i % 20) * 512:(i % 20 + 1) * 512]
+        torch.cuda.synchronize(); t0 = time.perf_counter()
+        nodes = np.asarray(list(ul.extend_nodes(b, num_neg=100)))
+        t1 = time.perf_counter()
+        embs = g(nodes); torch.cuda.synchronize(); t2 = time.perf_counter()
+        loss = utils.supervised_loss(cls, embs, wl["labels"][nodes]) if hasattr(utils, "supervised_loss") else None
+        loss.backward(); opt.step(); opt.zero_grad(); torch.cuda.synchronize(); t3 = time.perf_counter()
+        if i >= 2:
+            T["extend"].append(t1 - t0); T["forward"].append(t2 - t1); T["rest"].append(t3 - t2)
+    print("device_balls", mode, {k: round(float(np.median(v)) * 1e3, 2) for k, v in T.items()}, flush=True)
