@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #ifndef GS_SELECT_SMALL
 #define GS_SELECT_SMALL 1
@@ -312,6 +313,28 @@ inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize
     } else if (GS_SELECT_SMALL && k <= 32 && n < (int64_t(1) << 31)) {
         if (k <= 16 && select_fast16(rng, n, k, out)) return;
         select_chunked(rng, n, k, out);
+    } else if (n <= (int64_t(1) << 24)) {
+        // selected-set branch for larger k (extend_nodes' num_neg = 100 over
+        // far lists of ~10^4): the selected values in a thread-local bitmap
+        // (cleared through out[] afterwards) instead of a scan of all of them
+        // per word — the same words consumed, the same values in order.
+        thread_local std::vector<uint64_t> seen;
+        const size_t words = static_cast<size_t>((n + 63) >> 6);
+        if (seen.size() < words) seen.resize(words, 0);
+        const int sh = 32 - (64 - __builtin_clzll(static_cast<uint64_t>(n)));
+        int64_t cnt = 0;
+        while (cnt < k) {
+            const uint32_t r = rng.next() >> sh;
+            if (static_cast<int64_t>(r) < n) {
+                uint64_t& w = seen[r >> 6];
+                const uint64_t bit = uint64_t(1) << (r & 63);
+                if (!(w & bit)) {
+                    w |= bit;
+                    out[cnt++] = static_cast<OutT>(r);
+                }
+            }
+        }
+        for (int64_t t = 0; t < k; ++t) seen[static_cast<size_t>(out[t]) >> 6] = 0;
     } else {
         // selected-set branch: j = randbelow(n), redrawn while j in selected.
         // Both a rejected word (r >= n) and a repeat are simply skipped, so

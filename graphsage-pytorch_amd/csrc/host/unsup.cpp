@@ -314,36 +314,55 @@ void negative_pairs(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_threads
 // else a fresh set, whose order is ascending ids when its final table has a
 // home slot per id (mask + 1 >= n_nodes), and otherwise comes from the host
 // emulator on the node's ball bits.
-void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg) {
+void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_threads) {
+    static const bool prof = std::getenv("GS_UNSUP_PROF") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     const int64_t n = static_cast<int64_t>(u.nodes.size());
     std::vector<int64_t> bsize(n), tib(n);
     gs::unsup_dev_balls(u.dev, u.nodes.data(), static_cast<int>(n), u.n_walk_len, bsize.data(), tib.data());
+    const auto t1 = clk::now();
     const int64_t setsize = gs::sample_setsize(num_neg);
-    std::vector<int32_t> pool;
-    std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
-    std::vector<int32_t> req_r, req_j, host_far;
-    std::vector<uint8_t> req_kind;
-    std::vector<int32_t> direct;      // ids picked on the host (fallback nodes), request order
-    std::vector<uint8_t> is_direct;   // per request
-    std::vector<uint64_t> bits;
+    // far-list order per node: 0 copy order, 1 ascending ids, 2 a fresh set
+    // whose table has fewer slots than ids — its order comes from the host
+    // emulator, over the node's whole far list in set(train) order (fetched
+    // from the device in one batch of select queries)
+    std::vector<int> kind(n);
+    std::vector<int32_t> k2;           // fresh-set nodes
+    std::vector<int64_t> k2base(1, 0);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = u.n_train_set - tib[i];
-        int kind = 0;
-        if (!((u.n_train_set >> 2) > bsize[i])) kind = fresh_mask(len) + 1 >= static_cast<size_t>(u.g->n_nodes) ? 1 : 2;
-        if (kind == 2) {  // the host emulator on this node's ball
-            if (bits.empty()) gs::unsup_dev_ball_bits(u.dev, static_cast<int>(n), bits);
-            const uint64_t* S = bits.data() + (i >> 6) * u.g->n_nodes;
-            host_far.clear();
-            for (int32_t x : u.train_order)
-                if (!((S[x] >> (i & 63)) & 1)) host_far.push_back(x);
-            fresh_set_order(host_far);
+        kind[i] = (u.n_train_set >> 2) > bsize[i] ? 0 : (fresh_mask(len) + 1 >= static_cast<size_t>(u.g->n_nodes) ? 1 : 2);
+        if (kind[i] == 2) {
+            k2.push_back(static_cast<int32_t>(i));
+            k2base.push_back(k2base.back() + len);
         }
+    }
+    std::vector<int32_t> host_far;
+    gs::unsup_dev_far_lists(u.dev, k2, k2base, host_far);
+    // the fresh sets' orders are independent per node: emulate them on the
+    // worker threads, ahead of the draws
+    std::vector<std::vector<int32_t>> fars(k2.size());
+    run_workers(std::max<int32_t>(1, n_threads), static_cast<int64_t>(k2.size()), [&](int64_t q, int32_t) {
+        fars[static_cast<size_t>(q)].assign(host_far.begin() + k2base[q], host_far.begin() + k2base[q + 1]);
+        fresh_set_order(fars[static_cast<size_t>(q)]);
+    });
+    size_t k2i = 0;
+    std::vector<int32_t> pool;
+    std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
+    std::vector<int32_t> req_r, req_j;
+    std::vector<uint8_t> req_kind;
+    std::vector<int32_t> direct;      // ids picked on the host (fresh-set nodes), request order
+    std::vector<uint8_t> is_direct;   // per request
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t len = u.n_train_set - tib[i];
+        const std::vector<int32_t>* farp = kind[i] == 2 ? &fars[k2i++] : nullptr;
         auto want = [&](int64_t j) {
             req_r.push_back(static_cast<int32_t>(i));
             req_j.push_back(static_cast<int32_t>(j));
-            req_kind.push_back(static_cast<uint8_t>(kind == 1));
-            is_direct.push_back(kind == 2);
-            if (kind == 2) direct.push_back(host_far[static_cast<size_t>(j)]);
+            req_kind.push_back(static_cast<uint8_t>(kind[i] == 1));
+            is_direct.push_back(kind[i] == 2);
+            if (kind[i] == 2) direct.push_back((*farp)[static_cast<size_t>(j)]);
         };
         if (num_neg < len) {
             if (len <= setsize) pool.resize(static_cast<size_t>(len));
@@ -355,12 +374,19 @@ void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg) {
             u.neg_cnt[i] = len;
         }
     }
+    const auto t2 = clk::now();
     std::vector<int32_t> ids;
     gs::unsup_dev_select(u.dev, req_r, req_j, req_kind, ids);
     size_t dq = 0;
+    u.neg.reserve(2 * req_r.size());
     for (size_t q = 0; q < req_r.size(); ++q) {
         u.neg.push_back(u.nodes[static_cast<size_t>(req_r[q])]);
         u.neg.push_back(is_direct[q] ? direct[dq++] : ids[q]);
+    }
+    if (prof) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
+        std::fprintf(stderr, "[unsup dev] balls %.2f draws %.2f select %.2f ms (%zu picks)\n", ms(t0, t1), ms(t1, t2),
+                     ms(t2, clk::now()), req_r.size());
     }
 }
 #endif
@@ -376,7 +402,7 @@ int gs_unsup_attach_device(gs_unsup* u, void* stream) {
     (void)stream;
     gs::fail(GS_EINVAL, "host-only build: no device");
 #else
-    if (!u->dev) u->dev = gs::unsup_dev_create(*u->g, u->copy_order, stream);
+    if (!u->dev) u->dev = gs::unsup_dev_create(*u->g, u->copy_order, u->train_order, stream);
 #endif
     GS_API_END
 }
@@ -424,13 +450,18 @@ int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, i
     u->neg_cnt.assign(n, 0);
     u->has_pos.assign(n, 0);
     u->subset_ok = 0;
+    static const bool prof = std::getenv("GS_UNSUP_PROF") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto tw = clk::now();
     if (parts & 1) walk_pairs(*u, rng);
+    const auto tn = clk::now();
 #ifndef GS_HOST_ONLY
-    if ((parts & 2) && u->dev) negative_pairs_dev(*u, rng, num_neg);
+    if ((parts & 2) && u->dev) negative_pairs_dev(*u, rng, num_neg, n_threads);
     else
 #endif
     if (parts & 2) negative_pairs(*u, rng, num_neg, n_threads);
 
+    const auto tu = clk::now();
     PySet a, b;  // models.py:146
     for (int64_t x : u->pos) a.add(static_cast<int32_t>(x));
     for (int64_t x : u->neg) b.add(static_cast<int32_t>(x));
@@ -446,6 +477,11 @@ int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, i
     for (int64_t x : u->nodes) ok = ok && r.find_slot(static_cast<int32_t>(x)) >= 0;
     u->subset_ok = ok ? 1 : 0;
 
+    if (prof) {
+        auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double>(y - x).count() * 1e3; };
+        std::fprintf(stderr, "[unsup] walks %.2f negatives %.2f unique+subset %.2f ms\n", ms(tw, tn), ms(tn, tu),
+                     ms(tu, clk::now()));
+    }
     sizes[0] = static_cast<int64_t>(u->unique.size());
     sizes[1] = static_cast<int64_t>(u->pos.size() / 2);
     sizes[2] = static_cast<int64_t>(u->neg.size() / 2);

@@ -146,27 +146,46 @@ __global__ __launch_bounds__(64) void far_prefix_kernel(int32_t* __restrict__ pr
     if (lane == 0) p[n_chunks] = run;
 }
 
+// The three far orders: set(train).copy(), ascending ids, set(train) itself.
+struct FarOrders {
+    const unsigned long long* M[3];
+    const int32_t* pre[3];
+    const int32_t* order[3];
+};
+
 // The picks: request q = (ball r, order kind, position j) -> order[entry].
 __global__ void far_select_kernel(const int32_t* __restrict__ req_r, const int32_t* __restrict__ req_j,
                                   const uint8_t* __restrict__ req_kind, int n_req, int n_chunks,
-                                  const unsigned long long* __restrict__ M0, const int32_t* __restrict__ pre0,
-                                  const int32_t* __restrict__ order0, const unsigned long long* __restrict__ M1,
-                                  const int32_t* __restrict__ pre1, const int32_t* __restrict__ order1,
-                                  int32_t* __restrict__ out) {
+                                  FarOrders o, int32_t* __restrict__ out) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n_req) return;
     const int r = req_r[q], j = req_j[q];
-    const bool k1 = req_kind[q] != 0;
-    const int32_t* p = (k1 ? pre1 : pre0) + static_cast<int64_t>(r) * (n_chunks + 1);
+    const int kd = req_kind[q];
+    const int32_t* p = o.pre[kd] + static_cast<int64_t>(r) * (n_chunks + 1);
     int lo = 0, hi = n_chunks - 1;  // last chunk with p[c] <= j
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (p[mid] <= j) lo = mid;
         else hi = mid - 1;
     }
-    unsigned long long m = (k1 ? M1 : M0)[static_cast<int64_t>(r) * n_chunks + lo];
+    unsigned long long m = o.M[kd][static_cast<int64_t>(r) * n_chunks + lo];
     for (int t = j - p[lo]; t > 0; --t) m &= m - 1;
-    out[q] = (k1 ? order1 : order0)[64 * lo + __ffsll(m) - 1];
+    out[q] = o.order[kd][64 * lo + __ffsll(m) - 1];
+}
+
+// Whole far lists in set(train) order (order kind 2) for the listed balls:
+// one wave per ball walks its chunk masks and writes every entry at its rank.
+__global__ __launch_bounds__(64) void far_list_kernel(const int32_t* __restrict__ balls, const int64_t* __restrict__ base,
+                                                      int n_chunks, FarOrders o, int32_t* __restrict__ out) {
+    const int q = blockIdx.x, lane = threadIdx.x;
+    const int r = balls[q];
+    const unsigned long long* M = o.M[2] + static_cast<int64_t>(r) * n_chunks;
+    const int32_t* p = o.pre[2] + static_cast<int64_t>(r) * (n_chunks + 1);
+    int32_t* dst = out + base[q];
+    for (int c = 0; c < n_chunks; ++c) {
+        const unsigned long long m = M[c];
+        if ((m >> lane) & 1ull) dst[p[c] + __popcll(m & ((1ull << lane) - 1ull))] = o.order[2][64 * c + lane];
+    }
 }
 
 }  // namespace
@@ -179,14 +198,20 @@ struct UnsupDev {
     const int32_t* col = nullptr;
     int32_t* copy_order = nullptr;  // list(set(train).copy())
     int32_t* asc_order = nullptr;   // sorted(set(train))
+    int32_t* set_order = nullptr;   // list(set(train))
     int cap_roots = 0;
     unsigned long long *S = nullptr, *E = nullptr, *X = nullptr;
     int32_t* roots = nullptr;
     int64_t* counts = nullptr;  // [2][cap_roots]
-    unsigned long long *M0 = nullptr, *M1 = nullptr;
-    int32_t *pre0 = nullptr, *pre1 = nullptr;
+    unsigned long long* M[3] = {};
+    int32_t* pre[3] = {};
     int cap_req = 0;
     int32_t *req_r = nullptr, *req_j = nullptr, *picks = nullptr;
+    int cap_lists = 0;
+    int64_t cap_list_out = 0;
+    int32_t* list_balls = nullptr;
+    int64_t* list_base = nullptr;
+    int32_t* list_out = nullptr;
     uint8_t* req_kind = nullptr;
     hipStream_t st = nullptr;
 
@@ -203,7 +228,8 @@ struct UnsupDev {
     }
 };
 
-UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_order, void* stream) {
+UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_order,
+                           const std::vector<int32_t>& set_order, void* stream) {
     auto d = std::make_unique<UnsupDev>();
     d->st = as_stream(stream);
     d->n_nodes = g.n_nodes;
@@ -220,6 +246,7 @@ UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_orde
     std::sort(asc.begin(), asc.end());
     d->copy_order = static_cast<int32_t*>(up(copy_order.data(), copy_order.size() * sizeof(int32_t)));
     d->asc_order = static_cast<int32_t*>(up(asc.data(), asc.size() * sizeof(int32_t)));
+    d->set_order = static_cast<int32_t*>(up(set_order.data(), set_order.size() * sizeof(int32_t)));
     return d.release();
 }
 
@@ -238,10 +265,10 @@ static void reserve_roots(UnsupDev* d, int n) {
     d->X = d->alloc<unsigned long long>(words * d->n_nodes);
     d->roots = d->alloc<int32_t>(cap);
     d->counts = d->alloc<int64_t>(2 * cap);
-    d->M0 = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
-    d->M1 = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
-    d->pre0 = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
-    d->pre1 = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
+    for (int o = 0; o < 3; ++o) {
+        d->M[o] = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
+        d->pre[o] = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
+    }
     d->cap_roots = cap;
 }
 
@@ -267,27 +294,19 @@ void unsup_dev_balls(UnsupDev* d, const int64_t* nodes, int n, int hops, int64_t
     ball_count_kernel<<<n_words, 256, 0, st>>>(d->S, d->n_nodes, d->asc_order, d->n_order, n, d->counts,
                                                d->counts + d->cap_roots);
     check_launch("ball_count_kernel");
-    // far masks and their prefixes for both orders (needed by the picks)
+    // far masks and their prefixes for the three orders (needed by the picks)
     const dim3 mg(static_cast<unsigned>(d->n_chunks), static_cast<unsigned>(n_words));
-    far_mask_kernel<<<mg, 64, 0, st>>>(d->S, d->n_nodes, d->copy_order, d->n_order, d->n_chunks, n, d->M0, d->pre0);
-    check_launch("far_mask_kernel");
-    far_mask_kernel<<<mg, 64, 0, st>>>(d->S, d->n_nodes, d->asc_order, d->n_order, d->n_chunks, n, d->M1, d->pre1);
-    check_launch("far_mask_kernel");
-    far_prefix_kernel<<<n, 64, 0, st>>>(d->pre0, d->n_chunks);
-    check_launch("far_prefix_kernel");
-    far_prefix_kernel<<<n, 64, 0, st>>>(d->pre1, d->n_chunks);
-    check_launch("far_prefix_kernel");
+    const int32_t* orders[3] = {d->copy_order, d->asc_order, d->set_order};
+    for (int o = 0; o < 3; ++o) {
+        far_mask_kernel<<<mg, 64, 0, st>>>(d->S, d->n_nodes, orders[o], d->n_order, d->n_chunks, n, d->M[o], d->pre[o]);
+        check_launch("far_mask_kernel");
+        far_prefix_kernel<<<n, 64, 0, st>>>(d->pre[o], d->n_chunks);
+        check_launch("far_prefix_kernel");
+    }
     hip_ok(hipMemcpyAsync(ball_size, d->counts, n * sizeof(int64_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(train_in_ball, d->counts + d->cap_roots, n * sizeof(int64_t), hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync");
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-}
-
-void unsup_dev_ball_bits(UnsupDev* d, int n, std::vector<uint64_t>& bits) {
-    const int64_t total = static_cast<int64_t>((n + 63) / 64) * d->n_nodes;
-    bits.resize(static_cast<size_t>(total));
-    hip_ok(hipMemcpyAsync(bits.data(), d->S, total * 8, hipMemcpyDeviceToHost, d->st), "hipMemcpyAsync");
-    hip_ok(hipStreamSynchronize(d->st), "hipStreamSynchronize");
 }
 
 void unsup_dev_select(UnsupDev* d, const std::vector<int32_t>& req_r, const std::vector<int32_t>& req_j,
@@ -307,11 +326,42 @@ void unsup_dev_select(UnsupDev* d, const std::vector<int32_t>& req_r, const std:
     hip_ok(hipMemcpyAsync(d->req_r, req_r.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(d->req_j, req_j.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(d->req_kind, req_kind.data(), n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-    far_select_kernel<<<(n + 255) / 256, 256, 0, st>>>(d->req_r, d->req_j, d->req_kind, n, d->n_chunks, d->M0,
-                                                        d->pre0, d->copy_order, d->M1, d->pre1, d->asc_order,
-                                                        d->picks);
+    const FarOrders fo{{d->M[0], d->M[1], d->M[2]}, {d->pre[0], d->pre[1], d->pre[2]},
+                       {d->copy_order, d->asc_order, d->set_order}};
+    far_select_kernel<<<(n + 255) / 256, 256, 0, st>>>(d->req_r, d->req_j, d->req_kind, n, d->n_chunks, fo, d->picks);
     check_launch("far_select_kernel");
     hip_ok(hipMemcpyAsync(out.data(), d->picks, n * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+}
+
+}  // namespace gs
+
+namespace gs {
+
+void unsup_dev_far_lists(UnsupDev* d, const std::vector<int32_t>& balls, const std::vector<int64_t>& base,
+                         std::vector<int32_t>& out) {
+    const int n = static_cast<int>(balls.size());
+    const int64_t total = n ? base[n] : 0;
+    out.resize(static_cast<size_t>(total));
+    if (!n || !total) return;
+    if (n > d->cap_lists) {
+        d->list_balls = d->alloc<int32_t>(n);
+        d->list_base = d->alloc<int64_t>(n + 1);
+        d->cap_lists = n;
+    }
+    if (total > d->cap_list_out) {
+        d->list_out = d->alloc<int32_t>(total);
+        d->cap_list_out = total;
+    }
+    hipStream_t st = d->st;
+    hip_ok(hipMemcpyAsync(d->list_balls, balls.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(d->list_base, base.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st),
+           "hipMemcpyAsync");
+    const FarOrders fo{{d->M[0], d->M[1], d->M[2]}, {d->pre[0], d->pre[1], d->pre[2]},
+                       {d->copy_order, d->asc_order, d->set_order}};
+    far_list_kernel<<<n, 64, 0, st>>>(d->list_balls, d->list_base, d->n_chunks, fo, d->list_out);
+    check_launch("far_list_kernel");
+    hip_ok(hipMemcpyAsync(out.data(), d->list_out, total * sizeof(int32_t), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
 }
 
