@@ -182,6 +182,7 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
             const int lo = max(0, static_cast<int>(floorf(mean_pre - 6.f * sd)) - 16);
             const int hi = static_cast<int>(ceilf(mean_pre + 6.f * sd)) + 16;
             hb.blo[b] = lo;
+            hb.bw[b] = (hi - lo + 63) & ~63;  // this block's window (the hop-wide W bounds it)
             hb.dbase[b] = draw_pre;
             atomicMax(&s_maxw, hi - lo);
             atomicMax(&s_maxlo, lo);
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
         const int nb = (n + R - 1) / R;
         hb.dbase[nb] = draw_tot;
         hb.blo[nb] = 0;  // never an entry window (the last group's exit is absolute)
+        hb.bw[nb] = 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -334,7 +336,8 @@ __global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __res
     const HopCtl& h = c->hop[hop];
     const int b = blockIdx.x;
     if (b >= h.n_blocks) return;
-    const int W = h.W;
+    const int Wst = h.W;                 // table stride
+    const int W = min(hb.bw[b], Wst);    // this block's entries
     const int tid = threadIdx.x;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
     int32_t* sdeg = reinterpret_cast<int32_t*>(smem);  // sampled nodes' degrees, in order
@@ -412,7 +415,7 @@ __global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __res
     }
     if (tid == 0 && s_bad) atomicOr(&c->status, kStOrder);
     const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    uint16_t* E = hb.tab + static_cast<int64_t>(b) * W;
+    uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
     for (int e = tid; e < W; e += 1024) {
         const int x = U[emap[e]];
         const int dr = x == INT_MAX ? -1 : x - e - ndr;
@@ -426,28 +429,32 @@ __global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __res
 // group's block maps are staged in LDS.
 __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, int hop) {
     extern __shared__ uint16_t tabs[];
-    __shared__ int los[kComposeEntries / 64 + 1];
+    __shared__ int los[kComposeEntries / 64 + 1], wid[kComposeEntries / 64 + 1];
     const HopCtl& h = c->hop[hop];
     const int gi = blockIdx.x;
     if (gi >= h.n_groups) return;
     const int W = h.W, G = h.G;
     const int b0 = gi * G, nbk = min(G, h.n_blocks - b0);
     const bool last_group = gi == h.n_groups - 1;
-    {  // W is a multiple of 64: 16-byte loads
-        const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0) * W);
-        uint4* dst = reinterpret_cast<uint4*>(tabs);
-        for (int i = threadIdx.x; i < nbk * W / 8; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i <= nbk; i += blockDim.x) {  // blo[nb] exists (setup)
+        los[i] = hb.blo[b0 + i];
+        wid[i] = i < nbk ? min(hb.bw[b0 + i], W) : W;
     }
-    for (int i = threadIdx.x; i <= nbk; i += blockDim.x) los[i] = hb.blo[b0 + i];  // blo[nb] exists (setup)
+    __syncthreads();
+    for (int q = 0; q < nbk; ++q) {  // widths are multiples of 64: 16-byte loads
+        const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0 + q) * W);
+        uint4* dst = reinterpret_cast<uint4*>(tabs + q * W);
+        for (int i = threadIdx.x; i < wid[q] / 8; i += blockDim.x) dst[i] = src[i];
+    }
     __syncthreads();
     int32_t* path = hb.path + static_cast<int64_t>(b0) * W;
-    for (int e = threadIdx.x; e < W; e += blockDim.x) {
+    for (int e = threadIdx.x; e < wid[0]; e += blockDim.x) {
         int j = los[0] + e;
         for (int q = 0; q < nbk; ++q) {
             path[q * W + e] = j;
             if (j < 0) continue;
             const int t = j - los[q];
-            if (t < 0 || t >= W) {
+            if (t < 0 || t >= wid[q]) {
                 j = -1;
                 continue;
             }
@@ -458,7 +465,8 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
             hb.gexit_last[e] = j;
         } else {
             const int t = j - los[nbk];
-            hb.gexit[static_cast<int64_t>(gi) * W + e] = (j < 0 || t < 0 || t >= W) ? 0xFFFF : static_cast<uint16_t>(t);
+            hb.gexit[static_cast<int64_t>(gi) * W + e] =
+                (j < 0 || t < 0 || t >= hb.bw[b0 + nbk]) ? 0xFFFF : static_cast<uint16_t>(t);
         }
     }
 }
@@ -486,7 +494,7 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
             gentry[gi] = j;
             const int lo = hb.blo[gi * G];
             const int t = j - lo;
-            if (j < 0 || t < 0 || t >= W) {
+            if (j < 0 || t < 0 || t >= min(hb.bw[gi * G], W)) {
                 j = -1;
                 for (int q = gi + 1; q < ng; ++q) gentry[q] = -1;
                 break;
@@ -508,7 +516,7 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
         const int gi = b / G;
         const int jg = gentry[gi];
         const int t = jg - hb.blo[gi * G];
-        hb.entry[b] = (jg < 0 || t < 0 || t >= W) ? -1 : hb.path[static_cast<int64_t>(b) * W + t];
+        hb.entry[b] = (jg < 0 || t < 0 || t >= min(hb.bw[gi * G], W)) ? -1 : hb.path[static_cast<int64_t>(b) * W + t];
     }
 }
 
@@ -724,8 +732,15 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
     const size_t tab_lds = (R + 2 * kWMax) * sizeof(int32_t) + kWMax * sizeof(uint16_t) +
                            (kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
-    if (k <= 16)
+    // selected-set values in registers: the unrolled duplicate test costs KMAX per word
+    if (k <= 8)
+        draw_tables_kernel<8><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    else if (k <= 12)
+        draw_tables_kernel<12><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    else if (k <= 16)
         draw_tables_kernel<16><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    else if (k <= 25)
+        draw_tables_kernel<25><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else
         draw_tables_kernel<32><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     gs::check_launch("draw_tables_kernel");
@@ -827,6 +842,7 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
         h.mv = ds->alloc<float2>(ndj);
         h.pos_ptr = ds->alloc<int32_t>(ndj + 1);
         h.blo = ds->alloc<int32_t>(nb + 1);
+        h.bw = ds->alloc<int32_t>(nb + 1);
         h.dbase = ds->alloc<int32_t>(nb + 1);
         h.tab = ds->alloc<uint16_t>(nb * kWMax);
         h.path = ds->alloc<int32_t>(nb * kWMax);

@@ -60,6 +60,7 @@ struct HopBufs {
     float2* mv;                // rejection moments per node
     int32_t* pos_ptr;          // [nd_max + 1]
     int32_t* blo;              // block windows' first entry, [nb_max + 1]
+    int32_t* bw;               // block windows' widths (multiples of 64, <= W), [nb_max + 1]
     int32_t* dbase;            // draws before each block, [nb_max + 1]
     uint16_t* tab;             // block maps [nb_max][kWMax]
     int32_t* path;             // group paths [nb_max][kWMax]
