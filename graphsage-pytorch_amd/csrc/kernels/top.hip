@@ -19,9 +19,14 @@
 // is the fmaf chain the f32 MFMA kernels form (within each 16-wide k block
 // the order 0,4,8,12, 1,5,9,13, ... of four v_mfma_f32_16x16x4_f32 over the
 // four k-lane groups; blocks ascending); the head is cls_rows_kernel's code.
-// The two GEMMs run on the matrix cores with the linear kernels' own tiles
-// and operand order (the 4 rows padded to a 16-row tile), from a copy of W2 in
-// LDS that an LDS-DMA fills under the gather.  Measured alternatives: W2
+// The two GEMMs run on the matrix cores in the linear kernels' k order, from a
+// copy of W2 in LDS that an LDS-DMA fills under the gather: E on 16x16x4 tiles
+// (the 4 rows padded to 16; two accumulators alternate to hide the 40-cycle
+// dependent latency), dIn on 4x4x1 multi-block MFMAs (the 4 rows are one
+// block's rows, 16 blocks = 64 columns per instruction).  Measured (tools/lab/
+// top_lab.hip, per launch): dIn 4.09 -> 2.49 us on 4x4x1; E on 4x4x1 took
+// 5.0 us against 3.3 — one accumulator per output chain (the k order is fixed)
+// leaves its dependent latency exposed at 32 columns per wave.  Measured alternatives: W2
 // streamed from L2 through registers took the kernel to 31 us (latency-bound
 // at ~25 GB/s per CU); VALU fmaf chains from LDS spent 3.4 + 3.7 us in the
 // two GEMMs, bound by the LDS broadcast reads of the rows.
@@ -313,55 +318,42 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     }
 
     GS_TOP_STAMP(5);
-    // ---- stage 5: dIn = dZ · W2 on the matrix cores (linear_dx_body's
-    // tiles): wave w owns input columns 64w .. 64w+63 (four 16-wide tiles)
+    // ---- stage 5: dIn = dZ · W2 on the matrix cores, 4x4x1 multi-block as
+    // stage 2: wave w owns input columns 64w .. 64w+63, the 16 blocks x 4
+    // columns of one instruction (lane l: column 64w + l), one h per
+    // instruction in linear_dx_body's order (0,4,8,12, 1,5,9,13, ... per
+    // 16-wide h block): the same fmaf chains, bit for bit.
     {
-        const int r = lane & 15, kq = lane >> 4;
-        const bool rowok = r < nr;
-        const float* zr = sZ[min(r, nr - 1)];
-        f32x4 acc[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // operands one h block ahead; the four tiles' MFMAs alternate (j-major)
-        auto ld = [&](int g, float4& z, float (&wv)[4][4]) {
-            const int hb = 16 * g + 4 * kq;
-            z = *reinterpret_cast<const float4*>(zr + hb);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int kc = 64 * w + 16 * t + r;  // this lane's input column
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int h = hb + j;
-                    wv[t][j] = sW2[h * K + 4 * ((kc >> 2) ^ (h & 15)) + (kc & 3)];
-                }
-            }
-        };
-        float4 zn;
-        float wn[4][4];
-        ld(0, zn, wn);
+        const int arow = lane & 3, kc = 64 * w + lane;
+        const bool rowok = arow < nr;
+        const float4* zr = reinterpret_cast<const float4*>(sZ[min(arow, nr - 1)]);
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
         for (int g = 0; g < H / 16; ++g) {
-            float4 z = zn;
-            float wv[4][4];
+            float zv[16], wv[16];
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int q = 0; q < 4; ++q) {
+                float4 z = zr[4 * g + q];
+                if (!rowok) z = make_float4(0.f, 0.f, 0.f, 0.f);
+                zv[4 * q] = z.x;
+                zv[4 * q + 1] = z.y;
+                zv[4 * q + 2] = z.z;
+                zv[4 * q + 3] = z.w;
+            }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) wv[t][j] = wn[t][j];
-            ld(min(g + 1, H / 16 - 1), zn, wn);
-            if (!rowok) z = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float z4[4] = {z.x, z.y, z.z, z.w};
+            for (int t = 0; t < 16; ++t) {
+                const int h = 16 * g + t;
+                wv[t] = sW2[h * K + 4 * ((kc >> 2) ^ (h & 15)) + (kc & 3)];
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(z4[j], wv[t][j], acc[t], 0, 0, 0);
+                for (int kq = 0; kq < 4; ++kq)
+                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(zv[4 * kq + j], wv[4 * kq + j], acc, 0, 0, 0);
         }
-        if (kq == 0) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int j = 0; j < kTopRows; ++j)
-                    if (j < nr) a.dIn[static_cast<int64_t>(r0 + j) * K + 64 * w + 16 * t + r] = acc[t][j];
-        }
+        for (int j = 0; j < kTopRows; ++j)
+            if (j < nr) a.dIn[static_cast<int64_t>(r0 + j) * K + kc] = acc[j];
     }
     GS_TOP_STAMP(6);
 }
