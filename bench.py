@@ -214,19 +214,21 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 
 
 def load_traffic(config_name, batch, kernel):
-    """Per-launch HBM bytes of the timed layer-1 kernel from the newest
-    committed rocprofv3 --pmc summary (profiles/*pmc*.json) recorded for this
-    config, this batch size and this kernel (its short name), else None."""
-    short = kernel.split("<")[0].split("(")[0].split("::")[-1].strip()
+    """Per-launch HBM bytes of `kernel` (its launched name) from the newest
+    committed rocprofv3 --pmc summary (profiles/*pmc*.json, tools/pmc_summary.py)
+    recorded for this config and this batch size, else None."""
+    key = kernel.split("(")[0].strip()
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("config") == config_name and int(d.get("batch", -1)) == int(batch) and short and \
-                short in d.get("layer1_kernel", "") and "layer1_hbm_bytes_per_launch" in d:
-            best = d
+        if d.get("config") != config_name or int(d.get("batch", -1)) != int(batch):
+            continue
+        k = d.get("kernels", {}).get(key)
+        if k and "hbm_bytes" in k:
+            best = {"hbm_bytes": k["hbm_bytes"], "source": os.path.relpath(p, ROOT)}
     return best
 
 
@@ -599,10 +601,11 @@ def main():
                 peak = MFMA_PEAK_TFS[cfg["dtype"]]
                 achieved, unit, bound = gemm_flops / (us * 1e-6) / 1e12, "TFLOP/s", "mfma"
                 work = {"algo_flops_per_launch": int(gemm_flops)}
-            tr = load_traffic(args.config, cfg["batch"], names[site]) if site == 0 else None
+            tr = load_traffic(args.config, cfg["batch"], names[site])
             rooflines[SITE_NAMES[site]] = dict(
                 bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
-                traffic=(tr["layer1_hbm_bytes_per_launch"] if tr else None), kernel=names[site],
+                traffic=(tr["hbm_bytes"] if tr else None), traffic_source=(tr["source"] if tr else None),
+                kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
                 timed_in=("measured steps" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,

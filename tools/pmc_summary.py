@@ -38,6 +38,7 @@ def main():
         if line.startswith('{"metric"'):
             bench = json.loads(line)
     summary = {"config": config, "kernels": kernels,
+               "batch": int(bench.get("config", {}).get("global_batch", 0)) // max(1, int(bench.get("n_gpus", 1))),
                "note": "read_bytes = 2 x FETCH_SIZE (gfx950 half-count of wide reads); bytes per dispatch"}
     if agg:
         summary["layer1_kernel"] = agg[0]
