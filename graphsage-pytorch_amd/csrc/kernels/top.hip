@@ -25,8 +25,9 @@
 // dependent latency), dIn on 4x4x1 multi-block MFMAs (the 4 rows are one
 // block's rows, 16 blocks = 64 columns per instruction).  Measured (tools/lab/
 // top_lab.hip, per launch): dIn 4.09 -> 2.49 us on 4x4x1; E on 4x4x1 took
-// 5.0 us against 3.3 — one accumulator per output chain (the k order is fixed)
-// leaves its dependent latency exposed at 32 columns per wave.  Measured alternatives: W2
+// 5.0 us (4.15 with its operands one k block ahead) against 3.3 — one
+// accumulator per output chain (the k order is fixed) leaves its dependent
+// latency exposed at 32 columns per wave.  Measured alternatives: W2
 // streamed from L2 through registers took the kernel to 31 us (latency-bound
 // at ~25 GB/s per CU); VALU fmaf chains from LDS spent 3.4 + 3.7 us in the
 // two GEMMs, bound by the LDS broadcast reads of the rows.
