@@ -291,6 +291,37 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     __syncthreads();
     GS_TOP_STAMP(4);
 
+    // ---- stage 4: this block's classifier partial slab (cls_rows_kernel's
+    // sums): out[c][d] = Σ_rows dlogits[row][c] · [E[row] | 1][d].  Thread t
+    // owns class t / 16 (its 4 dlogits in registers) and columns t % 16 + 16 j;
+    // the E reads are LDS broadcasts across the class groups (per launch
+    // 15.4-15.6 us against 16.3 for one thread per flat slab element, the
+    // fallback above 16 classes; same sums).
+#ifndef GS_TOP_SLAB_FLAT
+    if (C * 16 <= kTopThreads) {
+        const int per = C * (D + 1);
+        float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
+        const int c = tid >> 4;
+        if (c < C) {
+            float dl[kTopRows];
+#pragma unroll
+            for (int ii = 0; ii < kTopRows; ++ii) dl[ii] = ii < nr ? sdl[ii * C + c] : 0.f;
+            for (int d = tid & 15; d <= D; d += 16) {
+                float s = 0.f;
+#pragma unroll
+                for (int ii = 0; ii < kTopRows; ++ii)
+                    if (ii < nr) s = fmaf(dl[ii], d < D ? sE[ii][d] : 1.f, s);
+                out[c * (D + 1) + d] = s;
+            }
+        }
+        if (tid >= kTopThreads - 64) {
+            float s = 0.f;
+            for (int ii = tid - (kTopThreads - 64); ii < nr; ii += 64) s += sloss[ii];
+            s = wave_sum(s);
+            if (tid == kTopThreads - 64) out[per] = s;
+        }
+    } else
+#endif
     // ---- stage 4: this block's classifier partial slab (cls_rows_kernel's)
     {
         const int per = C * (D + 1);
