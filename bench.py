@@ -494,7 +494,7 @@ def main():
     rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
     calib = min(50, args.steps)  # untimed steps after the measured ones that time the other kernels
     sustain = max(0, args.sustain)  # then a steady-state window (sampler threads running ahead)
-    total_steps = args.warmup + args.steps + calib + sustain
+    total_steps = args.warmup + 2 * args.steps + calib + sustain  # warmup, cold and steady windows, calib, sustain
     batches = []
     epoch = 0
     while len(batches) < total_steps:
@@ -524,20 +524,55 @@ def main():
         dist.barrier()
     runner.stats(reset=True)
     no_timer = bool(os.environ.get("GS_BENCH_NO_TIMER"))  # A/B of the in-window timer's cost
-    gs._lib.check(lib.gs_trainer_time_kernels(trainer._h, 0 if no_timer else 1 << dominant, args.steps))
+    # an event-bound launch idles the queue a few us on either side of it
+    # (rocprofv3 trace: 4.4 us each side): time one launch in `every` of the
+    # measured steps, spread over both windows, not all of them
+    every = max(4, args.steps // 16)
+    gs._lib.check(lib.gs_trainer_time_kernels_every(trainer._h, 0 if no_timer else 1 << dominant, 2 * args.steps,
+                                                    every))
+
+    def timed_window(wait_sampled):
+        """K steps between barrier + synchronize on both sides; with
+        wait_sampled the clock also runs until the sampler threads have
+        finished as many new batches as the window consumed."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        s0, c0 = runner.progress()
+        ta = time.perf_counter()
+        if not wait_sampled:  # cold: the sampler threads start the window's batches now
+            runner.release(total_steps)
+        runner.run(args.steps)
+        if wait_sampled:
+            want = min(s0 + args.steps, total_steps)
+            deadline = time.perf_counter() + 60.0
+            while runner.progress()[0] < want:
+                if time.perf_counter() > deadline:
+                    raise SystemExit("bench: sampler threads stalled inside the timed window")
+                time.sleep(50e-6)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - ta
+        s1, c1 = runner.progress()
+        tt = torch.tensor([el], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item()), {"presampled_at_t0": s0 - c0, "sampled_in_timed_region": s1 - s0,
+                                  "sampled_ahead_at_t1": s1 - c1}
+
     thr0 = cgroup_throttle()
-    sampled0, consumed0 = runner.progress()
-    t0 = time.perf_counter()
-    runner.release(args.warmup + args.steps)
-    runner.run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    sampled1, consumed1 = runner.progress()
+    # cold window: nothing past the warmup batches sampled before t0, so the
+    # window pays the pipeline fill (the first batch's whole sampling latency)
+    cold_elapsed, cold_proof = timed_window(wait_sampled=False)
+    # steady window (`value`): straight after it, the pipeline running as in
+    # any later step of a training run; the clock stops only once the window
+    # has also sampled as many new batches as it consumed, so the sampling
+    # work of every step it counts is inside the timed region
+    elapsed, proof = timed_window(wait_sampled=True)
     thr1 = cgroup_throttle()
     st = runner.stats()
-    times = {} if no_timer else {dominant: kernel_times_ms(trainer, args.steps, dominant)}
+    times = {} if no_timer else {dominant: kernel_times_ms(trainer, 2 * args.steps // every, dominant)}
     # calibration steps after the measured ones time the other sites (an
     # event-bound launch costs the stream a little: never inside the timed steps)
     runner.release(total_steps)
@@ -571,10 +606,6 @@ def main():
         sus = {"value": round(cfg["batch"] * sustain * world / te, 1), "unit": "root nodes/s", "steps": sustain,
                "ms_per_step": round(te / sustain * 1e3, 4), "sampled_ahead_at_start": ss0 - sc0,
                "sampled_in_window": ss1 - ss0, "sampled_ahead_at_end": ss1 - sc1}
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
     value = cfg["batch"] * args.steps * world / elapsed
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
     n_edges = float(sizes[:L, 1].sum()) * args.steps
@@ -607,7 +638,7 @@ def main():
                 traffic=(tr["hbm_bytes"] if tr else None), traffic_source=(tr["source"] if tr else None),
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
-                timed_in=("measured steps" if site == dominant else f"{calib} calibration steps after them"),
+                timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
                 **work)
         roof = dict(rooflines[SITE_NAMES[dominant]])
@@ -628,9 +659,11 @@ def main():
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
                        "sampler_contexts_warmed": not args.no_warm,
-                       "presampled_at_t0": sampled0 - consumed0,
-                       "sampled_in_timed_region": sampled1 - sampled0,
-                       "sampled_ahead_at_t1": sampled1 - consumed1,
+                       "window": "steady (after a cold window of the same length; the clock waits until the "
+                                 "window has sampled as many new batches as it consumed)",
+                       **proof,
+                       "cold_start": {"value": round(cfg["batch"] * args.steps * world / cold_elapsed, 1),
+                                      "ms_per_step": round(cold_elapsed / args.steps * 1e3, 4), **cold_proof},
                        "allreduce_buckets": args.ar_buckets if world > 1 else 0,
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),

@@ -132,6 +132,7 @@ _SIGS = {
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
     "gs_trainer_time_kernels": (_i32, [_vp, _i32, _i64]),
+    "gs_trainer_time_kernels_every": (_i32, [_vp, _i32, _i64, _i64]),
     "gs_trainer_kernel_name": (ctypes.c_char_p, [_vp, _i32]),
     "gs_trainer_grads": (_vp, [_vp]),
     "gs_trainer_layer1_fused": (_i32, [_vp]),

@@ -27,6 +27,7 @@ struct gs_trainer {
     struct Timer {
         std::vector<hipEvent_t> ev0, ev1;
         int64_t n = 0;
+        int64_t every = 1, calls = 0;  // time one launch of every `every`, the last of each run
         std::string kernel;  // demangled name of the kernel the site last timed
     } timer[kSites];
     std::vector<hipEvent_t>& ev0 = timer[0].ev0;
@@ -92,6 +93,7 @@ static inline void ok(int rc) {
 static inline bool timed_arm(gs_trainer& T, int site) {
     auto& tm = T.timer[site];
     if (tm.n >= static_cast<int64_t>(tm.ev0.size())) return false;
+    if (++tm.calls % tm.every) return false;
     g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
     return true;
 }
@@ -529,8 +531,12 @@ int gs_trainer_forward_gathered(gs_trainer* t, const int32_t* pack, const int64_
 }
 
 int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity) {
+    return gs_trainer_time_kernels_every(t, site_mask, capacity, 1);
+}
+
+int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capacity, int64_t every) {
     GS_API_BEGIN
-    GS_REQUIRE(t && capacity >= 0, GS_EINVAL, "bad arguments");
+    GS_REQUIRE(t && capacity >= 0 && every >= 1, GS_EINVAL, "bad arguments");
     for (int s = 0; s < gs_trainer::kSites; ++s) {
         auto& tm = t->timer[s];
         for (auto e : tm.ev0) (void)hipEventDestroy(e);
@@ -543,6 +549,8 @@ int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity) 
                            hipEventCreateWithFlags(&tm.ev1[i], gs::timer_event_flags()) == hipSuccess,
                        GS_EHIP, "hipEventCreate");
         tm.n = 0;
+        tm.every = every;
+        tm.calls = 0;
         tm.kernel.clear();
     }
     GS_API_END

@@ -513,8 +513,13 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
  * s) for their next `capacity` launches and disarms the others;
  * gs_trainer_time_agg(t, n) == gs_trainer_time_kernels(t, 1, n).  Every
  * armed launch is an event-bound hipExtLaunchKernel, which costs the stream
- * a little: time the GEMM sites in their own steps, not the measured ones. */
+ * a little (a few microseconds of idle queue on either side of it): time the
+ * GEMM sites in their own steps, not the measured ones.
+ * gs_trainer_time_kernels_every times one launch in `every` of each armed
+ * site (the every-th, 2·every-th, ... launch since arming), so a measured
+ * window pays the event cost on a fraction of its steps. */
 int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity);
+int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capacity, int64_t every);
 int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap);
 /* Demangled name of the kernel timer site `site` timed since it was last
  * armed ("" before its first timed launch) — the variant actually launched. */

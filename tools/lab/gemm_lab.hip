@@ -311,6 +311,84 @@ __global__ __launch_bounds__(NW * 64) void fwd_2ph_kernel(int n, int F, int H, c
     }
 }
 
+// W-stationary: a wave owns one 16-column tile; its W slice (16 columns x K)
+// sits in registers for the whole launch, and the wave walks row tiles
+// t = bx, bx + RG, ..., loading each tile's A rows (self | agg) straight into
+// registers in the MFMA operand layout (lane (r, kq): quad 4g + kq of row r
+// for k group g), no LDS and no barriers.  Same operands in the same order as
+// the chunked kernel: bitwise equal.  PF: the next tile's A is loaded under
+// the current tile's MFMAs.
+template <bool PF>
+__global__ __launch_bounds__(256, 2) void fwd_wreg_kernel(int n, int F, int H, const float* __restrict__ Xs,
+                                                          int64_t ldxs, const int* __restrict__ sidx,
+                                                          const float* __restrict__ A, int64_t lda,
+                                                          const float* __restrict__ W, float* __restrict__ out,
+                                                          int64_t ldo, unsigned long long* __restrict__ stamps) {
+    unsigned long long t_start = 0;
+    if (stamps) t_start = __builtin_amdgcn_s_memrealtime();
+    constexpr int K = 512, NG = 32, R = 16;  // A ring: 16 groups = one half (self or agg) of a tile
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int ct = blockIdx.y * 4 + wave;
+    uint4 w[NG];
+    {
+        const float* wrow = W + (int64_t)(16 * ct + r) * K + 4 * kq;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) w[g] = *reinterpret_cast<const uint4*>(wrow + 16 * g);
+    }
+    const int ntiles = (n + 15) / 16;
+    uint4 a[R];
+    unsigned long long t_a = 0;
+    int t = blockIdx.x;
+    if (t >= ntiles) return;
+    // half h of tile t: h = 0 the self row X[sidx], 1 the aggregate row
+    auto src = [&](int tt, int h) -> const float* {
+        const int row = min(16 * tt + r, n - 1);
+        return (h ? A + (int64_t)row * lda : Xs + (int64_t)sidx[row] * ldxs) + 4 * kq;
+    };
+    {
+        const float* p = src(t, 0);
+#pragma unroll
+        for (int g = 0; g < R; ++g) a[g] = *reinterpret_cast<const uint4*>(p + 16 * g);
+    }
+    for (; t < ntiles; t += gridDim.x) {
+        const int tn = t + gridDim.x;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* p1 = src(t, 1);
+#pragma unroll
+        for (int g = 0; g < R; ++g) {  // self half; refill with the agg half
+            acc = gs::mfma_slot<float>(a[g], w[g], acc);
+            a[g] = *reinterpret_cast<const uint4*>(p1 + 16 * g);
+        }
+        const bool more = PF && tn < ntiles;
+        const float* p0 = more ? src(tn, 0) : p1;
+#pragma unroll
+        for (int g = 0; g < R; ++g) {  // agg half; refill with the next tile's self half
+            acc = gs::mfma_slot<float>(a[g], w[R + g], acc);
+            if (more) a[g] = *reinterpret_cast<const uint4*>(p0 + 16 * g);
+        }
+        if (stamps && t_a == 0) t_a = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * t + 4 * kq + j;
+            if (row < n) {
+                const float v = acc[j];
+                out[(int64_t)row * ldo + 16 * ct + r] = (!(v > 0.f) && v == v) ? 0.f : v;
+            }
+        }
+        if (!PF && tn < ntiles) {
+            const float* q = src(tn, 0);
+#pragma unroll
+            for (int g = 0; g < R; ++g) a[g] = *reinterpret_cast<const uint4*>(q + 16 * g);
+        }
+    }
+    if (stamps && lane == 0) {
+        const unsigned long long t_e = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* p = stamps + 3 * (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave);
+        p[0] = t_start; p[1] = t_a ? t_a : t_e; p[2] = t_e;
+    }
+}
+
 }  // namespace lab
 
 static unsigned long long* g_stamps = nullptr;  // set for one instrumented launch
@@ -343,6 +421,14 @@ static void run_t32(int n, int F, int H, const float* X, const int* sidx, const 
     const int tiles = (n + 31) / 32;
     const int nb = ((tiles + 7) / 8) * 16;
     lab::fwd_t32_kernel<KS, D><<<nb, 256 * KS, 0, st>>>(n, F, H, X, F, sidx, A, F, Wp, out, H, g_stamps);
+}
+
+template <bool PF, int RG>
+static void run_wreg(int n, int F, int H, const float* X, const int* sidx, const float* A, const float* W,
+                     const float* Wp, float* out, hipStream_t st) {
+    const int tiles = (n + 15) / 16;
+    dim3 grid(std::min(tiles, RG), H / 64);
+    lab::fwd_wreg_kernel<PF><<<grid, 256, 0, st>>>(n, F, H, X, F, sidx, A, F, W, out, H, g_stamps);
 }
 
 template <int NW, int D>
@@ -423,7 +509,11 @@ int main(int argc, char** argv) {
         {"2ph NW4 D4 (64 cols)", run_2ph<4, 4>, 4},
         {"2ph NW4 D2 (64 cols)", run_2ph<4, 2>, 4},
         {"2ph NW2 D4 (32 cols)", run_2ph<2, 4>, 2},
-        {"2ph NW16 D2", run_2ph<16, 2>, 16},
+        {"wreg RG256", run_wreg<false, 256>, 4},
+        {"wreg RG all", run_wreg<false, 1 << 20>, 4},
+        {"wreg RG138", run_wreg<false, 138>, 4},
+        {"wreg PF RG256", run_wreg<true, 256>, 4},
+        {"wreg PF RG138", run_wreg<true, 138>, 4},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
