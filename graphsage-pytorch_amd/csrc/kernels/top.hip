@@ -254,14 +254,16 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         const int ii = w;
         const float* e = sE[ii];
         const int y = y_w;
-        const int DQ = (D + 3) / 4;
-        const int d_lo = min(D, dq * DQ), d_hi = min(D, d_lo + DQ);
+        static_assert(D % 4 == 0, "whole D quarters");
+        constexpr int DQ = D / 4;  // whole quarters: a straight-line chain
+        const int d_lo = dq * DQ;
         float mx = -INFINITY;
         for (int c0 = 0; c0 < C; c0 += 16) {
             const int c = c0 + cl;
             const float* wr = sW + static_cast<int64_t>(min(c, C - 1)) * wp;
             float pz = 0.f;
-            for (int d = d_lo; d < d_hi; ++d) pz = fmaf(e[d], wr[d], pz);
+#pragma unroll
+            for (int t = 0; t < DQ; ++t) pz = fmaf(e[d_lo + t], wr[d_lo + t], pz);
             pz += __shfl_xor(pz, 16, 64);
             pz += __shfl_xor(pz, 32, 64);
             const float z = pz + (c0 == 0 ? b_lane : a.bc[min(c, C - 1)]);
@@ -282,7 +284,18 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         __builtin_amdgcn_wave_barrier();
         for (int d = lane; d < D; d += 64) {
             float s = 0.f;
-            for (int c = 0; c < C; ++c) s = fmaf(sdl[ii * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
+            int c = 0;
+            for (; c + 8 <= C; c += 8) {  // eight classes' operands read ahead of their chain
+                float g[8], v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    g[u] = sdl[ii * C + c + u];
+                    v[u] = sW[static_cast<int64_t>(c + u) * wp + d];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s = fmaf(g[u], v[u], s);
+            }
+            for (; c < C; ++c) s = fmaf(sdl[ii * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
             if (!(e[d] > 0.f)) s = 0.f;
             sZ[ii][d] = s;
             a.dZ[static_cast<int64_t>(r0 + ii) * D + d] = s;
@@ -306,12 +319,31 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             float dl[kTopRows];
 #pragma unroll
             for (int ii = 0; ii < kTopRows; ++ii) dl[ii] = ii < nr ? sdl[ii * C + c] : 0.f;
-            for (int d = tid & 15; d <= D; d += 16) {
-                float s = 0.f;
+            if (nr == kTopRows) {  // every block but a ragged last one: straight-line, same sums
+                float s[D / 16];
 #pragma unroll
-                for (int ii = 0; ii < kTopRows; ++ii)
-                    if (ii < nr) s = fmaf(dl[ii], d < D ? sE[ii][d] : 1.f, s);
-                out[c * (D + 1) + d] = s;
+                for (int j = 0; j < D / 16; ++j) {
+                    const int d = (tid & 15) + 16 * j;
+                    s[j] = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < kTopRows; ++ii) s[j] = fmaf(dl[ii], sE[ii][d], s[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < D / 16; ++j) out[c * (D + 1) + (tid & 15) + 16 * j] = s[j];
+                if ((tid & 15) == 0) {
+                    float sb = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < kTopRows; ++ii) sb = fmaf(dl[ii], 1.f, sb);
+                    out[c * (D + 1) + D] = sb;
+                }
+            } else {
+                for (int d = tid & 15; d <= D; d += 16) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < kTopRows; ++ii)
+                        if (ii < nr) s = fmaf(dl[ii], d < D ? sE[ii][d] : 1.f, s);
+                    out[c * (D + 1) + d] = s;
+                }
             }
         }
         if (tid >= kTopThreads - 64) {
