@@ -7,6 +7,10 @@
 //   A = [dW_l slabs: gx·gy·S blocks][dIn_l: (n/16)·(K/64)][classifier reduce]
 //   B = [Σ slabs -> dW_l (+ norm partials)][agg backward -> dH_{l-1}]
 // Heavy roles come first in the grid so they are dispatched first.
+// After the fused top layer (top.hip wrote dIn_2) a 2-layer step needs one
+// launch here, not two: T = [dW_2 slabs][classifier reduce][agg backward ->
+// dH_1], and the Σ of the dW_2 slabs moves into the layer-1 slab-sum launch
+// (sum_slabs_pair_launch), which runs after the layer-1 dW anyway.
 #include "agg_dev.hpp"
 #include "cls_dev.hpp"
 #include "internal.hpp"
@@ -87,6 +91,33 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_b_kernel(BwdB b) {
     }
     agg_bwd_body<OP, 4, G>(bx - b.sum_nb, b.n_src, b.F, b.tptr, b.tidx, b.ptr, b.dA, b.dSelf, b.ldd, b.argmax,
                            b.Hprev, b.F, b.dH);
+}
+
+struct BwdT {
+    BwdA a;     // dW slabs + classifier reduce roles (dx_nb == 0)
+    BwdB b;     // agg backward role (sum_nb == 0)
+    int cls_nb;
+};
+
+template <int OP, int G>
+__global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
+    int b = blockIdx.x;
+    if (b < t.a.dw_nb) {
+        const int g2 = t.a.dw_gx * t.a.dw_gy;
+        linear_dw_body<float, true, false, true, true>(b % t.a.dw_gx, (b % g2) / t.a.dw_gx, b / g2, t.a.n, t.a.F,
+                                                       t.a.H, t.a.K, t.a.rps, t.a.Xs, t.a.ldxs, t.a.sidx, t.a.A,
+                                                       t.a.F, t.a.dZ, nullptr, t.a.H, t.a.target,
+                                                       static_cast<int64_t>(t.a.H) * t.a.K);
+        return;
+    }
+    b -= t.a.dw_nb;
+    if (b < t.cls_nb) {
+        cls_reduce_body(b, t.a.B, t.a.D, t.a.C, t.a.cls_rows, t.a.cls_slab, t.a.dWc, t.a.dbc, t.a.loss, t.a.cls_part);
+        return;
+    }
+    b -= t.cls_nb;
+    agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd, t.b.argmax,
+                           t.b.Hprev, t.b.F, t.b.dH);
 }
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
@@ -186,6 +217,67 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
 #undef GS_BWDB
     check_launch("layer_bwd(B)");
     return Bq.sum_nb;
+}
+
+int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st) {
+    GS_REQUIRE(layer_bwd_fusable(a) && a.din_ready && a.Xs, GS_EINVAL, "top backward: not the fused top path");
+    const int64_t K = 2 * a.fin;
+    const int S = dw_splits(a.n, K, a.H);
+    const int rps = dw_rows_per_split(a.n, K, a.H);
+    GS_REQUIRE(S == 1 || a.slab_bytes >= static_cast<int64_t>(S) * K * a.H * 4, GS_EINVAL, "workspace too small");
+    BwdT t{};
+    BwdA& A = t.a;
+    A.n = static_cast<int>(a.n);
+    A.F = static_cast<int>(a.fin);
+    A.H = static_cast<int>(a.H);
+    A.K = static_cast<int>(K);
+    A.rps = rps;
+    A.Xs = a.Xs;
+    A.ldxs = a.ldxs;
+    A.sidx = a.sidx;
+    A.A = a.A;
+    A.dZ = a.dZ;
+    A.target = S > 1 ? a.slabs : a.dW;
+    A.dw_gx = static_cast<int>((K + 63) / 64);
+    A.dw_gy = static_cast<int>((a.H + 63) / 64);
+    A.dw_nb = A.dw_gx * A.dw_gy * S;
+    A.B = static_cast<int>(cls.B);
+    A.D = static_cast<int>(cls.D);
+    A.C = static_cast<int>(cls.C);
+    A.cls_rows = cls.n_row_blocks;
+    A.cls_slab = cls.slab;
+    A.dWc = cls.dWc;
+    A.dbc = cls.dbc;
+    A.loss = cls.loss;
+    A.cls_part = cls.part;
+    t.cls_nb = cls_reduce_blocks(cls.C, cls.D);
+    BwdB& Bq = t.b;
+    Bq.n_src = static_cast<int>(a.n_src);
+    Bq.F = static_cast<int>(a.H);
+    Bq.tptr = a.tptr;
+    Bq.tidx = a.tidx;
+    Bq.ptr = a.ptr;
+    Bq.dSelf = a.dIn;
+    Bq.dA = a.dIn + a.fin;
+    Bq.ldd = K;
+    Bq.argmax = a.argmax;
+    Bq.Hprev = a.Hprev;
+    Bq.dH = a.dH;
+    const int G = pick_group(static_cast<int>(a.H), 4);
+    const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
+    const dim3 grid(static_cast<unsigned>(A.dw_nb + t.cls_nb + agg_nb));
+#define GS_BWDT(OP)                                                                     \
+    do {                                                                                \
+        if (G == 16) layer_bwd_top_kernel<OP, 16><<<grid, kThreads, 0, st>>>(t);        \
+        else if (G == 32) layer_bwd_top_kernel<OP, 32><<<grid, kThreads, 0, st>>>(t);   \
+        else layer_bwd_top_kernel<OP, 64><<<grid, kThreads, 0, st>>>(t);                \
+    } while (0)
+    if (a.agg == GS_AGG_MEAN) GS_BWDT(GS_AGG_MEAN);
+    else GS_BWDT(GS_AGG_MAX);
+#undef GS_BWDT
+    check_launch("layer_bwd_top");
+    *deferred = SlabSum{a.slabs, S, a.H * K, a.dW, nullptr};
+    return S > 1 ? sum_slabs_blocks(a.H * K) : 0;
 }
 
 }  // namespace gs

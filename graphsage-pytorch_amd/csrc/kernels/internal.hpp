@@ -23,6 +23,18 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st);
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
+// One slab sum: out = Σ_s slabs[s] (S slabs of len floats), norm partials to part.
+struct SlabSum {
+    const float* slabs;
+    int S;
+    int64_t len;
+    float* out;
+    float* part;
+};
+// Both sums in one launch (s1 the split layer-1 sum, s2 a deferred layer-2
+// sum, S2 <= 1 = nothing to add); returns s1's partial count.
+bool sum_slabs_pair_ok(int64_t len1);
+int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st);
 int sum_slabs_grid(int64_t len);
 
 // agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)
@@ -76,6 +88,11 @@ struct ClsReduce {
     float* loss;
     float* part;                          // norm partials of (dWc, dbc), one per reduce block
 };
+// The fused top path's one backward launch for layer 2 (bwd.hip): dW_2 slabs,
+// classifier reduce and the agg backward to dH_1; the dW_2 slab sum is left
+// in *deferred (S <= 1: dW_2 written directly) for sum_slabs_pair_launch.
+// Returns the norm partials that sum will write (placed first, as layer_bwd's).
+int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st);
 
 bool layer_bwd_fusable(const LayerBwd& a);
 int cls_reduce_grid(int64_t C, int64_t D);

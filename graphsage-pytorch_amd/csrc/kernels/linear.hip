@@ -20,13 +20,12 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
 // loads instead of S: at the layer-1 dW (31 slabs of 64 Ki floats) and 8
 // waves, one round of 4 loads instead of eight rounds, over 256 blocks
 // instead of 65.  len % 4 == 0.
-__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const float* __restrict__ slabs, int S,
-                                                                          int64_t len, float* __restrict__ out,
-                                                                          float* __restrict__ part) {
+__device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __restrict__ slabs, int S, int64_t len,
+                                                     float* __restrict__ out, float* __restrict__ part) {
     __shared__ float4 red[kSlabParts - 1][64];
     const int q = threadIdx.x >> 6, c = threadIdx.x & 63;
     const int64_t n4 = len / 4;
-    const int64_t i = blockIdx.x * int64_t(64) + c;
+    const int64_t i = bx * int64_t(64) + c;
     const int per = (S + kSlabParts - 1) / kSlabParts;
     const int t0 = min(S, q * per), t1 = min(S, t0 + per);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -49,7 +48,27 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const 
         *reinterpret_cast<float4*>(out + 4 * i) = s;
         sq = fmaf(s.x, s.x, sq); sq = fmaf(s.y, s.y, sq); sq = fmaf(s.z, s.z, sq); sq = fmaf(s.w, s.w, sq);
     }
-    if (part) block_sum_to(sq, part + blockIdx.x);
+    if (part) block_sum_to(sq, part + bx);
+}
+
+__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const float* __restrict__ slabs, int S,
+                                                                          int64_t len, float* __restrict__ out,
+                                                                          float* __restrict__ part) {
+    sum_slabs_split_body(blockIdx.x, slabs, S, len, out, part);
+}
+
+// Two slab sums in one launch (the 2-layer step after the fused top layer):
+// blocks [0, nb1) sum the layer-1 dW slabs as sum_slabs_split_kernel, blocks
+// [nb1, nb1 + nb2) the layer-2 dW slabs as sum_slabs_body over nb2 blocks of
+// kThreads (the other threads of these wider blocks only join the partial's
+// reduction) -- each bitwise its standalone kernel, partials where those write.
+__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2) {
+    const int bx = blockIdx.x;
+    if (bx < nb1) {
+        sum_slabs_split_body(bx, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+        return;
+    }
+    sum_slabs_body(bx - nb1, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
 }
 
 static bool slab_split_on(int64_t len) {
@@ -268,6 +287,17 @@ int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* 
     sum_slabs_kernel<<<dim3(sum_slabs_blocks(len)), kThreads, 0, st>>>(slabs, S, len, out, part);
     check_launch("sum_slabs");
     return sum_slabs_blocks(len);
+}
+
+bool sum_slabs_pair_ok(int64_t len1) { return slab_split_on(len1); }
+
+int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st) {
+    GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1, GS_EINVAL, "slab pair: layer-1 sum not split");
+    const int nb1 = static_cast<int>(slab_split_blocks(s1.len));
+    const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
+    sum_slabs_pair_kernel<<<dim3(static_cast<unsigned>(nb1 + nb2)), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2);
+    check_launch("sum_slabs_pair");
+    return nb1;
 }
 
 int sum_slabs_grid(int64_t len) {  // norm partials a slab sum of len floats may write (capacity bound)

@@ -654,9 +654,12 @@ __global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
 // writes Σ out[i]² over its elements to part[bx] (the clip norm's partial).
 constexpr int kSlabParts = 8;
 
+// `active` false: a thread of a wider block that only joins the partial's
+// block reduction (adding +0 leaves it bitwise unchanged).
 __device__ __forceinline__ void sum_slabs_body(int bx, int nblk, const float* __restrict__ slabs, int S,
-                                               int64_t len, float* __restrict__ out, float* __restrict__ part) {
-    const int64_t n4 = len / 4;
+                                               int64_t len, float* __restrict__ out, float* __restrict__ part,
+                                               bool active = true) {
+    const int64_t n4 = active ? len / 4 : 0;
     const int per = (S + kSlabParts - 1) / kSlabParts;
     float sq = 0.f;
     for (int64_t i = bx * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(nblk) * kThreads) {
@@ -676,7 +679,8 @@ __device__ __forceinline__ void sum_slabs_body(int bx, int nblk, const float* __
         *reinterpret_cast<float4*>(out + 4 * i) = s;
         sq = fmaf(s.x, s.x, sq); sq = fmaf(s.y, s.y, sq); sq = fmaf(s.z, s.z, sq); sq = fmaf(s.w, s.w, sq);
     }
-    for (int64_t i = 4 * n4 + bx * int64_t(kThreads) + threadIdx.x; i < len; i += int64_t(nblk) * kThreads) {
+    for (int64_t i = 4 * (len / 4) + bx * int64_t(kThreads) + threadIdx.x; active && i < len;
+         i += int64_t(nblk) * kThreads) {
         float s = 0.f;
         for (int q = 0; q < kSlabParts; ++q) {
             const int t0 = min(S, q * per), t1 = min(S, t0 + per);

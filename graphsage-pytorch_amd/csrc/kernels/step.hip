@@ -217,6 +217,9 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         }
     }
     char* dw_ws = cv.take<char>(dw_need);
+    // the fused top path's dW_2 slabs outlive the layer-1 dW (their sum runs with layer 1's)
+    const int64_t dw2_need = L == 2 ? gs_sage_linear_bwd_weight_ws(rows[1], T.w_cols[1], H) : 0;
+    char* dw2_ws = dw2_need > 0 ? cv.take<char>(dw2_need) : nullptr;
     float* dIn = cv.take<float>(dx_rows * (c.gcn ? H : 2 * H));
     float* dbuf[2] = {cv.take<float>(dprev_rows * H), cv.take<float>(dprev_rows * H)};
     if (!ws) return cv.at + 256;
@@ -314,22 +317,43 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
             const ClsReduce cr{B, H, c.n_classes, cls_rows, cls_ws, G + T.cls_w_off, G + T.cls_b_off, loss,
                                T.norm_part + T.pstride};
+            const int64_t K1 = T.w_cols[0];
+            // top path, 2 layers, no bucketed all-reduce hook: one backward launch for
+            // layer 2 and its slab sum beside layer 1's (same sums, partials, order)
+            static const bool split_b = std::getenv("GS_BWD_SPLIT_B") != nullptr;  // A/B: launches A + B
+            const bool defer = top && lb.size() == 1 && !T.upper_hook && !split_b && dw2_ws &&
+                               sum_slabs_pair_ok(H * K1);
             int np = 0;
             bool parts = true;
-            for (size_t i = 0; i < lb.size(); ++i) {
-                const int n = layer_bwd(lb[i], i == 0 ? &cr : nullptr, T.norm_part + np, st);
-                parts = parts && n > 0;
-                np += n;
+            SlabSum d2{};
+            if (defer) {
+                lb[0].slabs = reinterpret_cast<float*>(dw2_ws);
+                lb[0].slab_bytes = dw2_need;
+                np = layer_bwd_top(lb[0], cr, &d2, st);
+                parts = np > 0;
+            } else {
+                for (size_t i = 0; i < lb.size(); ++i) {
+                    const int n = layer_bwd(lb[i], i == 0 ? &cr : nullptr, T.norm_part + np, st);
+                    parts = parts && n > 0;
+                    np += n;
+                }
+                if (T.upper_hook) T.upper_hook(st);
             }
-            if (T.upper_hook) T.upper_hook(st);
-            const int64_t K1 = T.w_cols[0];
             const bool armed = timed_arm(T, 2);
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
                                            c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0],
                                            dw_ws, dw_need, st);
             g_launch_events = {};
             timed_done(T, 2, armed);
-            if (S1 > 1) {
+            if (defer && S1 > 1) {
+                d2.part = T.norm_part;
+                np += sum_slabs_pair_launch(SlabSum{reinterpret_cast<const float*>(dw_ws), S1, H * K1,
+                                                    G + T.w_off[0], T.norm_part + np},
+                                            d2, st);
+            } else if (defer) {
+                if (d2.S > 1) sum_slabs_launch(d2.slabs, d2.S, d2.len, d2.out, nullptr, st);
+                parts = false;
+            } else if (S1 > 1) {
                 np += sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0],
                                        T.norm_part + np, st);
             } else {
