@@ -58,17 +58,17 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const 
 }
 
 // Two slab sums in one launch (the 2-layer step after the fused top layer):
-// blocks [0, nb1) sum the layer-1 dW slabs as sum_slabs_split_kernel, blocks
-// [nb1, nb1 + nb2) the layer-2 dW slabs as sum_slabs_body over nb2 blocks of
+// blocks [nb2, nb2 + nb1) sum the layer-1 dW slabs as sum_slabs_split_kernel,
+// blocks [0, nb2) the layer-2 dW slabs as sum_slabs_body over nb2 blocks of
 // kThreads (the other threads of these wider blocks only join the partial's
 // reduction) -- each bitwise its standalone kernel, partials where those write.
 __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2) {
     const int bx = blockIdx.x;
-    if (bx < nb1) {
-        sum_slabs_split_body(bx, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+    if (bx < nb2) {  // the longer per-block chains first
+        sum_slabs_body(bx, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
         return;
     }
-    sum_slabs_body(bx - nb1, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
+    sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part);
 }
 
 static bool slab_split_on(int64_t len) {

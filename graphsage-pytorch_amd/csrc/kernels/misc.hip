@@ -3,6 +3,7 @@
 // clipping + SGD (utils.py:185-187) and the f32 -> bf16 weight cast.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "cls_dev.hpp"
 
@@ -274,6 +275,59 @@ __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ 
     }
 }
 
+// sgd_kernel on float4 (every group offset a multiple of 4, 16-B aligned
+// arrays): each thread's first g / p quads are loaded before the partial fold,
+// so the two dependent rounds overlap; the same per-element arithmetic.
+__global__ __launch_bounds__(kTb) void sgd4_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
+                                                   const float* __restrict__ part, float scale, float max_norm,
+                                                   float lr) {
+    __shared__ float mult[8];
+    const int64_t n4 = G.off[G.n] / 4;
+    const int64_t i0 = blockIdx.x * int64_t(kTb) + threadIdx.x;
+    float4* g4 = reinterpret_cast<float4*>(g);
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), pv = gv;
+    if (i0 < n4) {
+        gv = g4[i0];
+        pv = p4[i0];
+    }
+    const int lane = threadIdx.x & 63;
+    for (int grp = threadIdx.x >> 6; grp < G.n; grp += kTb / 64) {
+        const float* pg = part + grp * G.pstride;
+        const int np = G.npart[grp];
+        float t = 0.f;
+#pragma unroll 4
+        for (int b = lane; b < np; b += 64) t += pg[b];
+        t = wave_sum(t);
+        if (lane == 0) {
+            const float norm = sqrtf(t) * scale;
+            mult[grp] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+        }
+    }
+    __syncthreads();
+    for (int64_t i = i0; i < n4; i += int64_t(gridDim.x) * kTb) {
+        if (i != i0) {
+            gv = g4[i];
+            pv = p4[i];
+        }
+        int grp = 0;
+        while (4 * i >= G.off[grp + 1]) ++grp;
+        const float m = mult[grp];
+        float4 gi;
+        gi.x = gv.x * m;
+        gi.y = gv.y * m;
+        gi.z = gv.z * m;
+        gi.w = gv.w * m;
+        g4[i] = gi;
+        float4 pn;
+        pn.x = pv.x - lr * gi.x;
+        pn.y = pv.y - lr * gi.y;
+        pn.z = pv.z - lr * gi.z;
+        pn.w = pv.w - lr * gi.w;
+        p4[i] = pn;
+    }
+}
+
 }  // namespace gs
 
 extern "C" {
@@ -352,8 +406,16 @@ void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart
     for (int i = 0; i < n_groups; ++i) G.npart[i] = npart[i];
     for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
     const int64_t total = G.off[n_groups];
-    const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
-    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+    bool vec = aligned16(params) && aligned16(grads) && std::getenv("GS_SGD_SCALAR") == nullptr;
+    for (int i = 0; i <= n_groups; ++i) vec = vec && G.off[i] % 4 == 0;
+    if (vec) {  // 4.9 us -> see DESIGN §4 (rmat2m, ~100k parameters)
+        const int64_t n4 = total / 4;
+        const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + kTb - 1) / kTb, 512))));
+        sgd4_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+    } else {
+        const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
+        sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+    }
     check_launch("sgd");
 }
 
