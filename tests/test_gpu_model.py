@@ -327,7 +327,7 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name,
                                          ("MAX", "pubmed", 1536)])
 def test_top_launch_matches_separate_launches(gs, monkeypatch, agg, name, B):
     """The one-launch top layer + loss head (kernels/top.hip: layer-2
-    aggregate, linear, relu, NLL head, dZ and dIn on the VALU) against the
+    aggregate, linear, relu, NLL head, dZ and dIn on the matrix cores) against the
     separate launches it replaces (agg_fwd, the MFMA linear, cls_rows, the
     MFMA dIn role): it repeats their product chains in the f32 MFMA order, so
     loss, every gradient and the updated parameters are bitwise equal,

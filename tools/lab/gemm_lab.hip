@@ -389,6 +389,132 @@ __global__ __launch_bounds__(256, 2) void fwd_wreg_kernel(int n, int F, int H, c
     }
 }
 
+template <int N>
+__device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), other counters untouched
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// W-stationary, one block per CU: block b owns column half h = (b >> 3) & 1
+// and the row tiles p, p + NP, p + 2 NP of pair p = (b >> 4) * 8 + (b & 7)
+// (blocks b and b + 8 -- one XCD under round-robin placement -- are the two
+// halves of a pair, so a tile's A rows come from HBM once).  Wave w keeps its
+// 16-column slice of W (all K) in registers, loaded once; the block's tiles
+// (16 rows of [X[sidx] | A], 2 KiB each) land in LDS by DMA (one 1 KiB
+// row-half per wave instruction: waves 0, 2 the self halves, 1, 3 the agg
+// halves), issued tile 0 first, then W, then the rest; every count is a
+// compile-time constant (CNT tiles) so the waits are exact.  Same MFMA
+// operands in the same order as the chunked kernel: bitwise equal.
+template <int CNT, bool PACKED>
+__device__ __forceinline__ void wstat_body(int n, int H, const float* __restrict__ Xs, int64_t ldxs,
+                                           const int* __restrict__ sidx, const float* __restrict__ A, int64_t lda,
+                                           const float* __restrict__ W, float* __restrict__ out, int64_t ldo,
+                                           int h, int p, int NP, float* sA, unsigned long long* stamp) {
+    constexpr int K = 512, NG = 32, PITCH = K + 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int half = wave & 1;
+    // this wave's source rows: lane l < 8 * CNT -> tile l >> 3, row (wave >> 1) + 2 (l & 7)
+    int myrow = 0;
+    {
+        const int li = min(lane, 8 * CNT - 1);
+        const int gr = min(16 * (p + (li >> 3) * NP) + (wave >> 1) + 2 * (li & 7), n - 1);
+        myrow = half ? gr : sidx[gr];
+    }
+    const float* base = half ? A : Xs;
+    const int64_t ld = half ? lda : ldxs;
+    // register staging: tile i's 8 row-halves of this wave, 16 B per lane
+    // each, two tiles in flight (tile 2 reuses tile 0's registers once they
+    // are in LDS)
+    // (eight named registers per tile: no private array for the compiler to
+    // leave in scratch)
+#define GS_LAB_STG(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7)
+    uint4 s0_0, s0_1, s0_2, s0_3, s0_4, s0_5, s0_6, s0_7;
+    uint4 s1_0, s1_1, s1_2, s1_3, s1_4, s1_5, s1_6, s1_7;
+#define GS_LAB_LD(q) dst##q = *reinterpret_cast<const uint4*>(base + (int64_t)__builtin_amdgcn_readlane(myrow, 8 * i + q) * ld + 4 * lane);
+#define GS_LAB_ST(q) *reinterpret_cast<uint4*>(sA + (i * 16 + (wave >> 1) + 2 * q) * PITCH + half * (K / 2) + 4 * lane) = src##q;
+    auto load_tile = [&](int i, uint4& dst0, uint4& dst1, uint4& dst2, uint4& dst3, uint4& dst4, uint4& dst5,
+                         uint4& dst6, uint4& dst7) __attribute__((always_inline)) { GS_LAB_STG(GS_LAB_LD) };
+    auto stage = [&](int i, const uint4& src0, const uint4& src1, const uint4& src2, const uint4& src3,
+                     const uint4& src4, const uint4& src5, const uint4& src6, const uint4& src7)
+                     __attribute__((always_inline)) {
+        GS_LAB_STG(GS_LAB_ST)
+        __syncthreads();
+    };
+#define GS_LAB_S0 s0_0, s0_1, s0_2, s0_3, s0_4, s0_5, s0_6, s0_7
+#define GS_LAB_S1 s1_0, s1_1, s1_2, s1_3, s1_4, s1_5, s1_6, s1_7
+    load_tile(0, GS_LAB_S0);
+    uint4 w[NG];
+    if constexpr (PACKED) {  // Wp[g][ct][lane]: one coalesced 1 KiB read per group
+        const uint4* wp = reinterpret_cast<const uint4*>(W) + (4 * h + wave) * 64 + lane;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) w[g] = wp[(int64_t)g * (H / 16) * 64];
+    } else {
+        const float* wrow = W + (int64_t)(64 * h + 16 * wave + r) * K + 4 * kq;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) w[g] = *reinterpret_cast<const uint4*>(wrow + 16 * g);
+    }
+    if constexpr (CNT > 1) load_tile(1, GS_LAB_S1);
+    auto compute = [&](int i) __attribute__((always_inline)) {
+        const float* ar = sA + (i * 16 + r) * PITCH + 4 * kq;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const uint4 a = *reinterpret_cast<const uint4*>(ar + 16 * g);
+            acc = gs::mfma_slot<float>(a, w[g], acc);
+        }
+        const int t = p + i * NP;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * t + 4 * kq + j;
+            if (row < n) {
+                const float v = acc[j];
+                out[(int64_t)row * ldo + 64 * h + 16 * wave + r] = (!(v > 0.f) && v == v) ? 0.f : v;
+            }
+        }
+    };
+    stage(0, GS_LAB_S0);
+    if (stamp && (threadIdx.x & 63) == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (CNT > 2) load_tile(2, GS_LAB_S0);
+    compute(0);
+    if constexpr (CNT > 1) {
+        stage(1, GS_LAB_S1);
+        compute(1);
+    }
+    if constexpr (CNT > 2) {
+        stage(2, GS_LAB_S0);
+        compute(2);
+    }
+}
+
+template <int MAXT, bool PACKED>
+__global__ __launch_bounds__(256, 1) void fwd_wstat_kernel(int n, int F, int H, const float* __restrict__ Xs,
+                                                           int64_t ldxs, const int* __restrict__ sidx,
+                                                           const float* __restrict__ A, int64_t lda,
+                                                           const float* __restrict__ W, float* __restrict__ out,
+                                                           int64_t ldo, unsigned long long* __restrict__ stamps) {
+    static_assert(MAXT >= 1 && MAXT <= 3, "tiles per block");
+    unsigned long long t_start = 0;
+    if (stamps) t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* ta = stamps ? stamps + 3 * ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) : nullptr;
+    extern __shared__ __attribute__((aligned(16))) float sA[];  // [MAXT * 16][K + 4]
+    const int b = blockIdx.x, NP = gridDim.x >> 1;
+    const int h = (b >> 3) & 1, p = (b >> 4) * 8 + (b & 7);
+    const int ntiles = (n + 15) / 16;
+    const int cnt = p < ntiles ? min(MAXT, (ntiles - p + NP - 1) / NP) : 0;
+    switch (cnt) {
+        case 1: wstat_body<1, PACKED>(n, H, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA, ta); break;
+        case 2: if constexpr (MAXT >= 2) wstat_body<2, PACKED>(n, H, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA, ta); break;
+        case 3: if constexpr (MAXT >= 3) wstat_body<3, PACKED>(n, H, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA, ta); break;
+        default: break;
+    }
+    if (stamps && (threadIdx.x & 63) == 0) {
+        const unsigned long long t_e = __builtin_amdgcn_s_memrealtime();
+        unsigned long long* q = stamps + 3 * ((int64_t)b * 4 + (threadIdx.x >> 6));
+        q[0] = t_start; if (cnt == 0) q[1] = t_e; q[2] = t_e;
+    }
+}
+
 }  // namespace lab
 
 static unsigned long long* g_stamps = nullptr;  // set for one instrumented launch
@@ -429,6 +555,23 @@ static void run_wreg(int n, int F, int H, const float* X, const int* sidx, const
     const int tiles = (n + 15) / 16;
     dim3 grid(std::min(tiles, RG), H / 64);
     lab::fwd_wreg_kernel<PF><<<grid, 256, 0, st>>>(n, F, H, X, F, sidx, A, F, W, out, H, g_stamps);
+}
+
+template <int MAXT, bool FILL, bool PACKED = false>
+static void run_wstat(int n, int F, int H, const float* X, const int* sidx, const float* A, const float* W,
+                      const float* Wp, float* out, hipStream_t st) {
+    static bool attr = false;
+    const int smem = MAXT * 16 * 516 * 4;
+    if (!attr) {
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(lab::fwd_wstat_kernel<MAXT, PACKED>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+        attr = true;
+    }
+    const int tiles = (n + 15) / 16;
+    int np = FILL ? 128 : ((tiles + MAXT - 1) / MAXT + 7) / 8 * 8;  // pairs (FILL: one block per CU)
+    while (np * MAXT < tiles) np += 8;
+    lab::fwd_wstat_kernel<MAXT, PACKED><<<2 * np, 256, smem, st>>>(n, F, H, X, F, sidx, A, F, PACKED ? Wp : W, out, H,
+                                                                   g_stamps);
 }
 
 template <int NW, int D>
@@ -499,21 +642,17 @@ int main(int argc, char** argv) {
     }
     Variant vs[] = {
         {"default wide<32>", run_default},
-        {"rows packed CW16 NW8 D8", run_rows<16, 8, 8, true>},
         {"rows packed CW16 NW4 D8 (64 cols)", run_rows<16, 4, 8, true>},
         {"rows packed CW16 NW4 D2 (64 cols)", run_rows<16, 4, 2, true>},
         {"t32 KS1 D2", run_t32<1, 2>, -4},
         {"t32 KS2 D2", run_t32<2, 2>, -8},
         {"2ph NW8 D4", run_2ph<8, 4>, 8},
-        {"2ph NW8 D2", run_2ph<8, 2>, 8},
-        {"2ph NW4 D4 (64 cols)", run_2ph<4, 4>, 4},
-        {"2ph NW4 D2 (64 cols)", run_2ph<4, 2>, 4},
-        {"2ph NW2 D4 (32 cols)", run_2ph<2, 4>, 2},
+        {"wstat MAXT3 256 blocks", run_wstat<3, true>, 4},
+        {"wstat MAXT3 184 blocks", run_wstat<3, false>, 4},
+        {"wstat packed MAXT3 256 blocks", run_wstat<3, true, true>, 4},
+        {"wstat packed MAXT3 184 blocks", run_wstat<3, false, true>, 4},
         {"wreg RG256", run_wreg<false, 256>, 4},
-        {"wreg RG all", run_wreg<false, 1 << 20>, 4},
-        {"wreg RG138", run_wreg<false, 138>, 4},
         {"wreg PF RG256", run_wreg<true, 256>, 4},
-        {"wreg PF RG138", run_wreg<true, 138>, 4},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
