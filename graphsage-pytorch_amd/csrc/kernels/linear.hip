@@ -1,4 +1,5 @@
 // C-ABI launchers of the SageLayer kernels (kernels/linear_dev.hpp).
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -69,6 +70,138 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum
         return;
     }
     sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+}
+
+// ------------------------------------------------- W-stationary forward
+// Layer-1 shape only (K = 512, H = 128, fp32, self rows): one block per CU.
+// Block b owns column half h = (b >> 3) & 1 and the row tiles p, p + NP,
+// p + 2 NP of pair p = (b >> 4) * 8 + (b & 7) (blocks b and b + 8, one XCD
+// under round-robin placement, are the two halves of a pair, so a tile's A
+// rows come from HBM once).  Wave w keeps its 16-column slice of W (all K)
+// in registers, loaded once; the block's 16-row tiles of [X[sidx] | A] are
+// register-staged into LDS (one 1 KiB row-half per wave instruction: waves 0
+// and 2 the self halves, 1 and 3 the aggregate halves), two tiles in flight.
+// Every count is a compile-time constant (CNT tiles), so the compiler's
+// waits are exact.  Same MFMA operands in the same order as the chunked
+// kernel: bitwise equal (tools/lab/gemm_lab.hip measured it 16.2 against
+// 16.8 us for the default 32-row kernel, warm, in the lab).
+constexpr int kWstatK = 512, kWstatPitch = kWstatK + 4, kWstatMaxTiles = 3;
+
+template <int CNT, bool RELU>
+__device__ __forceinline__ void wstat_body(int n, const float* __restrict__ Xs, int64_t ldxs,
+                                           const int* __restrict__ sidx, const float* __restrict__ A, int64_t lda,
+                                           const float* __restrict__ W, float* __restrict__ out, int64_t ldo, int h,
+                                           int p, int NP, float* sA) {
+    constexpr int K = kWstatK, NG = K / 16, PITCH = kWstatPitch;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 15, kq = lane >> 4;
+    const int half = wave & 1;
+    // this wave's source rows: lane l < 8 * CNT -> tile l >> 3, row (wave >> 1) + 2 (l & 7)
+    int myrow;
+    {
+        const int li = min(lane, 8 * CNT - 1);
+        const int gr = min(16 * (p + (li >> 3) * NP) + (wave >> 1) + 2 * (li & 7), n - 1);
+        myrow = half ? gr : sidx[gr];
+    }
+    const float* base = half ? A : Xs;
+    const int64_t ld = half ? lda : ldxs;
+    // eight named registers per staged tile (a private array would stay in scratch)
+#define GS_WST8(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7)
+    uint4 s0_0, s0_1, s0_2, s0_3, s0_4, s0_5, s0_6, s0_7;
+    uint4 s1_0, s1_1, s1_2, s1_3, s1_4, s1_5, s1_6, s1_7;
+#define GS_WST_LD(q) \
+    d##q = *reinterpret_cast<const uint4*>(base + (int64_t)__builtin_amdgcn_readlane(myrow, 8 * i + q) * ld + 4 * lane);
+#define GS_WST_ST(q) \
+    *reinterpret_cast<uint4*>(sA + (i * 16 + (wave >> 1) + 2 * q) * PITCH + half * (K / 2) + 4 * lane) = v##q;
+    auto load_tile = [&](int i, uint4& d0, uint4& d1, uint4& d2, uint4& d3, uint4& d4, uint4& d5, uint4& d6,
+                         uint4& d7) __attribute__((always_inline)) { GS_WST8(GS_WST_LD) };
+    auto stage = [&](int i, const uint4& v0, const uint4& v1, const uint4& v2, const uint4& v3, const uint4& v4,
+                     const uint4& v5, const uint4& v6, const uint4& v7) __attribute__((always_inline)) {
+        GS_WST8(GS_WST_ST)
+        __syncthreads();
+    };
+#define GS_WST_S0 s0_0, s0_1, s0_2, s0_3, s0_4, s0_5, s0_6, s0_7
+#define GS_WST_S1 s1_0, s1_1, s1_2, s1_3, s1_4, s1_5, s1_6, s1_7
+    load_tile(0, GS_WST_S0);
+    uint4 w[NG];
+    {
+        const float* wrow = W + (int64_t)(64 * h + 16 * wave + r) * K + 4 * kq;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) w[g] = *reinterpret_cast<const uint4*>(wrow + 16 * g);
+    }
+    if constexpr (CNT > 1) load_tile(1, GS_WST_S1);
+    auto compute = [&](int i) __attribute__((always_inline)) {
+        const float* ar = sA + (i * 16 + r) * PITCH + 4 * kq;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const uint4 a = *reinterpret_cast<const uint4*>(ar + 16 * g);
+            acc = mfma_slot<float>(a, w[g], acc);
+        }
+        const int t = p + i * NP;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * t + 4 * kq + j;
+            if (row < n) {
+                const float v = acc[j];
+                out[(int64_t)row * ldo + 64 * h + 16 * wave + r] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;
+            }
+        }
+    };
+    stage(0, GS_WST_S0);
+    if constexpr (CNT > 2) load_tile(2, GS_WST_S0);  // tile 0's registers are in LDS now
+    compute(0);
+    if constexpr (CNT > 1) {
+        stage(1, GS_WST_S1);
+        compute(1);
+    }
+    if constexpr (CNT > 2) {
+        stage(2, GS_WST_S0);
+        compute(2);
+    }
+#undef GS_WST8
+#undef GS_WST_LD
+#undef GS_WST_ST
+#undef GS_WST_S0
+#undef GS_WST_S1
+}
+
+template <bool RELU>
+__global__ __launch_bounds__(256, 1) void linear_fwd_wstat_kernel(int n, const float* __restrict__ Xs, int64_t ldxs,
+                                                                  const int* __restrict__ sidx,
+                                                                  const float* __restrict__ A, int64_t lda,
+                                                                  const float* __restrict__ W, float* __restrict__ out,
+                                                                  int64_t ldo) {
+    extern __shared__ __attribute__((aligned(16))) float sA[];  // [kWstatMaxTiles * 16][kWstatPitch]
+    const int b = blockIdx.x, NP = gridDim.x >> 1;
+    const int h = (b >> 3) & 1, p = (b >> 4) * 8 + (b & 7);
+    const int ntiles = (n + 15) / 16;
+    const int cnt = p < ntiles ? min(kWstatMaxTiles, (ntiles - p + NP - 1) / NP) : 0;
+    if (cnt == 1) wstat_body<1, RELU>(n, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA);
+    else if (cnt == 2) wstat_body<2, RELU>(n, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA);
+    else if (cnt == 3) wstat_body<3, RELU>(n, Xs, ldxs, sidx, A, lda, W, out, ldo, h, p, NP, sA);
+}
+
+static bool wstat_lds_ready() {
+    static int ok = -1;
+    if (ok < 0) {
+        const int want = kWstatMaxTiles * 16 * kWstatPitch * static_cast<int>(sizeof(float));
+        const bool a = hipFuncSetAttribute(reinterpret_cast<const void*>(linear_fwd_wstat_kernel<true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, want) == hipSuccess;
+        const bool b = hipFuncSetAttribute(reinterpret_cast<const void*>(linear_fwd_wstat_kernel<false>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, want) == hipSuccess;
+        (void)hipGetLastError();
+        ok = (a && b) ? 1 : 0;
+    }
+    return ok == 1;
+}
+
+// Pairs of blocks for n rows: at least one block per CU (256), at most three
+// 16-row tiles per block, whole groups of 8 pairs (the XCD pairing above).
+static int wstat_pairs(int64_t n) {
+    const int64_t tiles = (n + 15) / 16;
+    int64_t np = std::max<int64_t>(128, (tiles + kWstatMaxTiles - 1) / kWstatMaxTiles);
+    return static_cast<int>((np + 7) / 8 * 8);
 }
 
 static bool slab_split_on(int64_t len) {
@@ -146,6 +279,19 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     // the layer-1 shape (microbenchmark 14.5 against 10 us): each wave's
     // 16-row tile runs its whole K chain (2 x 128 MFMAs), and 1.1k such waves
     // on 1024 SIMDs leave a second round on some of them.  Opt-in.
+    // GS_LIN_FWD=wstat: the W-stationary kernel above (layer-1 shape only).
+    if (fwd_mode == "wstat" && dt == GS_F32 && vload && self && K == kWstatK && H == 128 && n < (int64_t(1) << 30) &&
+        wstat_lds_ready()) {
+        const int np = wstat_pairs(n);
+        const uint32_t smem = kWstatMaxTiles * 16 * kWstatPitch * sizeof(float);
+        const float* xs = static_cast<const float*>(Xs);
+        const float* a = static_cast<const float*>(A);
+        const float* w = static_cast<const float*>(Wd);
+        if (relu) launch_k(linear_fwd_wstat_kernel<true>, dim3(2 * np), dim3(kThreads), smem, st, nn, xs, ldxs, sidx, a, lda, w, out, ldo);
+        else launch_k(linear_fwd_wstat_kernel<false>, dim3(2 * np), dim3(kThreads), smem, st, nn, xs, ldxs, sidx, a, lda, w, out, ldo);
+        check_launch("gs_sage_linear_fwd(wstat)");
+        return GS_OK;
+    }
     const bool wres_on = fwd_mode == "wres";
     if (wres_on && dt == GS_F32 && vload && K % 256 == 0 && K <= 512 && H % kWresCols == 0 &&
         wres_lds_ready(K)) {

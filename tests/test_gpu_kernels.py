@@ -130,7 +130,8 @@ def test_sage_linear_fwd_bwd(n, F, H, gcn, dtype):
 
 
 @pytest.mark.parametrize("n,F,H", [(1, 256, 128), (37, 128, 128), (4321, 256, 128), (4400, 256, 128),
-                                   (513, 128, 64), (100, 64, 32), (2048, 256, 256)])
+                                   (513, 128, 64), (100, 64, 32), (2048, 256, 256), (6200, 256, 128),
+                                   (17, 256, 128)])
 @pytest.mark.parametrize("gcn", [False, True])
 def test_wres_forward_bitwise_equals_tiled_kernels(monkeypatch, n, F, H, gcn):
     """The W-resident fp32 forward (linear_fwd_wres_kernel: a 32-column W
@@ -145,7 +146,7 @@ def test_wres_forward_bitwise_equals_tiled_kernels(monkeypatch, n, F, H, gcn):
     K = F if gcn else 2 * F
     W = torch.randn(H, K, device=DEV) * 0.05
     outs = {}
-    for mode in ("wres", "wide32", "chunked"):
+    for mode in ("wres", "wide32", "chunked", "wstat"):
         monkeypatch.setenv("GS_LIN_FWD", mode)
         out = torch.full((n, H), float("nan"), device=DEV)
         ops.sage_linear_fwd(A, W, out, Xs=None if gcn else Xs, sidx=None if gcn else sidx)
@@ -153,6 +154,8 @@ def test_wres_forward_bitwise_equals_tiled_kernels(monkeypatch, n, F, H, gcn):
         outs[mode] = out
     assert torch.equal(outs["wres"], outs["wide32"])
     assert torch.equal(outs["wres"], outs["chunked"])
+    # the W-stationary kernel (layer-1 shape: K = 512, H = 128, self rows; other shapes fall back)
+    assert torch.equal(outs["wstat"], outs["chunked"])
 
 
 @pytest.mark.parametrize("agg", ["MEAN", "MAX"])
