@@ -1,4 +1,4 @@
-"""Drop-in ``UnsupervisedLoss`` (the reference's src/models.py:30-186).
+"""Drop-in ``UnsupervisedLoss`` (the reference's src/models.py:45-186).
 
 ``extend_nodes`` runs natively (host/unsup.cpp): the random walks, the
 5-hop balls and ``random.sample`` over ``set(train) - ball`` draw from the
@@ -50,7 +50,7 @@ def _per_node(nodes, arr, cnt, keep=None):
 
 
 class UnsupervisedLoss:
-    """UnsupervisedLoss(adj_lists, train_nodes, device) — models.py:30-186.
+    """UnsupervisedLoss(adj_lists, train_nodes, device) — models.py:45-186.
 
     adj_lists may be the reference's dict of sets (adopted with its set
     layouts) or a CSRGraph.  ``rng``: a sampler.RNG to draw from instead of the
