@@ -1,5 +1,5 @@
 """Pin the unsupervised-path oracle (oracle/unsup_semantics.py) against vectors
-captured from the reference's UnsupervisedLoss (models.py:30-186)."""
+captured from the reference's UnsupervisedLoss (models.py:45-186)."""
 import random
 
 import numpy as np
