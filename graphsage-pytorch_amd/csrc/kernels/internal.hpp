@@ -16,6 +16,8 @@ namespace gs {
 // so a caller can all-reduce the finished gradients [w1_floats, n_params)
 // under that GEMM (the runner's bucketed all-reduce).  Empty: no hook.
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
+// Called on the step's stream right after the layer-1 forward launch of a training step.
+void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
 int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip

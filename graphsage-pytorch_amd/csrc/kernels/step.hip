@@ -52,6 +52,7 @@ struct gs_trainer {
     int npart[2] = {0, 0};
     bool norm_ready = false;
     std::function<void(hipStream_t)> upper_hook;  // internal.hpp trainer_set_upper_hook
+    std::function<void(hipStream_t)> fwd1_hook;   // after the layer-1 forward launch (trainer_set_fwd1_hook)
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
         for (auto& tm : timer) {
@@ -247,6 +248,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                               dst_L, agg[0], F, W1, h[0], H, 1, st));
         g_launch_events = {};  // an alternative kernel that does not time leaves it armed
         timed_done(T, 1, armed);
+        if (T.fwd1_hook && !embed_out) T.fwd1_hook(st);
     }
     // a 2-layer training step runs layer 2, the loss head and layer 2's dIn in
     // one launch (top.hip) inside the fused backward below
@@ -399,6 +401,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
 }
 
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->upper_hook = std::move(hook); }
+void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->fwd1_hook = std::move(hook); }
 
 int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols[0]; }
 

@@ -123,6 +123,14 @@ struct gs_runner {
     hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
     hipEvent_t gathered[kDev] = {};        // side: pull + gather of the batch in entry k
+    // GS_RUNNER_GATE_FWD: the lookahead pull + gather of batch b waits (on the
+    // host) for the layer-1 forward of step b-2 instead of only for step b-3,
+    // so the side stream's work lands under that step's latency-bound launches
+    // rather than under its forward (A/B switch)
+    bool gate_fwd = false;
+    hipEvent_t fwd_done[kDev] = {};
+    bool fwd_busy[kDev] = {};
+    int cur_k = -1;                        // ring entry of the step being issued (fwd1 hook)
     hipStream_t side = nullptr;
     struct Inflight {
         int stream = -1, slot = -1;
@@ -240,6 +248,10 @@ bool gs_runner::issue(int64_t b, bool block) {
     if (slot.status != GS_OK) fail(slot.status, slot.error);
     const int k = static_cast<int>(b % kDev);
     if (dev_busy[k]) hip_ok(hipEventSynchronize(dev_done[k]), "hipEventSynchronize");  // batch b-3 done
+    if (gate_fwd && !block && b >= 2) {
+        const int kp = static_cast<int>((b - 2) % kDev);
+        if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
+    }
     stats.wait_ring_s += secs(tr, Clock::now());
     const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
     const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
@@ -271,6 +283,7 @@ gs_runner::~gs_runner() {
     // of it before any buffer is freed.
     if (side) (void)hipStreamSynchronize(side);
     if (comm_stream) (void)hipStreamSynchronize(comm_stream);
+    if (cfg.trainer && gate_fwd) gs::trainer_set_fwd1_hook(cfg.trainer, {});
     for (int d = 0; d < kDev; ++d)
         if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
     for (auto& s : streams)
@@ -283,6 +296,10 @@ gs_runner::~gs_runner() {
         }
     for (int d = 0; d < kDev; ++d) {
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
+        if (fwd_done[d]) {
+            (void)hipEventSynchronize(fwd_done[d]);
+            (void)hipEventDestroy(fwd_done[d]);
+        }
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
         if (dev[d]) (void)hipFree(dev[d]);
     }
@@ -438,6 +455,17 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             hip_ok(hipEventRecord(rp->upper_reduced, rp->comm_stream), "hipEventRecord");
         });
     }
+    r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
+    if (r->gate_fwd) {
+        for (int d = 0; d < gs_runner::kDev; ++d)
+            hip_ok(hipEventCreateWithFlags(&r->fwd_done[d], sync_event_flags()), "hipEventCreate");
+        gs_runner* rp = r.get();
+        trainer_set_fwd1_hook(cfg->trainer, [rp](hipStream_t st) {
+            if (rp->cur_k < 0) return;
+            hip_ok(hipEventRecord(rp->fwd_done[rp->cur_k], st), "hipEventRecord");
+            rp->fwd_busy[rp->cur_k] = true;
+        });
+    }
     for (auto& s : r->streams) {
         SamplerStream* sp = s.get();
         gs_runner* rp = r.get();
@@ -501,9 +529,11 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             if (rc != GS_OK) fail(rc, gs_last_error());
             t3 = Clock::now();
         } else {
+            r->cur_k = k;
             int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets,
                                                           pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
                                                           st);
+            r->cur_k = -1;
             if (rc != GS_OK) fail(rc, gs_last_error());
             t3 = Clock::now();
             // with a communicator (any world size, so one rank exercises the same
