@@ -313,7 +313,12 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     }
     if ((wide_on || wide32_on) && dt == GS_F32 && vload) {
         const int R = wide32_on ? 32 : kWideRows;
-        const dim3 gw(static_cast<unsigned>((n + R - 1) / R), static_cast<unsigned>((H + 63) / 64));
+        // XCD map (a 1-D grid, the kernel derives its tile): the column tiles of a row tile share
+        // an XCD's L2; GS_FWD_NOXCD=1 restores the 2-D grid (A/B)
+        static const bool noxcd = std::getenv("GS_FWD_NOXCD") != nullptr;
+        const int64_t gx = (n + R - 1) / R, gy = (H + 63) / 64;
+        const dim3 gw = (noxcd || gy == 1) ? dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy))
+                                           : dim3(static_cast<unsigned>((gx + 7) / 8 * 8 * gy));
         const float* xs = static_cast<const float*>(Xs);
         const float* a = static_cast<const float*>(A);
         const float* w = static_cast<const float*>(Wd);

@@ -266,7 +266,18 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, kq = lane >> 4;
     const int wr = wave % RT, wc = wave / RT;
-    const int m0 = blockIdx.x * ROWS, c0 = blockIdx.y * 64;
+    // 1-D grid (the launcher's XCD map): the gy column tiles of row tile x are
+    // blocks 8 apart in dispatch order, i.e. on one XCD under round-robin
+    // placement, so the second column tile re-reads the A rows from that
+    // XCD's L2 instead of HBM / MALL.  2-D grid: x = row tile, y = column tile.
+    int bx = blockIdx.x, by = blockIdx.y;
+    if (gridDim.y == 1 && H > 64) {
+        const int gy = (H + 63) / 64, b = blockIdx.x;
+        bx = (b / (8 * gy)) * 8 + (b & 7);
+        by = (b >> 3) % gy;
+        if (bx * ROWS >= n) return;  // spare blocks of the last group of 8
+    }
+    const int m0 = bx * ROWS, c0 = by * 64;
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
     const int arow_i = min(m0 + lr, n - 1);
     const float* arow = A + static_cast<int64_t>(arow_i) * lda;
