@@ -25,6 +25,42 @@ __global__ __launch_bounds__(kBlock) void resolve_ids_kernel(int n_dst, int k, c
     ids[t] = nb;
 }
 
+// The same resolve, plus a second role for the fused top launch (top.hip):
+// the roots' hop-1 lists padded to `tk` slots behind their self row, one
+// record of 1 + tk ids per root (-1 past the list), so the top launch loads a
+// root's whole neighbourhood in one round instead of three (ptr, list, rows).
+__global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, const int* __restrict__ ptr,
+                                                             const int* __restrict__ ent,
+                                                             const int* __restrict__ col,
+                                                             const int* __restrict__ dst_ids, int gcn,
+                                                             int* __restrict__ ids, int n_top, int tk,
+                                                             const int* __restrict__ tptr,
+                                                             const int* __restrict__ tnbr,
+                                                             const int* __restrict__ tself, int* __restrict__ tout) {
+    const int64_t t = blockIdx.x * int64_t(kBlock) + threadIdx.x;
+    const int64_t n1 = static_cast<int64_t>(n_dst) * k;
+    if (t < n1) {
+        const int r = static_cast<int>(t / k), j = static_cast<int>(t - static_cast<int64_t>(r) * k);
+        const int e = ptr[r] + j;
+        int nb = -1;
+        if (e < ptr[r + 1]) nb = col[ent[e]];
+        if (!gcn && nb == dst_ids[r]) nb = -1;
+        ids[t] = nb;
+        return;
+    }
+    const int64_t u = t - n1;
+    if (u >= static_cast<int64_t>(n_top) * (tk + 1)) return;
+    const int r = static_cast<int>(u / (tk + 1)), j = static_cast<int>(u - static_cast<int64_t>(r) * (tk + 1));
+    int v;
+    if (j == 0) {
+        v = tself[r];
+    } else {
+        const int e = tptr[r] + j - 1;
+        v = e < tptr[r + 1] ? tnbr[e] : -1;
+    }
+    tout[u] = v;
+}
+
 // A row chunk as loaded (one 16-byte vector per lane, or a scalar), unpacked
 // to floats only when accumulated.
 template <typename T, int VEC>
@@ -146,6 +182,20 @@ void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
     resolve_ids_kernel<<<dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
         static_cast<int>(n_dst), k, ptr, ent, col, dst_ids, gcn, ids);
     check_launch("resolve_ids");
+}
+
+void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
+                        const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st) {
+    GS_REQUIRE(n_dst >= 0 && k >= 1 && n_dst * k < (int64_t(1) << 31) && n_top >= 0 && tk >= 1 &&
+                   n_top * (tk + 1) < (int64_t(1) << 30),
+               GS_EINVAL, "bad sizes");
+    const int64_t total = n_dst * k + n_top * (tk + 1);
+    if (total == 0) return;
+    resolve_top_kernel<<<dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
+        static_cast<int>(n_dst), k, ptr, ent, col, dst_ids, gcn, ids, static_cast<int>(n_top), tk, tptr, tnbr, tself,
+        tout);
+    check_launch("resolve_top");
 }
 
 void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,

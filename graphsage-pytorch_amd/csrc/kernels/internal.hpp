@@ -42,6 +42,14 @@ int sum_slabs_grid(int64_t len);
 // agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)
 void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, hipStream_t st);
+// resolve_ids_launch plus the fused top launch's padded hop-1 records
+// (tout[r][0] = self, [1..tk] = the list, -1 past it; n_top roots).
+void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
+                        const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st);
+// Padded hop-1 records for the fused top launch, one buffer per gather slot
+// (2-layer training steps; B roots, fanout tk <= 31).
+void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk);
 void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
                     const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st);
 
@@ -106,9 +114,11 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
 // loss head and the layer's dIn in one launch (one block per 4 roots).
 // Returns the number of classifier partial slabs written (the loss head's).
 bool top_supported(int64_t H, int64_t C, bool gcn);
+// tids: optional padded hop-1 records (resolve_top_launch, 1 + tk ids per
+// root); nullptr reads the pack's lists (ptr, nbr, self).
 int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
                 const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
                 const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
-                hipStream_t st);
+                hipStream_t st, const int32_t* tids = nullptr, int tk = 0);
 
 }  // namespace gs

@@ -42,6 +42,11 @@ struct gs_trainer {
     // (k_ids slots per destination), when reserved with a fanout
     int32_t* ids_slot[kSlots] = {};
     int k_ids = 0;
+    // padded hop-1 records for the fused top launch, per gather slot (trainer_reserve_top)
+    int32_t* top_slot[kSlots] = {};
+    bool top_ready[kSlots] = {};
+    int64_t top_rows = 0;
+    int top_k = 0;
     // clip-norm partials produced by the fused backward's reduce launches
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
@@ -62,6 +67,8 @@ struct gs_trainer {
         for (void* p : a1_slot)
             if (p) (void)hipFree(p);
         for (int32_t* p : ids_slot)
+            if (p) (void)hipFree(p);
+        for (int32_t* p : top_slot)
             if (p) (void)hipFree(p);
     }
 };
@@ -156,7 +163,21 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     };
     const int64_t n_dst = hop_sizes[4 * (L - 1)];
     int32_t* ids = T.ids_slot[slot];
-    resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids, st);
+    const int64_t n_top = hop_sizes[0];
+    T.top_ready[slot] = T.top_k > 0 && L == 2 && !c.gcn && n_top <= T.top_rows && T.top_slot[slot] &&
+                        hop_sizes[3] <= n_top * T.top_k;  // every root's list fits tk slots
+    if (T.top_ready[slot]) {
+        auto f1 = [&](int f) -> const int32_t* {
+            const int64_t o = offsets[f];  // hop 1
+            GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
+            return pack + o;
+        };
+        resolve_top_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
+                           n_top, T.top_k, f1(GS_PK_NBR_PTR), f1(GS_PK_NBR), f1(GS_PK_SELF), T.top_slot[slot], st);
+    } else {
+        resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
+                           st);
+    }
     const bool timed = timed_arm(T, 0);
     agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim, n_dst,
                    T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, T.a1_slot[slot], c.feat_dim, st);
@@ -308,9 +329,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             int cls_rows;
             if (top) {
                 const bool armed = timed_arm(T, 3);
+                static const bool no_tids = std::getenv("GS_TOP_NO_TIDS") != nullptr;  // A/B: the pack's lists
+                const bool tids = !no_tids && a1_slot >= 0 && T.top_ready[a1_slot];
                 cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
                                        fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
-                                       roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st);
+                                       roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st,
+                                       tids ? T.top_slot[a1_slot] : nullptr, tids ? T.top_k : 0);
                 timed_done(T, 3, armed);
                 lb[0].din_ready = true;
             } else {
@@ -401,6 +425,20 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
 }
 
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->upper_hook = std::move(hook); }
+
+void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk) {
+    if (t->cfg.n_layers != 2 || t->cfg.gcn || tk < 1 || tk > 31 || B < 1) return;
+    if (B <= t->top_rows && tk == t->top_k) return;
+    for (int32_t*& p : t->top_slot) {
+        if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
+        p = nullptr;
+        GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(B * (tk + 1) * 4, 256)) == hipSuccess, GS_ENOMEM,
+                   "hipMalloc(top records)");
+    }
+    for (bool& r : t->top_ready) r = false;
+    t->top_rows = B;
+    t->top_k = tk;
+}
 void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->fwd1_hook = std::move(hook); }
 
 int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols[0]; }

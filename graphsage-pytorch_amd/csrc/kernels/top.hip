@@ -64,6 +64,8 @@ struct TopArgs {
     float* dZ;           // [B][H], masked by relu'(E)
     float* dIn;          // [B][2H]
     float* slab;         // classifier partials, one [C][H+1] + 1 slab per block
+    const int* tids;     // optional: per root [self | list padded to tk with -1] (resolve_top_launch)
+    int tk;
 };
 
 // k offset of step i (0..15) inside a 16-wide block: the MFMA kernels' order.
@@ -121,16 +123,32 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     const int y_w = a.labels[root];
 
     // ---- stage 1: the aggregate (agg_fwd_kernel<OP, float, 4, 32, explicit>)
-    // and the self row, one 32-lane group per row
+    // and the self row, one 32-lane group per row.  With the padded records
+    // (a.tids) the root's self index and whole list arrive in one load round
+    // (lane gl holds list entry gl, as the pack path's lanes do).
     {
         constexpr int G = 32, NR = 32;
         const int g = tid / G, gl = tid % G;
         if (g < nr) {
             const int r = r0 + g;
             const int f0 = gl * 4;
-            const int srow = a.self[r];
+            int srow, beg, end, pre = -1;
+            if (a.tids) {
+                const int* rec = a.tids + static_cast<int64_t>(r) * (a.tk + 1);
+                const int v = gl <= a.tk ? rec[gl] : -1;
+                srow = __shfl(v, 0, G);
+                pre = __shfl(v, min(gl + 1, G - 1), G);  // lane gl: list entry gl
+                if (gl + 1 > a.tk) pre = -1;
+                const unsigned long long have = __ballot(pre >= 0);
+                const int sh = (tid & 63) & ~(G - 1);  // this group's lanes in the wave's ballot
+                beg = 0;
+                end = __popcll((have >> sh) & ((G == 64) ? ~0ull : ((1ull << G) - 1)));
+            } else {
+                srow = a.self[r];
+                beg = a.ptr[r];
+                end = a.ptr[r + 1];
+            }
             const float4 xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
-            const int beg = a.ptr[r], end = a.ptr[r + 1];
             float acc[4];
             int am[4];
 #pragma unroll
@@ -142,7 +160,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             for (int base = beg; base < end; base += G) {
                 const int m = min(G, end - base);
                 const bool mine = gl < m;
-                const int e = a.nbr[mine ? base + gl : base];
+                const int e = a.tids ? pre : a.nbr[mine ? base + gl : base];
                 const int my = mine ? e : -1;
                 for (int j = 0; j < m; j += NR) {
                     int rows[NR];
@@ -451,13 +469,14 @@ bool top_supported(int64_t H, int64_t C, bool gcn) {
 int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
                 const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
                 const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
-                hipStream_t st) {
+                hipStream_t st, const int32_t* tids, int tk) {
     GS_REQUIRE(B >= 1 && B < (int64_t(1) << 30) && C >= 1 && C <= kTopMaxC, GS_EINVAL, "top: bad sizes");
+    GS_REQUIRE(!tids || (tk >= 1 && tk <= 31), GS_EINVAL, "top: padded lists need 1 <= tk <= 31");
     GS_REQUIRE(aligned16(Hprev) && aligned16(W) && aligned16(Wc) && aligned16(aggo) && aligned16(E) && aligned16(dZ) &&
                    aligned16(dIn) && (agg == GS_AGG_MEAN || (argmax && aligned16(argmax))),
                GS_EINVAL, "top: unaligned operand");
     TopArgs a{static_cast<int>(B), static_cast<int>(C), Hprev, ptr, nbr, self, W, Wc, bc, labels, roots,
-              aggo, argmax, E, dZ, dIn, slab};
+              aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
     if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);

@@ -402,6 +402,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         const int32_t k_last = r->fanouts[cfg->n_hops - 1];  // bounds every last-hop neighbourhood
         const int rc = gs_trainer_gather_reserve(cfg->trainer, nd * r->merge, k_last > 0 ? k_last : 0);
         if (rc != GS_OK) fail(rc, gs_last_error());
+        // the fused top launch's padded hop-1 records (2-layer training, fanout <= 31)
+        if (!cfg->embed_out && cfg->n_hops == 2 && !(cfg->flags & GS_SAMPLE_GCN) && r->fanouts[0] > 0)
+            trainer_reserve_top(cfg->trainer, cfg->batch, r->fanouts[0]);
         // The step workspace at the sampler's worst-case sizes, allocated once:
         // growing it on the first large batch synchronised the stream and
         // stalled that step by ~3 ms inside a measured window.
