@@ -117,6 +117,18 @@ inline thread_local LaunchEvents g_launch_events;
 // a timer site reports which kernel variant it actually timed.
 inline thread_local const char* g_launch_name = nullptr;
 
+// Host-visible step-completion flag (runtime/runner.hip): when set, the next
+// SGD launch of this thread stores `value` into `ptr` (fine-grained pinned
+// memory, system scope) from its first thread at kernel start -- by stream
+// order every earlier launch of the step has completed then -- and clears it.
+// This replaces an event record between steps (a marker packet that idled
+// the queue ~4.4 us, rocprofv3 trace).
+struct DoneFlag {
+    int64_t* ptr = nullptr;
+    int64_t value = 0;
+};
+inline thread_local DoneFlag g_done_flag;
+
 template <typename... KArgs, typename... Args>
 inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
     LaunchEvents ev = g_launch_events;

@@ -245,9 +245,15 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
 // every block) into clip_coef = max_norm / (||scale·g|| + 1e-6) clamped to 1,
 // then p -= lr · (scale · coef) · g and g is left scaled like torch's in-place
 // clip.
+__device__ __forceinline__ void signal_done(int64_t* done, int64_t value) {
+    if (done && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
                                                   const float* __restrict__ part, float scale, float max_norm,
-                                                  float lr) {
+                                                  float lr, int64_t* done, int64_t done_value) {
+    signal_done(done, done_value);
     __shared__ float mult[8];
     // wave w folds group w (lane-strided loads, all in flight, then a fixed
     // xor-tree): the same order in every block
@@ -280,7 +286,8 @@ __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ 
 // so the two dependent rounds overlap; the same per-element arithmetic.
 __global__ __launch_bounds__(kTb) void sgd4_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
                                                    const float* __restrict__ part, float scale, float max_norm,
-                                                   float lr) {
+                                                   float lr, int64_t* done, int64_t done_value) {
+    signal_done(done, done_value);
     __shared__ float mult[8];
     const int64_t n4 = G.off[G.n] / 4;
     const int64_t i0 = blockIdx.x * int64_t(kTb) + threadIdx.x;
@@ -411,11 +418,14 @@ void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart
     if (vec) {  // 4.9 us -> see DESIGN §4 (rmat2m, ~100k parameters)
         const int64_t n4 = total / 4;
         const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + kTb - 1) / kTb, 512))));
-        sgd4_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+        sgd4_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr, g_done_flag.ptr,
+                                          g_done_flag.value);
     } else {
         const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
-        sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr);
+        sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, part, grad_scale, max_norm, lr, g_done_flag.ptr,
+                                         g_done_flag.value);
     }
+    g_done_flag = {};
     check_launch("sgd");
 }
 
@@ -455,7 +465,9 @@ int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params, float
     group_sumsq_kernel<<<dim3(kNormBlocks, n_groups), kTb, 0, st>>>(G, grads, ws);
     const int64_t total = G.off[n_groups];
     const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + kTb - 1) / kTb, 512))));
-    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, ws, grad_scale, max_norm, lr);
+    sgd_kernel<<<grid, kTb, 0, st>>>(G, params, grads, ws, grad_scale, max_norm, lr, g_done_flag.ptr,
+                                     g_done_flag.value);
+    g_done_flag = {};
     check_launch("gs_clip_sgd");
     GS_API_END
 }

@@ -122,6 +122,34 @@ struct gs_runner {
     int32_t* dev[kDev] = {};
     hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
+    // Step completion without an event between steps: the step's SGD launch
+    // stores its batch index into done_host (fine-grained pinned memory) when
+    // it starts, i.e. once every launch that reads the step's ring entry has
+    // completed (stream order); the host polls it.  dev_done events remain for
+    // the last step of each gs_runner_run call (teardown) and as the
+    // GS_RUNNER_EVENTS=1 A/B path.
+    bool use_flag = false;
+    int64_t* done_host = nullptr;          // hipHostMalloc, coherent
+    int64_t* done_dev = nullptr;
+    int64_t flag_step[kDev] = {-1, -1, -1};  // batch whose SGD signals entry k free (-1: none pending)
+    void wait_entry(int k) {
+        if (flag_step[k] >= 0) {
+            const int64_t want = flag_step[k];
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint64_t spin = 0; __atomic_load_n(done_host, __ATOMIC_ACQUIRE) < want; ++spin) {
+                __builtin_ia32_pause();
+                if ((spin & 0xfffff) == 0xfffff &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                    // no progress for 5 s: let the runtime report a device error, then give up
+                    gs::hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+                    if (__atomic_load_n(done_host, __ATOMIC_ACQUIRE) < want)
+                        gs::fail(GS_EHIP, "runner: step completion flag never arrived");
+                }
+            }
+            flag_step[k] = -1;
+        }
+        if (dev_busy[k]) gs::hip_ok(hipEventSynchronize(dev_done[k]), "hipEventSynchronize");
+    }
     hipEvent_t gathered[kDev] = {};        // side: pull + gather of the batch in entry k
     // GS_RUNNER_GATE_FWD: the lookahead pull + gather of batch b waits (on the
     // host) for the layer-1 forward of step b-2 instead of only for step b-3,
@@ -247,7 +275,7 @@ bool gs_runner::issue(int64_t b, bool block) {
     GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
     if (slot.status != GS_OK) fail(slot.status, slot.error);
     const int k = static_cast<int>(b % kDev);
-    if (dev_busy[k]) hip_ok(hipEventSynchronize(dev_done[k]), "hipEventSynchronize");  // batch b-3 done
+    wait_entry(k);  // batch b-3 done
     if (gate_fwd && !block && b >= 2) {
         const int kp = static_cast<int>((b - 2) % kDev);
         if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
@@ -286,6 +314,7 @@ gs_runner::~gs_runner() {
     if (cfg.trainer && gate_fwd) gs::trainer_set_fwd1_hook(cfg.trainer, {});
     for (int d = 0; d < kDev; ++d)
         if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
+    if (done_host) (void)hipHostFree(done_host);
     for (auto& s : streams)
         for (auto& slot : s->slots) {
             if (slot.copied) {
@@ -390,6 +419,16 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     }
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
+    r->use_flag = std::getenv("GS_RUNNER_EVENTS") == nullptr && !cfg->embed_out;
+    if (r->use_flag) {
+        void* hp = nullptr;
+        hip_ok(hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc(done flag)");
+        r->done_host = static_cast<int64_t*>(hp);
+        *r->done_host = -1;
+        void* dp = nullptr;
+        hip_ok(hipHostGetDevicePointer(&dp, hp, 0), "hipHostGetDevicePointer");
+        r->done_dev = static_cast<int64_t*>(dp);
+    }
     {  // layer-1 destinations bound (the last hop's frontier), for the gather slots
         int64_t nn = 0, ne = 0, md = 0;
         GS_REQUIRE(gs_graph_dims(cfg->graph, &nn, &ne, &md) == GS_OK, GS_EINVAL, "gs_graph_dims");
@@ -522,6 +561,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             hip_ok(hipMalloc(&r->ws, r->ws_bytes), "hipMalloc(ws)");
         }
         const int64_t pack_total = slot.used - r->cfg.batch;
+        bool consumed_flag = false;
         int32_t* pk = r->dev[k];
         auto t3 = Clock::now();
         if (r->cfg.embed_out) {  // inference: the forward into this batch's output rows
@@ -550,13 +590,22 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
                 if (rc != GS_OK) fail(rc, gs_last_error());
             }
+            if (r->use_flag) g_done_flag = {r->done_dev, b};
             rc = r->cfg.comm
                      ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
                      : gs_trainer_update_local(r->cfg.trainer, st);
+            consumed_flag = r->use_flag && g_done_flag.ptr == nullptr;
+            g_done_flag = {};
             if (rc != GS_OK) fail(rc, gs_last_error());
         }
-        hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
-        r->dev_busy[k] = true;
+        if (consumed_flag) {
+            r->flag_step[k] = b;  // its SGD signals the entry free
+            r->dev_busy[k] = false;
+        }
+        if (!consumed_flag || step + 1 == n_steps) {
+            hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
+            r->dev_busy[k] = true;
+        }
         for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);
         r->stats.sample_s += slot.sample_s;
         s.copying.push_back(f.slot);
