@@ -402,3 +402,28 @@ def test_runner_distributed_path_single_rank(gs, agg):
     ra.close()
     rb.close()
     comm.close()
+
+
+@pytest.mark.parametrize("every", [1, 3])
+def test_kernel_timer_sites_strided(gs, every):
+    """The bench's kernel-bound timers (gs_trainer_time_kernels_every): with
+    every = e, one launch in e of each armed site is timed (the e-th, 2e-th,
+    ... since arming); durations are positive and the site names the kernel
+    variant it launched."""
+    lib = gs._lib.lib()
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:9]
+    t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), seed=824)
+    runner = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10], depth=2)
+    gs._lib.check(lib.gs_trainer_time_kernels_every(t._h, 0b1111, 9, every))
+    runner.run(9)
+    torch.cuda.synchronize()
+    for site in range(4):
+        out = np.zeros(9, np.float32)
+        got = int(lib.gs_trainer_kernel_times(t._h, site, out.ctypes.data, 9))
+        assert got == 9 // every, (site, got)
+        assert (out[:got] > 0).all()
+        assert lib.gs_trainer_kernel_name(t._h, site).decode().startswith(("void gs::", "gs::"))
+    runner.close()
