@@ -523,8 +523,14 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_sk_kernel(
 // write fp32 partials that sum_slabs_kernel adds in a fixed order.
 constexpr int kDwPitch = 64 + 16;  // rows 16 banks apart: (kq, r) reads of a column hit distinct banks
 constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are staged in LDS)
+#ifndef GS_DW_CHUNK
+#define GS_DW_CHUNK 16
+#endif
+constexpr int kDwCh = GS_DW_CHUNK;  // rows per LDS chunk (one barrier each); 16 or 32
+static_assert(kDwCh == 16 || kDwCh == 32, "dW chunk rows");
+constexpr int kDwRpt = kDwCh / 16;  // rows each thread loads per chunk
 #ifndef GS_DW_AHEAD
-#define GS_DW_AHEAD 4
+#define GS_DW_AHEAD (64 / GS_DW_CHUNK)
 #endif
 constexpr int kDwAhead = GS_DW_AHEAD;  // row chunks whose global loads are in flight ahead of the MFMAs
 
@@ -533,15 +539,15 @@ __device__ __forceinline__ void linear_dw_body(
     int bx, int by, int bz, int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
     const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
     const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
-    __shared__ float sZ[2][16 * kDwPitch];
-    __shared__ float sI[2][16 * kDwPitch];
+    __shared__ float sZ[2][kDwCh * kDwPitch];
+    __shared__ float sI[2][kDwCh * kDwPitch];
     __shared__ int sIdx[HAS_SELF ? kDwMaxSlab : 1];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane & 15, kq = lane >> 4;
     const int k0 = bx * 64, h0 = by * 64;
     const int i_beg = bz * rows_per_split;
     const int i_end = min(n, i_beg + rows_per_split);
-    const int nC = (i_end - i_beg + 15) / 16;
+    const int nC = (i_end - i_beg + kDwCh - 1) / kDwCh;
     const int lr = tid >> 4, lq = (tid & 15) * 4;
     if (HAS_SELF)
         for (int t = tid; t < i_end - i_beg; t += kThreads) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
@@ -549,35 +555,47 @@ __device__ __forceinline__ void linear_dw_body(
 
     // Rows past the slab read a valid row and are zeroed at the LDS store
     // (both operands: 0 · NaN would not vanish).  Chunks past the end re-read
-    // the last one (their data is never stashed).
-    auto load = [&](int c, float4& z, float4& o, float4& x) {
-        const int t = min(16 * min(c, nC - 1) + lr, i_end - i_beg - 1);
-        const int ic = i_beg + t;
-        z = row_quad_raw<ZVEC>(dout + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
-        if (RELU) o = row_quad_raw<ZVEC>(out + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
-        const T* arow = A + static_cast<int64_t>(ic) * lda;
-        const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sIdx[t]) * ldxs : nullptr;
-        x = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
+    // the last one (their data is never stashed).  Thread rows: lr + 16 q.
+    struct Ld {
+        float4 z[kDwRpt], o[kDwRpt], x[kDwRpt];
     };
-    auto stash = [&](int c, float4 z, float4 o, float4 x) {
-        z = mask_quad(z, h0 + lq, H);
-        if (RELU) z = relu_mask(z, o);
-        x = mask_quad(x, k0 + lq, K);
-        if (16 * c + lr >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(&sZ[c & 1][lr * kDwPitch + lq]) = z;
-        *reinterpret_cast<float4*>(&sI[c & 1][lr * kDwPitch + lq]) = x;
+    auto load = [&](int c, Ld& L) {
+#pragma unroll
+        for (int q = 0; q < kDwRpt; ++q) {
+            const int t = min(kDwCh * min(c, nC - 1) + lr + 16 * q, i_end - i_beg - 1);
+            const int ic = i_beg + t;
+            L.z[q] = row_quad_raw<ZVEC>(dout + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
+            if (RELU) L.o[q] = row_quad_raw<ZVEC>(out + static_cast<int64_t>(ic) * ldo, h0 + lq, H);
+            const T* arow = A + static_cast<int64_t>(ic) * lda;
+            const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sIdx[t]) * ldxs : nullptr;
+            L.x[q] = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
+        }
+    };
+    auto stash = [&](int c, const Ld& L) {
+#pragma unroll
+        for (int q = 0; q < kDwRpt; ++q) {
+            float4 z = mask_quad(L.z[q], h0 + lq, H);
+            if (RELU) z = relu_mask(z, L.o[q]);
+            float4 x = mask_quad(L.x[q], k0 + lq, K);
+            const int row = lr + 16 * q;
+            if (kDwCh * c + row >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(&sZ[c & 1][row * kDwPitch + lq]) = z;
+            *reinterpret_cast<float4*>(&sI[c & 1][row * kDwPitch + lq]) = x;
+        }
     };
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // One chunk: its 20 LDS operands are all read before its first MFMA (one
-    // wait instead of one per MFMA pair), then 16 MFMAs on 4 accumulators.
+    // One chunk: its LDS operands are all read before its first MFMA (one
+    // wait instead of one per MFMA pair), then the MFMAs on 4 accumulators,
+    // rows in ascending groups of 4 (the same sequence for any chunk size).
     auto compute = [&](int c) {
         const float* tz = sZ[c & 1];
         const float* ti = sI[c & 1];
-        float a[4], b[4][4];
+        constexpr int NS = kDwCh / 4;
+        float a[NS], b[NS][4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < NS; ++s) {
             const int row = 4 * s + kq;
             a[s] = tz[row * kDwPitch + wave * 16 + r];
 #pragma unroll
@@ -585,7 +603,7 @@ __device__ __forceinline__ void linear_dw_body(
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
     };
@@ -593,22 +611,22 @@ __device__ __forceinline__ void linear_dw_body(
     // sets, loop unrolled by its length); LDS stays double-buffered.  Slot u
     // holds chunk c (stashed one iteration earlier) when chunk c = u (mod
     // kDwAhead) is computed, and is refilled with chunk c + kDwAhead then.
-    float4 zr[kDwAhead], orr[kDwAhead], xr[kDwAhead];
+    Ld ring[kDwAhead];
 #pragma unroll
-    for (int u = 0; u < kDwAhead; ++u) load(u, zr[u], orr[u], xr[u]);
-    stash(0, zr[0], orr[0], xr[0]);
+    for (int u = 0; u < kDwAhead; ++u) load(u, ring[u]);
+    stash(0, ring[0]);
     for (int c0 = 0; c0 < nC; c0 += kDwAhead) {
 #pragma unroll
         for (int u = 0; u < kDwAhead; ++u) {
             const int c = c0 + u;
             if (c >= nC) break;
             __syncthreads();
-            load(c + kDwAhead, zr[u], orr[u], xr[u]);
+            load(c + kDwAhead, ring[u]);
             __builtin_amdgcn_sched_barrier(0);
             compute(c);
             __builtin_amdgcn_sched_barrier(0);
             const int un = (u + 1) % kDwAhead;
-            if (c + 1 < nC) stash(c + 1, zr[un], orr[un], xr[un]);
+            if (c + 1 < nC) stash(c + 1, ring[un]);
         }
     }
     float* slab = dst + static_cast<int64_t>(bz) * split_stride;
