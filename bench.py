@@ -17,6 +17,7 @@ restatement of the reference's algorithm) on a bounded sample of the same
 workload on this host.
 """
 import argparse
+import csv
 import glob
 import json
 import os
@@ -211,6 +212,25 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
         out["calibration"] = cal
         out["reference_estimate"] = round(out["value"] / cal["port_over_reference"], 1)
     return out
+
+
+# rocprofv3 --kernel-trace --stats summaries of the bench command, per config
+# and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
+# the kernel beside the live event-timed one
+ROCPROF_STATS = {("rmat2m", 512): "profiles/r02_kernel_stats_rmat2m_steps300.csv"}
+
+
+def load_rocprof_avg(config_name, batch, kernel):
+    rel = ROCPROF_STATS.get((config_name, int(batch)))
+    if not rel or not os.path.exists(os.path.join(ROOT, rel)):
+        return None
+    key = kernel.split("(")[0].strip()
+    with open(os.path.join(ROOT, rel)) as f:
+        for row in csv.DictReader(f):
+            if row.get("Name", "").split("(")[0].strip() == key:
+                return {"avg_us": round(float(row["AverageNs"]) / 1e3, 2), "min_us": round(float(row["MinNs"]) / 1e3, 2),
+                        "source": rel}
+    return None
 
 
 def load_traffic(config_name, batch, kernel):
@@ -636,6 +656,7 @@ def main():
             rooflines[SITE_NAMES[site]] = dict(
                 bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
                 traffic=(tr["hbm_bytes"] if tr else None), traffic_source=(tr["source"] if tr else None),
+                rocprof=load_rocprof_avg(args.config, cfg["batch"], names[site]),
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
                 timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
