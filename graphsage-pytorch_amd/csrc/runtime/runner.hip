@@ -61,9 +61,19 @@ static unsigned sync_event_flags() {
 __global__ __launch_bounds__(256) void pull_pack_kernel(const int4* __restrict__ src, int4* __restrict__ dst,
                                                         int64_t n16, const int32_t* __restrict__ src_tail,
                                                         int32_t* __restrict__ dst_tail, int n_tail) {
-    const int64_t i = blockIdx.x * int64_t(256) + threadIdx.x;
-    if (i < n16) dst[i] = src[i];
-    if (i < n_tail) dst_tail[i] = src_tail[i];
+    // grid-stride, four 16-B loads in flight per lane before their stores
+    const int64_t stride = gridDim.x * int64_t(256);
+    for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n16; i += 4 * stride) {
+        int4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * stride < n16) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * stride < n16) dst[i + u * stride] = v[u];
+    }
+    const int64_t t = blockIdx.x * int64_t(256) + threadIdx.x;
+    if (t < n_tail) dst_tail[t] = src_tail[t];
 }
 
 struct PackSlot {
@@ -156,6 +166,8 @@ struct gs_runner {
     // so the side stream's work lands under that step's latency-bound launches
     // rather than under its forward (A/B switch)
     bool gate_fwd = false;
+    int64_t pull_blocks = 1 << 30;  // GS_PULL_BLOCKS: cap on the pull kernel's grid (grid-stride)
+    bool pull_copy = false;  // GS_PULL_COPY=1: the pack pull as a runtime copy (copy engine) instead of a kernel
     hipEvent_t fwd_done[kDev] = {};
     bool fwd_busy[kDev] = {};
     int cur_k = -1;                        // ring entry of the step being issued (fwd1 hook)
@@ -281,12 +293,17 @@ bool gs_runner::issue(int64_t b, bool block) {
         if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
     }
     stats.wait_ring_s += secs(tr, Clock::now());
-    const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
-    const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
-    pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
-        reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(dev[k]), n16, slot.host + 4 * n16,
-        dev[k] + 4 * n16, static_cast<int>(tail));
-    hip_ok(hipGetLastError(), "pull_pack_kernel");
+    if (pull_copy) {
+        hip_ok(hipMemcpyAsync(dev[k], slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, side),
+               "hipMemcpyAsync");
+    } else {
+        const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, pull_blocks));
+        pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
+            reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(dev[k]), n16, slot.host + 4 * n16,
+            dev[k] + 4 * n16, static_cast<int>(tail));
+        hip_ok(hipGetLastError(), "pull_pack_kernel");
+    }
     hip_ok(hipEventRecord(slot.copied, side), "hipEventRecord");
     const int rc = gs_trainer_gather(cfg.trainer, dev[k], slot.hop_sizes, slot.offsets, k, side);
     if (rc != GS_OK) fail(rc, gs_last_error());
@@ -498,6 +515,8 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         });
     }
     r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
+    r->pull_copy = std::getenv("GS_PULL_COPY") != nullptr;
+    if (const char* e = std::getenv("GS_PULL_BLOCKS")) r->pull_blocks = std::max(1, std::atoi(e));
     if (r->gate_fwd) {
         for (int d = 0; d < gs_runner::kDev; ++d)
             hip_ok(hipEventCreateWithFlags(&r->fwd_done[d], sync_event_flags()), "hipEventCreate");
