@@ -474,8 +474,8 @@ def main():
                     help="N > 1: gradient all-reduce buckets (2 = upper layers + classifier under the layer-1 dW GEMM)")
     ap.add_argument("--sampler-streams", type=int, default=None,
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
-                         "default: min(12, host cores per GPU - 3): headroom for slower hosts, and one core "
-                         "each for the issuing thread, the HIP runtime and RCCL's proxy)")
+                         "default with helpers: min(8, (host cores per GPU - 2) / 2), two cores left for the "
+                         "issuing thread and the HIP runtime / RCCL's proxy; without: min(12, cores per GPU - 3))")
     ap.add_argument("--no-warm", action="store_true",
                     help="skip the sampler threads' throwaway warm-up batch (A/B of the cold first batches)")
     ap.add_argument("--sampler-helpers", type=int, default=None,
