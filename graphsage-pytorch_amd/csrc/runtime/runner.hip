@@ -102,6 +102,12 @@ struct SamplerStream {
 
 }  // namespace gs
 
+namespace gs {
+struct Inflight {
+    int stream = -1, slot = -1;
+};
+}  // namespace gs
+
 struct gs_runner {
     gs_runner_config cfg{};
     std::vector<int32_t> fanouts;
@@ -129,7 +135,15 @@ struct gs_runner {
     // three batches back released the ring entry, and that the gather of the
     // batch it is about to issue has completed.
     static constexpr int kDev = 3;
-    int32_t* dev[kDev] = {};
+    // Device pack buffers: a ring of 4 (b % kPack), one more than the gather
+    // ring, so batch b+1's pack can be pulled while batch b is gathered: the
+    // entry's previous user, step b-3, is the one wait_entry(b % kDev) has just
+    // waited for (GS_PULL_AHEAD).
+    static constexpr int kPack = 4;
+    int32_t* dev[kPack] = {};
+    gs::Inflight pulled_slot[kPack];       // sampler stream + slot of the pack in entry p
+    int64_t pulled = 0;                    // batches whose pack pull is issued
+    bool pull_ahead = false;
     hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
     // Step completion without an event between steps: the step's SGD launch
@@ -172,9 +186,7 @@ struct gs_runner {
     bool fwd_busy[kDev] = {};
     int cur_k = -1;                        // ring entry of the step being issued (fwd1 hook)
     hipStream_t side = nullptr;
-    struct Inflight {
-        int stream = -1, slot = -1;
-    } inflight[kDev];
+    gs::Inflight inflight[kDev];
     int64_t issued = 0;                    // batches whose pull + gather are issued
     void* ws = nullptr;
     int64_t ws_bytes = 0;
@@ -186,6 +198,8 @@ struct gs_runner {
     void sampler_loop(gs::SamplerStream& s);
     void recycle(gs::SamplerStream& s, bool block);
     bool issue(int64_t b, bool block);
+    int take_slot(int64_t b, bool block);
+    void pull(int64_t b, int slot_id);
 };
 
 // Hand the slots whose copy has completed back to their sampler; with
@@ -260,9 +274,9 @@ void gs_runner::sampler_loop(gs::SamplerStream& s) {
     }
 }
 
-// Pull batch b's pack to the device and gather its layer 1, both on the side
-// stream.  block == false: return false if b is not sampled yet.
-bool gs_runner::issue(int64_t b, bool block) {
+// Take batch b's sampled slot off its stream's ready queue (-1: not sampled
+// yet and !block).
+int gs_runner::take_slot(int64_t b, bool block) {
     using namespace gs;
     SamplerStream& s = *streams[b % cfg.n_streams];
     int slot_id;
@@ -274,18 +288,54 @@ bool gs_runner::issue(int64_t b, bool block) {
             s.ready.pop_front();
             break;
         }
-        if (!block) return false;
+        if (!block) return -1;
         // wait for a sampled batch, or free a slot for a starved sampler
         s.cv.wait(lk, [&] { return !s.ready.empty() || (s.free.empty() && !s.copying.empty()); });
         if (!s.ready.empty()) continue;
         lk.unlock();
         recycle(s, true);
     }
-    const auto tr = Clock::now();
-    stats.wait_sample_s += secs(tw, tr);
+    stats.wait_sample_s += secs(tw, Clock::now());
     PackSlot& slot = s.slots[slot_id];
     GS_REQUIRE(slot.batch == b, GS_EINVAL, "sampler ring out of order");
     if (slot.status != GS_OK) fail(slot.status, slot.error);
+    return slot_id;
+}
+
+// Batch b's pack: pinned slot -> device pack entry b % kPack on the side
+// stream (a kernel reading the mapped slot, or the copy engine).  The entry's
+// previous user, step b - kPack, must have completed.
+void gs_runner::pull(int64_t b, int slot_id) {
+    using namespace gs;
+    PackSlot& slot = streams[b % cfg.n_streams]->slots[slot_id];
+    int32_t* d = dev[b % kPack];
+    if (pull_copy) {
+        hip_ok(hipMemcpyAsync(d, slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, side),
+               "hipMemcpyAsync");
+    } else {
+        const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, pull_blocks));
+        pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
+            reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(d), n16, slot.host + 4 * n16,
+            d + 4 * n16, static_cast<int>(tail));
+        hip_ok(hipGetLastError(), "pull_pack_kernel");
+    }
+    hip_ok(hipEventRecord(slot.copied, side), "hipEventRecord");
+    pulled_slot[b % kPack] = {static_cast<int>(b % cfg.n_streams), slot_id};
+    pulled = b + 1;
+}
+
+// Pull batch b's pack to the device (unless pulled ahead) and gather its
+// layer 1, both on the side stream; with pull_ahead, then pull batch b+1's
+// pack if it is sampled.  block == false: return false if b is not sampled yet.
+bool gs_runner::issue(int64_t b, bool block) {
+    using namespace gs;
+    int slot_id = -1;
+    if (pulled <= b) {
+        slot_id = take_slot(b, block);
+        if (slot_id < 0) return false;
+    }
+    const auto tr = Clock::now();
     const int k = static_cast<int>(b % kDev);
     wait_entry(k);  // batch b-3 done
     if (gate_fwd && !block && b >= 2) {
@@ -293,23 +343,19 @@ bool gs_runner::issue(int64_t b, bool block) {
         if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
     }
     stats.wait_ring_s += secs(tr, Clock::now());
-    if (pull_copy) {
-        hip_ok(hipMemcpyAsync(dev[k], slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, side),
-               "hipMemcpyAsync");
-    } else {
-        const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, pull_blocks));
-        pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
-            reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(dev[k]), n16, slot.host + 4 * n16,
-            dev[k] + 4 * n16, static_cast<int>(tail));
-        hip_ok(hipGetLastError(), "pull_pack_kernel");
-    }
-    hip_ok(hipEventRecord(slot.copied, side), "hipEventRecord");
-    const int rc = gs_trainer_gather(cfg.trainer, dev[k], slot.hop_sizes, slot.offsets, k, side);
+    if (pulled <= b) pull(b, slot_id);
+    const Inflight f = pulled_slot[b % kPack];
+    PackSlot& slot = streams[f.stream]->slots[f.slot];
+    const int rc = gs_trainer_gather(cfg.trainer, dev[b % kPack], slot.hop_sizes, slot.offsets, k, side);
     if (rc != GS_OK) fail(rc, gs_last_error());
     hip_ok(hipEventRecord(gathered[k], side), "hipEventRecord");
-    inflight[k] = {static_cast<int>(b % cfg.n_streams), slot_id};
+    inflight[k] = f;
     issued = b + 1;
+    // entry (b+1) % kPack last held batch b-3, whose step wait_entry(k) saw complete
+    if (pull_ahead && b + 1 < n_units && pulled == b + 1) {
+        const int s1 = take_slot(b + 1, false);
+        if (s1 >= 0) pull(b + 1, s1);
+    }
     return true;
 }
 
@@ -340,6 +386,8 @@ gs_runner::~gs_runner() {
             }
             if (slot.host) (void)hipHostFree(slot.host);
         }
+    for (int d = 0; d < kPack; ++d)
+        if (dev[d]) (void)hipFree(dev[d]);
     for (int d = 0; d < kDev; ++d) {
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
         if (fwd_done[d]) {
@@ -347,7 +395,6 @@ gs_runner::~gs_runner() {
             (void)hipEventDestroy(fwd_done[d]);
         }
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
-        if (dev[d]) (void)hipFree(dev[d]);
     }
     if (cfg.trainer && comm_stream) gs::trainer_set_upper_hook(cfg.trainer, {});
     if (upper_ready) (void)hipEventDestroy(upper_ready);
@@ -433,8 +480,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     for (int d = 0; d < gs_runner::kDev; ++d) {
         hip_ok(hipEventCreateWithFlags(&r->dev_done[d], sync_event_flags()), "hipEventCreate");
         hip_ok(hipEventCreateWithFlags(&r->gathered[d], sync_event_flags()), "hipEventCreate");
-        hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     }
+    for (int d = 0; d < gs_runner::kPack; ++d)
+        hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
     r->use_flag = std::getenv("GS_RUNNER_EVENTS") == nullptr && !cfg->embed_out;
     if (r->use_flag) {
@@ -516,6 +564,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     }
     r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
     r->pull_copy = std::getenv("GS_PULL_COPY") != nullptr;
+    r->pull_ahead = std::getenv("GS_PULL_AHEAD") != nullptr;
     if (const char* e = std::getenv("GS_PULL_BLOCKS")) r->pull_blocks = std::max(1, std::atoi(e));
     if (r->gate_fwd) {
         for (int d = 0; d < gs_runner::kDev; ++d)
@@ -566,7 +615,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         hip_ok(hipEventSynchronize(r->gathered[k]), "hipEventSynchronize");  // normally long done
         const auto t1 = Clock::now();
         r->stats.wait_gather_s += secs(tg, t1);
-        const gs_runner::Inflight f = r->inflight[k];
+        const gs::Inflight f = r->inflight[k];
         SamplerStream& s = *r->streams[f.stream];
         PackSlot& slot = s.slots[f.slot];
         const auto t2 = t1;
@@ -581,7 +630,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         const int64_t pack_total = slot.used - r->cfg.batch;
         bool consumed_flag = false;
-        int32_t* pk = r->dev[k];
+        int32_t* pk = r->dev[b % gs_runner::kPack];
         auto t3 = Clock::now();
         if (r->cfg.embed_out) {  // inference: the forward into this batch's output rows
             const int rc = gs_trainer_forward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets, k, r->ws,
