@@ -137,7 +137,7 @@ class CSRGraph:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_graph_destroy(h)
             self._h = None
 

@@ -92,7 +92,7 @@ class RNG:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_rng_destroy(h)
             self._h = None
 
@@ -191,7 +191,7 @@ class Sample:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_sample_destroy(h)
             self._h = None
 
@@ -264,6 +264,6 @@ class DeviceSampler:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_dsampler_destroy(h)
             self._h = None

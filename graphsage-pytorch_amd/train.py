@@ -145,7 +145,7 @@ class NativeTrainer:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_trainer_destroy(h)
             self._h = None
 
@@ -406,7 +406,7 @@ class Runner:
 
     def close(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
             _lib._lib.gs_runner_destroy(h)
         self._h = None
 
