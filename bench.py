@@ -310,8 +310,11 @@ def run_apply_model_loop(args, cfg):
     torch.cuda.set_device(device)
     wl = pubmed_workload(cfg, device, args.seed)
     torch.manual_seed(args.seed)
+    # the forward's sampling with helper threads (same draws, same pack; the
+    # host is otherwise idle while the step's single stream samples)
+    helpers = args.helpers_cli if args.helpers_cli is not None else min(7, host_threads() - 1)
     gsage = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], device, agg_func=cfg["agg"],
-                             fanouts=list(cfg["fanouts"])).to(device)
+                             fanouts=list(cfg["fanouts"]), sampler_helpers=helpers).to(device)
     cls = models.Classification(128, cfg["classes"]).to(device)
     ul = unsup.UnsupervisedLoss(wl["graph"], wl["train"], device, n_threads=host_threads())
     params = [p for m in (gsage, cls) for p in m.parameters()]
@@ -343,7 +346,8 @@ def run_apply_model_loop(args, cfg):
         "config": {"workload": "pubmed: apply_model step (extend_nodes num_neg 100 + GraphSage fanouts (10, 10) "
                                "MEAN over the extended batch + sup NLL + backward + clip + SGD), B=512 roots",
                    "global_batch": cfg["batch"], "parallelism": "dp1",
-                   "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5)},
+                   "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5),
+                   "forward_sampler_helpers": helpers},
         "roofline": None,
         "cpu_baseline": cpu,
     }
@@ -483,6 +487,7 @@ def main():
                          "default 1 with >= 8 host cores per GPU")
     args = ap.parse_args()
     per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    args.helpers_cli = args.sampler_helpers  # before the runner default below (the pubmed loop has its own)
     if args.sampler_helpers is None:
         # one helper per stream where the cores allow: a batch then samples in
         # ~0.35-0.42 ms instead of ~0.5-0.57 (profiles/r02_ab_sampler_layouts.txt),

@@ -14,6 +14,7 @@ and the gfx950 kernels:
 
 There is no CPU execution path: raw_features must live on a HIP device.
 """
+import ctypes
 import random as _pyrandom
 
 import numpy as np
@@ -62,6 +63,18 @@ class DeviceSample:
         if off < 0:
             raise KeyError(f"hop {hop} has no '{name}' on the device")
         return self.buf[off:off + n]
+
+
+class _PackInfo:
+    """Hop sizes / pack offsets of a pack written by gs_sample_pack_run*."""
+
+    def __init__(self, n_hops, sizes, offsets):
+        self.n_hops = n_hops
+        self._sizes = [tuple(int(x) for x in sizes[4 * j:4 * j + 4]) for j in range(n_hops)]
+        self.offsets = offsets.reshape(_lib.GS_MAX_HOPS, _lib.GS_PK_NFIELDS)[:n_hops].tolist()
+
+    def sizes(self, j):
+        return self._sizes[j - 1]
 
 
 # ------------------------------------------------------------ shared compute
@@ -243,10 +256,15 @@ class GraphSage(nn.Module):
                 models.py:277); None entries mean "all neighbours".
       rng     : a sampler.RNG to draw from instead of the module-global
                 `random` (the reference always uses the global stream).
+      sampler_helpers : helper threads for the forward's sampling (gs_team:
+                the same draws from the same stream, bit-identical pack; the
+                per-node sets and neighbour lists are built beside the draws).
+                0 = none.  MAX keeps the team-less path, whose sample is
+                complete before the empty-neighbourhood IndexError.
     """
 
     def __init__(self, num_layers, input_size, out_size, raw_features, adj_lists, device, gcn=False,
-                 agg_func='MEAN', *, fanouts=None, rng=None):
+                 agg_func='MEAN', *, fanouts=None, rng=None, sampler_helpers=0):
         super().__init__()
         self.input_size = input_size
         self.out_size = out_size
@@ -260,6 +278,10 @@ class GraphSage(nn.Module):
         if len(self.fanouts) != num_layers:
             raise ValueError("need one fanout per layer")
         self.rng = rng
+        self.sampler_helpers = int(sampler_helpers)
+        self._team = None       # gs_team handle (lazy)
+        self._pin = None        # pinned pack buffer of the team path
+        self._pin_ev = None     # its last H2D copy
         self._graph = adj_lists if isinstance(adj_lists, CSRGraph) else None
         for index in range(1, num_layers + 1):
             layer_size = out_size if index != 1 else input_size
@@ -273,7 +295,14 @@ class GraphSage(nn.Module):
                             "save its state_dict() instead")
         state = self.__dict__.copy()
         state["_graph"] = None
+        state["_team"] = state["_pin"] = state["_pin_ev"] = None
         return state
+
+    def __del__(self):
+        t = getattr(self, "_team", None)
+        if t is not None and t.value and getattr(_lib, "_lib", None) is not None:  # _lib is None at interpreter exit
+            _lib._lib.gs_team_destroy(t)
+            self._team = None
 
     # -------------------------------------------------------------- helpers
     @property
@@ -288,6 +317,41 @@ class GraphSage(nn.Module):
         if self.rng is None:
             rng.to_python(_pyrandom)
         return s
+
+    def _draw_pack(self, roots, device):
+        """The forward's sample as a device pack, drawn with the helper team
+        (gs_sample_pack_run_multi_team) into a pinned buffer and copied
+        up; the same draws and the same pack as DeviceSample(self._draw(...))."""
+        lib = _lib.lib()
+        if self._team is None:
+            t = ctypes.c_void_p()
+            _lib.check(lib.gs_team_create(self.sampler_helpers, ctypes.byref(t)))
+            self._team = t
+        fan = np.array([(-1 if k is None else int(k)) for k in self.fanouts], np.int32)
+        roots = np.ascontiguousarray(roots, np.int64)
+        L, n = len(fan), len(roots)
+        bound = int(lib.gs_sample_pack_bound(self.graph.handle, n, fan.ctypes.data, L))
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()  # the previous copy out of the pinned buffer is done
+        if self._pin is None or self._pin.numel() < bound:
+            self._pin = torch.empty(bound, dtype=torch.int32, pin_memory=True)
+        sizes = np.empty(4 * L, np.int64)
+        offs = np.empty(_lib.GS_MAX_HOPS * _lib.GS_PK_NFIELDS, np.int64)
+        used = ctypes.c_int64()
+        rng = self.rng if self.rng is not None else RNG.from_python(_pyrandom)
+        flags = _lib.GS_SAMPLE_GCN if self.gcn else 0
+        _lib.check(lib.gs_sample_pack_run_multi_team(self.graph.handle, rng._h, roots.ctypes.data, n, n,
+                                                     fan.ctypes.data, L, flags, self._pin.data_ptr(),
+                                                     self._pin.numel(), sizes.ctypes.data, offs.ctypes.data,
+                                                     ctypes.byref(used), self._team))
+        if self.rng is None:
+            rng.to_python(_pyrandom)
+        dev = self._pin[:used.value].to(device, non_blocking=True)
+        self._pin_ev = torch.cuda.Event()
+        self._pin_ev.record()
+        ds = DeviceSample(_PackInfo(L, sizes, offs), device, buf=dev)
+        ds._native = (sizes, offs)
+        return ds
 
     @staticmethod
     def _roots(nodes_batch):
@@ -305,13 +369,16 @@ class GraphSage(nn.Module):
                                "cuda tensor (the reference's --cuda path, main.py:52)")
         if self.agg_func not in ("MEAN", "MAX"):
             raise ValueError(f"agg_func must be 'MEAN' or 'MAX', got {self.agg_func!r}")
-        s = self._draw(roots, self.fanouts)
-        if self.agg_func == "MAX":
-            for j in range(1, s.n_hops + 1):
-                if s.n_empty(j):
-                    raise IndexError("MAX aggregation over an empty neighbourhood "
-                                     "(reference: models.py:321-325)")
-        ds = DeviceSample(s, X.device)
+        if self.sampler_helpers > 0 and self.agg_func == "MEAN":
+            ds = self._draw_pack(roots, X.device)
+        else:
+            s = self._draw(roots, self.fanouts)
+            if self.agg_func == "MAX":
+                for j in range(1, s.n_hops + 1):
+                    if s.n_empty(j):
+                        raise IndexError("MAX aggregation over an empty neighbourhood "
+                                         "(reference: models.py:321-325)")
+            ds = DeviceSample(s, X.device)
         row_ptr, col = self.graph.device_csr(X.device)
         weights = [getattr(self, 'sage_layer' + str(i)).weight for i in range(1, self.num_layers + 1)]
         Xc = X if X.is_contiguous() else X.contiguous()

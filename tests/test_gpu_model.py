@@ -92,6 +92,34 @@ def test_graphsage_vs_oracle_bench_fanouts(gs, agg, fanouts):
                                    atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("name,gcn,fanouts", [("pubmed", False, [10, 10]), ("cora", True, [10, 10]),
+                                               ("rmat", False, [25, 10]), ("rmat", False, [5, 3, 2])])
+def test_graphsage_sampler_helpers_bitwise(gs, name, gcn, fanouts):
+    """sampler_helpers > 0 (the forward's sampling on a gs_team into a pinned
+    pack): embeddings, weight gradients and the global `random` state after
+    the forward are bitwise those of the team-less path, over two batches."""
+    graph, g, n = _graph(gs, name)
+    X = torch.from_numpy(_features(name, n)).to(DEV)
+    out = []
+    for helpers in (0, 3):
+        torch.manual_seed(5)
+        model = models.GraphSage(len(fanouts), X.shape[1], 128, X, graph, DEV, gcn=gcn, fanouts=fanouts,
+                                 sampler_helpers=helpers).to(DEV)
+        random.seed(21)
+        embs, grads = [], []
+        for b in range(2):
+            roots = np.nonzero(graph.degrees())[0][b::5][:300].tolist()
+            emb = model(roots)
+            (emb * torch.from_numpy(uniform_features(8 + b, len(roots), 128)).to(DEV)).sum().backward()
+            embs.append(emb.detach().cpu())
+        grads = [getattr(model, f"sage_layer{i}").weight.grad.cpu() for i in range(1, len(fanouts) + 1)]
+        out.append((embs, grads, random.getstate()))
+    (e0, g0, s0), (e1, g1, s1) = out
+    assert s0 == s1
+    for a, b in zip(e0 + g0, e1 + g1):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("agg", ["MEAN", "MAX"])
 def test_graphsage_duplicate_roots_vs_oracle(gs, agg):
     """Repeated ids in nodes_batch: every occurrence is sampled on its own
