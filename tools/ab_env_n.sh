@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for i in $(seq 1 ${ROUNDS:-6}); do
   for e in "$@"; do
     timeout -k 10 200 env $e python bench.py --steps 300 --warmup 10 --sustain 300 --no-cpu-baseline > gpurun_out/ab.log 2>&1 || exit 1
-    python -c "import json;d=json.loads(open('gpurun_out/ab.log').read().splitlines()[-1]);print('$e', d['ms_per_step'], d['sustained']['ms_per_step'], d['roofline_kernels']['gather']['avg_launch_us'])" | tee -a gpurun_out/ab_n.txt
+    python -c "import json;d=json.loads(open('gpurun_out/ab.log').read().splitlines()[-1]);print('$e'.replace(' ', '+'), d['ms_per_step'], d['sustained']['ms_per_step'], d['roofline_kernels']['gather']['avg_launch_us'])" | tee -a gpurun_out/ab_n.txt
   done
 done
 python - <<'PY'
