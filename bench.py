@@ -394,7 +394,16 @@ def run_embed(args, cfg):
     n, B = wl["n"], cfg["batch"]
     n_used = n if args.full_graph else min(n, args.steps * world * B)
     weights = [w.to(device) for w in train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, args.seed)[0]]
-    emb = train.Embedder(wl["graph"], wl["X"], weights, cfg["fanouts"], cfg["agg"], merge=args.embed_merge)
+    # inference is sampler-throughput bound: by default more streams without
+    # helpers (≈ 30 % more batches per second than streams + helpers,
+    # profiles/r02_ab_sampler_layouts.txt; the latency a helper saves buys nothing here)
+    helpers = args.helpers_cli if args.helpers_cli is not None else 0
+    if args.streams_cli is None:
+        args.sampler_streams = (max(1, min(12, args.per_gpu - 3)) if not helpers
+                                else max(1, min(8, (args.per_gpu - 2) // (1 + helpers))))
+    args.sampler_helpers = helpers
+    emb = train.Embedder(wl["graph"], wl["X"], weights, cfg["fanouts"], cfg["agg"], merge=args.embed_merge,
+                         helpers=helpers)
     mine = utils.shard_ids(n_used, B, rank, world)
     warm = utils.shard_ids(min(n, args.warmup * world * B), B, rank, world)
     if len(warm):
@@ -442,7 +451,8 @@ def run_embed(args, cfg):
             "config": {"workload": f"rmat2m-embed: {n_used} of {n} node ids in batches of {B} (id order), "
                                    f"fanout {tuple(cfg['fanouts'])}, MEAN, forward only + all-gather",
                        "global_batch": B * world, "parallelism": f"dp{world}",
-                       "sampler_streams_per_gpu": args.sampler_streams, "batches_per_launch": emb.merge,
+                       "sampler_streams_per_gpu": args.sampler_streams,
+                       "sampler_helpers_per_stream": args.sampler_helpers, "batches_per_launch": emb.merge,
                        "host_sampler_ms_per_batch": round(1e3 * st["sample_s"] / max(1, n_b), 3),
                        "host_ms_per_batch": {k: round(1e3 * st[k + "_s"] / max(1, n_b), 4)
                                              for k in ("wait", "wait_sample", "wait_ring", "wait_gather", "issue")},
@@ -487,7 +497,9 @@ def main():
                          "default 1 with >= 8 host cores per GPU")
     args = ap.parse_args()
     per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
-    args.helpers_cli = args.sampler_helpers  # before the runner default below (the pubmed loop has its own)
+    # as given on the command line, before the training runner's defaults below
+    # (the pubmed loop and the inference runner pick their own)
+    args.helpers_cli, args.streams_cli, args.per_gpu = args.sampler_helpers, args.sampler_streams, per_gpu
     if args.sampler_helpers is None:
         # one helper per stream where the cores allow: a batch then samples in
         # ~0.35-0.42 ms instead of ~0.5-0.57 (profiles/r02_ab_sampler_layouts.txt),

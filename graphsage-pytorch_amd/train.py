@@ -430,7 +430,7 @@ class Embedder:
     one stream that is exactly the reference's sequence of GraphSage calls on
     one `random` stream, for any m."""
 
-    def __init__(self, graph, features, weights, fanouts, agg_func="MEAN", gcn=False, depth=4, merge=2):
+    def __init__(self, graph, features, weights, fanouts, agg_func="MEAN", gcn=False, depth=4, merge=2, helpers=0):
         weights = [w.detach() for w in weights]
         H = weights[0].shape[0]
         dev = features.device
@@ -441,6 +441,7 @@ class Embedder:
         self.graph, self.fanouts, self.gcn, self.agg = graph, list(fanouts), gcn, agg_func
         self.depth = depth
         self.merge = max(1, int(merge))
+        self.helpers = int(helpers)  # gs_team helper threads per sampler stream (same draws)
         self.last_stats = None
 
     def embed(self, nodes, batch, rngs):
@@ -452,7 +453,7 @@ class Embedder:
         if n_full:
             r = Runner(self.trainer, self.graph, nodes[:n_full * batch].reshape(n_full, batch), rngs, self.fanouts,
                        gcn=self.gcn, fail_empty=self.agg == "MAX", depth=self.depth, embed_out=out,
-                       merge=self.merge)
+                       merge=self.merge, helpers=self.helpers)
             try:
                 r.run(-(-n_full // self.merge))
                 self.last_stats = r.stats()

@@ -24,6 +24,7 @@ run steps300 --gpus 1 --steps 300 --warmup 5 --no-cpu-baseline || exit $?
 run pubmed --config pubmed --steps 20 --warmup 3 || exit $?
 run max_bf16 --config rmat2m-max-bf16 --steps 300 --warmup 5 --no-cpu-baseline || exit $?
 run rmat16m --config rmat16m --steps 300 --warmup 5 --no-cpu-baseline || exit $?
+run embed --config rmat2m-embed --full-graph --no-cpu-baseline || exit $?
 mkdir -p "$OUT/prof"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --steps 300 --warmup 5 --no-cpu-baseline > "$OUT/prof/bench.json" 2> "$OUT/prof/bench.err"
