@@ -9,6 +9,7 @@ smallest top-2 logit margin on the val set is 9e-4, far above fp32 drift);
 embeddings 1e-5; classifier weights after 2 epochs x 28 SGD steps 1e-4.
 """
 import importlib
+import inspect
 import os
 import random
 import types
@@ -134,7 +135,7 @@ def test_embedder_streams_match_module_forward(b_sz):
     E = utils.get_gnn_embeddings(gsage, dc, "g", b_sz=b_sz, sampler_streams=S, seed=11)
     n = len(dc.g_labels)
     rngs = [sampler.RNG(train.rank_seed(11, 0, w)) for w in range(S)]
-    m = train.Embedder.__init__.__defaults__[-1]  # the merge get_gnn_embeddings runs with
+    m = inspect.signature(train.Embedder.__init__).parameters["merge"].default  # get_gnn_embeddings' merge
     assert m > 1
     with torch.no_grad():
         for i, lo in enumerate(range(0, n, b_sz)):
