@@ -594,10 +594,14 @@ def main():
         if wait_sampled:
             want = min(s0 + args.steps, total_steps)
             deadline = time.perf_counter() + 60.0
+            # spin (no sleep: a 50 us sleep overshot the condition by up to ~0.1 ms of a
+            # ~1.3 ms window); the sampler threads are native and need no GIL
+            nap = float(os.environ.get("GS_BENCH_POLL_SLEEP", "0"))  # A/B of the poll
             while runner.progress()[0] < want:
                 if time.perf_counter() > deadline:
                     raise SystemExit("bench: sampler threads stalled inside the timed window")
-                time.sleep(50e-6)
+                if nap:
+                    time.sleep(nap)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
