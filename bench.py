@@ -574,8 +574,10 @@ def main():
     no_timer = bool(os.environ.get("GS_BENCH_NO_TIMER"))  # A/B of the in-window timer's cost
     # an event-bound launch idles the queue a few us on either side of it
     # (rocprofv3 trace: 4.4 us each side): time one launch in `every` of the
-    # measured steps, spread over both windows, not all of them
-    every = max(4, args.steps // 16)
+    # measured steps, spread over both windows, not all of them (one in 4 cost
+    # the 20-step line 2.4 % against no timer: 7.74 against 7.93 M, medians of
+    # six rounds; one in 8 leaves 6 timed launches over the two 20-step windows)
+    every = max(8, args.steps // 16)
     gs._lib.check(lib.gs_trainer_time_kernels_every(trainer._h, 0 if no_timer else 1 << dominant, 2 * args.steps,
                                                     every))
 
