@@ -52,6 +52,10 @@ CONFIGS = {
     # (fanouts 10,10) -> supervised NLL -> backward -> clip -> SGD, through the drop-in modules
     "pubmed": dict(graph="pubmed", feat=500, fanouts=(10, 10), agg="MEAN", dtype="fp32", batch=512, classes=3,
                    loop="apply_model"),
+    # configs[0]: the reference's CPU-runnable case (Cora, b_sz 20, supervised) through the same
+    # apply_model loop as pubmed (cites-file graph from tests/golden/graphs.npz)
+    "cora": dict(graph="cora", feat=1433, fanouts=(10, 10), agg="MEAN", dtype="fp32", batch=20, classes=7,
+                 loop="apply_model"),
     # configs[4] (per-GPU share of the 8-GPU job)
     "rmat16m": dict(scale=24, pairs=160_000_000, feat=128, fanouts=(25, 10), agg="MEAN", dtype="fp32",
                     batch=512, classes=16),
@@ -255,8 +259,10 @@ def load_traffic(config_name, batch, kernel):
 
 
 def pubmed_workload(cfg, device, seed=824):
+    """A citation graph from the reference's cites file (cfg["graph"]: pubmed or cora)."""
     g = np.load(os.path.join(ROOT, "tests", "golden", "graphs.npz"))
-    src, dst, n = g["pubmed_src"].astype(np.int64), g["pubmed_dst"].astype(np.int64), int(g["pubmed_n"][0])
+    name = cfg.get("graph", "pubmed")
+    src, dst, n = g[f"{name}_src"].astype(np.int64), g[f"{name}_dst"].astype(np.int64), int(g[f"{name}_n"][0])
     graph = gs.CSRGraph.from_pairs(src, dst, n)
     X = torch.empty(n, cfg["feat"], dtype=torch.float32, device=device)
     ops.fill_uniform(X, seed)
@@ -301,8 +307,9 @@ def cpu_baseline_loop(wl, cfg, batches, seconds_budget=25.0, seed=824):
 
 
 def run_apply_model_loop(args, cfg):
-    """configs[1]: timed steps of the reference's training loop body through the
-    drop-in modules (UnsupervisedLoss / GraphSage / fused head, utils.train_step)."""
+    """configs[1] (pubmed) and configs[0] (cora): timed steps of the reference's
+    training loop body through the drop-in modules (UnsupervisedLoss /
+    GraphSage / fused head, utils.train_step)."""
     import random as pyrandom
     unsup = import_module("graphsage-pytorch_amd.unsup")
     utils = import_module("graphsage-pytorch_amd.utils")
@@ -342,10 +349,13 @@ def run_apply_model_loop(args, cfg):
         "value": round(cfg["batch"] * args.steps / elapsed, 1), "unit": "root nodes/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
-        "data": "Pubmed citation graph (reference cites file), synthetic U(-1,1) 500-d features, labels id%3",
-        "config": {"workload": "pubmed: apply_model step (extend_nodes num_neg 100 + GraphSage fanouts (10, 10) "
-                               "MEAN over the extended batch + sup NLL + backward + clip + SGD), B=512 roots",
+        "data": f"{cfg['graph'].capitalize()} citation graph (reference cites file), synthetic U(-1,1) "
+                f"{cfg['feat']}-d features, labels id%{cfg['classes']}",
+        "config": {"workload": f"{args.config}: apply_model step (extend_nodes num_neg 100 + GraphSage fanouts "
+                               f"{tuple(cfg['fanouts'])} {cfg['agg']} over the extended batch + sup NLL + backward + "
+                               f"clip + SGD), B={cfg['batch']} roots",
                    "global_batch": cfg["batch"], "parallelism": "dp1",
+                   "epoch_s": round(len(wl["train"]) // cfg["batch"] * elapsed / args.steps, 4),
                    "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5),
                    "forward_sampler_helpers": helpers},
         "roofline": None,
@@ -516,7 +526,7 @@ def main():
         cfg["batch"] = args.batch
     if cfg.get("loop") == "apply_model":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            raise SystemExit("the pubmed (apply_model) config runs on one GPU")
+            raise SystemExit("the apply_model configs (pubmed, cora) run on one GPU")
         return run_apply_model_loop(args, cfg)
     if cfg.get("loop") == "embed":
         return run_embed(args, cfg)
