@@ -1,4 +1,5 @@
-"""Phase times of the pubmed apply_model step (bench.py --config pubmed):
+"""Phase times of the apply_model step (bench.py --config pubmed, or the
+config named by argv[1], e.g. cora):
 extend_nodes (device balls) / GraphSage forward (host sampler + kernels) /
 head + backward + clip + SGD."""
 import sys, time, importlib, random
@@ -8,11 +9,12 @@ bench = importlib.import_module("bench")
 models = importlib.import_module("graphsage-pytorch_amd.models")
 unsup = importlib.import_module("graphsage-pytorch_amd.unsup")
 utils = importlib.import_module("graphsage-pytorch_amd.utils")
-cfg = dict(bench.CONFIGS["pubmed"])
+cfg = dict(bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "pubmed"])
 dev = torch.device("cuda", 0)
 wl = bench.pubmed_workload(cfg, dev)
 torch.manual_seed(824)
-g = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], dev, agg_func="MEAN", fanouts=[10, 10]).to(dev)
+g = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], dev, agg_func="MEAN", fanouts=[10, 10],
+                     sampler_helpers=int(sys.argv[2]) if len(sys.argv) > 2 else 0).to(dev)
 cls = models.Classification(128, cfg["classes"]).to(dev)
 for mode in (True, False):
     ul = unsup.UnsupervisedLoss(wl["graph"], wl["train"], dev, n_threads=16, device_balls=mode)
@@ -21,7 +23,8 @@ for mode in (True, False):
     random.seed(824)
     T = {"extend": [], "forward": [], "rest": []}
     for i in range(12):
-        b = order[(i % 20) * 512:(i % 20 + 1) * 512]
+        B = cfg["batch"]
+        b = order[(i % 20) * B:(i % 20 + 1) * B]
         torch.cuda.synchronize(); t0 = time.perf_counter()
         nodes = np.asarray(list(ul.extend_nodes(b, num_neg=100)))
         t1 = time.perf_counter()
