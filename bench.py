@@ -357,7 +357,8 @@ def run_apply_model_loop(args, cfg):
                    "global_batch": cfg["batch"], "parallelism": "dp1",
                    "epoch_s": round(len(wl["train"]) // cfg["batch"] * elapsed / args.steps, 4),
                    "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5),
-                   "forward_sampler_helpers": helpers},
+                   "forward_sampler_helpers": helpers,
+                   "extend_balls": "device" if ul.device_balls else "host"},
         "roofline": None,
         "cpu_baseline": cpu,
     }

@@ -49,6 +49,19 @@ def _per_node(nodes, arr, cnt, keep=None):
     return out
 
 
+# Below this many ids the host's bit-parallel BFS beats the device one, whose
+# launches and host round trips cost ~1 ms per batch (apply_model phases, num_neg
+# 100, 16 host threads: Cora 2,708 ids host 0.44 ms / device 1.30 ms; Pubmed
+# 19,717 ids host 8.7 ms / device 3.3 ms; tools/lab/pubmed_phases.py).  Both
+# paths give identical results and leave the same stream state.
+DEVICE_BALLS_MIN_NODES = 8192
+
+
+def device_balls_default(device, n_nodes):
+    """extend_nodes' balls on the GPU: HIP device and a graph of at least DEVICE_BALLS_MIN_NODES ids."""
+    return torch.device(device).type == "cuda" and int(n_nodes) >= DEVICE_BALLS_MIN_NODES
+
+
 class UnsupervisedLoss:
     """UnsupervisedLoss(adj_lists, train_nodes, device) — models.py:45-186.
 
@@ -57,7 +70,8 @@ class UnsupervisedLoss:
     module-global ``random`` (the reference always uses the global stream).
     ``device_balls``: grow extend_nodes' 5-hop balls and pick the far-list
     negatives on the GPU (gs_unsup_attach_device; same results and stream);
-    default: when ``device`` is a HIP device."""
+    default: when ``device`` is a HIP device and the graph has at least
+    DEVICE_BALLS_MIN_NODES ids (``device_balls_default``)."""
 
     def __init__(self, adj_lists, train_nodes, device, *, rng=None, n_threads=None, device_balls=None):
         self.Q = 10
@@ -73,7 +87,6 @@ class UnsupervisedLoss:
         self.rng = rng
         self.n_threads = n_threads or _threads()
         dev = torch.device(device) if device is not None else torch.device("cpu")
-        self.device_balls = (dev.type == "cuda") if device_balls is None else bool(device_balls)
         self._reset_pairs()
         if isinstance(adj_lists, CSRGraph):
             self.graph = adj_lists
@@ -82,6 +95,8 @@ class UnsupervisedLoss:
             tr = np.asarray(train_nodes, np.int64).reshape(-1)
             n = max(max(keys, default=-1), int(tr.max(initial=-1))) + 1
             self.graph = CSRGraph.from_adj_lists(adj_lists, n_nodes=n)
+        self.device_balls = (device_balls_default(dev, self.graph.n_nodes) if device_balls is None
+                             else bool(device_balls))
         self._h = None
         self._make_handle()
 

@@ -56,6 +56,16 @@ def test_extend_nodes_matches_reference(tag):
     _replay(tag)
 
 
+def test_device_balls_default_rule():
+    # host BFS below DEVICE_BALLS_MIN_NODES ids (Cora), device balls above (Pubmed), never on CPU
+    m = U.DEVICE_BALLS_MIN_NODES
+    assert not U.device_balls_default("cpu", 10 * m)
+    assert not U.device_balls_default(torch.device("cuda", 0), 2708)
+    assert U.device_balls_default(torch.device("cuda", 0), 19717)
+    assert U.device_balls_default("cuda", m) and not U.device_balls_default("cuda", m - 1)
+    assert not U.UnsupervisedLoss(_graph("cora"), np.arange(100), "cpu").device_balls
+
+
 def test_extend_nodes_thread_count_invariant():
     for t in (1, 3, 8):
         _replay("cora_n100", threads=t)
