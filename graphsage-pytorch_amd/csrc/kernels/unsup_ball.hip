@@ -66,27 +66,34 @@ __global__ void ball_step_kernel(int64_t total, unsigned long long* __restrict__
     X[i] = 0;
 }
 
-// Per ball (one block per word, lane b of every wave counting ball 64w+b):
-// len(neighbors) over all nodes and |train ∩ ball| over the train ids.
+// Per ball (blockIdx.x = word, lane b of every wave counting ball 64w+b;
+// blockIdx.y = one of gridDim.y slices of the node and train ranges, so a
+// batch of a few words still fills the chip): len(neighbors) over all nodes
+// and |train ∩ ball| over the train ids.  Slices add into zeroed counters
+// with integer atomics (order-free, so the counts are exact).
 __global__ __launch_bounds__(256) void ball_count_kernel(const unsigned long long* __restrict__ S, int64_t n_nodes,
                                                           const int32_t* __restrict__ train, int n_train,
                                                           int n_roots, int64_t* __restrict__ size,
                                                           int64_t* __restrict__ in_train) {
     __shared__ int64_t acc[2][4][64];
     const int w = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t P = gridDim.y, p = blockIdx.y;
     const unsigned long long* Sw = S + static_cast<int64_t>(w) * n_nodes;
     int64_t cs = 0, ct = 0;
-    for (int64_t base = 64 * wave; base < n_nodes; base += 256) {
+    const int64_t ns = (n_nodes + 255) / 256, ne = min(n_nodes, (ns * (p + 1) / P) * 256);
+    for (int64_t base = (ns * p / P) * 256 + 64 * wave; base < ne; base += 256) {
         const int64_t u = base + lane;
-        const unsigned long long x = u < n_nodes ? Sw[u] : 0ull;
+        const unsigned long long x = u < ne ? Sw[u] : 0ull;
         for (int b = 0; b < 64; ++b) {
             const int c = __popcll(__ballot((x >> b) & 1ull));
             if (lane == b) cs += c;
         }
     }
-    for (int base = 64 * wave; base < n_train; base += 256) {
-        const int t = base + lane;
-        const unsigned long long x = t < n_train ? Sw[train[t]] : 0ull;
+    const int64_t ts = (static_cast<int64_t>(n_train) + 255) / 256;
+    const int64_t te = min(static_cast<int64_t>(n_train), (ts * (p + 1) / P) * 256);
+    for (int64_t base = (ts * p / P) * 256 + 64 * wave; base < te; base += 256) {
+        const int64_t t = base + lane;
+        const unsigned long long x = t < te ? Sw[train[t]] : 0ull;
         for (int b = 0; b < 64; ++b) {
             const int c = __popcll(__ballot((x >> b) & 1ull));
             if (lane == b) ct += c;
@@ -98,8 +105,10 @@ __global__ __launch_bounds__(256) void ball_count_kernel(const unsigned long lon
     if (wave == 0) {
         const int r = 64 * w + lane;
         if (r < n_roots) {
-            size[r] = acc[0][0][lane] + acc[0][1][lane] + acc[0][2][lane] + acc[0][3][lane];
-            in_train[r] = acc[1][0][lane] + acc[1][1][lane] + acc[1][2][lane] + acc[1][3][lane];
+            const int64_t a = acc[0][0][lane] + acc[0][1][lane] + acc[0][2][lane] + acc[0][3][lane];
+            const int64_t b = acc[1][0][lane] + acc[1][1][lane] + acc[1][2][lane] + acc[1][3][lane];
+            if (a) atomicAdd(reinterpret_cast<unsigned long long*>(size + r), static_cast<unsigned long long>(a));
+            if (b) atomicAdd(reinterpret_cast<unsigned long long*>(in_train + r), static_cast<unsigned long long>(b));
         }
     }
 }
@@ -291,8 +300,11 @@ void unsup_dev_balls(UnsupDev* d, const int64_t* nodes, int n, int hops, int64_t
         ball_step_kernel<<<nb, 256, 0, st>>>(total, d->S, d->E, d->X);
         check_launch("ball_step_kernel");
     }
-    ball_count_kernel<<<n_words, 256, 0, st>>>(d->S, d->n_nodes, d->asc_order, d->n_order, n, d->counts,
-                                               d->counts + d->cap_roots);
+    // >= ~512 blocks however few words the batch has
+    const unsigned slices = static_cast<unsigned>(std::min(64, std::max(1, (512 + n_words - 1) / n_words)));
+    hip_ok(hipMemsetAsync(d->counts, 0, 2 * static_cast<size_t>(d->cap_roots) * sizeof(int64_t), st), "hipMemsetAsync");
+    ball_count_kernel<<<dim3(static_cast<unsigned>(n_words), slices), 256, 0, st>>>(
+        d->S, d->n_nodes, d->asc_order, d->n_order, n, d->counts, d->counts + d->cap_roots);
     check_launch("ball_count_kernel");
     // far masks and their prefixes for the three orders (needed by the picks)
     const dim3 mg(static_cast<unsigned>(d->n_chunks), static_cast<unsigned>(n_words));
