@@ -43,16 +43,22 @@ __global__ void ball_seed_kernel(const int32_t* __restrict__ roots, int n_roots,
 
 // One BFS level (models.py:156-161: current |= adj[outer] for outer in
 // frontier): every node with frontier bits pushes them to its neighbours.
+// kPushLanes lanes per (word, node) stride over the row, so a hub's pushes
+// are spread instead of one lane's serial loop (OR is order-free).
+constexpr int kPushLanes = 8;
 __global__ void ball_push_kernel(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                                  int64_t n_nodes, int n_words, const unsigned long long* __restrict__ E,
                                  unsigned long long* __restrict__ X) {
-    const int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    const int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    const int64_t i = t / kPushLanes;
+    const int sub = static_cast<int>(t % kPushLanes);
     if (i >= n_nodes * n_words) return;
     const unsigned long long f = E[i];
     if (!f) return;
     const int64_t w = i / n_nodes, u = i - w * n_nodes;
     unsigned long long* Xw = X + w * n_nodes;
-    for (int64_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e) atomicOr(&Xw[col[e]], f);
+    const int64_t end = row_ptr[u + 1];
+    for (int64_t e = row_ptr[u] + sub; e < end; e += kPushLanes) atomicOr(&Xw[col[e]], f);
 }
 
 // frontier = current - neighbors; neighbors |= current (models.py:160-161)
@@ -294,8 +300,9 @@ void unsup_dev_balls(UnsupDev* d, const int64_t* nodes, int n, int hops, int64_t
     ball_seed_kernel<<<(n + 255) / 256, 256, 0, st>>>(d->roots, n, d->n_nodes, d->S, d->E);
     check_launch("ball_seed_kernel");
     const unsigned nb = static_cast<unsigned>((total + 255) / 256);
+    const unsigned nb_push = static_cast<unsigned>((total * kPushLanes + 255) / 256);
     for (int h = 0; h < hops; ++h) {
-        ball_push_kernel<<<nb, 256, 0, st>>>(d->row_ptr, d->col, d->n_nodes, n_words, d->E, d->X);
+        ball_push_kernel<<<nb_push, 256, 0, st>>>(d->row_ptr, d->col, d->n_nodes, n_words, d->E, d->X);
         check_launch("ball_push_kernel");
         ball_step_kernel<<<nb, 256, 0, st>>>(total, d->S, d->E, d->X);
         check_launch("ball_step_kernel");
