@@ -93,11 +93,32 @@ def host_threads():
     return max(1, min(16, host_cores()))
 
 
-def build_workload(cfg, device, seed=824):
+def build_workload(cfg, device, seed=824, world=1):
+    """R-MAT pairs -> host CSR (CPython-set row order), hashed features, labels.
+    With several ranks the CSR is built once per node: local rank
+    0 generates the pairs, builds it and writes its image to /dev/shm; the
+    other ranks map that image read-only (no pairs, no build, no copy)."""
     t0 = time.perf_counter()
-    src, dst = gs.rmat_pairs(cfg["scale"], cfg["pairs"], seed=seed, n_threads=host_threads())
     n = 1 << cfg["scale"]
-    graph = gs.CSRGraph.from_pairs(src, dst, n, n_threads=host_threads())
+    src = dst = None
+
+    def build():
+        nonlocal src, dst
+        src, dst = gs.rmat_pairs(cfg["scale"], cfg["pairs"], seed=seed, n_threads=host_threads())
+        return gs.CSRGraph.from_pairs(src, dst, n, n_threads=host_threads())
+
+    shm = None
+    if world > 1:
+        shm = f"/dev/shm/gs_csr_s{cfg['scale']}_p{cfg['pairs']}_{seed}_{os.environ.get('MASTER_PORT', '0')}.bin"
+        graph = gs.CSRGraph.shared(build, shm, int(os.environ.get("LOCAL_RANK", "0")), dist.barrier)
+        dist.barrier()  # every rank has mapped the image: the file can go (the mappings stay)
+        if int(os.environ.get("LOCAL_RANK", "0")) == 0 and os.path.exists(shm):
+            os.unlink(shm)
+        if src is not None:
+            del src, dst  # the cpu_baseline leg (the only pair-list user) runs at world 1
+            src = dst = None
+    else:
+        graph = build()
     t_graph = time.perf_counter() - t0
     dt = torch.bfloat16 if cfg["dtype"] == "bf16" else torch.float32
     X = torch.empty(n, cfg["feat"], dtype=dt, device=device)
@@ -106,7 +127,7 @@ def build_workload(cfg, device, seed=824):
     deg = graph.degrees()
     candidates = np.nonzero(deg > 0)[0]
     return dict(src=src, dst=dst, n=n, graph=graph, X=X, labels=labels, candidates=candidates,
-                t_graph=t_graph, deg=deg)
+                t_graph=t_graph, deg=deg, shm=shm, csr_shared=shm is not None)
 
 
 def kernel_times_ms(trainer, n, site=0):
@@ -165,6 +186,25 @@ def agg1_ids_bytes(n_dst, n_pos, F, elem, k):
     resolved ids (agg_ids_kernel): one feature row per sampled edge, the
     destination's k padded neighbour ids (4 B each), one output row."""
     return n_pos * F * elem + n_dst * (k * 4 + F * elem)
+
+
+def replay_frontiers(graph, batches, n_streams, fanouts, seed, rank, upto):
+    """Per batch i < upto: (B, |L1|, |L0|) — the roots and both hops' unique
+    frontiers, the reference's `nodes_batch_layers` (models.py:246-251).  The
+    runner never materialises the last hop's union (the layer-1 gather needs
+    only the sampled positions), so its size comes from replaying the same
+    streams afterwards: stream w drew batches w, w+S, ... in order from
+    make_rng(seed, rank, w), and the same draws on a copy give the identical
+    hops (bit-exact sampler), here with the last union materialised."""
+    rngs = [train.make_rng(seed, rank, w) for w in range(n_streams)]
+    out = np.zeros((upto, 3), np.int64)
+    for i in range(upto):
+        smp = gs.sampler.sample(graph, rngs[i % n_streams], batches[i], list(fanouts), full=True)
+        L = smp.n_hops
+        out[i, 0] = len(batches[i])
+        out[i, 1] = smp.sizes(1)[2]  # hop 1's union: |L1|
+        out[i, 2] = smp.sizes(L)[2]  # the last hop's union: |L0|
+    return out
 
 
 def port_calibration():
@@ -401,7 +441,7 @@ def run_embed(args, cfg):
     rank, world = train.init_distributed()
     device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(device)
-    wl = build_workload(cfg, device, args.seed)
+    wl = build_workload(cfg, device, args.seed, world)
     n, B = wl["n"], cfg["batch"]
     n_used = n if args.full_graph else min(n, args.steps * world * B)
     weights = [w.to(device) for w in train.reference_init(2, cfg["feat"], 128, cfg["classes"], False, args.seed)[0]]
@@ -522,6 +562,11 @@ def main():
         else:
             args.sampler_streams = max(1, min(12, per_gpu - 3))
 
+    # the training layout needs S streams x (1 + helpers) sampler threads plus
+    # two cores (the issuing thread, the HIP runtime / RCCL proxy); with fewer
+    # host cores per GPU the sampler, not the GPU, sets the pace
+    args.layout_cores = args.sampler_streams * (1 + args.sampler_helpers) + 2
+    args.layout_short = per_gpu < 8 or per_gpu < args.layout_cores
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
@@ -538,7 +583,7 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    wl = build_workload(cfg, device, args.seed)
+    wl = build_workload(cfg, device, args.seed, world)
     trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2,
                                   hidden=128, fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=args.seed)
     rngs = [train.make_rng(args.seed, rank, w) for w in range(args.sampler_streams)]
@@ -656,6 +701,8 @@ def main():
     if sustain:
         if world > 1:
             dist.barrier()
+        runner.stats(reset=True)
+        sthr0 = cgroup_throttle()
         ss0, sc0 = runner.progress()
         ts = time.perf_counter()
         runner.run(sustain)
@@ -668,9 +715,16 @@ def main():
         if world > 1:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         te = float(tt.item())
+        sthr1 = cgroup_throttle()
+        sst = runner.stats()
+        ns = max(1, sst["steps"])
         sus = {"value": round(cfg["batch"] * sustain * world / te, 1), "unit": "root nodes/s", "steps": sustain,
                "ms_per_step": round(te / sustain * 1e3, 4), "sampled_ahead_at_start": ss0 - sc0,
-               "sampled_in_window": ss1 - ss0, "sampled_ahead_at_end": ss1 - sc1}
+               "sampled_in_window": ss1 - ss0, "sampled_ahead_at_end": ss1 - sc1,
+               "lookahead_misses": sst["lookahead_misses"], "max_step_ms": round(1e3 * sst["max_step_s"], 3),
+               "host_ms_per_step": {k: round(1e3 * sst[k + "_s"] / ns, 4)
+                                    for k in ("sample", "wait", "wait_sample", "wait_ring", "wait_gather", "issue")},
+               "cgroup_throttled_ms": (round((sthr1 - sthr0) / 1e3, 3) if sthr0 is not None else None)}
     value = cfg["batch"] * args.steps * world / elapsed
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
     n_edges = float(sizes[:L, 1].sum()) * args.steps
@@ -681,6 +735,25 @@ def main():
     else:  # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
         agg_bytes = agg1_ids_bytes(n1, e1, cfg["feat"], elem, cfg["fanouts"][-1])
     gemm_flops = 2.0 * n1 * (2 * cfg["feat"]) * 128  # 2·|L1|·2F·H per layer-1 GEMM
+
+    # the BASELINE metric literally: sampled nodes (B + |L1| + |L0|, the
+    # reference's nodes_batch_layers) per second over the steady window's batches
+    w0 = args.warmup + args.steps  # the steady window's first batch
+    fr = replay_frontiers(wl["graph"], batches, args.sampler_streams, cfg["fanouts"], args.seed, rank,
+                          w0 + args.steps)[w0:]
+    nodes_t = torch.tensor([float(fr.sum())], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(nodes_t)
+    sampled_nodes_per_s = float(nodes_t.item()) / elapsed
+    # sampler capacity: S streams, each a batch per mean sampling time
+    per_batch_s = st["sample_s"] / max(1, st["steps"])
+    cap_batches = args.sampler_streams / per_batch_s if per_batch_s > 0 else float("inf")
+    produced = proof["sampled_in_timed_region"] / elapsed
+    sampler_bound = args.layout_short or cap_batches * cfg["batch"] < 1.05 * value / world
+    if sampler_bound and rank == 0:
+        print(f"warning: sampler-bound layout: {args.per_gpu} host cores per GPU for {args.sampler_streams} "
+              f"streams x (1 + {args.sampler_helpers}) threads + 2 (needs {args.layout_cores}); sampler capacity "
+              f"{cap_batches * cfg['batch']:.0f} roots/s per GPU", file=sys.stderr)
 
     if rank == 0:
         rooflines = {}
@@ -716,6 +789,7 @@ def main():
             "metric": "sampled nodes/sec (2-layer, fanout 25,10) at 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "root nodes/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "sampled_nodes_per_s": round(sampled_nodes_per_s, 1),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": cfg["dtype"],
             "data": "synthetic (R-MAT graph, hashed U(-1,1) features, labels id%16)",
             "config": {"workload": f"{args.config}: R-MAT scale {cfg['scale']} "
@@ -725,6 +799,15 @@ def main():
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
                        "sampler_contexts_warmed": not args.no_warm,
+                       "sampled_nodes": {"per_step_mean": [round(float(x), 1) for x in fr.mean(0)],
+                                         "fields": "B, |L1|, |L0| (unique frontiers, models.py:246-251)",
+                                         "per_s": round(sampled_nodes_per_s, 1)},
+                       "sampler": {"host_cores_per_gpu": args.per_gpu, "layout_cores": args.layout_cores,
+                                   "ms_per_batch": round(per_batch_s * 1e3, 4),
+                                   "capacity_batches_per_s": round(cap_batches, 1),
+                                   "capacity_roots_per_s": round(cap_batches * cfg["batch"], 1),
+                                   "produced_batches_per_s_in_window": round(produced, 1),
+                                   "sampler_bound": bool(sampler_bound)},
                        "window": "steady (after a cold window of the same length; the clock waits until the "
                                  "window has sampled as many new batches as it consumed)",
                        **proof,
@@ -733,6 +816,8 @@ def main():
                        "allreduce_buckets": args.ar_buckets if world > 1 else 0,
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
+                       "host_csr": "one per node, /dev/shm image mapped by every rank" if wl["csr_shared"]
+                       else "built in-process",
                        "host_ms_per_step": {"sampler": round(1e3 * st["sample_s"] / max(1, st["steps"]), 3),
                                             "wait_for_batch": round(1e3 * st["wait_s"] / max(1, st["steps"]), 3),
                                             "issue": round(1e3 * st["issue_s"] / max(1, st["steps"]), 3),

@@ -69,6 +69,9 @@ _SIGS = {
     "gs_graph_dims": (_i32, [_vp, _p(_i64), _p(_i64), _p(_i64)]),
     "gs_graph_row_ptr": (_vp, [_vp]),
     "gs_graph_col": (_vp, [_vp]),
+    "gs_graph_image_bytes": (_i64, [_vp]),
+    "gs_graph_write_image": (_i32, [_vp, _vp, _i64]),
+    "gs_graph_from_image": (_i32, [_vp, _i64, _p(_vp)]),
     "gs_rmat_pairs": (_i32, [_i32, _i64, _f64, _f64, _f64, _u64, _i32, _i32, _vp, _vp, _p(_i64)]),
     "gs_sample_run": (_i32, [_vp, _vp, _vp, _i64, _vp, _i32, _i32, _p(_vp)]),
     "gs_sample_destroy": (None, [_vp]),

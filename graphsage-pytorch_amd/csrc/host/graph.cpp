@@ -97,7 +97,7 @@ Graph* build_graph(const int64_t* src, const int64_t* dst, int64_t n_pairs, int6
     auto* g = new Graph();
     g->n_nodes = n_nodes;
     g->row_ptr.assign(n_nodes + 1, 0);
-    for (int64_t v = 0; v < n_nodes; ++v) g->row_ptr[v + 1] = g->row_ptr[v] + deg[v];
+    for (int64_t v = 0; v < n_nodes; ++v) g->row_ptr.own[v + 1] = g->row_ptr.own[v] + deg[v];
     g->n_entries = g->row_ptr[n_nodes];
     g->col.resize(g->n_entries);
     g->slot.resize(g->n_entries);
@@ -108,8 +108,8 @@ Graph* build_graph(const int64_t* src, const int64_t* dst, int64_t n_pairs, int6
         for (int64_t v = lo; v < hi; ++v) {
             const int64_t d = deg[v];
             if (!d) continue;
-            std::memcpy(&g->col[g->row_ptr[v]], &tkey[ins_ptr[v]], d * sizeof(int32_t));
-            std::memcpy(&g->slot[g->row_ptr[v]], &tslot[ins_ptr[v]], d * sizeof(uint32_t));
+            std::memcpy(&g->col.own[g->row_ptr[v]], &tkey[ins_ptr[v]], d * sizeof(int32_t));
+            std::memcpy(&g->slot.own[g->row_ptr[v]], &tslot[ins_ptr[v]], d * sizeof(uint32_t));
         }
     });
     return g;
@@ -146,6 +146,77 @@ Graph* graph_from_tables(int64_t n_nodes, const int64_t* row_ptr, const int32_t*
         g->max_degree = std::max(g->max_degree, d);
     }
     return guard.release();
+}
+
+// ---- flat image of a graph (one node-wide CSR shared by the rank processes)
+//
+// [header: 8 x int64 = magic, version, n_nodes, n_entries, max_degree, has_dirty,
+//  0, 0] then row_ptr, col, slot, log2size, dirty, each 64-byte aligned.
+namespace {
+constexpr int64_t kImgMagic = 0x4753435352494d47;  // "GMIRSCSG"
+constexpr int64_t kImgVersion = 1;
+inline int64_t al64(int64_t b) { return (b + 63) & ~int64_t(63); }
+struct ImgLayout {
+    int64_t row_ptr, col, slot, log2size, dirty, total;
+};
+ImgLayout img_layout(int64_t n_nodes, int64_t n_entries, bool has_dirty) {
+    ImgLayout L{};
+    int64_t at = 64;
+    L.row_ptr = at;
+    at = al64(at + (n_nodes + 1) * 8);
+    L.col = at;
+    at = al64(at + n_entries * 4);
+    L.slot = at;
+    at = al64(at + n_entries * 4);
+    L.log2size = at;
+    at = al64(at + n_nodes);
+    L.dirty = at;
+    at = al64(at + (has_dirty ? n_nodes : 0));
+    L.total = at;
+    return L;
+}
+}  // namespace
+
+int64_t graph_image_bytes(const Graph& g) { return img_layout(g.n_nodes, g.n_entries, !g.dirty.empty()).total; }
+
+void graph_write_image(const Graph& g, void* dst, int64_t cap) {
+    const ImgLayout L = img_layout(g.n_nodes, g.n_entries, !g.dirty.empty());
+    GS_REQUIRE(dst && cap >= L.total, GS_EINVAL, "image buffer below gs_graph_image_bytes");
+    auto* b = static_cast<uint8_t*>(dst);
+    int64_t hdr[8] = {kImgMagic, kImgVersion, g.n_nodes, g.n_entries, g.max_degree, g.dirty.empty() ? 0 : 1, 0, 0};
+    std::memcpy(b, hdr, sizeof(hdr));
+    std::memcpy(b + L.row_ptr, g.row_ptr.data(), (g.n_nodes + 1) * 8);
+    if (g.n_entries) {
+        std::memcpy(b + L.col, g.col.data(), g.n_entries * 4);
+        std::memcpy(b + L.slot, g.slot.data(), g.n_entries * 4);
+    }
+    std::memcpy(b + L.log2size, g.log2size.data(), g.n_nodes);
+    if (!g.dirty.empty()) std::memcpy(b + L.dirty, g.dirty.data(), g.n_nodes);
+}
+
+Graph* graph_from_image(const void* img, int64_t bytes) {
+    GS_REQUIRE(img && bytes >= 64, GS_EINVAL, "image too small");
+    int64_t hdr[8];
+    std::memcpy(hdr, img, sizeof(hdr));
+    GS_REQUIRE(hdr[0] == kImgMagic && hdr[1] == kImgVersion, GS_EINVAL, "not a graph image (magic/version)");
+    const int64_t n_nodes = hdr[2], n_entries = hdr[3];
+    GS_REQUIRE(n_nodes > 0 && n_nodes < (int64_t(1) << 31) && n_entries >= 0, GS_EINVAL, "bad image dims");
+    const ImgLayout L = img_layout(n_nodes, n_entries, hdr[5] != 0);
+    GS_REQUIRE(bytes >= L.total, GS_EINVAL, "image truncated");
+    GS_REQUIRE(reinterpret_cast<uintptr_t>(img) % 64 == 0, GS_EINVAL, "image not 64-byte aligned");
+    const auto* b = static_cast<const uint8_t*>(img);
+    auto g = std::make_unique<Graph>();
+    g->n_nodes = n_nodes;
+    g->n_entries = n_entries;
+    g->max_degree = hdr[4];
+    g->row_ptr.view(reinterpret_cast<const int64_t*>(b + L.row_ptr), n_nodes + 1);
+    g->col.view(reinterpret_cast<const int32_t*>(b + L.col), n_entries);
+    g->slot.view(reinterpret_cast<const uint32_t*>(b + L.slot), n_entries);
+    g->log2size.view(b + L.log2size, n_nodes);
+    if (hdr[5]) g->dirty.view(b + L.dirty, n_nodes);
+    GS_REQUIRE(g->row_ptr.data()[0] == 0 && g->row_ptr.data()[n_nodes] == n_entries, GS_EINVAL,
+               "image row_ptr inconsistent with its entry count");
+    return g.release();
 }
 
 int64_t rmat_pairs(int32_t scale, int64_t n_pairs, double a, double b, double c, uint64_t seed,
@@ -248,6 +319,24 @@ const int64_t* gs_graph_row_ptr(const gs_graph* g) {
 
 const int32_t* gs_graph_col(const gs_graph* g) {
     return g ? reinterpret_cast<const Graph*>(g)->col.data() : nullptr;
+}
+
+int64_t gs_graph_image_bytes(const gs_graph* g) {
+    return g ? gs::graph_image_bytes(*reinterpret_cast<const Graph*>(g)) : -1;
+}
+
+int gs_graph_write_image(const gs_graph* g, void* dst, int64_t cap) {
+    GS_API_BEGIN
+    GS_REQUIRE(g, GS_EINVAL, "graph is NULL");
+    gs::graph_write_image(*reinterpret_cast<const Graph*>(g), dst, cap);
+    GS_API_END
+}
+
+int gs_graph_from_image(const void* img, int64_t bytes, gs_graph** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(out, GS_EINVAL, "out is NULL");
+    *out = reinterpret_cast<gs_graph*>(gs::graph_from_image(img, bytes));
+    GS_API_END
 }
 
 int gs_rmat_pairs(int32_t scale, int64_t n_pairs, double a, double b, double c, uint64_t seed,

@@ -319,6 +319,7 @@ void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_thr
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     const int64_t n = static_cast<int64_t>(u.nodes.size());
+    if (n == 0) return;  // no nodes, no negatives (and no device launch)
     std::vector<int64_t> bsize(n), tib(n);
     gs::unsup_dev_balls(u.dev, u.nodes.data(), static_cast<int>(n), u.n_walk_len, bsize.data(), tib.data());
     const auto t1 = clk::now();

@@ -237,16 +237,34 @@ struct UnsupDev {
         owned.push_back(p);
         return static_cast<T*>(p);
     }
+    // A grown buffer replaces the old one, which is freed at once: every call
+    // ends with a stream synchronise, so no launch still reads it.
+    template <typename T>
+    void regrow(T*& p, int64_t n) {
+        if (p) {
+            owned.erase(std::remove(owned.begin(), owned.end(), static_cast<void*>(p)), owned.end());
+            hip_ok(hipFree(p), "hipFree(unsup dev)");
+        }
+        p = alloc<T>(n);
+    }
     void free_all() {
+        if (st) (void)hipStreamSynchronize(st);
         for (void* p : owned) (void)hipFree(p);
         owned.clear();
+        if (st) (void)hipStreamDestroy(st);
+        st = nullptr;
     }
+    ~UnsupDev() { free_all(); }
 };
 
+// The device half owns a non-blocking stream on the current device: its calls
+// synchronise only their own work (not the caller's queued model launches, so
+// the host can draw while the previous step's backward runs) and never depend
+// on a caller stream's lifetime.  It reads no caller tensors.
 UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_order,
-                           const std::vector<int32_t>& set_order, void* stream) {
+                           const std::vector<int32_t>& set_order, void* /*stream: unused*/) {
     auto d = std::make_unique<UnsupDev>();
-    d->st = as_stream(stream);
+    hip_ok(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking), "hipStreamCreate(unsup dev)");
     d->n_nodes = g.n_nodes;
     d->n_order = static_cast<int>(copy_order.size());
     d->n_chunks = std::max(1, (d->n_order + 63) / 64);
@@ -265,29 +283,26 @@ UnsupDev* unsup_dev_create(const Graph& g, const std::vector<int32_t>& copy_orde
     return d.release();
 }
 
-void unsup_dev_destroy(UnsupDev* d) {
-    if (!d) return;
-    d->free_all();
-    delete d;
-}
+void unsup_dev_destroy(UnsupDev* d) { delete d; }
 
 static void reserve_roots(UnsupDev* d, int n) {
     if (n <= d->cap_roots) return;
     const int cap = std::max(n, 64);
     const int64_t words = (cap + 63) / 64;
-    d->S = d->alloc<unsigned long long>(words * d->n_nodes);
-    d->E = d->alloc<unsigned long long>(words * d->n_nodes);
-    d->X = d->alloc<unsigned long long>(words * d->n_nodes);
-    d->roots = d->alloc<int32_t>(cap);
-    d->counts = d->alloc<int64_t>(2 * cap);
+    d->regrow(d->S, words * d->n_nodes);
+    d->regrow(d->E, words * d->n_nodes);
+    d->regrow(d->X, words * d->n_nodes);
+    d->regrow(d->roots, cap);
+    d->regrow(d->counts, 2 * cap);
     for (int o = 0; o < 3; ++o) {
-        d->M[o] = d->alloc<unsigned long long>(static_cast<int64_t>(cap) * d->n_chunks);
-        d->pre[o] = d->alloc<int32_t>(static_cast<int64_t>(cap) * (d->n_chunks + 1));
+        d->regrow(d->M[o], static_cast<int64_t>(cap) * d->n_chunks);
+        d->regrow(d->pre[o], static_cast<int64_t>(cap) * (d->n_chunks + 1));
     }
     d->cap_roots = cap;
 }
 
 void unsup_dev_balls(UnsupDev* d, const int64_t* nodes, int n, int hops, int64_t* ball_size, int64_t* train_in_ball) {
+    if (n <= 0) return;  // no balls: no launch (a zero-block grid is an error)
     reserve_roots(d, n);
     const int n_words = (n + 63) / 64;
     const int64_t total = static_cast<int64_t>(n_words) * d->n_nodes;
@@ -335,10 +350,10 @@ void unsup_dev_select(UnsupDev* d, const std::vector<int32_t>& req_r, const std:
     if (!n) return;
     if (n > d->cap_req) {
         const int cap = std::max(n, 1024);
-        d->req_r = d->alloc<int32_t>(cap);
-        d->req_j = d->alloc<int32_t>(cap);
-        d->picks = d->alloc<int32_t>(cap);
-        d->req_kind = d->alloc<uint8_t>(cap);
+        d->regrow(d->req_r, cap);
+        d->regrow(d->req_j, cap);
+        d->regrow(d->picks, cap);
+        d->regrow(d->req_kind, cap);
         d->cap_req = cap;
     }
     hipStream_t st = d->st;
@@ -363,14 +378,16 @@ void unsup_dev_far_lists(UnsupDev* d, const std::vector<int32_t>& balls, const s
     const int64_t total = n ? base[n] : 0;
     out.resize(static_cast<size_t>(total));
     if (!n || !total) return;
-    if (n > d->cap_lists) {
-        d->list_balls = d->alloc<int32_t>(n);
-        d->list_base = d->alloc<int64_t>(n + 1);
-        d->cap_lists = n;
+    if (n > d->cap_lists) {  // geometric growth: a long run settles after a few batches
+        const int cap = std::max(n, d->cap_lists + d->cap_lists / 2);
+        d->regrow(d->list_balls, cap);
+        d->regrow(d->list_base, static_cast<int64_t>(cap) + 1);
+        d->cap_lists = cap;
     }
     if (total > d->cap_list_out) {
-        d->list_out = d->alloc<int32_t>(total);
-        d->cap_list_out = total;
+        const int64_t cap = std::max(total, d->cap_list_out + d->cap_list_out / 2);
+        d->regrow(d->list_out, cap);
+        d->cap_list_out = cap;
     }
     hipStream_t st = d->st;
     hip_ok(hipMemcpyAsync(d->list_balls, balls.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, st), "hipMemcpyAsync");

@@ -559,7 +559,6 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             const int rc = gs_comm_allreduce_sum(rp->cfg.comm, gs_trainer_grads(rp->cfg.trainer) + w1, n - w1,
                                                  rp->comm_stream);
             if (rc != GS_OK) fail(rc, gs_last_error());
-            hip_ok(hipEventRecord(rp->upper_reduced, rp->comm_stream), "hipEventRecord");
         });
     }
     r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
@@ -599,6 +598,23 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     hipStream_t st = as_stream(stream);
     const int64_t n_params = gs_trainer_n_params(r->cfg.trainer);
     float* grads = gs_trainer_grads(r->cfg.trainer);
+    // If a step throws (e.g. MAX over an empty neighbourhood in take_slot),
+    // the steps issued before it signal completion only through the pinned
+    // flag: record an event on the step stream for every ring entry still
+    // pending, so the destructor drains them before freeing what they read.
+    struct Unwind {
+        gs_runner* r;
+        hipStream_t st;
+        bool armed = true;
+        ~Unwind() {
+            if (!armed) return;
+            for (int k = 0; k < gs_runner::kDev; ++k)
+                if (r->flag_step[k] >= 0 && hipEventRecord(r->dev_done[k], st) == hipSuccess) {
+                    r->flag_step[k] = -1;
+                    r->dev_busy[k] = true;
+                }
+        }
+    } unwind{r, st};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();
@@ -650,9 +666,16 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             // with a communicator (any world size, so one rank exercises the same
             // path): sum the gradients, then clip the averaged sum; without one
             // the clip uses the norm partials of the step's own reductions
-            if (r->cfg.comm && r->comm_stream) {  // bucketed: W1 here, the rest went out under its GEMM
-                rc = gs_comm_allreduce_sum(r->cfg.comm, grads, trainer_w1_floats(r->cfg.trainer), st);
+            if (r->cfg.comm && r->comm_stream) {
+                // bucketed: the upper gradients went out on comm_stream under the
+                // layer-1 dW GEMM; W1's collective follows them on the SAME stream,
+                // so every rank issues the two collectives on one communicator in
+                // one stream order (not by host issue order across two streams)
+                hip_ok(hipEventRecord(r->upper_ready, st), "hipEventRecord");  // dW1 final
+                hip_ok(hipStreamWaitEvent(r->comm_stream, r->upper_ready, 0), "hipStreamWaitEvent");
+                rc = gs_comm_allreduce_sum(r->cfg.comm, grads, trainer_w1_floats(r->cfg.trainer), r->comm_stream);
                 if (rc != GS_OK) fail(rc, gs_last_error());
+                hip_ok(hipEventRecord(r->upper_reduced, r->comm_stream), "hipEventRecord");
                 hip_ok(hipStreamWaitEvent(st, r->upper_reduced, 0), "hipStreamWaitEvent");
             } else if (r->cfg.comm) {
                 rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
@@ -686,6 +709,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         r->stats.update_s += secs(t3, t4);
         r->stats.max_step_s = std::max(r->stats.max_step_s, secs(t0, t4));
     }
+    unwind.armed = false;
     GS_API_END
 }
 

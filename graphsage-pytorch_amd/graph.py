@@ -10,6 +10,7 @@ keeps both, built natively (libgraphsage_amd ``gs_graph_build``), and mirrors
 the CSR to the GPU for the device-side expansion of the last hop.
 """
 import ctypes
+import mmap
 import os
 import sys
 
@@ -99,6 +100,57 @@ class CSRGraph:
         check(lib().gs_graph_from_tables(n_nodes, ptr(row_ptr), ptr(col), ptr(slot), ptr(log2),
                                          ptr(dirty), ctypes.byref(h)))
         return cls(h.value, n_nodes)
+
+    # ------------------------------------------------- node-wide sharing
+    def write_image(self, path):
+        """Write this graph's flat image to `path` (atomically: a temporary
+        file renamed into place), for other processes to map (``from_image``)."""
+        nb = int(lib().gs_graph_image_bytes(self._h))
+        if nb <= 0:
+            raise RuntimeError("gs_graph_image_bytes failed")
+        tmp = f"{path}.tmp{os.getpid()}"
+        with open(tmp, "wb+") as f:
+            f.truncate(nb)
+            mm = mmap.mmap(f.fileno(), nb)
+            try:
+                buf = (ctypes.c_char * nb).from_buffer(mm)
+                check(lib().gs_graph_write_image(self._h, ctypes.addressof(buf), nb))
+                del buf
+                mm.flush()
+            finally:
+                mm.close()
+        os.replace(tmp, path)
+        return nb
+
+    @classmethod
+    def from_image(cls, path):
+        """Adopt the image at `path` mapped read-only (no copy): the graph's
+        arrays are the mapping's pages, shared by every process that maps it."""
+        with open(path, "rb") as f:
+            nb = os.fstat(f.fileno()).st_size
+            mm = mmap.mmap(f.fileno(), nb, prot=mmap.PROT_READ)
+        view = np.frombuffer(mm, dtype=np.uint8)  # read-only; its address is the mapping's
+        h = ctypes.c_void_p()
+        check(lib().gs_graph_from_image(view.ctypes.data, nb, ctypes.byref(h)))
+        n = ctypes.c_int64()
+        check(lib().gs_graph_dims(h, ctypes.byref(n), None, None))
+        g = cls(h.value, n.value)
+        g._mapping = (mm, view)  # keep the pages mapped for the handle's lifetime
+        return g
+
+    @classmethod
+    def shared(cls, build, path, local_rank, barrier):
+        """One graph per node: local rank 0 runs ``build()`` and writes its
+        image to ``path``; after ``barrier()`` every other rank maps it.  Rank
+        0 keeps its built graph (identical bytes)."""
+        g = None
+        if local_rank == 0:
+            g = build()
+            g.write_image(path)
+        barrier()
+        if g is None:
+            g = cls.from_image(path)
+        return g
 
     # --------------------------------------------------------------- views
     def row_ptr(self):

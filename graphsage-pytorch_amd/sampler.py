@@ -217,13 +217,19 @@ class DeviceSampler:
     ``rng`` moves between host and device with ``set_rng`` / ``get_rng``
     (``RNG`` objects or ``random.getstate()``-style (mt, pos) pairs)."""
 
-    def __init__(self, graph, fanouts, max_roots, gcn=False, fail_empty=False):
+    def __init__(self, graph, fanouts, max_roots, gcn=False, fail_empty=False, device=None):
         from ._lib import GS_SAMPLE_GCN
         self.fanouts = np.ascontiguousarray(fanouts, np.int32)
         flags = (GS_SAMPLE_GCN if gcn else 0) | (4 if fail_empty else 0)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("DeviceSampler runs on a HIP device")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         h = ctypes.c_void_p()
-        check(lib().gs_dsampler_create(graph._h, ptr(self.fanouts), len(self.fanouts), int(max_roots), flags,
-                                       ctypes.byref(h)))
+        with torch.cuda.device(self.device):
+            check(lib().gs_dsampler_create(graph._h, ptr(self.fanouts), len(self.fanouts), int(max_roots), flags,
+                                           ctypes.byref(h)))
         self._h = h
         self.graph = graph  # keep the host graph alive (pack bounds)
         self.n_hops = len(self.fanouts)
@@ -231,17 +237,17 @@ class DeviceSampler:
     def set_rng(self, rng):
         mt, pos = rng.getstate() if isinstance(rng, RNG) else rng
         mt = np.ascontiguousarray(mt, np.uint32)
-        check(lib().gs_dsampler_set_rng(self._h, ptr(mt), int(pos), _lib.stream_ptr()))
+        check(lib().gs_dsampler_set_rng(self._h, ptr(mt), int(pos), _lib.stream_ptr(self.device)))
 
     def get_rng(self):
         mt = np.zeros(624, np.uint32)
         pos = ctypes.c_int64()
-        check(lib().gs_dsampler_get_rng(self._h, ptr(mt), ctypes.byref(pos), _lib.stream_ptr()))
+        check(lib().gs_dsampler_get_rng(self._h, ptr(mt), ctypes.byref(pos), _lib.stream_ptr(self.device)))
         return mt, int(pos.value)
 
     def words(self, n):
         out = np.zeros(max(int(n), 1), np.uint32)
-        check(lib().gs_dsampler_words(self._h, int(n), ptr(out), _lib.stream_ptr()))
+        check(lib().gs_dsampler_words(self._h, int(n), ptr(out), _lib.stream_ptr(self.device)))
         return out[:int(n)]
 
     def pack_bound(self, n_roots):
@@ -249,12 +255,18 @@ class DeviceSampler:
 
     def run(self, roots, pack=None):
         """Sample one batch; returns (pack, hop_sizes[n_hops, 4], offsets[8, 8], used)."""
-        roots = torch.as_tensor(np.asarray(roots, np.int64).astype(np.int32)).cuda() \
-            if not isinstance(roots, torch.Tensor) else roots.to(torch.int32)
+        if not isinstance(roots, torch.Tensor):
+            roots = torch.as_tensor(np.asarray(roots, np.int64).astype(np.int32))
+        # device pointers only: a CPU or strided roots tensor would hand the
+        # kernels host memory or the wrong ids
+        roots = roots.to(device=self.device, dtype=torch.int32).contiguous().view(-1)
         n = int(roots.numel())
         if pack is None:
-            pack = torch.zeros(self.pack_bound(n), dtype=torch.int32, device=roots.device)
-        check(lib().gs_dsampler_run(self._h, ptr(roots), n, ptr(pack), int(pack.numel()), _lib.stream_ptr()))
+            pack = torch.zeros(self.pack_bound(n), dtype=torch.int32, device=self.device)
+        elif not (isinstance(pack, torch.Tensor) and pack.dtype == torch.int32 and pack.is_contiguous()
+                  and pack.device == self.device):
+            raise ValueError(f"pack must be a contiguous int32 tensor on {self.device}")
+        check(lib().gs_dsampler_run(self._h, ptr(roots), n, ptr(pack), int(pack.numel()), _lib.stream_ptr(self.device)))
         hs = np.zeros(4 * _lib.GS_MAX_HOPS, np.int64)
         off = np.zeros(_lib.GS_MAX_HOPS * _lib.GS_PK_NFIELDS, np.int64)
         used = ctypes.c_int64()

@@ -108,7 +108,11 @@ class UnsupervisedLoss:
                                     self.N_WALK_LEN, ctypes.byref(h)))
         self._h = h
         if self.device_balls:
-            check(lib().gs_unsup_attach_device(h, _lib.stream_ptr()))
+            # the device half allocates on, and owns a stream of, the current
+            # device: make it this module's device
+            dev = torch.device(self.device)
+            with torch.cuda.device(dev if dev.index is not None else torch.cuda.current_device()):
+                check(lib().gs_unsup_attach_device(h, None))
         self._params = (self.N_WALKS, self.WALK_LEN, self.N_WALK_LEN)
 
     def _run(self, nodes, num_neg, parts):

@@ -92,6 +92,16 @@ int gs_graph_dims(const gs_graph* g, int64_t* n_nodes, int64_t* n_entries,
 /* Borrowed views, valid until gs_graph_destroy: row_ptr[n_nodes+1], col[n_entries]. */
 const int64_t* gs_graph_row_ptr(const gs_graph* g);
 const int32_t* gs_graph_col(const gs_graph* g);
+/* One node-wide CSR shared by the rank processes (the replicated
+ * adjacency of dataCenter.py:33-41, built once per node).  A flat image —
+ * header, row_ptr, col, slot, log2size, dirty, 64-byte aligned — that local
+ * rank 0 writes (to a /dev/shm file) and every rank maps read-only and adopts
+ * without a copy.  gs_graph_from_image keeps pointers into `img`: the caller
+ * keeps it mapped until gs_graph_destroy.  The sampler reads an adopted graph
+ * exactly as one it built itself. */
+int64_t gs_graph_image_bytes(const gs_graph* g);
+int gs_graph_write_image(const gs_graph* g, void* dst, int64_t cap);
+int gs_graph_from_image(const void* img, int64_t bytes, gs_graph** out);
 
 /* Synthetic R-MAT(a,b,c,1-a-b-c) pair list: `scale` id bits,
  * n_pairs draws, self pairs dropped, optional seeded id permutation.
@@ -259,8 +269,9 @@ void gs_unsup_destroy(gs_unsup* u);
  * negatives' far-list elements there (select queries over set(train)'s order
  * with the ball's members skipped); the draws of models.py:164 stay on the
  * calling thread in node order, so every result and the rng stream are those
- * of the host path.  Uploads the CSR once; `stream` orders
- * the device work (each extend synchronises it). */
+ * of the host path.  Uploads the CSR once to the current
+ * device.  The device half owns a non-blocking stream there (each extend
+ * synchronises only that stream); `stream` is unused and may be NULL. */
 int gs_unsup_attach_device(gs_unsup* u, void* stream);
 /* parts: 1 = the walks only (get_positive_nodes, models.py:149), 2 = the
  * negatives only (get_negtive_nodes, :152), 3 = both (extend_nodes).

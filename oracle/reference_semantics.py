@@ -29,19 +29,29 @@ import torch.nn.functional as F
 class Adjacency:
     """Lazily materialised dict-of-sets adjacency (dataCenter.py:33-41)."""
 
-    def __init__(self, src, dst, n_nodes):
+    def __init__(self, src, dst, n_nodes, sort_device=None):
+        """sort_device: optionally a torch device for the one stable sort of
+        the insertion list by endpoint (a generic library sort; at the 16M-node
+        / 160M-pair size numpy's stable sort of 320M keys takes minutes)."""
         src = np.asarray(src, np.int64)
         dst = np.asarray(dst, np.int64)
         self.n_nodes = int(n_nodes)
-        ends = np.empty(2 * len(src), np.int64)   # adds in order: adj[a].add(b); adj[b].add(a)
-        other = np.empty(2 * len(src), np.int64)
+        small = self.n_nodes < (1 << 31)
+        kt = np.int32 if small else np.int64
+        ends = np.empty(2 * len(src), kt)   # adds in order: adj[a].add(b); adj[b].add(a)
+        other = np.empty(2 * len(src), kt)
         ends[0::2], other[0::2] = src, dst
         ends[1::2], other[1::2] = dst, src
-        order = np.argsort(ends, kind="stable")
+        if sort_device is None:
+            order = np.argsort(ends, kind="stable")
+        else:
+            keys = torch.from_numpy(ends).to(sort_device)
+            order = torch.sort(keys, stable=True)[1].cpu().numpy()
+            del keys
         self._ins = other[order]
+        del order
         self._ptr = np.zeros(self.n_nodes + 1, np.int64)
-        np.add.at(self._ptr, ends + 1, 1)
-        self._ptr = np.cumsum(self._ptr)
+        self._ptr[1:] = np.cumsum(np.bincount(ends, minlength=self.n_nodes))
         self._sets = {}
 
     def __getitem__(self, v):

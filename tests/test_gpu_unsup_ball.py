@@ -71,3 +71,31 @@ def test_device_balls_match_host(name, n_train_frac, num_neg, B):
         assert got[3] == want[3]
         np.testing.assert_array_equal(got[4][0], want[4][0])
         assert got[4][1] == want[4][1]
+
+
+@pytest.mark.parametrize("parts", ["extend", "negatives"])
+def test_device_balls_empty_batch_matches_host(parts):
+    """An empty node list on the device path (no launch, no division by the
+    empty word count) behaves as the host path: extend_nodes([]) reaches the
+    models.py:147 assertion; get_negtive_nodes([]) returns no pairs; the
+    stream is untouched either way."""
+    G_ = _graph("pubmed")
+    train = np.arange(0, G_.n_nodes, 2)
+    dev = U.UnsupervisedLoss(G_, train, torch.device("cuda", 0), n_threads=4, device_balls=True)
+    host = U.UnsupervisedLoss(G_, train, "cpu", n_threads=4)
+    res = []
+    for ul in (dev, host):
+        rng = gs.RNG(5)
+        ul.rng = rng
+        if parts == "extend":
+            with pytest.raises(AssertionError):
+                ul.extend_nodes([], num_neg=100)
+            res.append((list(ul.unique_nodes_batch), rng.getstate()))
+        else:
+            res.append((list(ul.get_negtive_nodes([], 100)), rng.getstate()))
+    assert res[0][0] == res[1][0]
+    np.testing.assert_array_equal(res[0][1][0], res[1][1][0])
+    assert res[0][1][1] == res[1][1][1]
+    # the device half still works after an empty batch
+    nodes = train[:64]
+    assert _outputs(dev, nodes, 100, 9)[0] == _outputs(host, nodes, 100, 9)[0]

@@ -1,0 +1,111 @@
+"""One node-wide host CSR shared by the rank processes.
+
+The replicated object is the reference's adjacency (dataCenter.py:33-41):
+local rank 0 builds it once and writes its flat image to /dev/shm
+(CSRGraph.write_image), every other rank maps that file read-only and adopts
+it without a copy (CSRGraph.from_image, gs_graph_from_image).  Two gloo ranks
+on CPU check that
+
+* both ranks see byte-identical CSR arrays;
+* the mapped graph samples exactly what a graph built locally from the same
+  pairs samples (bit-exact packs, same rng stream end state), on every rank's
+  own stream (train.rank_seed) and on a common one;
+* the non-zero rank's graph really is a view of the shared mapping.
+"""
+import hashlib
+import importlib
+import json
+import os
+import socket
+import tempfile
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+gs = importlib.import_module("graphsage-pytorch_amd")
+train = importlib.import_module("graphsage-pytorch_amd.train")
+
+SCALE, PAIRS, SEED, FAN, B = 15, 300_000, 824, [25, 10], 64
+
+
+def _build():
+    src, dst = gs.rmat_pairs(SCALE, PAIRS, seed=SEED, n_threads=2)
+    return gs.CSRGraph.from_pairs(src, dst, 1 << SCALE, n_threads=2)
+
+
+def _pack(graph, rng, roots):
+    s = gs.sample(graph, rng, roots, FAN)
+    buf = torch.zeros(s.pack_total, dtype=torch.int32)  # padding words zeroed: compare whole buffers
+    s.pack_into(buf)
+    return buf.numpy()
+
+
+def _digest(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def _worker(rank, world, port, shm_path, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = gs.CSRGraph.shared(_build, shm_path, local_rank=rank, barrier=dist.barrier)
+    mapped = hasattr(g, "_mapping")
+    csr = _digest(g.row_ptr(), g.col())
+    cands = np.nonzero(g.degrees() > 0)[0]
+    batches = list(train.rank_batches(cands, B, rank, world, SEED + 1000))[:3]
+    common = np.sort(cands)[:B]
+    own_rng, common_rng = train.make_rng(SEED, rank), gs.RNG(SEED)
+    packs = [_pack(g, own_rng, b) for b in batches] + [_pack(g, common_rng, common)]
+    ends = [own_rng.getstate(), common_rng.getstate()]
+    # the same draws on a graph built locally from the same pairs
+    local = _build()
+    lrng, lcommon = train.make_rng(SEED, rank), gs.RNG(SEED)
+    lpacks = [_pack(local, lrng, b) for b in batches] + [_pack(local, lcommon, common)]
+    same_as_local = (all(np.array_equal(a, b) for a, b in zip(packs, lpacks))
+                     and all(np.array_equal(a[0], b[0]) and a[1] == b[1]
+                             for a, b in zip(ends, [lrng.getstate(), lcommon.getstate()])))
+    rec = dict(csr=csr, mapped=mapped, same_as_local=bool(same_as_local), common=_digest(packs[-1]),
+               local_csr=_digest(local.row_ptr(), local.col()))
+    got = [None] * world
+    dist.all_gather_object(got, rec)
+    if rank == 0:
+        with open(os.path.join(out_dir, "records.json"), "w") as f:
+            json.dump(got, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shared_csr_is_one_image_and_samples_identically():
+    world = 2
+    port = _free_port()
+    shm_path = f"/dev/shm/gs_csr_test_{os.getpid()}_{port}.bin"
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            mp.spawn(_worker, args=(world, port, shm_path, d), nprocs=world, join=True)
+            with open(os.path.join(d, "records.json")) as f:
+                recs = json.load(f)
+    finally:
+        if os.path.exists(shm_path):
+            os.unlink(shm_path)
+    assert recs[0]["csr"] == recs[1]["csr"] == recs[0]["local_csr"] == recs[1]["local_csr"]
+    assert not recs[0]["mapped"] and recs[1]["mapped"]  # rank 0 built it, rank 1 maps the image
+    assert recs[0]["same_as_local"] and recs[1]["same_as_local"]
+    assert recs[0]["common"] == recs[1]["common"]  # one stream, one graph image: identical packs
+
+
+def test_image_rejects_garbage(tmp_path):
+    p = tmp_path / "bad.bin"
+    p.write_bytes(b"\0" * 4096)
+    import pytest
+    with pytest.raises(Exception):
+        gs.CSRGraph.from_image(str(p))
