@@ -675,6 +675,8 @@ def main():
     # cold window: nothing past the warmup batches sampled before t0, so the
     # window pays the pipeline fill (the first batch's whole sampling latency)
     cold_elapsed, cold_proof = timed_window(wait_sampled=False)
+    cst = runner.stats(reset=True)  # the cold window's host stats; the line's own are the steady window's
+    cold_proof.update(lookahead_misses=cst["lookahead_misses"], max_step_ms=round(1e3 * cst["max_step_s"], 3))
     # steady window (`value`): straight after it, the pipeline running as in
     # any later step of a training run; the clock stops only once the window
     # has also sampled as many new batches as it consumed, so the sampling

@@ -48,55 +48,47 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
     return y;
 }
 
-// One wave extends the stream from c->gen_end until it covers `need`
+// One block extends the stream from c->gen_end until it covers `need`
 // (absolute word index, exclusive): stages of 227 words, each word
 // x[A] = x[A-227] ^ ((y >> 1) ^ (y & 1 ? MATRIX_A : 0)), y = (x[A-624] & UPPER)
 // | (x[A-623] & LOWER) — CPython's twist loop written on absolute indices (its
-// three index ranges are this one recurrence).  Lane l owns the residues
-// l, l+64, l+128, l+192 (< 227) of A - g0 mod 227, so x[A-227] is the lane's
-// own previous value (a register) and x[A-624], x[A-623] were written to the
-// LDS ring three stages ago: no dependent LDS round trip per stage.  Every word
-// goes to both rings (raw for the state, tempered for the draws).
-__global__ __launch_bounds__(64) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr, Ctl* c,
-                                                    int64_t need_fixed, int need_hop) {
+// three index ranges are this one recurrence).  Thread i < 227 owns residue i
+// of A - g0 mod 227, so x[A-227] is its own previous value (a register); the
+// two older words were written to the LDS ring at least two stages earlier
+// (A-623 <= g-397), so one barrier per stage orders every read after its
+// write.  Only the tempered words go to global memory (what the draws read);
+// the raw words the next launch and getstate need are the last 624, written
+// once at the end.
+constexpr int kGenThreads = 256;
+__global__ __launch_bounds__(kGenThreads) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr,
+                                                             Ctl* c, int64_t need_fixed, int need_hop) {
     __shared__ uint32_t L[1024];
-    const int lane = threadIdx.x;
+    const int i = threadIdx.x;
     const int64_t g0 = c->gen_end;
     const int64_t need = need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
     if (g0 >= need) return;
-    for (int i = lane; i < 624; i += 64) {
-        const int64_t A = g0 - 624 + i;
+    for (int q = i; q < 624; q += kGenThreads) {
+        const int64_t A = g0 - 624 + q;
         L[A & 1023] = xr[A & kRingMask];
     }
     __syncthreads();
-    uint32_t prev[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int i = lane + 64 * q;
-        prev[q] = i < 227 ? L[(g0 - 227 + i) & 1023] : 0u;
-    }
+    uint32_t prev = i < 227 ? L[(g0 - 227 + i) & 1023] : 0u;
     int64_t g = g0;
     while (g < need) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int i = lane + 64 * q;
-            if (i < 227) {
-                const int64_t A = g + i;
-                const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023];
-                const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-                const uint32_t x = prev[q] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-                prev[q] = x;
-                L[A & 1023] = x;
-                xr[A & kRingMask] = x;
-                wr[A & kRingMask] = temper(x);
-            }
+        if (i < 227) {
+            const int64_t A = g + i;
+            const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023];
+            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+            const uint32_t x = prev ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+            prev = x;
+            L[A & 1023] = x;
+            xr[A & kRingMask] = x;
+            wr[A & kRingMask] = temper(x);
         }
-        // x[A-623] of the next stage's last word is this stage's first word (A-623
-        // = g+227+226-623 = g-170 <  g: written two stages ago) — every read is
-        // at least 170 words back, so one wave's in-order LDS traffic suffices
+        __syncthreads();
         g += 227;
     }
-    if (lane == 0) c->gen_end = g;
+    if (i == 0) c->gen_end = g;
 }
 
 // Seed the stream from random.setstate's (mt[624], pos): block 0 = mt, the
@@ -134,6 +126,8 @@ __device__ __forceinline__ void rejection_moments(uint32_t d, int k, int setsize
     }
 }
 
+constexpr int kSetupBatch = 8;
+
 // Per hop, one 1024-thread block: degrees of the frontier, the scans of the
 // sampled counts (pos_ptr) and draw counts, the rejection-count windows of
 // the blocks, the word need of the hop, and (last hop) the pack offsets.
@@ -152,11 +146,24 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
     const int r0 = min(n, static_cast<int>(threadIdx.x) * per), r1 = min(n, r0 + per);
     int cnt_sum = 0, draw_sum = 0;
     float mean_sum = 0.f, var_sum = 0.f;
+    // degrees, kSetupBatch nodes at a time: every id, then every row_ptr pair,
+    // loaded before any is used (independent loads in flight together)
+    for (int rb = r0; rb < r1; rb += kSetupBatch) {
+        int32_t vv[kSetupBatch];
+        int64_t lo[kSetupBatch], hi[kSetupBatch];
+#pragma unroll
+        for (int q = 0; q < kSetupBatch; ++q) vv[q] = rb + q < r1 ? hb.dst[rb + q] : 0;
+#pragma unroll
+        for (int q = 0; q < kSetupBatch; ++q) {
+            lo[q] = rb + q < r1 ? g.row_ptr[vv[q]] : 0;
+            hi[q] = rb + q < r1 ? g.row_ptr[vv[q] + 1] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < kSetupBatch; ++q)
+            if (rb + q < r1) hb.deg[rb + q] = static_cast<int32_t>(hi[q] - lo[q]);
+    }
     for (int r = r0; r < r1; ++r) {
-        const int32_t v = hb.dst[r];
-        const int64_t d64 = g.row_ptr[v + 1] - g.row_ptr[v];
-        const int32_t d = static_cast<int32_t>(d64);
-        hb.deg[r] = d;
+        const int32_t d = hb.deg[r];
         const bool sampled = k > 0 && d >= k;
         cnt_sum += sampled ? k : d;
         draw_sum += sampled ? k : 0;
@@ -698,6 +705,7 @@ struct gs_dsampler {
     UnionBufs ub[GS_MAX_HOPS];
     int32_t* pack_cur = nullptr;
     uint64_t* mark = nullptr;  // first-occurrence marks of the frontier unions (shared by the hops)
+    int32_t* lid = nullptr;    // union key -> frontier position (shared by the hops)
     hipEvent_t done = nullptr;
     hipStream_t last_stream = nullptr;
     bool ran = false;
@@ -727,7 +735,7 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     const HopBufs& hb = ds->hb[hop];
     hop_setup_kernel<<<1, 1024, 0, st>>>(ds->g, ds->ctl, hb, hop, k, setsize, R, last ? 1 : 0, n_roots, gcn);
     gs::check_launch("hop_setup_kernel");
-    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
+    mt_gen_kernel<<<1, kGenThreads, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
     gs::check_launch("mt_gen_kernel");
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
     const size_t tab_lds = (R + 2 * kWMax) * sizeof(int32_t) + kWMax * sizeof(uint16_t) +
@@ -861,11 +869,14 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
             u.ubef = ds->alloc<int32_t>(ndj + 1);
             u.fresh = ds->alloc<int32_t>(ds->npos_max[j] + ndj);
             u.tcnt = ds->alloc<int32_t>(ds->nd_max[j + 1] + 1);
+            u.fmask = ds->alloc<uint64_t>(ndj);
             if (!ds->mark) {
                 ds->mark = ds->alloc<uint64_t>(g.n_nodes);
                 hip_ok(hipMemset(ds->mark, 0, g.n_nodes * sizeof(uint64_t)), "hipMemset(mark)");
+                ds->lid = ds->alloc<int32_t>(g.n_nodes);
             }
             u.mark = ds->mark;
+            u.lid = ds->lid;
         }
     }
     hip_ok(hipEventCreateWithFlags(&ds->done, hipEventDisableTiming), "hipEventCreate");
@@ -905,7 +916,7 @@ int gs_dsampler_get_rng(gs_dsampler* ds, uint32_t* mt624, int64_t* pos, void* st
         blk -= 1;
         idx = 624;
     }
-    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, 624 * (blk + 1), -1);
+    mt_gen_kernel<<<1, kGenThreads, 0, st>>>(ds->xr, ds->wr, ds->ctl, 624 * (blk + 1), -1);
     gs::check_launch("mt_gen_kernel");
     ensure_tmp(ds, 624);
     copy_block_kernel<<<1, 256, 0, st>>>(ds->xr, 624 * blk, ds->tmp);
@@ -922,7 +933,7 @@ int gs_dsampler_words(gs_dsampler* ds, int64_t n, uint32_t* out, void* stream) {
     hipStream_t st = gs::as_stream(stream);
     if (ds->ran) hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
     const int64_t p = pos_now(ds, st);
-    mt_gen_kernel<<<1, 64, 0, st>>>(ds->xr, ds->wr, ds->ctl, p + n, -1);
+    mt_gen_kernel<<<1, kGenThreads, 0, st>>>(ds->xr, ds->wr, ds->ctl, p + n, -1);
     gs::check_launch("mt_gen_kernel");
     ensure_tmp(ds, n);
     copy_words_kernel<<<64, 256, 0, st>>>(ds->wr, p, n, ds->tmp);

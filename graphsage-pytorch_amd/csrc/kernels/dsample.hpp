@@ -80,6 +80,8 @@ struct UnionBufs {
     int32_t* ubef;             // union size before run r, [nd_max]
     int32_t* fresh;            // keys new to the union, in insertion order, [npos_max + nd_max]
     int32_t* tcnt;             // transposed counts / cursors, [nd_next_max + 1]
+    uint64_t* fmask;           // per run: bit q = item q is new to the union, [nd_max]
+    int32_t* lid;              // [n_nodes]: a union key's position in the next frontier (this hop's keys only)
 };
 
 constexpr int kSmallSet = 128;      // table slots of one samp_neighs set (k <= 32)

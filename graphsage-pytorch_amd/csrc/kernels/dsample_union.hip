@@ -36,8 +36,10 @@ namespace ds {
 
 namespace {
 
-constexpr int kLaneSet = kSmallSet + 40;  // table + resize scratch per lane (ints)
-constexpr int kMaxItems = 33;             // |samp_neighs[r]| <= k + 1 <= 33
+constexpr int kTmpSet = 40;                         // resize scratch per lane (ints)
+constexpr int kMaxK = 32;                           // fanouts of hops before the last
+constexpr int kLaneSet = kSmallSet + kTmpSet + kMaxK;  // table + scratch + staged sample ids per lane
+constexpr int kMaxItems = 33;                       // |samp_neighs[r]| <= k + 1 <= 33
 
 __device__ __forceinline__ void ps_clear(int32_t* T, uint32_t n) {
     for (uint32_t i = 0; i < n; ++i) T[i] = -1;
@@ -136,13 +138,22 @@ __global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb
     const int n = c->hop[hop].n_dst;
     if (r >= n) return;
     LSet s{lds + threadIdx.x * kLaneSet, lds + threadIdx.x * kLaneSet + kSmallSet, 7, 0};
+    int32_t* keys = lds + threadIdx.x * kLaneSet + kSmallSet + kTmpSet;  // the sample's ids, staged
     ps_clear(s.T, 8);
     const int32_t v = hb.dst[r];
     const int d = hb.deg[r];
     if (k > 0 && d >= k) {
-        // set(random.sample(...)) in result order, then the copy that `|` makes
+        // set(random.sample(...)) in result order, then the copy that `|` makes.
+        // Every id is fetched before the first insert (independent loads in
+        // flight together, not one dependent pair per add).
         const int32_t* ent = hb.ent + hb.pos_ptr[r];
-        for (int i = 0; i < k; ++i) ls_add(s, g.col[ent[i]]);
+        int32_t e[kMaxK];
+#pragma unroll
+        for (int i = 0; i < kMaxK; ++i) e[i] = i < k ? ent[i] : 0;
+#pragma unroll
+        for (int i = 0; i < kMaxK; ++i)
+            if (i < k) keys[i] = g.col[e[i]];
+        for (int i = 0; i < k; ++i) ls_add(s, keys[i]);
         uint32_t nm = 7;
         if (s.used * 5 >= 21) nm = mask_for(2 * s.used);
         if (nm != s.mask) {
@@ -182,16 +193,47 @@ __global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb
     } else {
         ls_add(s, v);
     }
+    // the set in iteration order, and each item's first-occurrence mark for
+    // the frontier union (union.hip header): run 0's keys are in the union
+    // from the start (never new); item q of run r >= 1 has merge-order key
+    // t = pos_ptr[r] + r + q (increasing in merge order), the largest mark
+    // value is the earliest occurrence
+    const uint64_t E = static_cast<uint64_t>(static_cast<uint32_t>(c->epoch + 1)) << 32;
+    const uint32_t t0 = static_cast<uint32_t>(hb.pos_ptr[r] + r);
     int32_t* out = ub.set_items + hb.pos_ptr[r] + r;
     int q = 0;
     for (uint32_t i = 0; i <= s.mask; ++i)
-        if (s.T[i] != -1) out[q++] = s.T[i];
+        if (s.T[i] != -1) {
+            const int32_t key = s.T[i];
+            out[q] = key;
+            atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[key]),
+                      static_cast<unsigned long long>(E | (r == 0 ? 0xFFFFFFFFu : 0xFFFFFFFEu - (t0 + q))));
+            ++q;
+        }
     ub.set_cnt[r] = s.used;
     if (r == 0) {
         for (uint32_t i = 0; i <= s.mask; ++i) ub.first_tab[i] = s.T[i];
         ub.first_meta[0] = static_cast<int32_t>(s.mask);
         ub.first_meta[1] = s.used;
     }
+}
+
+// Per run r >= 1 (one wave, lane q = item q): the items new to the union —
+// those whose mark is their own (the union's first occurrence of the key).
+__global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBufs ub, int hop) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    if (r >= c->hop[hop].n_dst) return;
+    const uint64_t E = static_cast<uint64_t>(static_cast<uint32_t>(c->epoch + 1)) << 32;
+    const int cn = ub.set_cnt[r];
+    bool fresh = false;
+    if (r > 0 && lane < cn) {
+        const uint32_t t = static_cast<uint32_t>(hb.pos_ptr[r] + r + lane);
+        const int32_t key = ub.set_items[hb.pos_ptr[r] + r + lane];
+        fresh = __hip_atomic_load(&ub.mark[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                (E | (0xFFFFFFFEu - t));
+    }
+    const uint64_t m = __ballot(fresh);
+    if (lane == 0) ub.fmask[r] = m;
 }
 
 // Priority-displacement insertion of the keys this thread owns (on[q]) into
@@ -231,89 +273,55 @@ __device__ __forceinline__ void settle(uint32_t* T, uint32_t mask, const int32_t
     }
 }
 
-__device__ __forceinline__ uint32_t find_slot(const uint32_t* T, uint32_t mask, int32_t key) {
-    uint32_t ps = pr_init(key, mask);
-    for (int guard = 0; guard < 4 * kUnionMax; ++guard) {
-        const uint32_t s = pr_slot(ps);
-        if (T[s] == static_cast<uint32_t>(key)) return s;
-        ps = pr_next(ps, key, mask);
-    }
-    return 0;
-}
-
-__global__ __launch_bounds__(1024) void union_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop,
-                                                     int gcn, int32_t* __restrict__ pack, int nd_next_max) {
+// The union's table (one block, LDS): the runs' new keys in merge order,
+// the resize schedule, the stages, then the next frontier in slot order and
+// each key's position in it (lid), the pack layout of this hop.
+__global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop,
+                                                      int gcn, int32_t* __restrict__ pack, int nd_next_max) {
     extern __shared__ uint32_t T[];
-    uint16_t* rank = reinterpret_cast<uint16_t*>(T + kUnionMax);
     __shared__ int shi[17];
-    __shared__ uint64_t s_epoch;
     __shared__ int st_run[kMaxStages + 1];
     __shared__ uint32_t st_mask[kMaxStages];
-    __shared__ int s_nst, s_best, s_bad;
+    __shared__ int s_nst, s_best, s_bad, s_epoch;
     HopCtl& h = c->hop[hop];
     const int n = h.n_dst;
     const int tid = threadIdx.x;
     const int used0 = ub.set_cnt[0];
     const uint32_t m_first = static_cast<uint32_t>(ub.first_meta[0]);
     if (tid == 0) {
-        const int e = c->epoch + 1;
-        c->epoch = e;
-        s_epoch = static_cast<uint64_t>(static_cast<uint32_t>(e)) << 32;
+        s_epoch = c->epoch + 1;
         s_bad = 0;
     }
-    // runs 1..n-1 in contiguous chunks, one per thread
+    // runs 1..n-1 in contiguous chunks, one per thread: item and new-key counts
     const int per = (n - 1 + 1023) / 1024;
     const int ra = min(n, 1 + tid * per), rb = min(n, ra + per);
-    int my_items = 0;
-    for (int r = ra; r < rb; ++r) my_items += ub.set_cnt[r];
-    int items_tot;
-    int t0 = block_excl_scan(my_items, shi, &items_tot);  // also a barrier (s_epoch visible)
-    const uint64_t E = s_epoch;
-    {
-        int t = t0;
-        for (int r = ra; r < rb; ++r) {
-            ub.tpre[r] = t;
-            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
-            const int cn = ub.set_cnt[r];
-            for (int q = 0; q < cn; ++q, ++t)
-                atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[it[q]]),
-                          static_cast<unsigned long long>(E | (0xFFFFFFFEu - static_cast<uint32_t>(t))));
-        }
-        if (tid == 0) {
-            ub.tpre[0] = 0;
-            ub.tpre[n] = items_tot;
-        }
-        for (int q = tid; q < used0; q += 1024)
-            atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[ub.set_items[q]]),
-                      static_cast<unsigned long long>(E | 0xFFFFFFFFu));
+    int my_items = 0, my_fresh = 0;
+    for (int r = ra; r < rb; ++r) {
+        my_items += ub.set_cnt[r];
+        my_fresh += __popcll(ub.fmask[r]);
     }
-    __threadfence();
-    __syncthreads();
-    auto is_fresh = [&](int32_t key, int t) {
-        const uint64_t m = __hip_atomic_load(&ub.mark[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return m == (E | (0xFFFFFFFEu - static_cast<uint32_t>(t)));
-    };
-    int my_fresh = 0;
-    {
-        int t = t0;
-        for (int r = ra; r < rb; ++r) {
-            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
-            const int cn = ub.set_cnt[r];
-            for (int q = 0; q < cn; ++q, ++t) my_fresh += is_fresh(it[q], t);
-        }
-    }
-    int fresh_tot;
+    int items_tot, fresh_tot;
+    int tp = block_excl_scan(my_items, shi, &items_tot);
     int f = block_excl_scan(my_fresh, shi, &fresh_tot);
-    {
-        int t = t0;
-        for (int r = ra; r < rb; ++r) {
-            ub.ubef[r] = used0 + f;
-            const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
-            const int cn = ub.set_cnt[r];
-            for (int q = 0; q < cn; ++q, ++t)
-                if (is_fresh(it[q], t)) ub.fresh[f++] = it[q];
-        }
-        if (tid == 0) ub.ubef[n] = used0 + fresh_tot;
+    for (int r = ra; r < rb; ++r) {
+        ub.tpre[r] = tp;
+        ub.ubef[r] = used0 + f;
+        // this run's new keys at their merge-order place (all loads first)
+        const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
+        const int cn = ub.set_cnt[r];
+        const uint64_t fm = ub.fmask[r];
+        int32_t key[kMaxItems];
+#pragma unroll
+        for (int q = 0; q < kMaxItems; ++q) key[q] = ((fm >> q) & 1) ? it[q] : 0;
+#pragma unroll
+        for (int q = 0; q < kMaxItems; ++q)
+            if ((fm >> q) & 1) ub.fresh[f++] = key[q];
+        tp += cn;
+    }
+    if (tid == 0) {
+        ub.tpre[0] = 0;
+        ub.tpre[n] = items_tot;
+        ub.ubef[n] = used0 + fresh_tot;
     }
     __threadfence_block();
     __syncthreads();
@@ -410,7 +418,7 @@ __global__ __launch_bounds__(1024) void union_kernel(Ctl* c, HopBufs hb, UnionBu
         if (tid == 0) c->status |= kStTable;
         return;
     }
-    // the next frontier: keys in slot order, and each slot's rank
+    // the next frontier: keys in slot order, each key's position (lid)
     const uint32_t mf = prev_mask;
     const int sper = static_cast<int>((mf + 1 + 1023) / 1024);
     const uint32_t sa = min<uint32_t>(mf + 1, tid * sper), sb = min<uint32_t>(mf + 1, sa + sper);
@@ -424,15 +432,15 @@ __global__ __launch_bounds__(1024) void union_kernel(Ctl* c, HopBufs hb, UnionBu
     }
     for (uint32_t i = sa; i < sb; ++i)
         if (T[i] != 0xFFFFFFFFu) {
-            rank[i] = static_cast<uint16_t>(rk);
+            ub.lid[T[i]] = rk;
             next.dst[rk++] = static_cast<int32_t>(T[i]);
         }
     // pack layout of this hop
     const int g1 = gcn ? 0 : 1;
     const int n_nbr = used0 + items_tot - n * g1;
-    __shared__ int off[GS_PK_NFIELDS];
     if (tid == 0) {
         int at = c->total;
+        int off[GS_PK_NFIELDS];
         off[GS_PK_NBR_PTR] = at;
         at += al4(n + 1);
         off[GS_PK_NBR] = at;
@@ -444,40 +452,39 @@ __global__ __launch_bounds__(1024) void union_kernel(Ctl* c, HopBufs hb, UnionBu
         off[GS_PK_TIDX] = at;
         at += al4(n_nbr + n);
         c->total = at;
-        for (int f = 0; f < GS_PK_NFIELDS; ++f) h.off[f] = (f >= GS_PK_NBR_PTR) ? off[f] : -1;
+        for (int f2 = 0; f2 < GS_PK_NFIELDS; ++f2) h.off[f2] = (f2 >= GS_PK_NBR_PTR) ? off[f2] : -1;
         h.n_src = n_src;
         h.n_nbr = n_nbr;
         pack[off[GS_PK_NBR_PTR] + n] = n_nbr;
-    }
-    __syncthreads();
-    // neighbourhoods in frontier-local ids, ascending (the dense mask's
-    // column order, models.py:305-308); non-gcn drops self (:297-298)
-    for (int r = tid; r < n; r += 1024) {
-        const int32_t v = hb.dst[r];
-        const int32_t* it = ub.set_items + hb.pos_ptr[r] + r;
-        const int cn = ub.set_cnt[r];
-        const int base = r == 0 ? 0 : used0 + ub.tpre[r] - r * g1;
-        int loc[kMaxItems];
-#pragma unroll
-        for (int q = 0; q < kMaxItems; ++q) {
-            loc[q] = INT_MAX;
-            if (q < cn) {
-                const int32_t kk = it[q];
-                if (!(g1 && kk == v)) loc[q] = rank[find_slot(T, mf, kk)];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kMaxItems; ++q) {
-            if (loc[q] == INT_MAX) continue;
-            int pos = 0;
-#pragma unroll
-            for (int p = 0; p < kMaxItems; ++p) pos += loc[p] < loc[q];
-            pack[off[GS_PK_NBR] + base + pos] = loc[q];
-        }
-        pack[off[GS_PK_NBR_PTR] + r] = base;
-        pack[off[GS_PK_SELF] + r] = rank[find_slot(T, mf, v)];
+        c->epoch = s_epoch;  // every kernel of this hop read epoch + 1 before this launch's end
     }
     for (int i = tid; i <= n_src; i += 1024) ub.tcnt[i] = 0;
+}
+
+// Per run (one wave, lane q = item q): the destination's neighbourhood in
+// frontier-local ids, ascending (the dense mask's column order,
+// models.py:305-308; non-gcn drops self, :297-298), and its self id.
+__global__ __launch_bounds__(64) void uout_kernel(Ctl* c, HopBufs hb, UnionBufs ub, int hop, int gcn,
+                                                  int32_t* __restrict__ pack) {
+    const HopCtl& h = c->hop[hop];
+    const int r = blockIdx.x, lane = threadIdx.x;
+    if (r >= h.n_dst || h.n_src < 0 || (c->status & (kStTable | kStSize))) return;
+    const int g1 = gcn ? 0 : 1;
+    const int32_t v = hb.dst[r];
+    const int cn = ub.set_cnt[r];
+    const int32_t key = lane < cn ? ub.set_items[hb.pos_ptr[r] + r + lane] : -1;
+    const bool keep = lane < cn && !(g1 && key == v);
+    const int loc = keep ? ub.lid[key] : INT_MAX;
+    int pos = 0;
+#pragma unroll
+    for (int p = 0; p < kMaxItems; ++p) pos += __shfl(loc, p, 64) < loc;
+    const int used0 = ub.set_cnt[0];
+    const int base = r == 0 ? 0 : used0 + ub.tpre[r] - r * g1;
+    if (keep) pack[h.off[GS_PK_NBR] + base + pos] = loc;
+    if (lane == 0) {
+        pack[h.off[GS_PK_NBR_PTR] + r] = base;
+        pack[h.off[GS_PK_SELF] + r] = ub.lid[v];
+    }
 }
 
 // ---- transposed lists (GS_PK_TPTR / GS_PK_TIDX)
@@ -547,18 +554,22 @@ __global__ void tsort_kernel(Ctl* c, int hop, int32_t* __restrict__ pack) {
 void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& ub, const HopBufs& next, int hop,
                       int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st) {
     static const bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(union_kernel),
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(ublock_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kUnionMax * (sizeof(uint32_t) + sizeof(uint16_t))) == hipSuccess;
+                                   kUnionMax * sizeof(uint32_t)) == hipSuccess;
     }();
-    if (!attr) fail(GS_EHIP, "union_kernel: cannot raise its LDS limit");
+    if (!attr) fail(GS_EHIP, "ublock_kernel: cannot raise its LDS limit");
     const int gcn = (flags & GS_SAMPLE_GCN) ? 1 : 0;
     const unsigned nb64 = static_cast<unsigned>((nd_max + 63) / 64);
     sets_kernel<<<nb64, 64, 64 * kLaneSet * sizeof(int32_t), st>>>(g, c, hb, ub, hop, k);
     check_launch("sets_kernel");
-    union_kernel<<<1, 1024, kUnionMax * (sizeof(uint32_t) + sizeof(uint16_t)), st>>>(
-        c, hb, ub, next, hop, gcn, pack, static_cast<int>(nd_next_max));
-    check_launch("union_kernel");
+    ufresh_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop);
+    check_launch("ufresh_kernel");
+    ublock_kernel<<<1, 1024, kUnionMax * sizeof(uint32_t), st>>>(c, hb, ub, next, hop, gcn, pack,
+                                                                   static_cast<int>(nd_next_max));
+    check_launch("ublock_kernel");
+    uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);
+    check_launch("uout_kernel");
     const unsigned nb256 = static_cast<unsigned>((nd_max + 255) / 256);
     tcount_kernel<<<nb256, 256, 0, st>>>(c, hop, pack, ub.tcnt);
     check_launch("tcount_kernel");
