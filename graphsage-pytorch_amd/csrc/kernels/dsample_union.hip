@@ -27,8 +27,8 @@
 //                 Then: the frontier in slot order, each destination's
 //                 neighbourhood in frontier-local ids (ascending), its self id.
 //   t*_kernels    the transposed lists (per source, ascending destination;
-//                 self entries -(r+1) first), counted, scanned, scattered and
-//                 sorted per source.
+//                 self entries -(r+1) first), counted (in uout_kernel),
+//                 scanned, scattered and sorted per source.
 #include "dsample.hpp"
 
 namespace gs {
@@ -38,7 +38,9 @@ namespace {
 
 constexpr int kTmpSet = 40;                         // resize scratch per lane (ints)
 constexpr int kMaxK = 32;                           // fanouts of hops before the last
-constexpr int kLaneSet = kSmallSet + kTmpSet + kMaxK;  // table + scratch + staged sample ids per lane
+// table + scratch + staged sample ids per lane; odd, so the lanes' tables
+// start in different LDS banks
+constexpr int kLaneSet = kSmallSet + kTmpSet + kMaxK + 1;
 constexpr int kMaxItems = 33;                       // |samp_neighs[r]| <= k + 1 <= 33
 
 __device__ __forceinline__ void ps_clear(int32_t* T, uint32_t n) {
@@ -238,26 +240,22 @@ __global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBuf
 
 // Priority-displacement insertion of the keys this thread owns (on[q]) into
 // the LDS table T (all slots EMPTY or holding priorities); returns when every
-// key of the block sits in its final slot.  Rounds: every unplaced key walks
-// its probe sequence until it wins a slot; then every key checks it still
-// holds its slot (a higher-priority key may have taken it) and, if not,
-// steps past it — so rounds follow displacement chains, not probe lengths.
+// key of the block sits in its final slot.  Each round every unplaced key
+// claims ONE slot — its current probe slot — with an atomicMin of its
+// priority (the claims of a thread's keys are independent, so they issue
+// back to back), then every key checks that it still holds its slot; a key
+// that lost it (to a higher priority, now or in an earlier round) steps to
+// its next probe slot.  A slot's value only decreases, so a key never has to
+// revisit a slot it left: the assignment converges to the sequential one.
 __device__ __forceinline__ void settle(uint32_t* T, uint32_t mask, const int32_t (&key)[kKPT],
                                        const uint32_t (&prio)[kKPT], uint32_t (&ps)[kKPT], const bool (&on)[kKPT]) {
     bool placed[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) placed[q] = false;
     for (;;) {
-        // claim: walk the probe sequence until a slot is won (empty, or held
-        // by a lower-priority key, which notices below and moves on)
 #pragma unroll
         for (int q = 0; q < kKPT; ++q)
-            if (on[q] && !placed[q])
-                for (;;) {
-                    const uint32_t old = atomicMin(&T[pr_slot(ps[q])], prio[q]);
-                    if (old > prio[q]) break;
-                    ps[q] = pr_next(ps[q], key[q], mask);
-                }
+            if (on[q] && !placed[q]) atomicMin(&T[pr_slot(ps[q])], prio[q]);
         __syncthreads();
         int any = 0;
 #pragma unroll
@@ -480,23 +478,19 @@ __global__ __launch_bounds__(64) void uout_kernel(Ctl* c, HopBufs hb, UnionBufs 
     for (int p = 0; p < kMaxItems; ++p) pos += __shfl(loc, p, 64) < loc;
     const int used0 = ub.set_cnt[0];
     const int base = r == 0 ? 0 : used0 + ub.tpre[r] - r * g1;
-    if (keep) pack[h.off[GS_PK_NBR] + base + pos] = loc;
+    if (keep) {
+        pack[h.off[GS_PK_NBR] + base + pos] = loc;
+        atomicAdd(&ub.tcnt[loc], 1);  // the transposed lists' counts (tscan_kernel)
+    }
     if (lane == 0) {
+        const int sl = ub.lid[v];
         pack[h.off[GS_PK_NBR_PTR] + r] = base;
-        pack[h.off[GS_PK_SELF] + r] = ub.lid[v];
+        pack[h.off[GS_PK_SELF] + r] = sl;
+        atomicAdd(&ub.tcnt[sl], 1);
     }
 }
 
 // ---- transposed lists (GS_PK_TPTR / GS_PK_TIDX)
-
-__global__ void tcount_kernel(Ctl* c, int hop, const int32_t* __restrict__ pack, int32_t* tcnt) {
-    const HopCtl& h = c->hop[hop];
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= h.n_dst || h.n_src <= 0) return;
-    atomicAdd(&tcnt[pack[h.off[GS_PK_SELF] + r]], 1);
-    const int32_t* np = pack + h.off[GS_PK_NBR_PTR];
-    for (int e = np[r]; e < np[r + 1]; ++e) atomicAdd(&tcnt[pack[h.off[GS_PK_NBR] + e]], 1);
-}
 
 __global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
     __shared__ int shi[17];
@@ -519,14 +513,17 @@ __global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* _
     if (threadIdx.x == 0) tp[ns] = tot;
 }
 
-__global__ void tfill_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
+// One wave per destination r: its self entry -(r+1) and its neighbour
+// entries r at the sources' cursors (order fixed by tsort_kernel).
+__global__ __launch_bounds__(64) void tfill_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
     const HopCtl& h = c->hop[hop];
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.x, lane = threadIdx.x;
     if (r >= h.n_dst || h.n_src <= 0) return;
     int32_t* tidx = pack + h.off[GS_PK_TIDX];
-    tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_SELF] + r]], 1)] = -(r + 1);
     const int32_t* np = pack + h.off[GS_PK_NBR_PTR];
-    for (int e = np[r]; e < np[r + 1]; ++e) tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_NBR] + e]], 1)] = r;
+    const int e0 = np[r], e1 = np[r + 1];
+    if (lane == 0) tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_SELF] + r]], 1)] = -(r + 1);
+    for (int e = e0 + lane; e < e1; e += 64) tidx[atomicAdd(&tcnt[pack[h.off[GS_PK_NBR] + e]], 1)] = r;
 }
 
 // per source: ascending destination, a destination's self entry before its
@@ -570,12 +567,9 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     check_launch("ublock_kernel");
     uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);
     check_launch("uout_kernel");
-    const unsigned nb256 = static_cast<unsigned>((nd_max + 255) / 256);
-    tcount_kernel<<<nb256, 256, 0, st>>>(c, hop, pack, ub.tcnt);
-    check_launch("tcount_kernel");
     tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt);
     check_launch("tscan_kernel");
-    tfill_kernel<<<nb256, 256, 0, st>>>(c, hop, pack, ub.tcnt);
+    tfill_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hop, pack, ub.tcnt);
     check_launch("tfill_kernel");
     tsort_kernel<<<static_cast<unsigned>((nd_next_max + 255) / 256), 256, 0, st>>>(c, hop, pack);
     check_launch("tsort_kernel");
