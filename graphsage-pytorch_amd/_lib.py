@@ -158,6 +158,7 @@ _SIGS = {
     "gs_dsampler_pack_bound": (_i64, [_vp, _i64]),
     "gs_dsampler_run": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
     "gs_dsampler_result": (_i32, [_vp, _vp, _vp, _p(_i64)]),
+    "gs_dsampler_debug": (_i32, [_vp, _vp, _i32]),
 }
 
 

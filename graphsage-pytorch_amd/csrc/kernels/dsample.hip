@@ -972,6 +972,14 @@ int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int3
     GS_API_END
 }
 
+int gs_dsampler_debug(gs_dsampler* ds, int64_t* out, int32_t n) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && ds->ran && out && n >= 0 && n <= 64, GS_EINVAL, "bad arguments");
+    hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    std::memcpy(out, ds->ctl_host->dbg, n * sizeof(int64_t));
+    GS_API_END
+}
+
 int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
     GS_API_BEGIN
     GS_REQUIRE(ds && ds->ran, GS_EINVAL, "no run to report");

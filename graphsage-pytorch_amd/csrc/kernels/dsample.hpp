@@ -52,6 +52,7 @@ struct Ctl {
     int32_t total;             // pack elements before the roots
     int32_t used;
     HopCtl hop[GS_MAX_HOPS];
+    int64_t dbg[64];           // diagnostics of the last run (gs_dsampler_debug)
 };
 
 struct HopBufs {

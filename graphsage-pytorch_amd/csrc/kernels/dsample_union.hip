@@ -128,9 +128,13 @@ __device__ __forceinline__ uint32_t pr_next(uint32_t ps, int32_t key, uint32_t m
     return i | (steps << 20);
 }
 
-constexpr int kOldPT = kUnionMax / 2 / 1024;          // previous-table slots per thread
-constexpr int kFreshPT = (kUnionMax * 3 / 5) / 1024 + 1;  // new keys per thread per stage
-constexpr int kKPT = kOldPT + kFreshPT;
+// Keys of one stage, densely indexed in priority order (the previous table's
+// keys in slot order, then the stage's new keys in merge order): key t is
+// thread t % 1024's q-th key (q = t / 1024), and t is its priority.  A stage's
+// table is at most 3/5 full, so kKPT keys per thread cover kUnionMax slots.
+constexpr int kKPT = (kUnionMax * 3 / 5) / 1024 + 1;
+constexpr int kStageKeys = kKPT * 1024;
+constexpr size_t kUnionLds = (kUnionMax + kStageKeys) * sizeof(uint32_t);  // table + a stage's old keys
 
 }  // namespace
 
@@ -238,37 +242,49 @@ __global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBuf
     if (lane == 0) ub.fmask[r] = m;
 }
 
-// Priority-displacement insertion of the keys this thread owns (on[q]) into
-// the LDS table T (all slots EMPTY or holding priorities); returns when every
-// key of the block sits in its final slot.  Each round every unplaced key
-// claims ONE slot — its current probe slot — with an atomicMin of its
-// priority (the claims of a thread's keys are independent, so they issue
-// back to back), then every key checks that it still holds its slot; a key
-// that lost it (to a higher priority, now or in an earlier round) steps to
-// its next probe slot.  A slot's value only decreases, so a key never has to
-// revisit a slot it left: the assignment converges to the sequential one.
-__device__ __forceinline__ void settle(uint32_t* T, uint32_t mask, const int32_t (&key)[kKPT],
-                                       const uint32_t (&prio)[kKPT], uint32_t (&ps)[kKPT], const bool (&on)[kKPT]) {
+// Priority-displacement insertion of this thread's keys (t = tid + 1024 q <
+// nk, priority t) into the LDS table T (every slot EMPTY or holding a
+// priority); returns the rounds once every key sits in its final slot.  In a
+// round every unplaced key walks its probe sequence until it wins a slot — an
+// empty one, or one held by a lower priority (whose key notices below and
+// moves on); then every key checks it still holds its slot and, if not, steps
+// past it.  A slot's value only decreases, so no key revisits a slot it left,
+// and the assignment converges to the sequential one (the highest priority
+// always keeps its first free slot, and by induction every later key).
+__device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const int32_t (&key)[kKPT],
+                                      uint32_t (&ps)[kKPT]) {
+    const uint32_t tid = threadIdx.x;
     bool placed[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) placed[q] = false;
-    for (;;) {
+    int rounds = 0;
+    for (;; ++rounds) {
 #pragma unroll
-        for (int q = 0; q < kKPT; ++q)
-            if (on[q] && !placed[q]) atomicMin(&T[pr_slot(ps[q])], prio[q]);
+        for (int q = 0; q < kKPT; ++q) {
+            const uint32_t t = tid + 1024u * q;
+            if (t < static_cast<uint32_t>(nk) && !placed[q])
+                for (;;) {
+                    const uint32_t old = atomicMin(&T[pr_slot(ps[q])], t);
+                    if (old > t) break;
+                    ps[q] = pr_next(ps[q], key[q], mask);
+                }
+        }
         __syncthreads();
         int any = 0;
 #pragma unroll
-        for (int q = 0; q < kKPT; ++q)
-            if (on[q]) {
-                placed[q] = T[pr_slot(ps[q])] == prio[q];
+        for (int q = 0; q < kKPT; ++q) {
+            const uint32_t t = tid + 1024u * q;
+            if (t < static_cast<uint32_t>(nk)) {
+                placed[q] = T[pr_slot(ps[q])] == t;
                 if (!placed[q]) {
                     ps[q] = pr_next(ps[q], key[q], mask);
                     any = 1;
                 }
             }
+        }
         if (!__syncthreads_or(any)) break;
     }
+    return rounds + 1;
 }
 
 // The union's table (one block, LDS): the runs' new keys in merge order,
@@ -289,6 +305,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     if (tid == 0) {
         s_epoch = c->epoch + 1;
         s_bad = 0;
+        c->dbg[0] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     }
     // runs 1..n-1 in contiguous chunks, one per thread: item and new-key counts
     const int per = (n - 1 + 1023) / 1024;
@@ -323,45 +340,51 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     }
     __threadfence_block();
     __syncthreads();
+    if (tid == 0) c->dbg[1] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     // resize schedule: stage 0 is the copy of samp_neighs[0] (resized to
     // 2 * used when used * 5 >= 21) plus the runs up to the first merge whose
-    // pre-resize fires; every such merge starts a stage
-    if (tid == 0) {
-        const uint32_t mu = used0 * 5 >= 21 ? mask_for(2 * used0) : 7u;
-        st_run[0] = 1;
-        st_mask[0] = mu;
-        s_nst = 1;
-    }
+    // pre-resize fires, (used + other.used) * 5 >= mask * 3 (no dummies: fill
+    // == used); every such merge starts a stage.  The runs' sizes after their
+    // merge are staged in LDS; one wave finds the triggers with ballots.
+    int32_t* need = reinterpret_cast<int32_t*>(T + kUnionMax);  // [kStageKeys], free until the stages
+    const bool need_lds = n <= kStageKeys;
+    if (need_lds)
+        for (int r = ra; r < rb; ++r) need[r] = ub.ubef[r] + ub.set_cnt[r];
     __syncthreads();
-    for (;;) {
-        const int cur_r = st_run[s_nst - 1] + (s_nst > 1 ? 1 : 0);
-        const int64_t cur_m = st_mask[s_nst - 1];
-        if (tid == 0) s_best = INT_MAX;
-        __syncthreads();
-        for (int r = max(ra, cur_r); r < rb; ++r) {
-            if ((static_cast<int64_t>(ub.ubef[r]) + ub.set_cnt[r]) * 5 >= cur_m * 3) {
-                atomicMin(&s_best, r);
-                break;
+    if (tid < 64) {
+        const int lane = tid;
+        int64_t cur_m = used0 * 5 >= 21 ? mask_for(2 * used0) : 7u;
+        int cur = 1, nst = 1;
+        if (lane == 0) {
+            st_run[0] = 1;
+            st_mask[0] = static_cast<uint32_t>(cur_m);
+        }
+        for (int base = 1; base < n; base += 64) {
+            const int r = base + lane;
+            const int64_t v = r < n ? (need_lds ? need[r] : ub.ubef[r] + ub.set_cnt[r]) : 0;
+            uint64_t bits = __ballot(r < n && r >= cur && v * 5 >= cur_m * 3);
+            while (bits) {
+                const int rr = base + __ffsll(static_cast<unsigned long long>(bits)) - 1;
+                const int64_t vr = __shfl(v, rr - base, 64);
+                if (nst >= kMaxStages) {
+                    if (lane == 0) s_bad = 1;
+                    break;
+                }
+                cur_m = mask_for(2 * vr);
+                if (lane == 0) {
+                    st_run[nst] = rr;
+                    st_mask[nst] = static_cast<uint32_t>(cur_m);
+                }
+                ++nst;
+                cur = rr + 1;
+                bits = __ballot(r < n && r >= cur && v * 5 >= cur_m * 3);
             }
         }
-        __syncthreads();
-        const int best = s_best;
-        if (best == INT_MAX) break;
-        if (tid == 0) {
-            if (s_nst >= kMaxStages) {
-                s_bad = 1;
-            } else {
-                st_run[s_nst] = best;
-                st_mask[s_nst] = mask_for(2 * (static_cast<int64_t>(ub.ubef[best]) + ub.set_cnt[best]));
-                ++s_nst;
-            }
+        if (lane == 0) {
+            s_nst = nst;
+            st_run[nst] = n;
+            if (cur_m + 1 > kUnionMax) s_bad = 1;
         }
-        __syncthreads();
-        if (s_bad) break;
-    }
-    if (tid == 0) {
-        st_run[s_nst] = n;
-        if (st_mask[s_nst - 1] + 1 > static_cast<uint32_t>(kUnionMax)) s_bad = 1;
     }
     __syncthreads();
     if (s_bad) {
@@ -369,52 +392,77 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         return;
     }
     const int nst = s_nst;
-    // stages
+    if (tid == 0) {
+        c->dbg[2] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        c->dbg[3] = nst;
+    }
+    // stages: the previous table's keys in slot order (samp_neighs[0]'s own
+    // table for stage 0), then the stage's new keys in merge order
+    int32_t* oldk = need;                    // [kStageKeys]
+    __shared__ int32_t oldslot[kSmallSet];   // stage 0: the first table's slots
     int32_t key[kKPT];
-    uint32_t prio[kKPT], ps[kKPT];
-    bool on[kKPT];
+    uint32_t ps[kKPT];
     uint32_t prev_mask = m_first;
     for (int s = 0; s < nst; ++s) {
         const uint32_t m = st_mask[s];
-        // previous table's keys (samp_neighs[0]'s own table for stage 0), priority = slot
-#pragma unroll
-        for (int q = 0; q < kOldPT; ++q) {
-            const uint32_t sl = tid + 1024u * q;
-            int32_t kk = -1;
-            if (sl <= prev_mask) kk = s == 0 ? ub.first_tab[sl] : static_cast<int32_t>(T[sl]);
-            key[q] = kk;
-            prio[q] = sl;
-            on[q] = kk != -1;
-            // stage 0 with the copy's table size equal to the set's: slot copy
-            ps[q] = (s == 0 && m == m_first) ? sl : pr_init(kk, m);
+        // compaction of the previous table
+        int n_old;
+        {
+            const int sp = static_cast<int>((prev_mask + 1 + 1023) / 1024);
+            const uint32_t a0 = min<uint32_t>(prev_mask + 1, tid * sp), a1 = min<uint32_t>(prev_mask + 1, a0 + sp);
+            int mine = 0;
+            for (uint32_t i = a0; i < a1; ++i) {
+                const int32_t kk = s == 0 ? ub.first_tab[i] : static_cast<int32_t>(T[i]);
+                mine += kk != -1;
+            }
+            int at = block_excl_scan(mine, shi, &n_old);
+            for (uint32_t i = a0; i < a1; ++i) {
+                const int32_t kk = s == 0 ? ub.first_tab[i] : static_cast<int32_t>(T[i]);
+                if (kk != -1) {
+                    oldk[at] = kk;
+                    if (s == 0) oldslot[at] = static_cast<int32_t>(i);
+                    ++at;
+                }
+            }
         }
         const int f0 = ub.ubef[st_run[s]] - used0, f1 = ub.ubef[st_run[s + 1]] - used0;
-#pragma unroll
-        for (int q = 0; q < kFreshPT; ++q) {
-            const int o = f0 + tid + 1024 * q;
-            const bool ok = o < f1;
-            const int32_t kk = ok ? ub.fresh[o] : -1;
-            key[kOldPT + q] = kk;
-            prio[kOldPT + q] = prev_mask + 1 + static_cast<uint32_t>(o - f0);
-            on[kOldPT + q] = ok;
-            ps[kOldPT + q] = pr_init(kk, m);
+        const int nk = n_old + (f1 - f0);
+        if (nk > kStageKeys) {  // uniform: every thread sees the same counts
+            if (tid == 0) c->status |= kStTable;
+            return;
         }
-        if (tid == 0 && f1 - f0 > 1024 * kFreshPT) s_bad = 1;
-        __syncthreads();
+        __syncthreads();  // oldk complete; T free to clear
+        // stage 0 with the copy's table size equal to the set's: slot copy
+        const bool copy = s == 0 && m == m_first;
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q) {
+            const int t = tid + 1024 * q;
+            int32_t kk = -1;
+            uint32_t p0 = 0;
+            if (t < n_old) {
+                kk = oldk[t];
+                p0 = copy ? static_cast<uint32_t>(oldslot[t]) : pr_init(kk, m);
+            } else if (t < nk) {
+                kk = ub.fresh[f0 + t - n_old];
+                p0 = pr_init(kk, m);
+            }
+            key[q] = kk;
+            ps[q] = p0;
+        }
         for (uint32_t i = tid; i <= m; i += 1024) T[i] = 0xFFFFFFFFu;
         __syncthreads();
-        if (s_bad) break;
-        settle(T, m, key, prio, ps, on);
+        const int rounds = settle(T, m, nk, key, ps);
+        if (tid == 0 && s < 16) {
+            c->dbg[8 + 3 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+            c->dbg[9 + 3 * s] = rounds;
+            c->dbg[10 + 3 * s] = (static_cast<int64_t>(f1 - f0) << 32) | m;
+        }
         // priorities -> keys (every slot has one owner)
 #pragma unroll
         for (int q = 0; q < kKPT; ++q)
-            if (on[q]) T[pr_slot(ps[q])] = static_cast<uint32_t>(key[q]);
+            if (tid + 1024 * q < static_cast<uint32_t>(nk)) T[pr_slot(ps[q])] = static_cast<uint32_t>(key[q]);
         __syncthreads();
         prev_mask = m;
-    }
-    if (s_bad) {
-        if (tid == 0) c->status |= kStTable;
-        return;
     }
     // the next frontier: keys in slot order, each key's position (lid)
     const uint32_t mf = prev_mask;
@@ -454,6 +502,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         h.n_src = n_src;
         h.n_nbr = n_nbr;
         pack[off[GS_PK_NBR_PTR] + n] = n_nbr;
+        c->dbg[4] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         c->epoch = s_epoch;  // every kernel of this hop read epoch + 1 before this launch's end
     }
     for (int i = tid; i <= n_src; i += 1024) ub.tcnt[i] = 0;
@@ -553,7 +602,7 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(ublock_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   kUnionMax * sizeof(uint32_t)) == hipSuccess;
+                                   kUnionLds) == hipSuccess;
     }();
     if (!attr) fail(GS_EHIP, "ublock_kernel: cannot raise its LDS limit");
     const int gcn = (flags & GS_SAMPLE_GCN) ? 1 : 0;
@@ -562,7 +611,7 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     check_launch("sets_kernel");
     ufresh_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop);
     check_launch("ufresh_kernel");
-    ublock_kernel<<<1, 1024, kUnionMax * sizeof(uint32_t), st>>>(c, hb, ub, next, hop, gcn, pack,
+    ublock_kernel<<<1, 1024, kUnionLds, st>>>(c, hb, ub, next, hop, gcn, pack,
                                                                    static_cast<int>(nd_next_max));
     check_launch("ublock_kernel");
     uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);

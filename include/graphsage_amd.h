@@ -247,6 +247,10 @@ int64_t gs_dsampler_pack_bound(const gs_dsampler* ds, int64_t n_roots);
 int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int32_t* pack,
                     int64_t cap, void* stream);
 int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+/* Diagnostics of the last run (waits for it): n <= 64 words — per-phase
+ * device timestamps (100 MHz) and round counts of the frontier union's
+ * stages; the layout is documented in kernels/dsample_union.hip. */
+int gs_dsampler_debug(gs_dsampler* ds, int64_t* out, int32_t n);
 
 /* ------------------------------------------------- unsupervised-loss batch
  * UnsupervisedLoss (models.py:30-186) over the same graph and rng:
