@@ -138,37 +138,101 @@ constexpr size_t kUnionLds = (kUnionMax + kStageKeys) * sizeof(uint32_t);  // ta
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb, UnionBufs ub, int hop, int k) {
-    extern __shared__ int32_t lds[];
-    const int r = blockIdx.x * 64 + threadIdx.x;
+// ---- one wave per set: CPython's set operations on a 128-slot LDS table,
+// each probe run (slots i .. i+9) read by ten lanes at once
+
+__device__ __forceinline__ int wlane() { return static_cast<int>(threadIdx.x & 63); }
+
+__device__ __forceinline__ void w_clear(volatile int32_t* T, uint32_t nslots) {
+    for (uint32_t i = wlane(); i < nslots; i += 64) T[i] = -1;
+}
+
+// set_add_entry (no dummies): the first slot of the probe sequence holding
+// the key (already present: false) or empty (the key goes there: true).
+__device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_t key) {
+    const int lane = wlane();
+    uint32_t i = static_cast<uint32_t>(key) & mask;
+    uint32_t perturb = static_cast<uint32_t>(key);
+    for (;;) {
+        const uint32_t probes = (i + 9 <= mask) ? 9u : 0u;
+        const bool in = static_cast<uint32_t>(lane) <= probes;
+        const int32_t x = in ? T[i + lane] : 0;
+        const uint64_t hit = __ballot(in && (x == -1 || x == key));
+        if (hit) {
+            const int l = __ffsll(static_cast<unsigned long long>(hit)) - 1;
+            if (__shfl(x, l, 64) == key) return false;
+            if (lane == 0) T[i + l] = key;
+            return true;
+        }
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// The keys of T (mask + 1 <= 128 slots) in slot order into K; returns their count.
+__device__ __forceinline__ int w_compact(const volatile int32_t* T, uint32_t mask, volatile int32_t* K) {
+    const int lane = wlane();
+    int n = 0;
+    for (uint32_t b = 0; b <= mask; b += 64) {
+        const uint32_t sl = b + lane;
+        const int32_t x = sl <= mask ? T[sl] : -1;
+        const uint64_t bal = __ballot(x != -1);
+        if (x != -1) K[n + __popcll(bal & ((1ull << lane) - 1ull))] = x;
+        n += __popcll(bal);
+    }
+    return n;
+}
+
+// set_table_resize: smallest power of two > minused, keys re-inserted in slot order.
+__device__ __forceinline__ uint32_t w_resize(volatile int32_t* T, uint32_t mask, int minused, volatile int32_t* K) {
+    const int n = w_compact(T, mask, K);
+    uint32_t ns = 8;
+    while (ns <= static_cast<uint32_t>(minused)) ns <<= 1;
+    w_clear(T, ns);
+    for (int q = 0; q < n; ++q) (void)w_add(T, ns - 1, K[q]);
+    return ns - 1;
+}
+
+// samp_neighs[r] = set(random.sample(...)) | {node} (models.py:282, :285), or
+// the adjacency set itself | {node} when deg < k; then its iteration order,
+// each item's first-occurrence mark for the frontier union (item q of run
+// r >= 1 has merge-order key t = pos_ptr[r] + r + q, increasing in merge
+// order; the largest mark is the earliest occurrence; run 0's keys are in the
+// union from the start, never new), and samp_neighs[0]'s table.
+constexpr int kSetWaves = 4;
+__global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb, UnionBufs ub, int hop,
+                                                              int k) {
+    __shared__ int32_t tabs[kSetWaves][kSmallSet], keys[kSetWaves][kSmallSet];
+    const int wave = static_cast<int>(threadIdx.x >> 6), lane = wlane();
+    const int r = blockIdx.x * kSetWaves + wave;
     const int n = c->hop[hop].n_dst;
     if (r >= n) return;
-    LSet s{lds + threadIdx.x * kLaneSet, lds + threadIdx.x * kLaneSet + kSmallSet, 7, 0};
-    int32_t* keys = lds + threadIdx.x * kLaneSet + kSmallSet + kTmpSet;  // the sample's ids, staged
-    ps_clear(s.T, 8);
+    volatile int32_t* T = tabs[wave];
+    volatile int32_t* K = keys[wave];
     const int32_t v = hb.dst[r];
     const int d = hb.deg[r];
+    uint32_t mask = 7;
+    int used = 0;
+    w_clear(T, 8);
     if (k > 0 && d >= k) {
-        // set(random.sample(...)) in result order, then the copy that `|` makes.
-        // Every id is fetched before the first insert (independent loads in
-        // flight together, not one dependent pair per add).
-        const int32_t* ent = hb.ent + hb.pos_ptr[r];
-        int32_t e[kMaxK];
-#pragma unroll
-        for (int i = 0; i < kMaxK; ++i) e[i] = i < k ? ent[i] : 0;
-#pragma unroll
-        for (int i = 0; i < kMaxK; ++i)
-            if (i < k) keys[i] = g.col[e[i]];
-        for (int i = 0; i < k; ++i) ls_add(s, keys[i]);
+        // set(list): set_add_key per item in result order, resizing to used * 4
+        const int32_t e = lane < k ? hb.ent[hb.pos_ptr[r] + lane] : 0;
+        const int32_t mine = lane < k ? g.col[e] : 0;
+        for (int i = 0; i < k; ++i) {
+            if (w_add(T, mask, __shfl(mine, i, 64))) {
+                ++used;
+                if (static_cast<uint32_t>(used) * 5 >= mask * 3) mask = w_resize(T, mask, used * 4, K);
+            }
+        }
+        // the copy `|` makes: resized to 2 * used when used * 5 >= 21, else
+        // the same size (then a slot copy)
         uint32_t nm = 7;
-        if (s.used * 5 >= 21) nm = mask_for(2 * s.used);
-        if (nm != s.mask) {
-            int m = 0;
-            for (uint32_t i = 0; i <= s.mask; ++i)
-                if (s.T[i] != -1) s.tmp[m++] = s.T[i];
-            ps_clear(s.T, nm + 1);
-            for (int q = 0; q < m; ++q) ps_insert_clean(s.T, nm, s.tmp[q]);
-            s.mask = nm;
+        if (used * 5 >= 21) nm = mask_for(2 * used);
+        if (nm != mask) {
+            const int m = w_compact(T, mask, K);
+            w_clear(T, nm + 1);
+            for (int q = 0; q < m; ++q) (void)w_add(T, nm, K[q]);
+            mask = nm;
         }
     } else {
         // the adjacency set itself, copied by `|`: its own layout when the
@@ -179,48 +243,50 @@ __global__ __launch_bounds__(64) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb
         uint32_t ns = 8;
         if (d * 5 >= 21)
             while (ns <= static_cast<uint32_t>(2 * d)) ns <<= 1;
-        ps_clear(s.T, ns);
-        s.mask = ns - 1;
-        s.used = d;
-        if (s.mask == m0 && !dirty)
-            for (int t = 0; t < d; ++t) s.T[g.slot[rs + t]] = g.col[rs + t];
-        else
-            for (int t = 0; t < d; ++t) ps_insert_clean(s.T, s.mask, g.col[rs + t]);
+        mask = ns - 1;
+        used = d;
+        w_clear(T, ns);
+        if (mask == m0 && !dirty) {
+            if (lane < d) T[g.slot[rs + lane]] = g.col[rs + lane];
+        } else {
+            const int32_t mine = lane < d ? g.col[rs + lane] : 0;
+            for (int t = 0; t < d; ++t) (void)w_add(T, mask, __shfl(mine, t, 64));
+        }
     }
     // | set([node]): set_merge with a one-element set
-    if ((s.used + 1) * 5 >= static_cast<int>(s.mask) * 3) ls_resize(s, (s.used + 1) * 2);
-    if (s.used == 0 && s.mask == 7) {
-        ps_clear(s.T, 8);
-        s.T[v & 7] = v;
-        s.used = 1;
-    } else if (s.used == 0) {
-        s.used = 1;
-        ps_insert_clean(s.T, s.mask, v);
-    } else {
-        ls_add(s, v);
+    if (static_cast<uint32_t>(used + 1) * 5 >= mask * 3) mask = w_resize(T, mask, (used + 1) * 2, K);
+    if (used == 0 && mask == 7) {
+        w_clear(T, 8);
+        if (lane == 0) T[v & 7] = v;
+        used = 1;
+    } else if (w_add(T, mask, v)) {
+        ++used;
+        if (static_cast<uint32_t>(used) * 5 >= mask * 3) mask = w_resize(T, mask, used > 50000 ? used * 2 : used * 4, K);
     }
-    // the set in iteration order, and each item's first-occurrence mark for
-    // the frontier union (union.hip header): run 0's keys are in the union
-    // from the start (never new); item q of run r >= 1 has merge-order key
-    // t = pos_ptr[r] + r + q (increasing in merge order), the largest mark
-    // value is the earliest occurrence
+    // iteration order, marks
     const uint64_t E = static_cast<uint64_t>(static_cast<uint32_t>(c->epoch + 1)) << 32;
     const uint32_t t0 = static_cast<uint32_t>(hb.pos_ptr[r] + r);
     int32_t* out = ub.set_items + hb.pos_ptr[r] + r;
-    int q = 0;
-    for (uint32_t i = 0; i <= s.mask; ++i)
-        if (s.T[i] != -1) {
-            const int32_t key = s.T[i];
-            out[q] = key;
-            atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[key]),
+    int q0 = 0;
+    for (uint32_t b = 0; b <= mask; b += 64) {
+        const uint32_t sl = b + lane;
+        const int32_t x = sl <= mask ? T[sl] : -1;
+        const uint64_t bal = __ballot(x != -1);
+        if (x != -1) {
+            const int q = q0 + __popcll(bal & ((1ull << lane) - 1ull));
+            out[q] = x;
+            atomicMax(reinterpret_cast<unsigned long long*>(&ub.mark[x]),
                       static_cast<unsigned long long>(E | (r == 0 ? 0xFFFFFFFFu : 0xFFFFFFFEu - (t0 + q))));
-            ++q;
         }
-    ub.set_cnt[r] = s.used;
+        q0 += __popcll(bal);
+    }
+    if (lane == 0) ub.set_cnt[r] = used;
     if (r == 0) {
-        for (uint32_t i = 0; i <= s.mask; ++i) ub.first_tab[i] = s.T[i];
-        ub.first_meta[0] = static_cast<int32_t>(s.mask);
-        ub.first_meta[1] = s.used;
+        for (uint32_t i = lane; i <= mask; i += 64) ub.first_tab[i] = T[i];
+        if (lane == 0) {
+            ub.first_meta[0] = static_cast<int32_t>(mask);
+            ub.first_meta[1] = used;
+        }
     }
 }
 
@@ -252,7 +318,7 @@ __global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBuf
 // and the assignment converges to the sequential one (the highest priority
 // always keeps its first free slot, and by induction every later key).
 __device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const int32_t (&key)[kKPT],
-                                      uint32_t (&ps)[kKPT]) {
+                                      uint32_t (&ps)[kKPT], int64_t& first_round) {
     const uint32_t tid = threadIdx.x;
     bool placed[kKPT];
 #pragma unroll
@@ -282,6 +348,7 @@ __device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const 
                 }
             }
         }
+        if (rounds == 0 && threadIdx.x == 0) first_round = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         if (!__syncthreads_or(any)) break;
     }
     return rounds + 1;
@@ -451,11 +518,13 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         }
         for (uint32_t i = tid; i <= m; i += 1024) T[i] = 0xFFFFFFFFu;
         __syncthreads();
-        const int rounds = settle(T, m, nk, key, ps);
-        if (tid == 0 && s < 16) {
-            c->dbg[8 + 3 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
-            c->dbg[9 + 3 * s] = rounds;
-            c->dbg[10 + 3 * s] = (static_cast<int64_t>(f1 - f0) << 32) | m;
+        int64_t first_round = 0;
+        if (tid == 0 && s < 12) c->dbg[8 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        const int rounds = settle(T, m, nk, key, ps, first_round);
+        if (tid == 0 && s < 12) {
+            c->dbg[9 + 4 * s] = first_round;
+            c->dbg[10 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+            c->dbg[11 + 4 * s] = (static_cast<int64_t>(rounds) << 48) | (static_cast<int64_t>(nk) << 32) | m;
         }
         // priorities -> keys (every slot has one owner)
 #pragma unroll
@@ -606,8 +675,8 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     }();
     if (!attr) fail(GS_EHIP, "ublock_kernel: cannot raise its LDS limit");
     const int gcn = (flags & GS_SAMPLE_GCN) ? 1 : 0;
-    const unsigned nb64 = static_cast<unsigned>((nd_max + 63) / 64);
-    sets_kernel<<<nb64, 64, 64 * kLaneSet * sizeof(int32_t), st>>>(g, c, hb, ub, hop, k);
+    sets_kernel<<<static_cast<unsigned>((nd_max + kSetWaves - 1) / kSetWaves), 64 * kSetWaves, 0, st>>>(g, c, hb, ub,
+                                                                                                    hop, k);
     check_launch("sets_kernel");
     ufresh_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop);
     check_launch("ufresh_kernel");

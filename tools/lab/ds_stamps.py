@@ -21,9 +21,10 @@ for b in range(6):
     nst = int(d[3])
     line = f"batch {b}: scans+compact {us(0,1):.1f} us, schedule {us(1,2):.1f} us, stages {nst}:"
     prev = d[2]
-    for s in range(min(nst, 16)):
-        t, rounds, km = d[8 + 3 * s], d[9 + 3 * s], d[10 + 3 * s]
-        line += f" [{(t - prev) / 100.0:.1f}us r{rounds} f{km >> 32} m{km & 0xffffffff}]"
-        prev = t
+    for s in range(min(nst, 12)):
+        t0, t1, t2, x = d[8 + 4 * s], d[9 + 4 * s], d[10 + 4 * s], d[11 + 4 * s]
+        line += (f" [prep {(t0 - prev) / 100.0:.1f} r1 {(t1 - t0) / 100.0:.1f} rest {(t2 - t1) / 100.0:.1f}us "
+                 f"r{x >> 48} k{(x >> 32) & 0xffff} m{x & 0xffffffff}]")
+        prev = t2
     line += f" frontier {(d[4] - prev) / 100.0:.1f} us; total {us(0, 4):.1f} us"
     print(line, flush=True)
