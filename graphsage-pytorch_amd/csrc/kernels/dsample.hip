@@ -444,25 +444,27 @@ __global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __res
 // selected-set branch reads the accepted word's value once for its repeat
 // test.  A walk past its node's mask window (more than kRejBudget rejections
 // in the block) continues word by word, so the result is exact either way.
-constexpr int kRejBudget = 256;   // rejections a block may add beyond its entry window, mask-covered
-constexpr int kMaskU64 = 6144;    // masks per phase (48 KiB); more nodes take several phases
-constexpr int kMaxEPT = kWMax / 1024;  // entries per thread
+//
+// One 256-thread workgroup per (block, 256 entries): the work is the block's
+// window width times its draws, so wide blocks (late in the hop) are split
+// over several CUs, and each workgroup builds masks only over the words its
+// 256 entries can reach.
+constexpr int kMEntries = 256;                                    // entries per workgroup
+constexpr int kRejBudget = 192;                                   // mask-covered rejections per block
+constexpr int kMChunks = (kMEntries + kRejBudget + 63) / 64 + 1;  // mask words per draw (+1 for the 2-word window)
 
 template <int KMAX>
-__device__ __forceinline__ int walk_masked(const uint64_t* __restrict__ M, int C, int a, int u, uint32_t d, int k,
+__device__ __forceinline__ int walk_masked(const uint64_t* __restrict__ M, int a, int u, uint32_t d, int k,
                                            bool pool, const uint32_t* __restrict__ w, int nvalid) {
     if (u < 0) return -1;
     int rel = u - a;
-    const int lim = (C - 1) * 64;
+    constexpr int lim = (kMChunks - 1) * 64;
     if (pool) {
         for (int i = 0; i < k; ++i) {
-            uint64_t win = 0;
-            if (rel < lim) {
-                const uint64_t* Mi = M + i * C;
-                const int j = rel >> 6, b = rel & 63;
-                const uint64_t lo = Mi[j], hi = Mi[j + 1];
-                win = b ? (lo >> b) | (hi << (64 - b)) : lo;
-            }
+            const uint64_t* Mi = M + i * kMChunks;
+            const int j = min(rel >> 6, kMChunks - 2), b = rel & 63;
+            const uint64_t lo = Mi[j], hi = Mi[j + 1];
+            const uint64_t win = rel < lim ? (lo >> b) | ((hi << 1) << (63 - b)) : 0ull;
             if (win) {
                 rel += __ffsll(static_cast<unsigned long long>(win));
             } else {
@@ -482,12 +484,9 @@ __device__ __forceinline__ int walk_masked(const uint64_t* __restrict__ M, int C
     uint32_t sel[KMAX];
     int cnt = 0;
     while (cnt < k) {
-        uint64_t win = 0;
-        if (rel < lim) {
-            const int j = rel >> 6, b = rel & 63;
-            const uint64_t lo = M[j], hi = M[j + 1];
-            win = b ? (lo >> b) | (hi << (64 - b)) : lo;
-        }
+        const int j = min(rel >> 6, kMChunks - 2), b = rel & 63;
+        const uint64_t lo = M[j], hi = M[j + 1];
+        const uint64_t win = rel < lim ? (lo >> b) | ((hi << 1) << (63 - b)) : 0ull;
         uint32_t val;
         if (win) {
             const int p = rel + __ffsll(static_cast<unsigned long long>(win)) - 1;
@@ -512,11 +511,9 @@ __device__ __forceinline__ int walk_masked(const uint64_t* __restrict__ M, int C
 }
 
 template <int KMAX>
-__global__ __launch_bounds__(1024) void draw_masked_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, int hop,
-                                                           int k, int setsize, int R) {
+__global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
+                                                                int hop, int k, int setsize, int R) {
     extern __shared__ uint64_t smem64[];
-    uint64_t* masks = smem64;                                    // [kMaskU64]
-    uint32_t* w = reinterpret_cast<uint32_t*>(masks + kMaskU64);  // the block's words
     __shared__ int s_d[256], s_moff[257];
     __shared__ int s_nsr;
     const HopCtl& h = c->hop[hop];
@@ -524,81 +521,77 @@ __global__ __launch_bounds__(1024) void draw_masked_kernel(const uint32_t* __res
     if (b >= h.n_blocks) return;
     const int Wst = h.W;
     const int bw = min(hb.bw[b], Wst);
+    const int e0 = blockIdx.y * kMEntries;
+    if (e0 >= bw) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
-    const int lo = hb.blo[b];
-    const int nw = Wst + 3 * R * max(k, 1) + 64;
-    const int nvalid = load_words(wr, c, h.P0 + hb.dbase[b] + lo, nw, w);
-    const int C = (bw + kRejBudget + 63) / 64 + 1;  // mask words per draw (one spare for the 2-word window)
-    if (tid == 0) {
-        // the sampled nodes in order; each makes exactly k draws, so node m's
-        // first word is m * k (block-relative) plus the rejections so far
+    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
+    // masks: [node][draw][kMChunks] (pool: k draws, selected-set: 1), then the words
+    uint64_t* masks = smem64;
+    uint32_t* w = reinterpret_cast<uint32_t*>(masks + R * max(k, 1) * kMChunks);
+    // words from this workgroup's first entry on (entry e0 starts at word e0 of the block)
+    const int nw = kMEntries + ndr + 3 * R * max(k, 1) + 64;
+    const int nvalid = load_words(wr, c, h.P0 + hb.dbase[b] + hb.blo[b] + e0, nw, w);
+    if (tid < 64) {  // the sampled nodes in order, compacted by one wave
         int m = 0, off = 0;
-        for (int q = 0; q < nr; ++q) {
-            const int d = hb.deg[r0 + q];
-            if (k > 0 && d >= k) {
-                s_d[m] = d;
-                s_moff[m] = off;
-                off += (static_cast<uint32_t>(d) <= static_cast<uint32_t>(setsize) ? k : 1) * C;
-                ++m;
+        for (int q0 = 0; q0 < nr; q0 += 64) {
+            const int q = q0 + lane;
+            const int d = q < nr ? hb.deg[r0 + q] : 0;
+            const bool smp = q < nr && k > 0 && d >= k;
+            const uint64_t bal = __ballot(smp);
+            const int at = m + __popcll(bal & ((1ull << lane) - 1ull));
+            const int sz = smp ? (static_cast<uint32_t>(d) <= static_cast<uint32_t>(setsize) ? k : 1) * kMChunks : 0;
+            // exclusive prefix of the mask sizes in this chunk of nodes
+            int inc = sz;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += t;
             }
+            if (smp) {
+                s_d[at] = d;
+                s_moff[at] = off + inc - sz;
+            }
+            m += __popcll(bal);
+            off += __shfl(inc, 63, 64);
         }
-        s_moff[m] = off;
-        s_nsr = m;
+        if (lane == 0) {
+            s_moff[m] = off;
+            s_nsr = m;
+        }
     }
     __syncthreads();
     const int nsr = s_nsr;
-    int u[kMaxEPT];
-#pragma unroll
-    for (int q = 0; q < kMaxEPT; ++q) u[q] = tid + 1024 * q;
-    for (int q0 = 0; q0 < nsr;) {
-        // this phase: the nodes whose masks fit
-        int q1 = q0 + 1;
-        while (q1 < nsr && s_moff[q1 + 1] - s_moff[q0] <= kMaskU64) ++q1;
-        const int base = s_moff[q0];
-        if (s_moff[q1] - base > kMaskU64) {  // one node's masks alone exceed the budget (kWMax bounds C)
-            if (tid == 0) atomicOr(&c->status, kStWindow);
-            return;
-        }
-        for (int t = wave; t < (q1 - q0) * C; t += 16) {
-            const int q = q0 + t / C, ch = t % C;
-            const uint32_t d = static_cast<uint32_t>(s_d[q]);
-            const int pos = q * k + 64 * ch + lane;
-            const bool ok = pos < nvalid;
-            const uint32_t x = ok ? w[pos] : 0u;
-            uint64_t* M = masks + (s_moff[q] - base) + ch;
-            if (d <= static_cast<uint32_t>(setsize)) {
-                for (int i = 0; i < k; ++i) {
-                    const uint32_t m = d - i;
-                    const uint64_t bal = __ballot(ok && (x >> __clz(m)) < m);
-                    if (lane == 0) M[i * C] = bal;
-                }
-            } else {
-                const uint64_t bal = __ballot(ok && (x >> __clz(d)) < d);
-                if (lane == 0) M[0] = bal;
+    // build: node m's window starts at word m * k (entry e0, no rejections yet)
+    for (int t = wave; t < nsr * kMChunks; t += kMEntries / 64) {
+        const int q = t / kMChunks, ch = t - q * kMChunks;
+        const uint32_t d = static_cast<uint32_t>(s_d[q]);
+        const int pos = q * k + 64 * ch + lane;
+        const bool ok = pos < nvalid;
+        const uint32_t x = ok ? w[pos] : 0u;
+        uint64_t* M = masks + s_moff[q] + ch;
+        if (d <= static_cast<uint32_t>(setsize)) {
+            for (int i = 0; i < k; ++i) {
+                const uint32_t m = d - i;
+                const uint64_t bal = __ballot(ok && (x >> __clz(m)) < m);
+                if (lane == 0) M[i * kMChunks] = bal;
             }
+        } else {
+            const uint64_t bal = __ballot(ok && (x >> __clz(d)) < d);
+            if (lane == 0) M[0] = bal;
         }
-        __syncthreads();
-        for (int q = q0; q < q1; ++q) {
-            const uint32_t d = static_cast<uint32_t>(s_d[q]);
-            const bool pool = d <= static_cast<uint32_t>(setsize);
-            const uint64_t* M = masks + (s_moff[q] - base);
-#pragma unroll
-            for (int e = 0; e < kMaxEPT; ++e)
-                if (tid + 1024 * e < bw) u[e] = walk_masked<KMAX>(M, C, q * k, u[e], d, k, pool, w, nvalid);
-        }
-        __syncthreads();
-        q0 = q1;
     }
-    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
-#pragma unroll
-    for (int e = 0; e < kMaxEPT; ++e) {
-        const int ent = tid + 1024 * e;
-        if (ent < bw) {
-            const int dr = u[e] < 0 ? -1 : u[e] - ent - ndr;
-            E[ent] = (dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
-        }
+    __syncthreads();
+    const int ent = e0 + tid;
+    int u = ent < bw ? tid : -1;  // word index relative to e0
+    for (int q = 0; q < nsr; ++q) {
+        const uint32_t d = static_cast<uint32_t>(s_d[q]);
+        u = walk_masked<KMAX>(masks + s_moff[q], q * k, u, d, k, d <= static_cast<uint32_t>(setsize), w, nvalid);
+    }
+    if (ent < bw) {
+        uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
+        const int dr = u < 0 ? -1 : u - tid - ndr;
+        E[ent] = (dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
     }
 }
 
@@ -912,20 +905,22 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
     const size_t tab_lds = (R + 2 * kWMax) * sizeof(int32_t) + kWMax * sizeof(uint16_t) +
                            (kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
-    const size_t mask_lds = kMaskU64 * sizeof(uint64_t) + (kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
+    const size_t mask_lds = static_cast<size_t>(R) * std::max(k, 1) * kMChunks * sizeof(uint64_t) +
+                            (kMEntries + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
     static const bool walk_tables = std::getenv("GS_DS_WALK_TABLES") != nullptr;  // A/B: word-by-word walks
     // selected-set values in registers: the unrolled duplicate test costs KMAX per accepted word
     if (!walk_tables) {
+        const dim3 grid(static_cast<unsigned>(nb_max), kWMax / kMEntries);
         if (k <= 8)
-            draw_masked_kernel<8><<<nb_max, 1024, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+            draw_masked_kernel<8><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
         else if (k <= 12)
-            draw_masked_kernel<12><<<nb_max, 1024, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+            draw_masked_kernel<12><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
         else if (k <= 16)
-            draw_masked_kernel<16><<<nb_max, 1024, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+            draw_masked_kernel<16><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
         else if (k <= 25)
-            draw_masked_kernel<25><<<nb_max, 1024, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+            draw_masked_kernel<25><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
         else
-            draw_masked_kernel<32><<<nb_max, 1024, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+            draw_masked_kernel<32><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     } else if (k <= 8)
         draw_tables_kernel<8><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 12)

@@ -28,3 +28,5 @@ for b in range(6):
         prev = t2
     line += f" frontier {(d[4] - prev) / 100.0:.1f} us; total {us(0, 4):.1f} us"
     print(line, flush=True)
+    print(f"  tables last block (hop 2): load+nodes+build {(d[46]-d[40])/100:.1f} us, walk {(d[41]-d[46])/100:.1f} us; "
+          f"bw {d[42]} nsr {d[43]} C {d[44]} nvalid {d[45]}; slow pool {d[48]} slow set {d[49]}", flush=True)
