@@ -453,60 +453,89 @@ constexpr int kMEntries = 256;                                    // entries per
 constexpr int kRejBudget = 192;                                   // mask-covered rejections per block
 constexpr int kMChunks = (kMEntries + kRejBudget + 63) / 64 + 1;  // mask words per draw (+1 for the 2-word window)
 
+// Walk one node from block word u (relative to the workgroup's first word),
+// the node's words starting at a; M: its masks as 32-bit words, kMChunks * 2
+// per draw.  The 32-bit window at the walk's position is one alignbit of
+// two adjacent mask words; its first set bit is the next accepted word.
+// The exact word-by-word walk of one node from block word u (the fallback
+// of walk_masked for a walk that leaves its mask window).
 template <int KMAX>
-__device__ __forceinline__ int walk_masked(const uint64_t* __restrict__ M, int a, int u, uint32_t d, int k,
-                                           bool pool, const uint32_t* __restrict__ w, int nvalid) {
-    if (u < 0) return -1;
-    int rel = u - a;
-    constexpr int lim = (kMChunks - 1) * 64;
+__device__ __noinline__ int walk_words(const uint32_t* __restrict__ w, int nvalid, int u, uint32_t d, int k, bool pool) {
     if (pool) {
         for (int i = 0; i < k; ++i) {
-            const uint64_t* Mi = M + i * kMChunks;
-            const int j = min(rel >> 6, kMChunks - 2), b = rel & 63;
-            const uint64_t lo = Mi[j], hi = Mi[j + 1];
-            const uint64_t win = rel < lim ? (lo >> b) | ((hi << 1) << (63 - b)) : 0ull;
-            if (win) {
-                rel += __ffsll(static_cast<unsigned long long>(win));
-            } else {
-                const uint32_t m = d - i;
-                const int sh = __clz(m);
-                for (;;) {
-                    const int uu = a + rel;
-                    if (uu >= nvalid) return -1;
-                    ++rel;
-                    if ((w[uu] >> sh) < m) break;
-                }
+            const uint32_t m = d - i;
+            const int sh = __clz(m);
+            for (;;) {
+                if (u >= nvalid) return -1;
+                if ((w[u++] >> sh) < m) break;
             }
         }
-        return a + rel;
+        return u;
     }
     const int sh = __clz(d);
     uint32_t sel[KMAX];
     int cnt = 0;
     while (cnt < k) {
-        const int j = min(rel >> 6, kMChunks - 2), b = rel & 63;
-        const uint64_t lo = M[j], hi = M[j + 1];
-        const uint64_t win = rel < lim ? (lo >> b) | ((hi << 1) << (63 - b)) : 0ull;
-        uint32_t val;
-        if (win) {
-            const int p = rel + __ffsll(static_cast<unsigned long long>(win)) - 1;
-            val = w[a + p] >> sh;
-            rel = p + 1;
-        } else {
-            const int uu = a + rel;
-            if (uu >= nvalid) return -1;
-            val = w[uu] >> sh;
-            ++rel;
-            if (val >= d) continue;
-        }
-        bool fresh = true;
+        if (u >= nvalid) return -1;
+        const uint32_t v = w[u++] >> sh;
+        bool fresh = v < d;
 #pragma unroll
-        for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == val);
+        for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == v);
 #pragma unroll
         for (int t = 0; t < KMAX; ++t)
-            if (t == cnt) sel[t] = val;
+            if (t == cnt) sel[t] = v;
         cnt += fresh;
     }
+    return u;
+}
+
+// Walk one node from block word u (relative to the workgroup's first word),
+// the node's words starting at a; M: its masks as 32-bit words, kMChunks * 2
+// per draw.  The 32-bit window at the walk's position is one alignbit of
+// two adjacent mask words; its first set bit is the next accepted word.  A
+// walk that finds no accepted word in its window (more rejections than the
+// masks cover) redoes the node word by word; the draw loop itself has a
+// fixed trip count and no per-lane exit.
+template <int KMAX>
+__device__ __forceinline__ int walk_masked(const uint32_t* __restrict__ M, int a, int u, uint32_t d, int k,
+                                           bool pool, const uint32_t* __restrict__ w, int nvalid) {
+    constexpr int C32 = 2 * kMChunks;
+    constexpr int lim = (C32 - 1) * 32;
+    if (u < 0) return -1;
+    int rel = u - a;
+    bool bad = false;
+    if (pool) {
+        for (int i = 0; i < k; ++i) {
+            const uint32_t* Mi = M + i * C32;
+            const int j = min(rel >> 5, C32 - 2);
+            // both mask words read unconditionally (j is clamped), the window
+            // zeroed past the masks: no branch around the LDS read
+            const uint32_t win = __builtin_amdgcn_alignbit(Mi[j + 1], Mi[j], rel & 31) & (0u - (rel < lim));
+            const int adv = __ffs(win);  // 1 + the accepted word's offset; 0: none in the window
+            bad |= adv == 0;
+            rel += adv;
+        }
+    } else {
+        const int sh = __clz(d);
+        uint32_t sel[KMAX];
+        int cnt = 0;
+        while (cnt < k && !bad) {
+            const int j = min(rel >> 5, C32 - 2);
+            const uint32_t win = __builtin_amdgcn_alignbit(M[j + 1], M[j], rel & 31) & (0u - (rel < lim));
+            const int adv = __ffs(win);
+            bad = adv == 0;
+            rel += adv;
+            const uint32_t val = w[a + max(rel - 1, 0)] >> sh;
+            bool fresh = !bad;
+#pragma unroll
+            for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == val);
+#pragma unroll
+            for (int t = 0; t < KMAX; ++t)
+                if (t == cnt) sel[t] = val;
+            cnt += fresh;
+        }
+    }
+    if (bad) return walk_words<KMAX>(w, nvalid, u, d, k, pool);
     return a + rel;
 }
 
@@ -586,7 +615,8 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     int u = ent < bw ? tid : -1;  // word index relative to e0
     for (int q = 0; q < nsr; ++q) {
         const uint32_t d = static_cast<uint32_t>(s_d[q]);
-        u = walk_masked<KMAX>(masks + s_moff[q], q * k, u, d, k, d <= static_cast<uint32_t>(setsize), w, nvalid);
+        u = walk_masked<KMAX>(reinterpret_cast<const uint32_t*>(masks + s_moff[q]), q * k, u, d, k,
+                              d <= static_cast<uint32_t>(setsize), w, nvalid);
     }
     if (ent < bw) {
         uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
