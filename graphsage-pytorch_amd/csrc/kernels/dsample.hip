@@ -239,44 +239,6 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
     }
 }
 
-// Consumption of one block's draws from word index idx (into the block's LDS
-// words); returns the index after the block, or -1 past the loaded words.
-template <int KMAX>
-__device__ __forceinline__ int walk_block(const uint32_t* __restrict__ w, int nvalid, int idx,
-                                          const int32_t* __restrict__ bdeg, int nr, int k, int setsize) {
-    for (int q = 0; q < nr; ++q) {
-        const uint32_t d = static_cast<uint32_t>(bdeg[q]);
-        if (k <= 0 || d < static_cast<uint32_t>(k)) continue;
-        if (d <= static_cast<uint32_t>(setsize)) {
-            for (int i = 0; i < k; ++i) {
-                const uint32_t m = d - i;
-                const int sh = __clz(m);
-                for (;;) {
-                    if (idx >= nvalid) return -1;
-                    const uint32_t v = w[idx++] >> sh;
-                    if (v < m) break;
-                }
-            }
-        } else {
-            const int sh = __clz(d);
-            uint32_t sel[KMAX];
-            int cnt = 0;
-            while (cnt < k) {
-                if (idx >= nvalid) return -1;
-                const uint32_t v = w[idx++] >> sh;
-                bool fresh = v < d;
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == v);
-#pragma unroll
-                for (int t = 0; t < KMAX; ++t)
-                    if (t == cnt) sel[t] = v;
-                cnt += fresh;
-            }
-        }
-    }
-    return idx;
-}
-
 // Words of block b's window into LDS: relative positions dbase + lo .. , as
 // many as are generated (the count is returned).
 __device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const Ctl* c, int64_t A0, int nw,
@@ -287,154 +249,10 @@ __device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const
     return nvalid;
 }
 
-// One frontier node's consumption from word u (a word per iteration, so the
-// lanes of a wave stay together apart from the last draw); -1 past the words.
-template <int KMAX>
-__device__ __forceinline__ int walk_root(const uint32_t* __restrict__ w, int nvalid, int u, uint32_t d, int k,
-                                         bool pool) {
-    if (u < 0) return -1;
-    if (pool) {
-        int i = 0;
-        uint32_t m = d;
-        int sh = __clz(m);
-        while (i < k) {
-            if (u >= nvalid) return -1;
-            const uint32_t v = w[u++] >> sh;
-            if (v < m) {
-                ++i;
-                m = d - i;
-                sh = __clz(m | 1u);
-            }
-        }
-        return u;
-    }
-    const int sh = __clz(d);
-    uint32_t sel[KMAX];
-    int cnt = 0;
-    while (cnt < k) {
-        if (u >= nvalid) return -1;
-        const uint32_t v = w[u++] >> sh;
-        bool fresh = v < d;
-#pragma unroll
-        for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == v);
-#pragma unroll
-        for (int t = 0; t < KMAX; ++t)
-            if (t == cnt) sel[t] = v;
-        cnt += fresh;
-    }
-    return u;
-}
-
-// Block maps: E[b][e] = rejections inside block b when it is entered with
-// lo_b + e rejections so far (0xFFFF: ran past the loaded words).  The W
-// entry states are advanced node by node; two states at the same word at a
-// node boundary have the same future, so after every node the states are
-// deduplicated (they stay sorted: a later start never finishes a node
-// earlier; checked) and only the distinct ones are walked on.  Paths from
-// neighbouring entries coalesce slowly — a start one word later is one draw
-// behind on the same words, and the two draws' bounds accept nearly the same
-// words — so this saves ~40 % of the walks (507 against 878 us per hop-2
-// launch at rmat2m), not the W-fold that the window costs.
-template <int KMAX>
-__global__ __launch_bounds__(1024) void draw_tables_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, int hop,
-                                                           int k, int setsize, int R) {
-    extern __shared__ uint32_t smem[];
-    __shared__ int shi[17];
-    __shared__ int s_nsr, s_bad;
-    const HopCtl& h = c->hop[hop];
-    const int b = blockIdx.x;
-    if (b >= h.n_blocks) return;
-    const int Wst = h.W;                 // table stride
-    const int W = min(hb.bw[b], Wst);    // this block's entries
-    const int tid = threadIdx.x;
-    const int r0 = b * R, nr = min(R, h.n_dst - r0);
-    int32_t* sdeg = reinterpret_cast<int32_t*>(smem);  // sampled nodes' degrees, in order
-    int32_t* U = sdeg + R;                              // distinct states (word index), ascending
-    int32_t* nx = U + kWMax;                            // their successors / the rank map
-    uint16_t* emap = reinterpret_cast<uint16_t*>(nx + kWMax);  // entry -> state index
-    uint32_t* w = reinterpret_cast<uint32_t*>(emap + kWMax);
-    const int lo = hb.blo[b];
-    const int nw = W + 3 * R * max(k, 1) + 64;
-    const int nvalid = load_words(wr, c, h.P0 + hb.dbase[b] + lo, nw, w);
-    if (tid == 0) {
-        int m = 0;
-        for (int q = 0; q < nr; ++q) {
-            const int d = hb.deg[r0 + q];
-            if (k > 0 && d >= k) sdeg[m++] = d;
-        }
-        s_nsr = m;
-        s_bad = 0;
-    }
-    for (int e = tid; e < W; e += 1024) {
-        U[e] = e;
-        emap[e] = static_cast<uint16_t>(e);
-    }
-    __syncthreads();
-    const int nsr = s_nsr;
-    int nU = W;
-    for (int q = 0; q < nsr; ++q) {
-        const uint32_t d = static_cast<uint32_t>(sdeg[q]);
-        const bool pool = d <= static_cast<uint32_t>(setsize);
-        const int per = (nU + 1023) / 1024;
-        const int ua = min(nU, tid * per), ub = min(nU, ua + per);
-        for (int u = ua; u < ub; ++u) {
-            const int x = walk_root<KMAX>(w, nvalid, U[u] == INT_MAX ? -1 : U[u], d, k, pool);
-            nx[u] = x < 0 ? INT_MAX : x;
-        }
-        __syncthreads();
-        int f = 0;
-        int prev = ua > 0 ? nx[ua - 1] : -1;
-        for (int u = ua; u < ub; ++u) {
-            const int x = nx[u];
-            if (x < prev) s_bad = 1;
-            f += (u == 0 || x != prev);
-            prev = x;
-        }
-        int tot;
-        int rk = block_excl_scan(f, shi, &tot) - 1;
-        int keep[4], rks[4];
-        prev = ua > 0 ? nx[ua - 1] : -1;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int u = ua + t;
-            keep[t] = -1;
-            rks[t] = 0;
-            if (u < ub) {
-                const int x = nx[u];
-                if (u == 0 || x != prev) ++rk;
-                keep[t] = (u == 0 || x != prev) ? x : -1;
-                rks[t] = rk;
-                prev = x;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int u = ua + t;
-            if (u < ub) {
-                if (keep[t] >= 0) U[rks[t]] = keep[t];
-                nx[u] = rks[t];
-            }
-        }
-        __syncthreads();
-        for (int e = tid; e < W; e += 1024) emap[e] = static_cast<uint16_t>(nx[emap[e]]);
-        nU = tot;
-        __syncthreads();
-    }
-    if (tid == 0 && s_bad) atomicOr(&c->status, kStOrder);
-    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
-    for (int e = tid; e < W; e += 1024) {
-        const int x = U[emap[e]];
-        const int dr = x == INT_MAX ? -1 : x - e - ndr;
-        E[e] = (dr < 0 || dr >= 0xFFFF) ? 0xFFFF : static_cast<uint16_t>(dr);
-    }
-}
-
-// ---- block maps by acceptance bitmasks (the default)
+// ---- block maps by acceptance bitmasks
 //
-// The same E[b][e] as draw_tables_kernel, without its divergent
-// word-by-word walks.  For every sampled node of the block and every one of
+// Block maps: E[b][e] = rejections inside block b when it is entered with
+// lo_b + e rejections so far (0xFFFF: ran past the loaded words).  For every sampled node of the block and every one of
 // its draws, the words that draw would accept form a bitmask over the node's
 // word window: pool branch, draw i accepts word x iff
 // (x >> clz(d - i)) < d - i; selected-set branch, every draw accepts
@@ -613,11 +431,21 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     __syncthreads();
     const int ent = e0 + tid;
     int u = ent < bw ? tid : -1;  // word index relative to e0
+    uint8_t* rej = hb.rej + static_cast<int64_t>(b) * R * kWMax + ent;
+    bool rej_over = false;
     for (int q = 0; q < nsr; ++q) {
         const uint32_t d = static_cast<uint32_t>(s_d[q]);
+        const int u0 = u;
         u = walk_masked<KMAX>(reinterpret_cast<const uint32_t*>(masks + s_moff[q]), q * k, u, d, k,
                               d <= static_cast<uint32_t>(setsize), w, nvalid);
+        // this node's rejections on this entry's path (the emit's node starts)
+        if (u >= 0) {
+            const int rj = u - u0 - k;
+            rej_over |= rj > 254;
+            rej[static_cast<int64_t>(q) * kWMax] = static_cast<uint8_t>(min(rj, 255));
+        }
     }
+    if (rej_over) atomicOr(&c->status, kStWords);  // a node with > 254 rejections: never seen, reported
     if (ent < bw) {
         uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
         const int dr = u < 0 ? -1 : u - tid - ndr;
@@ -722,12 +550,14 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
     }
 }
 
-// Every block from its true entry, one wave: the wave walks the block's
-// nodes in order, 64 words per step — a ballot of the words acceptable for the
-// current draw finds the next accepted one — and emits each node's positions
-// in random.sample's result order as absolute CSR entries.  Pool branch: the
-// swapped pool slots live in lanes (key, value), looked up by ballot;
-// selected-set branch: the node's selected values live in lanes.
+// Every block from its true entry: the block's nodes in lanes (one wave,
+// 64 nodes at a time).  Node m's first word on the true path is m * k plus the
+// rejections of the nodes before it (recorded per entry by the table kernel,
+// summed by a wave scan), so every lane walks its own node from its own
+// start: random.sample's result order as absolute CSR entries — pool branch
+// with the swapped slots in registers, selected-set branch with the picks in
+// registers — and rows below k whole.
+template <int KMAX>
 __global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, DevGraph g,
                                                        int hop, int k, int setsize, int R, int last, int gcn,
                                                        int32_t* __restrict__ pack) {
@@ -739,95 +569,116 @@ __global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restric
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
     const int j = hb.entry[b];
     const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    const int nw = 4 * ndr + 128;
+    const int nw = ndr + 3 * R * max(k, 1) + 64;
     const int nvalid = j < 0 ? 0 : load_words(wr, c, h.P0 + hb.dbase[b] + j, nw, w);
     __syncthreads();
     if (j < 0) return;  // reported by the chain
+    const int e = j - hb.blo[b];
+    const uint8_t* rej = hb.rej + static_cast<int64_t>(b) * R * kWMax + e;
     int32_t* ent = last ? pack + h.off[GS_PK_POS] : hb.ent;
-    int u = 0;
+    int m0 = 0, rej0 = 0;  // sampled nodes and their rejections before this chunk of nodes
     bool over = false;
-    for (int q = 0; q < nr; ++q) {
+    for (int q0 = 0; q0 < nr; q0 += 64) {
+        const int q = q0 + lane;
+        const bool on = q < nr;
         const int r = r0 + q;
-        const int32_t v = hb.dst[r];
-        const uint32_t d = static_cast<uint32_t>(hb.deg[r]);
-        const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
-        int32_t* out = ent + hb.pos_ptr[r];
-        const bool sampled = k > 0 && d >= static_cast<uint32_t>(k);
-        const int cnt = sampled ? k : static_cast<int>(d);
-        if (!sampled) {
-            for (int t = lane; t < cnt; t += 64) out[t] = base + t;
-        } else if (d <= static_cast<uint32_t>(setsize)) {
-            uint32_t mk = 0, mv = 0;  // lane t < nm: pool slot mk holds mv
-            int nm = 0;
-            for (int i = 0; i < k && !over;) {
-                const uint32_t m = d - i;
-                const int sh = __clz(m);
-                const int at = u + lane;
-                const uint32_t x = at < nvalid ? w[at] >> sh : 0xFFFFFFFFu;
-                const uint64_t acc = __ballot(x < m);
-                if (!acc) {
-                    u += 64;
-                    if (u >= nvalid) over = true;
-                    continue;
-                }
-                const int p = __ffsll(static_cast<unsigned long long>(acc)) - 1;
-                const uint32_t xs = __shfl(x, p, 64);
-                u += p + 1;
-                const uint64_t hx = __ballot(lane < nm && mk == xs);
-                const uint64_t hl = __ballot(lane < nm && mk == m - 1);
-                const uint32_t val = hx ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hx)) - 1, 64) : xs;
-                const uint32_t lastv = hl ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hl)) - 1, 64) : m - 1;
-                if (hx) {
-                    if (lane == __ffsll(static_cast<unsigned long long>(hx)) - 1) mv = lastv;
-                } else {
-                    if (lane == nm) {
-                        mk = xs;
-                        mv = lastv;
-                    }
-                    ++nm;
-                }
-                if (lane == 0) out[i] = base + static_cast<int32_t>(val);
-                ++i;
-            }
-        } else {
-            const int sh = __clz(d);
-            uint32_t selv = 0xFFFFFFFFu;  // lane t < n_sel: the t-th selected value
-            int n_sel = 0;
-            while (n_sel < k && !over) {
-                const int at = u + lane;
-                const uint32_t x = at < nvalid ? w[at] >> sh : 0xFFFFFFFFu;
-                uint64_t cand = __ballot(x < d);
-                int consumed = 64;
-                while (cand) {
-                    const int p = __ffsll(static_cast<unsigned long long>(cand)) - 1;
-                    cand &= cand - 1;
-                    const uint32_t xs = __shfl(x, p, 64);
-                    if (!__ballot(lane < n_sel && selv == xs)) {
-                        if (lane == n_sel) selv = xs;
-                        if (lane == 0) out[n_sel] = base + static_cast<int32_t>(xs);
-                        ++n_sel;
-                        if (n_sel == k) {
-                            consumed = p + 1;
+        const int32_t v = on ? hb.dst[r] : 0;
+        const uint32_t d = on ? static_cast<uint32_t>(hb.deg[r]) : 0u;
+        const bool sampled = on && k > 0 && d >= static_cast<uint32_t>(k);
+        // this node's index among the block's sampled nodes, its rejections
+        const uint64_t sb = __ballot(sampled);
+        const int m = m0 + __popcll(sb & ((1ull << lane) - 1ull));
+        const int rj = sampled ? rej[static_cast<int64_t>(m) * kWMax] : 0;
+        int inc = rj;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        int u = m * k + rej0 + inc - rj;  // the node's first word on the true path
+        if (on) {
+            const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
+            int32_t* out = ent + hb.pos_ptr[r];
+            const int cnt = sampled ? k : static_cast<int>(d);
+            if (!sampled) {
+                for (int t = 0; t < cnt; ++t) out[t] = base + t;
+            } else if (d <= static_cast<uint32_t>(setsize)) {
+                // pool branch: pool[x] for the accepted x, then pool[x] = pool[m - 1]
+                uint32_t mk[KMAX], mv[KMAX];
+                int nm = 0;
+                for (int i = 0; i < k; ++i) {
+                    const uint32_t mm = d - i;
+                    const int sh = __clz(mm);
+                    uint32_t x;
+                    for (;;) {
+                        if (u >= nvalid) {
+                            over = true;
+                            x = 0;
                             break;
                         }
+                        x = w[u++] >> sh;
+                        if (x < mm) break;
+                    }
+                    uint32_t val = x, lastv = mm - 1;
+                    bool found = false;
+#pragma unroll
+                    for (int t = 0; t < KMAX; ++t) {
+                        const bool live = t < nm;
+                        if (live && mk[t] == x) val = mv[t];
+                        if (live && mk[t] == mm - 1) lastv = mv[t];
+                    }
+#pragma unroll
+                    for (int t = 0; t < KMAX; ++t)
+                        if (t < nm && mk[t] == x) {
+                            mv[t] = lastv;
+                            found = true;
+                        }
+#pragma unroll
+                    for (int t = 0; t < KMAX; ++t)
+                        if (!found && t == nm) {
+                            mk[t] = x;
+                            mv[t] = lastv;
+                        }
+                    nm += found ? 0 : 1;
+                    out[i] = base + static_cast<int32_t>(val);
+                }
+            } else {
+                const int sh = __clz(d);
+                uint32_t sel[KMAX];
+                int n_sel = 0;
+                while (n_sel < k) {
+                    if (u >= nvalid) {
+                        over = true;
+                        break;
+                    }
+                    const uint32_t x = w[u++] >> sh;
+                    bool fresh = x < d;
+#pragma unroll
+                    for (int t = 0; t < KMAX; ++t) fresh &= !(t < n_sel && sel[t] == x);
+                    if (fresh) {
+#pragma unroll
+                        for (int t = 0; t < KMAX; ++t)
+                            if (t == n_sel) sel[t] = x;
+                        out[n_sel] = base + static_cast<int32_t>(x);
+                        ++n_sel;
                     }
                 }
-                u += consumed;
-                if (n_sel < k && u >= nvalid) over = true;
             }
-        }
-        if (lane == 0) {
             // empty neighbourhood after the self rule (non-gcn): no entry, or
             // a lone entry that is the node itself
             if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
+            if (last) {
+                pack[h.off[GS_PK_DST_IDS] + r] = v;
+                pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
+                if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
+            }
         }
-        if (last && lane == 0) {
-            pack[h.off[GS_PK_DST_IDS] + r] = v;
-            pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
-            if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
-        }
+        m0 += __popcll(sb);
+        rej0 += __shfl(inc, 63, 64);
     }
-    if (lane == 0 && over) atomicOr(&c->status, kStWords);
+    if (__ballot(over)) {
+        if (lane == 0) atomicOr(&c->status, kStWords);
+    }
 }
 
 // Roots after the pack (the host sampler's layout), totals for the host.
@@ -933,43 +784,41 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     mt_gen_kernel<<<1, kGenThreads, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
     gs::check_launch("mt_gen_kernel");
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
-    const size_t tab_lds = (R + 2 * kWMax) * sizeof(int32_t) + kWMax * sizeof(uint16_t) +
-                           (kWMax + 3 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
     const size_t mask_lds = static_cast<size_t>(R) * std::max(k, 1) * kMChunks * sizeof(uint64_t) +
                             (kMEntries + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
-    static const bool walk_tables = std::getenv("GS_DS_WALK_TABLES") != nullptr;  // A/B: word-by-word walks
     // selected-set values in registers: the unrolled duplicate test costs KMAX per accepted word
-    if (!walk_tables) {
-        const dim3 grid(static_cast<unsigned>(nb_max), kWMax / kMEntries);
-        if (k <= 8)
-            draw_masked_kernel<8><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-        else if (k <= 12)
-            draw_masked_kernel<12><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-        else if (k <= 16)
-            draw_masked_kernel<16><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-        else if (k <= 25)
-            draw_masked_kernel<25><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-        else
-            draw_masked_kernel<32><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-    } else if (k <= 8)
-        draw_tables_kernel<8><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    const dim3 grid(static_cast<unsigned>(nb_max), kWMax / kMEntries);
+    if (k <= 8)
+        draw_masked_kernel<8><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 12)
-        draw_tables_kernel<12><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+        draw_masked_kernel<12><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 16)
-        draw_tables_kernel<16><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+        draw_masked_kernel<16><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 25)
-        draw_tables_kernel<25><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+        draw_masked_kernel<25><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else
-        draw_tables_kernel<32><<<nb_max, 1024, tab_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
-    gs::check_launch("draw_tables_kernel");
+        draw_masked_kernel<32><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    gs::check_launch("draw_masked_kernel");
     const int ng_max = (nb_max + kMinG - 1) / kMinG;
     draw_compose_kernel<<<ng_max, 256, kComposeEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
     gs::check_launch("draw_compose_kernel");
     draw_chain_kernel<<<1, 1024, kChainEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
     gs::check_launch("draw_chain_kernel");
-    const size_t emit_lds = (4 * R * std::max(k, 1) + 128) * sizeof(uint32_t);
-    draw_emit_kernel<<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R, last ? 1 : 0, gcn,
-                                                   ds->pack_cur);
+    const size_t emit_lds = (4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
+#define GS_EMIT(KM)                                                                                               \
+    draw_emit_kernel<KM><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R, last ? 1 : 0, \
+                                                       gcn, ds->pack_cur)
+    if (k <= 8)
+        GS_EMIT(8);
+    else if (k <= 12)
+        GS_EMIT(12);
+    else if (k <= 16)
+        GS_EMIT(16);
+    else if (k <= 25)
+        GS_EMIT(25);
+    else
+        GS_EMIT(32);
+#undef GS_EMIT
     gs::check_launch("draw_emit_kernel");
 }
 
@@ -1067,6 +916,7 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
         h.gexit = ds->alloc<uint16_t>(ng * kWMax);
         h.gexit_last = ds->alloc<int32_t>(kWMax);
         h.entry = ds->alloc<int32_t>(nb);
+        h.rej = ds->alloc<uint8_t>(nb * r_of(k) * kWMax);
         h.ent = j + 1 < n_hops ? ds->alloc<int32_t>(ds->npos_max[j]) : nullptr;
         if (j + 1 < n_hops) {
             GS_REQUIRE(k >= 1, GS_EINVAL, "device sampler: hops before the last need a fanout >= 1");

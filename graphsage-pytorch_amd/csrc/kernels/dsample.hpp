@@ -69,6 +69,7 @@ struct HopBufs {
     int32_t* gexit_last;       // the last group's absolute exits [kWMax]
     int32_t* entry;            // true entry per block [nb_max]
     int32_t* ent;              // absolute CSR entries of the hop's samples (hops before the last)
+    uint8_t* rej;              // rejections of sampled node m of block b from entry e: [(b * R + m) * kWMax + e]
 };
 
 struct UnionBufs {
