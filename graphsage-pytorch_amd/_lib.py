@@ -150,6 +150,7 @@ _SIGS = {
     "gs_runner_destroy": (None, [_vp]),
     "gs_runner_release": (_i32, [_vp, _i64]),
     "gs_runner_progress": (_i32, [_vp, _p(_i64), _p(_i64)]),
+    "gs_runner_sync_rngs": (_i32, [_vp]),
     "gs_dsampler_create": (_i32, [_vp, _vp, _i32, _i64, _i32, _p(_vp)]),
     "gs_dsampler_destroy": (None, [_vp]),
     "gs_dsampler_set_rng": (_i32, [_vp, _vp, _i64, _vp]),
@@ -177,6 +178,7 @@ class RunnerConfig(ctypes.Structure):
         ("fanouts", _vp), ("n_hops", _i32), ("flags", _i32), ("n_streams", _i32), ("rngs", _vp),
         ("depth", _i32), ("comm", _vp), ("world", _i32), ("embed_out", _vp), ("embed_ld", _i64),
         ("merge", _i32), ("hold", _i32), ("ar_buckets", _i32), ("helpers", _i32), ("warm", _i32),
+        ("device_sampler", _i32),
     ]
 
 

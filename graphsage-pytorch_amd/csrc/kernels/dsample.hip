@@ -849,6 +849,16 @@ void check_status(int status) {
 
 }  // namespace
 
+namespace gs {
+bool dsampler_ready(gs_dsampler* ds) {
+    if (!ds || !ds->ran) return true;
+    const hipError_t e = hipEventQuery(ds->done);
+    if (e == hipErrorNotReady) return false;
+    hip_ok(e, "hipEventQuery(dsampler)");
+    return true;
+}
+}  // namespace gs
+
 extern "C" {
 
 int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hops, int64_t max_roots, int32_t flags,

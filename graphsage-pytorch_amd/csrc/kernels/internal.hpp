@@ -7,6 +7,7 @@
 #include "kcommon.hpp"
 
 struct gs_trainer;
+struct gs_dsampler;
 
 namespace gs {
 
@@ -120,5 +121,8 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
                 const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
                 const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
                 hipStream_t st, const int32_t* tids = nullptr, int tk = 0);
+
+// dsample.hip: whether the last gs_dsampler_run has completed (no wait).
+bool dsampler_ready(gs_dsampler* ds);
 
 }  // namespace gs

@@ -194,6 +194,35 @@ struct gs_runner {
     int device = 0;
     gs_runner_stats stats{};
 
+    // cfg.device_sampler: one gs_dsampler per stream, each on its own HIP
+    // stream; packs are written straight into a device ring of S + 3 entries
+    // (batch b's entry was last read by step b - S - 3, which issue() has
+    // waited for before enqueuing b).
+    struct DevStream {
+        gs_dsampler* ds = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t t0 = nullptr, t1 = nullptr;  // around the run: its device time
+        int64_t next = 0;                       // next batch to enqueue (w, w + S, ...)
+        int64_t inflight = -1;                  // enqueued, result not read yet
+        bool counted = false;                   // inflight already counted in `sampled`
+    };
+    struct DevResult {
+        int64_t hop_sizes[4 * GS_MAX_HOPS];
+        int64_t offsets[GS_MAX_HOPS * GS_PK_NFIELDS];
+        int64_t used = 0;
+        double sample_s = 0;
+    };
+    bool devmode = false;
+    std::vector<DevStream> dstreams;
+    int32_t* roots_dev = nullptr;
+    int64_t n_dpack = 0, dcap = 0;
+    std::vector<int32_t*> dpack;
+    std::vector<DevResult> dres;
+    void dev_enqueue(int w);
+    bool dev_take(int64_t b, bool block);
+    void dev_poll();
+    void dev_sync_rngs();
+
     ~gs_runner();
     void sampler_loop(gs::SamplerStream& s);
     void recycle(gs::SamplerStream& s, bool block);
@@ -325,13 +354,79 @@ void gs_runner::pull(int64_t b, int slot_id) {
     pulled = b + 1;
 }
 
+// Device sampler: enqueue stream w's next batch (one in flight per stream:
+// its result must be read before the sampler's next run overwrites it).
+void gs_runner::dev_enqueue(int w) {
+    using namespace gs;
+    DevStream& d = dstreams[w];
+    if (d.inflight >= 0) return;
+    const int64_t b = d.next;
+    if (b >= n_units || b >= release_mark.load()) return;
+    hip_ok(hipEventRecord(d.t0, d.st), "hipEventRecord");
+    const int rc = gs_dsampler_run(d.ds, roots_dev + b * cfg.batch, cfg.batch, dpack[b % n_dpack], dcap, d.st);
+    if (rc != GS_OK) fail(rc, gs_last_error());
+    hip_ok(hipEventRecord(d.t1, d.st), "hipEventRecord");
+    d.inflight = b;
+    d.counted = false;
+    d.next = b + cfg.n_streams;
+}
+
+// Device sampler: batch b's result (hop sizes, layout) into dres[b % ring];
+// block == false: false while its sampling is still running.
+bool gs_runner::dev_take(int64_t b, bool block) {
+    using namespace gs;
+    DevStream& d = dstreams[b % cfg.n_streams];
+    GS_REQUIRE(d.inflight == b, GS_EINVAL, "device sampler: batch not enqueued (past the release mark?)");
+    if (!block && !dsampler_ready(d.ds)) return false;
+    const auto tw = Clock::now();
+    DevResult& R = dres[b % n_dpack];
+    const int rc = gs_dsampler_result(d.ds, R.hop_sizes, R.offsets, &R.used);
+    if (rc != GS_OK) fail(rc, gs_last_error());
+    hip_ok(hipEventSynchronize(d.t1), "hipEventSynchronize");
+    float ms = 0.f;
+    hip_ok(hipEventElapsedTime(&ms, d.t0, d.t1), "hipEventElapsedTime");
+    R.sample_s = 1e-3 * ms;
+    stats.wait_sample_s += secs(tw, Clock::now());
+    if (!d.counted) sampled.fetch_add(1);
+    d.inflight = -1;
+    d.counted = false;
+    return true;
+}
+
+// Device sampler: count finished sampling runs (progress()).
+void gs_runner::dev_poll() {
+    for (auto& d : dstreams)
+        if (d.inflight >= 0 && !d.counted && gs::dsampler_ready(d.ds)) {
+            d.counted = true;
+            sampled.fetch_add(1);
+        }
+}
+
+// Device sampler: every stream's state back into its rng (waits for the
+// stream's run in flight).
+void gs_runner::dev_sync_rngs() {
+    using namespace gs;
+    for (int w = 0; w < static_cast<int>(dstreams.size()); ++w) {
+        DevStream& d = dstreams[w];
+        if (!d.ds) continue;
+        uint32_t mt[624];
+        int64_t pos = 0;
+        int rc = gs_dsampler_get_rng(d.ds, mt, &pos, d.st);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+        rc = gs_rng_set_state(cfg.rngs[w], mt, pos);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+    }
+}
+
 // Pull batch b's pack to the device (unless pulled ahead) and gather its
 // layer 1, both on the side stream; with pull_ahead, then pull batch b+1's
 // pack if it is sampled.  block == false: return false if b is not sampled yet.
 bool gs_runner::issue(int64_t b, bool block) {
     using namespace gs;
     int slot_id = -1;
-    if (pulled <= b) {
+    if (devmode) {
+        if (!dev_take(b, block)) return false;
+    } else if (pulled <= b) {
         slot_id = take_slot(b, block);
         if (slot_id < 0) return false;
     }
@@ -343,6 +438,18 @@ bool gs_runner::issue(int64_t b, bool block) {
         if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
     }
     stats.wait_ring_s += secs(tr, Clock::now());
+    if (devmode) {
+        const DevResult& R = dres[b % n_dpack];
+        const int rc = gs_trainer_gather(cfg.trainer, dpack[b % n_dpack], R.hop_sizes, R.offsets, k, side);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+        hip_ok(hipEventRecord(gathered[k], side), "hipEventRecord");
+        inflight[k] = {-1, static_cast<int>(b % n_dpack)};
+        issued = b + 1;
+        // this stream's next batch, b + S, into the ring entry step b - 3 read
+        // (wait_entry above saw it complete)
+        dev_enqueue(static_cast<int>(b % cfg.n_streams));
+        return true;
+    }
     if (pulled <= b) pull(b, slot_id);
     const Inflight f = pulled_slot[b % kPack];
     PackSlot& slot = streams[f.stream]->slots[f.slot];
@@ -360,6 +467,20 @@ bool gs_runner::issue(int64_t b, bool block) {
 }
 
 gs_runner::~gs_runner() {
+    if (devmode) {
+        for (auto& d : dstreams)
+            if (d.st) (void)hipStreamSynchronize(d.st);
+        try {
+            dev_sync_rngs();
+        } catch (...) {
+        }
+        for (auto& d : dstreams) {
+            if (d.ds) gs_dsampler_destroy(d.ds);
+            if (d.t0) (void)hipEventDestroy(d.t0);
+            if (d.t1) (void)hipEventDestroy(d.t1);
+            if (d.st) (void)hipStreamDestroy(d.st);
+        }
+    }
     stop = true;
     for (auto& s : streams) {
         { std::lock_guard<std::mutex> lk(s->mu); }  // a sampler between its predicate check and its wait sees stop
@@ -388,6 +509,9 @@ gs_runner::~gs_runner() {
         }
     for (int d = 0; d < kPack; ++d)
         if (dev[d]) (void)hipFree(dev[d]);
+    for (int32_t* p : dpack)
+        if (p) (void)hipFree(p);
+    if (roots_dev) (void)hipFree(roots_dev);
     for (int d = 0; d < kDev; ++d) {
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
         if (fwd_done[d]) {
@@ -530,7 +654,41 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         hip_ok(hipMalloc(&r->ws, r->ws_bytes), "hipMalloc(ws)");
     }
     const int32_t S = cfg->n_streams;
-    for (int32_t w = 0; w < S; ++w) {
+    r->devmode = cfg->device_sampler != 0;
+    if (r->devmode) {
+        GS_REQUIRE(r->merge == 1, GS_EINVAL, "device_sampler: merge must be 1");
+        GS_REQUIRE(!(cfg->flags & GS_SAMPLE_FULL), GS_EINVAL, "device_sampler: no GS_SAMPLE_FULL");
+        std::vector<int32_t> r32(r->roots.size());
+        for (size_t i = 0; i < r32.size(); ++i) {
+            GS_REQUIRE(r->roots[i] >= 0 && r->roots[i] < (int64_t(1) << 31), GS_ERANGE, "root id out of range");
+            r32[i] = static_cast<int32_t>(r->roots[i]);
+        }
+        hip_ok(hipMalloc(&r->roots_dev, r32.size() * sizeof(int32_t)), "hipMalloc(roots)");
+        hip_ok(hipMemcpy(r->roots_dev, r32.data(), r32.size() * sizeof(int32_t), hipMemcpyHostToDevice), "hipMemcpy");
+        r->dstreams.resize(S);
+        for (int32_t w = 0; w < S; ++w) {
+            gs_runner::DevStream& d = r->dstreams[w];
+            hip_ok(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking), "hipStreamCreate(dsampler)");
+            hip_ok(hipEventCreate(&d.t0), "hipEventCreate");
+            hip_ok(hipEventCreate(&d.t1), "hipEventCreate");
+            int rc = gs_dsampler_create(cfg->graph, r->fanouts.data(), cfg->n_hops, cfg->batch,
+                                        cfg->flags & (GS_SAMPLE_GCN | GS_SAMPLE_FAIL_EMPTY), &d.ds);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            uint32_t mt[624];
+            int64_t pos = 0;
+            rc = gs_rng_get_state(cfg->rngs[w], mt, &pos);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            rc = gs_dsampler_set_rng(d.ds, mt, pos, d.st);
+            if (rc != GS_OK) fail(rc, gs_last_error());
+            d.next = w;
+        }
+        r->dcap = std::max<int64_t>(r->cap, gs_dsampler_pack_bound(r->dstreams[0].ds, cfg->batch));
+        r->n_dpack = S + 3;
+        r->dpack.assign(r->n_dpack, nullptr);
+        for (auto& p : r->dpack) hip_ok(hipMalloc(&p, r->dcap * sizeof(int32_t)), "hipMalloc(pack)");
+        r->dres.resize(r->n_dpack);
+    }
+    for (int32_t w = 0; w < S && !r->devmode; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
         if (cfg->helpers > 0 && gs_team_create(cfg->helpers, &s->team) != GS_OK) fail(GS_EINVAL, gs_last_error());
@@ -546,6 +704,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         r->streams.push_back(std::move(s));
     }
     r->release_mark = cfg->hold ? 0 : INT64_MAX;
+    for (int32_t w = 0; w < S && r->devmode; ++w) r->dev_enqueue(w);
     if (cfg->comm && cfg->ar_buckets == 2 && !cfg->embed_out && cfg->n_hops >= 2) {
         hip_ok(hipStreamCreateWithFlags(&r->comm_stream, hipStreamNonBlocking), "hipStreamCreate(comm)");
         hip_ok(hipEventCreateWithFlags(&r->upper_ready, hipEventDisableTiming), "hipEventCreate");
@@ -580,7 +739,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         gs_runner* rp = r.get();
         s->th = std::thread([rp, sp] { rp->sampler_loop(*sp); });
     }
-    if (cfg->warm) {
+    if (cfg->warm && !r->devmode) {
         std::unique_lock<std::mutex> lk(r->warm_mu);
         r->warm_cv.wait(lk, [&] { return r->warmed == static_cast<int>(r->streams.size()); });
     }
@@ -632,10 +791,25 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         const auto t1 = Clock::now();
         r->stats.wait_gather_s += secs(tg, t1);
         const gs::Inflight f = r->inflight[k];
-        SamplerStream& s = *r->streams[f.stream];
-        PackSlot& slot = s.slots[f.slot];
+        const int64_t* hop_sizes;
+        const int64_t* offsets;
+        int64_t used;
+        double sample_s;
+        if (r->devmode) {
+            const gs_runner::DevResult& R = r->dres[f.slot];
+            hop_sizes = R.hop_sizes;
+            offsets = R.offsets;
+            used = R.used;
+            sample_s = R.sample_s;
+        } else {
+            const PackSlot& slot = r->streams[f.stream]->slots[f.slot];
+            hop_sizes = slot.hop_sizes;
+            offsets = slot.offsets;
+            used = slot.used;
+            sample_s = slot.sample_s;
+        }
         const auto t2 = t1;
-        const int64_t need = gs_trainer_ws_bytes(r->cfg.trainer, slot.hop_sizes);
+        const int64_t need = gs_trainer_ws_bytes(r->cfg.trainer, hop_sizes);
         GS_REQUIRE(need >= 0, GS_EINVAL, gs_last_error());
         if (need > r->ws_bytes) {
             hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
@@ -644,12 +818,12 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             r->ws_bytes = need + need / 4 + (1 << 20);
             hip_ok(hipMalloc(&r->ws, r->ws_bytes), "hipMalloc(ws)");
         }
-        const int64_t pack_total = slot.used - r->cfg.batch;
+        const int64_t pack_total = used - r->cfg.batch;
         bool consumed_flag = false;
-        int32_t* pk = r->dev[b % gs_runner::kPack];
+        int32_t* pk = r->devmode ? r->dpack[f.slot] : r->dev[b % gs_runner::kPack];
         auto t3 = Clock::now();
         if (r->cfg.embed_out) {  // inference: the forward into this batch's output rows
-            const int rc = gs_trainer_forward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets, k, r->ws,
+            const int rc = gs_trainer_forward_gathered(r->cfg.trainer, pk, hop_sizes, offsets, k, r->ws,
                                                        r->ws_bytes,
                                                        r->cfg.embed_out + b * r->merge * r->cfg.batch * r->cfg.embed_ld,
                                                        st);
@@ -657,7 +831,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             t3 = Clock::now();
         } else {
             r->cur_k = k;
-            int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, slot.hop_sizes, slot.offsets,
+            int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, hop_sizes, offsets,
                                                           pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
                                                           st);
             r->cur_k = -1;
@@ -697,9 +871,9 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             hip_ok(hipEventRecord(r->dev_done[k], st), "hipEventRecord");  // ring entry k free again
             r->dev_busy[k] = true;
         }
-        for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(slot.hop_sizes[q]);
-        r->stats.sample_s += slot.sample_s;
-        s.copying.push_back(f.slot);
+        for (int q = 0; q < 4 * GS_MAX_HOPS; ++q) r->stats.hop_sizes[q] += static_cast<double>(hop_sizes[q]);
+        r->stats.sample_s += sample_s;
+        if (!r->devmode) r->streams[f.stream]->copying.push_back(f.slot);
         ++r->next_batch;
         ++r->stats.steps;
         const auto t4 = Clock::now();
@@ -732,12 +906,21 @@ int gs_runner_release(gs_runner* r, int64_t mark) {
         { std::lock_guard<std::mutex> lk(s->mu); }
         s->cv.notify_all();
     }
+    for (int w = 0; w < static_cast<int>(r->dstreams.size()); ++w) r->dev_enqueue(w);
+    GS_API_END
+}
+
+int gs_runner_sync_rngs(gs_runner* r) {
+    GS_API_BEGIN
+    GS_REQUIRE(r, GS_EINVAL, "NULL argument");
+    if (r->devmode) r->dev_sync_rngs();
     GS_API_END
 }
 
 int gs_runner_progress(const gs_runner* r, int64_t* sampled, int64_t* consumed) {
     GS_API_BEGIN
     GS_REQUIRE(r && sampled && consumed, GS_EINVAL, "NULL argument");
+    if (r->devmode) const_cast<gs_runner*>(r)->dev_poll();
     *sampled = r->sampled.load();
     *consumed = r->next_batch;
     GS_API_END

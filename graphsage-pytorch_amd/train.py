@@ -341,10 +341,19 @@ class Runner:
     `helpers`: helper threads per sampler stream (gs_team; same draws, lower
     per-batch latency).  `warm`: every sampler thread samples one throwaway
     batch (its last, from a copy of its rng) before the constructor returns,
-    so measured batches never pay a cold sampling context."""
+    so measured batches never pay a cold sampling context.
+    `sampler="device"`: the streams sample on the GPU instead (SURVEY §8 f-4,
+    gs_dsampler: one per stream, each on its own HIP stream), writing every
+    pack straight into the device ring — no host sampler threads; the same
+    packs and stream consumption as the host sampler.  The rngs are updated
+    at ``sync_rngs()`` and ``close()``."""
 
     def __init__(self, trainer, graph, batches, rngs, fanouts, gcn=False, fail_empty=False, depth=4,
-                 comm=None, embed_out=None, merge=1, hold=False, ar_buckets=1, helpers=0, warm=False):
+                 comm=None, embed_out=None, merge=1, hold=False, ar_buckets=1, helpers=0, warm=False,
+                 sampler="host"):
+        if sampler not in ("host", "device"):
+            raise ValueError("sampler must be 'host' or 'device'")
+        self.sampler = sampler
         self.trainer, self.graph = trainer, graph
         self.embed_out = embed_out
         self.rngs = list(rngs)
@@ -359,7 +368,8 @@ class Runner:
             n_hops=len(self.fanouts), flags=flags, n_streams=len(self.rngs),
             rngs=ctypes.cast(self._rng_ptrs, ctypes.c_void_p), depth=depth,
             comm=comm._h.value if comm is not None else None, world=comm.world if comm is not None else 1,
-            hold=int(bool(hold)), ar_buckets=int(ar_buckets), helpers=int(helpers), warm=int(bool(warm)))
+            hold=int(bool(hold)), ar_buckets=int(ar_buckets), helpers=int(helpers), warm=int(bool(warm)),
+            device_sampler=int(sampler == "device"))
         if embed_out is not None:
             n_rows = self.batches.shape[0] * self.batches.shape[1]
             if not (embed_out.is_contiguous() and embed_out.dtype == torch.float32
@@ -382,6 +392,11 @@ class Runner:
         check(lib().gs_runner_run(self._h, int(n_steps), self.trainer.loss.data_ptr(),
                                   _lib.stream_ptr(self.trainer.device)))
         return self.embed_out if self.embed_out is not None else self.trainer.loss
+
+    def sync_rngs(self):
+        """sampler="device": copy the device streams' states back into the rngs
+        (every batch sampled so far, consumed or not)."""
+        check(lib().gs_runner_sync_rngs(self._h))
 
     def release(self, mark):
         """hold=True runners: let the sampler threads start batches < mark."""

@@ -598,8 +598,9 @@ typedef struct {
      * 0) = one in-place all-reduce of the flat gradient after the backward;
      * 2 = the upper layers' and classifier's gradients [W2 .. | Wc | bc]
      * (final once the layers >= 2 backward has run) all-reduced on a comm
-     * stream under the layer-1 weight-gradient GEMM, then W1 on the main
-     * stream.  Same sums either way (the buckets are disjoint ranges). */
+     * stream under the layer-1 weight-gradient GEMM, then W1 after them on
+     * the same comm stream (one stream order on every rank).  Same sums
+     * either way (the buckets are disjoint ranges). */
     int32_t ar_buckets;
     /* Helper threads per sampler stream (gs_team): lower per-batch latency
      * for the same draws — for few streams (the reference-sequence S = 1
@@ -611,6 +612,15 @@ typedef struct {
      * sampled ahead — so that no measured batch pays the first-use costs of
      * the thread's sampling context (allocation, page faults). */
     int32_t warm;
+    /* device_sampler != 0 (training and merge <= 1 inference): the S streams
+     * sample on the GPU — one gs_dsampler per stream, each on
+     * its own HIP stream, seeded from rngs[w] — and write every pack straight
+     * into the device pack ring: no sampler threads, pinned slots or pulls.
+     * Stream w samples batches w, w+S, ... exactly as the host sampler would
+     * (same packs, same stream consumption); batch b+S is sampled while the
+     * device runs the steps before it.  The rngs are written back at
+     * gs_runner_sync_rngs and gs_runner_destroy. */
+    int32_t device_sampler;
 } gs_runner_config;
 
 typedef struct {
@@ -641,6 +651,11 @@ int gs_runner_release(gs_runner* r, int64_t mark);
  * completed, *consumed = steps issued by gs_runner_run; sampled - consumed
  * is the number of batches sampled ahead of the device at this instant. */
 int gs_runner_progress(const gs_runner* r, int64_t* sampled, int64_t* consumed);
+/* device_sampler runners: copy every device stream's state back into its
+ * rngs[w] (waits for the stream's sampling in flight; the state then
+ * includes every batch sampled so far, consumed or not — as the host
+ * sampler threads' rngs do).  Host-sampler runners: no-op. */
+int gs_runner_sync_rngs(gs_runner* r);
 void gs_runner_destroy(gs_runner* r);
 
 #ifdef __cplusplus

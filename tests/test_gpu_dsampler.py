@@ -172,3 +172,95 @@ def test_device_multi_hop_matches_host(graph, fan, gcn):
         mt_d, pos_d = ds.get_rng()
         assert pos_d == pos_h
         np.testing.assert_array_equal(mt_d, mt_h)
+
+
+# ---------------------------------------------------------------------------
+# Straight against the reference: the vectors captured by importing the
+# reference (tests/golden/make_golden.py: per-hop unions, sets and the
+# `random` state after GraphSage.forward's sampling, models.py:246-251,
+# :277-289) replayed through the device sampler alone — no host sampler in
+# the comparison.
+
+G = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden")
+
+
+def _golden_graph(name):
+    g = np.load(__import__("os").path.join(G, "graphs.npz"))
+    return gs.CSRGraph.from_pairs(g[f"{name}_src"], g[f"{name}_dst"], int(g[f"{name}_n"][0]))
+
+
+@pytest.mark.parametrize("name", ["cora", "pubmed", "rmat"])
+def test_device_sampler_replays_reference_vectors(name):
+    G_ = _golden_graph(name)
+    row_ptr, col = G_.row_ptr(), G_.col()
+    S = np.load(__import__("os").path.join(G, f"sample_{name}.npz"))
+    n_cases = 0
+    for key in sorted({k.split("__")[0] for k in S.files}):
+        seed = int(key.split("_")[0][1:])
+        fan = np.array([int(x) for x in key.split("_f")[1].split("-")], np.int32)
+        if fan.max() > 32 or (fan[:-1] < 1).any():
+            continue  # outside the device sampler's fanouts (<= 32; >= 1 before the last hop)
+        roots = S[key + "__roots"]
+        ds = gs.sampler.DeviceSampler(G_, fan, max(1, len(roots)))
+        ds.set_rng(gs.RNG(seed))
+        pack, sizes, offs, used = ds.run(roots)
+        pk = pack[:used].cpu().numpy()
+        L_ = len(fan)
+        frontier = np.asarray(roots, np.int64)
+        for j in range(1, L_ + 1):
+            nd = int(sizes[j - 1, 0])
+            assert nd == len(frontier), (key, j)
+            sp, si = S[f"{key}__h{j}_set_ptr"], S[f"{key}__h{j}_set_items"]
+            if j < L_:
+                union = S[f"{key}__h{j}_union"]
+                o = offs[j - 1]
+                nbr_ptr = pk[o[L.GS_PK_NBR_PTR]:o[L.GS_PK_NBR_PTR] + nd + 1]
+                nbr = pk[o[L.GS_PK_NBR]:o[L.GS_PK_NBR] + int(sizes[j - 1, 3])]
+                self_ = pk[o[L.GS_PK_SELF]:o[L.GS_PK_SELF] + nd]
+                for r in range(nd):
+                    got = set(union[nbr[nbr_ptr[r]:nbr_ptr[r + 1]]].tolist()) | {int(union[self_[r]])}
+                    assert got == set(si[sp[r]:sp[r + 1]].tolist()), (key, j, r)
+                # the next frontier in CPython set order = the next hop's destinations
+                o2 = offs[L_ - 1] if j + 1 == L_ else offs[j]
+                fld = L.GS_PK_DST_IDS if j + 1 == L_ else None
+                if fld is not None:
+                    np.testing.assert_array_equal(pk[o2[fld]:o2[fld] + len(union)], union, err_msg=key)
+                frontier = union
+            elif f"{key}__h{j}_set_ptr" in S.files:
+                o = offs[j - 1]
+                pos_ptr = pk[o[L.GS_PK_POS_PTR]:o[L.GS_PK_POS_PTR] + nd + 1]
+                pos = pk[o[L.GS_PK_POS]:o[L.GS_PK_POS] + int(sizes[j - 1, 1])]
+                dst = pk[o[L.GS_PK_DST_IDS]:o[L.GS_PK_DST_IDS] + nd]
+                for r in range(nd):
+                    got = set(col[pos[pos_ptr[r]:pos_ptr[r + 1]]].tolist()) | {int(dst[r])}
+                    assert got == set(si[sp[r]:sp[r + 1]].tolist()), (key, j, r)
+        mt, p = ds.get_rng()
+        np.testing.assert_array_equal(np.append(mt.astype(np.int64), p), S[key + "__state"], err_msg=key)
+        n_cases += 1
+    assert n_cases >= 4
+
+
+def test_device_sampler_fullsize_rmat2m_packs():
+    """The headline workload (bench.py rmat2m: scale 21, 20 M pairs, B = 512,
+    fanouts 25, 10): eight consecutive batches on one stream, pack and stream
+    state bit-identical to the host sampler after every batch."""
+    train = __import__("importlib").import_module("graphsage-pytorch_amd.train")
+    src, dst = gs.rmat_pairs(21, 20_000_000, seed=824, n_threads=16)
+    G_ = gs.CSRGraph.from_pairs(src, dst, 1 << 21, n_threads=16)
+    cand = np.nonzero(G_.degrees() > 0)[0]
+    batches = list(train.rank_batches(cand, 512, 0, 1, 1824))[:8]
+    fan = np.array([25, 10], np.int32)
+    rng = gs.RNG(824)
+    ds = gs.sampler.DeviceSampler(G_, fan, 512)
+    ds.set_rng(rng)
+    pack = torch.zeros(ds.pack_bound(512), dtype=torch.int32, device="cuda")
+    for b, roots in enumerate(batches):
+        ref, sizes, offs, used = host_pack(G_, rng, roots, fan)
+        p, dsz, doff, dused = ds.run(roots, pack)
+        assert dused == used
+        np.testing.assert_array_equal(dsz, sizes)
+        assert_packs_equal(p[:used].cpu().numpy(), ref, sizes, offs, 512, f"batch {b}")
+        mt_h, pos_h = rng.getstate()
+        mt_d, pos_d = ds.get_rng()
+        assert pos_d == pos_h
+        np.testing.assert_array_equal(mt_d, mt_h)

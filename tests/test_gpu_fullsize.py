@@ -188,3 +188,34 @@ def test_fullsize_f128_mean_runner_vs_oracle(wl, adj):
     ops.fill_uniform(X128, SEED)
     tr, losses, sizes = _held_runner(wl, X128, "MEAN")
     _oracle_steps(wl, adj, X128.cpu(), "MEAN", 128, False, 1e-4, tr, losses, sizes)
+
+
+@pytest.mark.parametrize("S_", [1, 2])
+def test_fullsize_device_sampler_runner_matches_host(wl, S_):
+    """SURVEY §8 f-4 as a training path: Runner(sampler="device") — packs
+    sampled on the GPU, no host sampler threads — over the same batches and
+    streams as the host-sampler runner (held until release, as the bench
+    runs): bitwise the same losses, parameters, hop sizes, and the same
+    stream states afterwards (the reference's `random` consumption)."""
+    out = {}
+    for mode in ("host", "device"):
+        tr = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], C, fanouts=FAN, seed=SEED)
+        rngs = [train.make_rng(SEED, 0, w) for w in range(S_)]
+        r = train.Runner(tr, wl["graph"], wl["batches"], rngs, FAN, depth=2, hold=True, sampler=mode)
+        time.sleep(0.1)
+        assert r.progress() == (0, 0)
+        r.release(len(wl["batches"]))
+        losses = []
+        for _ in wl["batches"]:
+            r.run(1)
+            losses.append(float(tr.loss.item()))
+        sizes = r.stats()["hop_sizes_sum"]
+        r.close()
+        out[mode] = (tr.p.params.clone(), losses, sizes, [g.getstate() for g in rngs])
+    (p_h, l_h, s_h, st_h), (p_d, l_d, s_d, st_d) = out["host"], out["device"]
+    assert l_h == l_d
+    assert torch.equal(p_h, p_d)
+    np.testing.assert_array_equal(s_h, s_d)
+    for (mt_h, pos_h), (mt_d, pos_d) in zip(st_h, st_d):
+        assert pos_h == pos_d
+        np.testing.assert_array_equal(mt_h, mt_d)
