@@ -261,10 +261,16 @@ class GraphSage(nn.Module):
                 per-node sets and neighbour lists are built beside the draws).
                 0 = none.  MAX keeps the team-less path, whose sample is
                 complete before the empty-neighbourhood IndexError.
+      device_sampler : sample on the GPU (sampler.DeviceSampler):
+                the stream's state moves to the device and back around each
+                forward, the pack is written in device memory — the same
+                draws, pack and `random` state as the host sampler (fanouts
+                1..32 before the last hop, <= 32 at it).  For large batches
+                (an apply_model forward over an extended batch).
     """
 
     def __init__(self, num_layers, input_size, out_size, raw_features, adj_lists, device, gcn=False,
-                 agg_func='MEAN', *, fanouts=None, rng=None, sampler_helpers=0):
+                 agg_func='MEAN', *, fanouts=None, rng=None, sampler_helpers=0, device_sampler=False):
         super().__init__()
         self.input_size = input_size
         self.out_size = out_size
@@ -283,6 +289,12 @@ class GraphSage(nn.Module):
         self._pin = None        # pinned pack buffer of the team path
         self._pin_ev = None     # its last H2D copy
         self._graph = adj_lists if isinstance(adj_lists, CSRGraph) else None
+        self.device_sampler = bool(device_sampler)
+        if self.device_sampler:
+            ks = self.fanouts
+            if any(k is None or int(k) > 32 for k in ks) or any(int(k) < 1 for k in ks[:-1]):
+                raise ValueError("device_sampler: fanouts must be <= 32 (and >= 1 before the last hop)")
+        self._dsampler = None   # sampler.DeviceSampler (lazy, grown with the batch)
         for index in range(1, num_layers + 1):
             layer_size = out_size if index != 1 else input_size
             setattr(self, 'sage_layer' + str(index), SageLayer(layer_size, out_size, gcn=self.gcn))
@@ -295,7 +307,7 @@ class GraphSage(nn.Module):
                             "save its state_dict() instead")
         state = self.__dict__.copy()
         state["_graph"] = None
-        state["_team"] = state["_pin"] = state["_pin_ev"] = None
+        state["_team"] = state["_pin"] = state["_pin_ev"] = state["_dsampler"] = None
         return state
 
     def __del__(self):
@@ -353,6 +365,40 @@ class GraphSage(nn.Module):
         ds._native = (sizes, offs)
         return ds
 
+    def _draw_device(self, roots, device):
+        """The forward's sample drawn on the GPU (gs_dsampler): the stream's
+        state in, the pack in device memory, the advanced state out — the
+        draws, pack and `random` state of the host sampler."""
+        from .sampler import DeviceSampler
+        n = len(roots)
+        dev = torch.device(device)
+        if self._dsampler is None or self._dsampler_cap < n or self._dsampler.device != dev:
+            cap = max(n, 512)
+            self._dsampler = DeviceSampler(self.graph, self.fanouts, cap, gcn=self.gcn,
+                                           fail_empty=self.agg_func == "MAX", device=dev)
+            self._dsampler_cap = cap
+        ds = self._dsampler
+        rng = self.rng if self.rng is not None else RNG.from_python(_pyrandom)
+        ds.set_rng(rng)
+        try:
+            pack, sizes, offs, used = ds.run(roots)
+        except IndexError:
+            # MAX over an empty neighbourhood: the reference raises after its
+            # sampling consumed the stream (models.py:321-325)
+            rng.setstate(*ds.get_rng())
+            if self.rng is None:
+                rng.to_python(_pyrandom)
+            raise IndexError("MAX aggregation over an empty neighbourhood (reference: models.py:321-325)")
+        rng.setstate(*ds.get_rng())
+        if self.rng is None:
+            rng.to_python(_pyrandom)
+        L = len(self.fanouts)
+        hs = np.zeros(4 * L, np.int64)
+        hs[:] = np.asarray(sizes, np.int64).reshape(-1)[:4 * L]
+        out = DeviceSample(_PackInfo(L, hs, np.asarray(offs, np.int64).reshape(-1)), device, buf=pack[:used])
+        out._native = (hs, np.asarray(offs, np.int64).reshape(-1))
+        return out
+
     @staticmethod
     def _roots(nodes_batch):
         if isinstance(nodes_batch, torch.Tensor):
@@ -369,7 +415,9 @@ class GraphSage(nn.Module):
                                "cuda tensor (the reference's --cuda path, main.py:52)")
         if self.agg_func not in ("MEAN", "MAX"):
             raise ValueError(f"agg_func must be 'MEAN' or 'MAX', got {self.agg_func!r}")
-        if self.sampler_helpers > 0 and self.agg_func == "MEAN":
+        if self.device_sampler:
+            ds = self._draw_device(roots, X.device)
+        elif self.sampler_helpers > 0 and self.agg_func == "MEAN":
             ds = self._draw_pack(roots, X.device)
         else:
             s = self._draw(roots, self.fanouts)

@@ -455,3 +455,35 @@ def test_kernel_timer_sites_strided(gs, every):
         assert (out[:got] > 0).all()
         assert lib.gs_trainer_kernel_name(t._h, site).decode().startswith(("void gs::", "gs::"))
     runner.close()
+
+
+@pytest.mark.parametrize("name,gcn,fanouts,agg", [("cora", False, [10, 10], "MEAN"), ("pubmed", False, [10, 10], "MEAN"),
+                                                  ("rmat", True, [25, 10], "MEAN"), ("rmat", False, [5, 4, 3], "MAX"),
+                                                  ("pubmed", False, [10, 10], "MAX")])
+def test_graphsage_device_sampler_bitwise(gs, name, gcn, fanouts, agg):
+    """device_sampler=True (the forward's sampling on the GPU,
+    the module-global `random` state moved to the device and back): the
+    embeddings, weight gradients and `random` state after every forward are
+    bitwise those of the host sampler, over three batches (one large)."""
+    graph, g, n = _graph(gs, name)
+    X = torch.from_numpy(_features(name, n)).to(DEV)
+    out = []
+    for on in (False, True):
+        torch.manual_seed(5)
+        model = models.GraphSage(len(fanouts), X.shape[1], 128, X, graph, DEV, gcn=gcn, fanouts=fanouts, agg_func=agg,
+                                 device_sampler=on).to(DEV)
+        random.seed(21)
+        embs, states = [], []
+        nz = np.nonzero(graph.degrees())[0]
+        for b, B in enumerate([300, 17, 2000]):
+            roots = nz[b::3][:B].tolist()
+            emb = model(roots)
+            (emb * torch.from_numpy(uniform_features(8 + b, len(roots), 128)).to(DEV)).sum().backward()
+            embs.append(emb.detach().cpu())
+            states.append(random.getstate())
+        grads = [getattr(model, f"sage_layer{i}").weight.grad.cpu() for i in range(1, len(fanouts) + 1)]
+        out.append((embs, grads, states))
+    (e0, g0, s0), (e1, g1, s1) = out
+    assert s0 == s1
+    for a, b in zip(e0 + g0, e1 + g1):
+        assert torch.equal(a, b)
