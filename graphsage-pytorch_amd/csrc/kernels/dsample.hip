@@ -940,6 +940,8 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
             u.fresh = ds->alloc<int32_t>(ds->npos_max[j] + ndj);
             u.tcnt = ds->alloc<int32_t>(ds->nd_max[j + 1] + 1);
             u.fmask = ds->alloc<uint64_t>(ndj);
+            u.sched = ds->alloc<int32_t>(2 * (kMaxStages + 1));
+            u.skeys = ds->alloc<int32_t>(2 * static_cast<int64_t>(kBigKeys));
             if (!ds->mark) {
                 ds->mark = ds->alloc<uint64_t>(g.n_nodes);
                 hip_ok(hipMemset(ds->mark, 0, g.n_nodes * sizeof(uint64_t)), "hipMemset(mark)");

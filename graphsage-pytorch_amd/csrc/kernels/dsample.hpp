@@ -38,6 +38,7 @@ struct HopCtl {
     int32_t j_end;
     int32_t n_empty;
     int32_t n_src, n_nbr;      // hops before the last (union, lists)
+    int32_t big;               // the union's table outgrew LDS uint32 slots: ubig_kernel builds it
     int64_t P0;                // absolute stream position at the hop's first draw
     int64_t need_end;          // words the hop may read (exclusive)
     int32_t off[GS_PK_NFIELDS];
@@ -83,11 +84,15 @@ struct UnionBufs {
     int32_t* fresh;            // keys new to the union, in insertion order, [npos_max + nd_max]
     int32_t* tcnt;             // transposed counts / cursors, [nd_next_max + 1]
     uint64_t* fmask;           // per run: bit q = item q is new to the union, [nd_max]
+    int32_t* sched;            // resize schedule (run, mask) of a big union, [2 * (kMaxStages + 1)]
+    int32_t* skeys;            // a big union's stage keys by priority, two stages, [2 * kBigKeys]
     int32_t* lid;              // [n_nodes]: a union key's position in the next frontier (this hop's keys only)
 };
 
 constexpr int kSmallSet = 128;      // table slots of one samp_neighs set (k <= 32)
-constexpr int kUnionMax = 16384;    // table slots of a frontier union in LDS
+constexpr int kUnionMax = 16384;    // table slots of a frontier union in LDS (uint32 priorities)
+constexpr int kUnionBig = 65536;    // ... with uint16 priorities, keys in global memory (ubig_kernel)
+constexpr int kBigKeys = kUnionBig * 3 / 5 + 1024;  // a big stage's keys (its table <= 3/5 full)
 constexpr int kMaxStages = 24;
 
 

@@ -354,6 +354,199 @@ __device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const 
     return rounds + 1;
 }
 
+// The next frontier in the final table's slot order, each key's position in
+// it (lid), the pack layout of this hop, the transposed counts zeroed.
+// key_at(slot) -> key or -1.
+template <typename KeyAt>
+__device__ __forceinline__ void finish_union(Ctl* c, const HopBufs& hb, const UnionBufs& ub, const HopBufs& next,
+                                             int hop, int gcn, int32_t* __restrict__ pack, int nd_next_max,
+                                             uint32_t mf, int used0, int epoch, KeyAt key_at, int* shi) {
+    HopCtl& h = c->hop[hop];
+    const int tid = threadIdx.x;
+    const int n = h.n_dst;
+    const int sper = static_cast<int>((mf + 1 + 1023) / 1024);
+    const uint32_t sa = min<uint32_t>(mf + 1, tid * sper), sb = min<uint32_t>(mf + 1, sa + sper);
+    int my_keys = 0;
+    for (uint32_t i = sa; i < sb; ++i) my_keys += key_at(i) != -1;
+    int n_src;
+    int rk = block_excl_scan(my_keys, shi, &n_src);
+    if (n_src > nd_next_max) {
+        if (tid == 0) c->status |= kStSize;
+        return;
+    }
+    for (uint32_t i = sa; i < sb; ++i) {
+        const int32_t key = key_at(i);
+        if (key != -1) {
+            ub.lid[key] = rk;
+            next.dst[rk++] = key;
+        }
+    }
+    const int g1 = gcn ? 0 : 1;
+    const int items_tot = ub.tpre[n];
+    const int n_nbr = used0 + items_tot - n * g1;
+    if (tid == 0) {
+        int at = c->total;
+        int off[GS_PK_NFIELDS];
+        off[GS_PK_NBR_PTR] = at;
+        at += al4(n + 1);
+        off[GS_PK_NBR] = at;
+        at += al4(n_nbr);
+        off[GS_PK_SELF] = at;
+        at += al4(n);
+        off[GS_PK_TPTR] = at;
+        at += al4(n_src + 1);
+        off[GS_PK_TIDX] = at;
+        at += al4(n_nbr + n);
+        c->total = at;
+        for (int f2 = 0; f2 < GS_PK_NFIELDS; ++f2) h.off[f2] = (f2 >= GS_PK_NBR_PTR) ? off[f2] : -1;
+        h.n_src = n_src;
+        h.n_nbr = n_nbr;
+        pack[off[GS_PK_NBR_PTR] + n] = n_nbr;
+        c->dbg[4] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        c->epoch = epoch;  // every kernel of this hop read epoch + 1 before this launch's end
+    }
+    for (int i = tid; i <= n_src; i += 1024) ub.tcnt[i] = 0;
+}
+
+// ---- a union whose final table exceeds kUnionMax slots (ublock_kernel's
+// schedule says so): the same stages on a table of uint16 priorities (up to
+// kUnionBig slots in LDS, two slots per 32-bit word, claimed by
+// compare-and-swap), the stage's keys by priority in global memory (skeys,
+// two stages), keys settled in priority chunks of kStageKeys (a chunk's keys
+// only compete among themselves: every earlier chunk holds higher
+// priorities, final before the chunk starts).
+
+__device__ __forceinline__ uint32_t t16_get(const uint32_t* T, uint32_t slot) {
+    return (T[slot >> 1] >> ((slot & 1) * 16)) & 0xFFFFu;
+}
+
+// Claim `slot` for priority t: true when t is now its holder (it was empty
+// or held a lower priority), false when a higher priority holds it.
+__device__ __forceinline__ bool t16_claim(uint32_t* T, uint32_t slot, uint32_t t) {
+    uint32_t* wp = T + (slot >> 1);
+    const uint32_t sh = (slot & 1) * 16;
+    uint32_t old = *reinterpret_cast<volatile uint32_t*>(wp);
+    for (;;) {
+        if (((old >> sh) & 0xFFFFu) <= t) return false;
+        const uint32_t nw = (old & ~(0xFFFFu << sh)) | (t << sh);
+        const uint32_t prev = atomicCAS(wp, old, nw);
+        if (prev == old) return true;
+        old = prev;
+    }
+}
+
+__device__ __forceinline__ void settle16(uint32_t* T, uint32_t mask, int t0, int t1, const int32_t (&key)[kKPT],
+                                         uint32_t (&ps)[kKPT]) {
+    const uint32_t tid = threadIdx.x;
+    bool placed[kKPT];
+#pragma unroll
+    for (int q = 0; q < kKPT; ++q) placed[q] = false;
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q) {
+            const int t = t0 + static_cast<int>(tid) + 1024 * q;
+            if (t < t1 && !placed[q])
+                while (!t16_claim(T, pr_slot(ps[q]), static_cast<uint32_t>(t))) ps[q] = pr_next(ps[q], key[q], mask);
+        }
+        __syncthreads();
+        int any = 0;
+#pragma unroll
+        for (int q = 0; q < kKPT; ++q) {
+            const int t = t0 + static_cast<int>(tid) + 1024 * q;
+            if (t < t1) {
+                placed[q] = t16_get(T, pr_slot(ps[q])) == static_cast<uint32_t>(t);
+                if (!placed[q]) {
+                    ps[q] = pr_next(ps[q], key[q], mask);
+                    any = 1;
+                }
+            }
+        }
+        if (!__syncthreads_or(any)) break;
+    }
+}
+
+__global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop, int gcn,
+                                                    int32_t* __restrict__ pack, int nd_next_max) {
+    extern __shared__ uint32_t T[];  // kUnionBig uint16 slots
+    __shared__ int shi[17];
+    __shared__ int32_t oldslot[kSmallSet];
+    HopCtl& h = c->hop[hop];
+    if (!h.big || (c->status & kStTable)) return;
+    const int tid = threadIdx.x;
+    const int n = h.n_dst;
+    const int used0 = ub.set_cnt[0];
+    const uint32_t m_first = static_cast<uint32_t>(ub.first_meta[0]);
+    const int nst = ub.sched[2 * kMaxStages + 1];
+    const int epoch = c->epoch + 1;
+    uint32_t prev_mask = m_first;
+    int32_t key[kKPT];
+    uint32_t ps[kKPT];
+    for (int s = 0; s < nst; ++s) {
+        const uint32_t m = static_cast<uint32_t>(ub.sched[2 * s + 1]);
+        int32_t* sk = ub.skeys + (s & 1) * static_cast<int64_t>(kBigKeys);
+        const int32_t* sk_prev = ub.skeys + ((s + 1) & 1) * static_cast<int64_t>(kBigKeys);
+        // the previous table's keys in slot order, by priority into sk
+        int n_old;
+        {
+            const int sp = static_cast<int>((prev_mask + 1 + 1023) / 1024);
+            const uint32_t a0 = min<uint32_t>(prev_mask + 1, tid * sp), a1 = min<uint32_t>(prev_mask + 1, a0 + sp);
+            auto key_of = [&](uint32_t i) -> int32_t {
+                if (s == 0) return ub.first_tab[i];
+                const uint32_t p = t16_get(T, i);
+                return p == 0xFFFFu ? -1 : sk_prev[p];
+            };
+            int mine = 0;
+            for (uint32_t i = a0; i < a1; ++i) mine += key_of(i) != -1;
+            int at = block_excl_scan(mine, shi, &n_old);
+            for (uint32_t i = a0; i < a1; ++i) {
+                const int32_t kk = key_of(i);
+                if (kk != -1) {
+                    sk[at] = kk;
+                    if (s == 0) oldslot[at] = static_cast<int32_t>(i);
+                    ++at;
+                }
+            }
+        }
+        const int f0 = ub.ubef[ub.sched[2 * s]] - used0, f1 = ub.ubef[ub.sched[2 * (s + 1)]] - used0;
+        const int nk = n_old + (f1 - f0);
+        if (nk > kBigKeys) {
+            if (tid == 0) c->status |= kStTable;
+            return;
+        }
+        for (int i = tid; i < f1 - f0; i += 1024) sk[n_old + i] = ub.fresh[f0 + i];
+        __threadfence_block();
+        __syncthreads();  // sk complete (and the previous table read): T may be cleared
+        for (uint32_t i = tid; i <= m / 2; i += 1024) T[i] = 0xFFFFFFFFu;
+        __syncthreads();
+        const bool copy = s == 0 && m == m_first;
+        for (int t0 = 0; t0 < nk; t0 += kStageKeys) {
+            const int t1 = min(nk, t0 + kStageKeys);
+#pragma unroll
+            for (int q = 0; q < kKPT; ++q) {
+                const int t = t0 + tid + 1024 * q;
+                int32_t kk = -1;
+                uint32_t p0 = 0;
+                if (t < t1) {
+                    kk = sk[t];
+                    p0 = (copy && t < n_old) ? static_cast<uint32_t>(oldslot[t]) : pr_init(kk, m);
+                }
+                key[q] = kk;
+                ps[q] = p0;
+            }
+            settle16(T, m, t0, t1, key, ps);
+            __syncthreads();
+        }
+        prev_mask = m;
+    }
+    const int32_t* sk_last = ub.skeys + ((nst - 1) & 1) * static_cast<int64_t>(kBigKeys);
+    finish_union(c, hb, ub, next, hop, gcn, pack, nd_next_max, prev_mask, used0, epoch,
+                 [&](uint32_t i) -> int32_t {
+                     const uint32_t p = t16_get(T, i);
+                     return p == 0xFFFFu ? -1 : sk_last[p];
+                 },
+                 shi);
+}
+
 // The union's table (one block, LDS): the runs' new keys in merge order,
 // the resize schedule, the stages, then the next frontier in slot order and
 // each key's position in it (lid), the pack layout of this hop.
@@ -363,7 +556,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     __shared__ int shi[17];
     __shared__ int st_run[kMaxStages + 1];
     __shared__ uint32_t st_mask[kMaxStages];
-    __shared__ int s_nst, s_best, s_bad, s_epoch;
+    __shared__ int s_nst, s_best, s_bad, s_epoch, s_big;
     HopCtl& h = c->hop[hop];
     const int n = h.n_dst;
     const int tid = threadIdx.x;
@@ -450,7 +643,10 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         if (lane == 0) {
             s_nst = nst;
             st_run[nst] = n;
-            if (cur_m + 1 > kUnionMax) s_bad = 1;
+            if (cur_m + 1 > kUnionBig) s_bad = 1;
+            s_big = cur_m + 1 > kUnionMax;
+            h.n_src = -1;
+            h.big = s_big;
         }
     }
     __syncthreads();
@@ -459,6 +655,14 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         return;
     }
     const int nst = s_nst;
+    if (s_big) {  // the table needs uint16 priorities: ubig_kernel takes over from the schedule
+        if (tid <= nst) {
+            ub.sched[2 * tid] = st_run[tid];
+            ub.sched[2 * tid + 1] = tid < nst ? static_cast<int32_t>(st_mask[tid]) : 0;
+        }
+        if (tid == 0) ub.sched[2 * kMaxStages + 1] = nst;
+        return;
+    }
     if (tid == 0) {
         c->dbg[2] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         c->dbg[3] = nst;
@@ -534,47 +738,8 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         prev_mask = m;
     }
     // the next frontier: keys in slot order, each key's position (lid)
-    const uint32_t mf = prev_mask;
-    const int sper = static_cast<int>((mf + 1 + 1023) / 1024);
-    const uint32_t sa = min<uint32_t>(mf + 1, tid * sper), sb = min<uint32_t>(mf + 1, sa + sper);
-    int my_keys = 0;
-    for (uint32_t i = sa; i < sb; ++i) my_keys += T[i] != 0xFFFFFFFFu;
-    int n_src;
-    int rk = block_excl_scan(my_keys, shi, &n_src);
-    if (n_src > nd_next_max) {
-        if (tid == 0) c->status |= kStSize;
-        return;
-    }
-    for (uint32_t i = sa; i < sb; ++i)
-        if (T[i] != 0xFFFFFFFFu) {
-            ub.lid[T[i]] = rk;
-            next.dst[rk++] = static_cast<int32_t>(T[i]);
-        }
-    // pack layout of this hop
-    const int g1 = gcn ? 0 : 1;
-    const int n_nbr = used0 + items_tot - n * g1;
-    if (tid == 0) {
-        int at = c->total;
-        int off[GS_PK_NFIELDS];
-        off[GS_PK_NBR_PTR] = at;
-        at += al4(n + 1);
-        off[GS_PK_NBR] = at;
-        at += al4(n_nbr);
-        off[GS_PK_SELF] = at;
-        at += al4(n);
-        off[GS_PK_TPTR] = at;
-        at += al4(n_src + 1);
-        off[GS_PK_TIDX] = at;
-        at += al4(n_nbr + n);
-        c->total = at;
-        for (int f2 = 0; f2 < GS_PK_NFIELDS; ++f2) h.off[f2] = (f2 >= GS_PK_NBR_PTR) ? off[f2] : -1;
-        h.n_src = n_src;
-        h.n_nbr = n_nbr;
-        pack[off[GS_PK_NBR_PTR] + n] = n_nbr;
-        c->dbg[4] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
-        c->epoch = s_epoch;  // every kernel of this hop read epoch + 1 before this launch's end
-    }
-    for (int i = tid; i <= n_src; i += 1024) ub.tcnt[i] = 0;
+    finish_union(c, hb, ub, next, hop, gcn, pack, nd_next_max, prev_mask, used0, s_epoch,
+                 [&](uint32_t i) { return T[i] == 0xFFFFFFFFu ? -1 : static_cast<int32_t>(T[i]); }, shi);
 }
 
 // Per run (one wave, lane q = item q): the destination's neighbourhood in
@@ -683,6 +848,14 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     ublock_kernel<<<1, 1024, kUnionLds, st>>>(c, hb, ub, next, hop, gcn, pack,
                                                                    static_cast<int>(nd_next_max));
     check_launch("ublock_kernel");
+    static const bool attr_big = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(ubig_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   kUnionBig * sizeof(uint16_t)) == hipSuccess;
+    }();
+    if (!attr_big) fail(GS_EHIP, "ubig_kernel: cannot raise its LDS limit");
+    ubig_kernel<<<1, 1024, kUnionBig * sizeof(uint16_t), st>>>(c, hb, ub, next, hop, gcn, pack,
+                                                               static_cast<int>(nd_next_max));
+    check_launch("ubig_kernel");
     uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);
     check_launch("uout_kernel");
     tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt);

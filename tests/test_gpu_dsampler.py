@@ -264,3 +264,31 @@ def test_device_sampler_fullsize_rmat2m_packs():
         mt_d, pos_d = ds.get_rng()
         assert pos_d == pos_h
         np.testing.assert_array_equal(mt_d, mt_h)
+
+
+@pytest.mark.parametrize("B,fan", [(4096, [10, 5]), (3000, [25, 3])])
+def test_device_big_union_matches_host(B, fan):
+    """Frontier unions whose final table exceeds the LDS uint32 table
+    (ubig_kernel: uint16 priorities, keys staged in global memory, priority
+    chunks) — e.g. an apply_model forward over an extended batch: whole packs
+    and stream states equal to the host sampler's."""
+    src, dst = gs.rmat_pairs(16, 1_000_000, seed=7, n_threads=8)
+    G_ = gs.CSRGraph.from_pairs(src, dst, 1 << 16, n_threads=8)
+    cand = np.nonzero(G_.degrees() > 0)[0]
+    fan = np.array(fan, np.int32)
+    rng_h = gs.RNG(17)
+    ds = gs.sampler.DeviceSampler(G_, fan, B)
+    ds.set_rng(rng_h)
+    rs = np.random.RandomState(3)
+    for b in range(2):
+        roots = rs.choice(cand, B, replace=False).astype(np.int64)
+        ref, sizes, offs, used = host_pack(G_, rng_h, roots, fan)
+        assert sizes[0, 2] > 6554  # |L1| past 0.4 * 16384: the union's last table has > 16384 slots
+        pack, dsz, doff, dused = ds.run(roots)
+        np.testing.assert_array_equal(dsz, sizes)
+        assert dused == used
+        assert_packs_equal(pack[:used].cpu().numpy(), ref, sizes, offs, B, f"batch {b}")
+        mt_h, pos_h = rng_h.getstate()
+        mt_d, pos_d = ds.get_rng()
+        assert pos_d == pos_h
+        np.testing.assert_array_equal(mt_d, mt_h)
