@@ -1064,8 +1064,9 @@ int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, in
         if (hop_sizes) {
             hop_sizes[4 * j] = on ? c.hop[j].n_dst : 0;
             hop_sizes[4 * j + 1] = on ? c.hop[j].n_pos : 0;
-            hop_sizes[4 * j + 2] = on && !last ? c.hop[j].n_src : -1;
-            hop_sizes[4 * j + 3] = on && !last ? c.hop[j].n_nbr : -1;
+            // as the host sampler: -1 = not materialised (the last hop), 0 past the hops
+            hop_sizes[4 * j + 2] = on ? (last ? -1 : c.hop[j].n_src) : 0;
+            hop_sizes[4 * j + 3] = on ? (last ? -1 : c.hop[j].n_nbr) : 0;
         }
         if (offsets)
             for (int f = 0; f < GS_PK_NFIELDS; ++f) {
