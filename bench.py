@@ -543,6 +543,9 @@ def main():
                          "issuing thread and the HIP runtime / RCCL's proxy; without: min(12, cores per GPU - 3))")
     ap.add_argument("--no-warm", action="store_true",
                     help="skip the sampler threads' throwaway warm-up batch (A/B of the cold first batches)")
+    ap.add_argument("--sampler", default="host", choices=("host", "device"),
+                    help="device: every stream samples on the GPU (gs_dsampler, SURVEY §8 f-4), no host sampler "
+                         "threads; default 1 stream (the reference's single random stream)")
     ap.add_argument("--sampler-helpers", type=int, default=None,
                     help="helper threads per sampler stream (same draws; lower per-batch latency); "
                          "default 1 with >= 8 host cores per GPU")
@@ -551,6 +554,10 @@ def main():
     # as given on the command line, before the training runner's defaults below
     # (the pubmed loop and the inference runner pick their own)
     args.helpers_cli, args.streams_cli, args.per_gpu = args.sampler_helpers, args.sampler_streams, per_gpu
+    if args.sampler == "device":
+        args.sampler_helpers = 0
+        if args.sampler_streams is None:
+            args.sampler_streams = 1
     if args.sampler_helpers is None:
         # one helper per stream where the cores allow: a batch then samples in
         # ~0.35-0.42 ms instead of ~0.5-0.57 (profiles/r02_ab_sampler_layouts.txt),
@@ -565,8 +572,8 @@ def main():
     # the training layout needs S streams x (1 + helpers) sampler threads plus
     # two cores (the issuing thread, the HIP runtime / RCCL proxy); with fewer
     # host cores per GPU the sampler, not the GPU, sets the pace
-    args.layout_cores = args.sampler_streams * (1 + args.sampler_helpers) + 2
-    args.layout_short = per_gpu < 8 or per_gpu < args.layout_cores
+    args.layout_cores = args.sampler_streams * (1 + args.sampler_helpers) + 2 if args.sampler == "host" else 2
+    args.layout_short = args.sampler == "host" and (per_gpu < 8 or per_gpu < args.layout_cores)
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["batch"] = args.batch
@@ -601,7 +608,7 @@ def main():
     # timed steps' batches are sampled inside the timed region (presampled_at_t0)
     runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
                           fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets,
-                          helpers=args.sampler_helpers, warm=not args.no_warm)
+                          helpers=args.sampler_helpers, warm=not args.no_warm, sampler=args.sampler)
     elem = 2 if cfg["dtype"] == "bf16" else 4
     L = len(cfg["fanouts"])
     lib = gs._lib.lib()
@@ -798,6 +805,7 @@ def main():
                                    f"({wl['n']} ids), {cfg['pairs']} pairs, feat {cfg['feat']}, "
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
+                       "sampler": args.sampler,
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
                        "sampler_contexts_warmed": not args.no_warm,
