@@ -376,8 +376,8 @@ void gs_runner::dev_enqueue(int w) {
 bool gs_runner::dev_take(int64_t b, bool block) {
     using namespace gs;
     DevStream& d = dstreams[b % cfg.n_streams];
+    if (!block && (d.inflight != b || !dsampler_ready(d.ds))) return false;  // not enqueued yet (held) or running
     GS_REQUIRE(d.inflight == b, GS_EINVAL, "device sampler: batch not enqueued (past the release mark?)");
-    if (!block && !dsampler_ready(d.ds)) return false;
     const auto tw = Clock::now();
     DevResult& R = dres[b % n_dpack];
     const int rc = gs_dsampler_result(d.ds, R.hop_sizes, R.offsets, &R.used);
