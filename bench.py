@@ -360,8 +360,10 @@ def run_apply_model_loop(args, cfg):
     # the forward's sampling with helper threads (same draws, same pack; the
     # host is otherwise idle while the step's single stream samples)
     helpers = args.helpers_cli if args.helpers_cli is not None else min(7, host_threads() - 1)
+    dev_samp = args.sampler == "device"
     gsage = models.GraphSage(2, cfg["feat"], 128, wl["X"], wl["graph"], device, agg_func=cfg["agg"],
-                             fanouts=list(cfg["fanouts"]), sampler_helpers=helpers).to(device)
+                             fanouts=list(cfg["fanouts"]), sampler_helpers=0 if dev_samp else helpers,
+                             device_sampler=dev_samp).to(device)
     cls = models.Classification(128, cfg["classes"]).to(device)
     ul = unsup.UnsupervisedLoss(wl["graph"], wl["train"], device, n_threads=host_threads())
     params = [p for m in (gsage, cls) for p in m.parameters()]
@@ -397,7 +399,8 @@ def run_apply_model_loop(args, cfg):
                    "global_batch": cfg["batch"], "parallelism": "dp1",
                    "epoch_s": round(len(wl["train"]) // cfg["batch"] * elapsed / args.steps, 4),
                    "extended_nodes_per_step": round(ext / args.steps, 1), "final_loss": round(float(loss), 5),
-                   "forward_sampler_helpers": helpers,
+                   "forward_sampler": "device" if dev_samp else "host",
+                   "forward_sampler_helpers": 0 if dev_samp else helpers,
                    "extend_balls": "device" if ul.device_balls else "host"},
         "roofline": None,
         "cpu_baseline": cpu,
@@ -805,7 +808,7 @@ def main():
                                    f"({wl['n']} ids), {cfg['pairs']} pairs, feat {cfg['feat']}, "
                                    f"fanout {tuple(cfg['fanouts'])}, {cfg['agg']}, B={cfg['batch']}/GPU",
                        "global_batch": cfg["batch"] * world, "parallelism": f"dp{world}",
-                       "sampler": args.sampler,
+                       "sampler_kind": args.sampler,
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
                        "sampler_contexts_warmed": not args.no_warm,
