@@ -117,13 +117,16 @@ __device__ __forceinline__ void rejection_moments(uint32_t d, int k, int setsize
     var = 0.f;
     if (k <= 0 || d < static_cast<uint32_t>(k)) return;
     const bool pool = d <= static_cast<uint32_t>(setsize);
+    // per draw, words until acceptance ~ geometric(p), p = m / 2^bitlen:
+    // E[rejections] = 1/p - 1, Var = (1/p)(1/p - 1) (window sizing only, so
+    // the fast reciprocal is enough)
     for (int i = 0; i < k; ++i) {
         const uint32_t m = d - i;
         const uint32_t span = pool ? m : d;
         const float full = ldexpf(1.f, 32 - __clz(span));
-        const float p = static_cast<float>(m) / full;
-        mean += (1.f - p) / p;
-        var += (1.f - p) / (p * p);
+        const float q = full * __frcp_rn(static_cast<float>(m));
+        mean += q - 1.f;
+        var += q * (q - 1.f);
     }
 }
 
@@ -245,7 +248,22 @@ __device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const
                                           uint32_t* __restrict__ dst) {
     const int64_t gen = c->gen_end;
     const int nvalid = static_cast<int>(max<int64_t>(0, min<int64_t>(nw, gen - A0)));
-    for (int i = threadIdx.x; i < nvalid; i += blockDim.x) dst[i] = wr[(A0 + i) & kRingMask];
+    // kLoadBatch loads in flight per thread before their LDS stores (a
+    // load-then-store loop waits out one global latency per iteration)
+    constexpr int kLoadBatch = 8;
+    for (int base = threadIdx.x; base < nvalid; base += kLoadBatch * blockDim.x) {
+        uint32_t v[kLoadBatch];
+#pragma unroll
+        for (int u = 0; u < kLoadBatch; ++u) {
+            const int i = base + u * static_cast<int>(blockDim.x);
+            v[u] = i < nvalid ? wr[(A0 + i) & kRingMask] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kLoadBatch; ++u) {
+            const int i = base + u * static_cast<int>(blockDim.x);
+            if (i < nvalid) dst[i] = v[u];
+        }
+    }
     return nvalid;
 }
 
@@ -471,10 +489,24 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
         wid[i] = i < nbk ? min(hb.bw[b0 + i], W) : W;
     }
     __syncthreads();
-    for (int q = 0; q < nbk; ++q) {  // widths are multiples of 64: 16-byte loads
+    // widths are multiples of 64: 16-byte loads, all of a block's in flight
+    // before its LDS stores
+    for (int q = 0; q < nbk; ++q) {
         const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0 + q) * W);
         uint4* dst = reinterpret_cast<uint4*>(tabs + q * W);
-        for (int i = threadIdx.x; i < wid[q] / 8; i += blockDim.x) dst[i] = src[i];
+        const int n16 = wid[q] / 8;
+        constexpr int kB = kWMax / 8 / 256;
+        uint4 v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < n16) v[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int i = threadIdx.x + 256 * u;
+            if (i < n16) dst[i] = v[u];
+        }
     }
     __syncthreads();
     int32_t* path = hb.path + static_cast<int64_t>(b0) * W;
@@ -550,134 +582,144 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
     }
 }
 
-// Every block from its true entry: the block's nodes in lanes (one wave,
-// 64 nodes at a time).  Node m's first word on the true path is m * k plus the
-// rejections of the nodes before it (recorded per entry by the table kernel,
-// summed by a wave scan), so every lane walks its own node from its own
-// start: random.sample's result order as absolute CSR entries — pool branch
-// with the swapped slots in registers, selected-set branch with the picks in
-// registers — and rows below k whole.
-template <int KMAX>
-__global__ __launch_bounds__(64) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb, DevGraph g,
-                                                       int hop, int k, int setsize, int R, int last, int gcn,
-                                                       int32_t* __restrict__ pack) {
-    extern __shared__ uint32_t w[];
+// Every frontier node from its start on the true path, one wave per node:
+// node m of block b starts m * k words plus the rejections of the block's
+// earlier sampled nodes (recorded per entry by the table kernel) after the
+// block's true entry.  The wave stages 256 of its words in LDS and walks
+// them 64 at a time — a ballot of the words acceptable for the current draw
+// finds the next accepted one — emitting random.sample's result order as
+// absolute CSR entries: pool branch with the swapped pool slots in lanes
+// (key, value), selected-set branch with the picks in lanes; rows below k
+// whole.
+constexpr int kEmitWaves = 4;
+constexpr int kEmitWords = 256;
+__global__ __launch_bounds__(64 * kEmitWaves) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
+                                                                    DevGraph g, int hop, int k, int setsize, int R,
+                                                                    int last, int gcn, int32_t* __restrict__ pack) {
+    __shared__ uint32_t wbuf[kEmitWaves][kEmitWords];
     HopCtl& h = c->hop[hop];
-    const int b = blockIdx.x;
-    if (b >= h.n_blocks) return;
-    const int lane = threadIdx.x;
-    const int r0 = b * R, nr = min(R, h.n_dst - r0);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = blockIdx.x * kEmitWaves + wave;
+    if (r >= h.n_dst) return;
+    const int b = r / R, r0 = b * R;
     const int j = hb.entry[b];
-    const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
-    const int nw = ndr + 3 * R * max(k, 1) + 64;
-    const int nvalid = j < 0 ? 0 : load_words(wr, c, h.P0 + hb.dbase[b] + j, nw, w);
-    __syncthreads();
     if (j < 0) return;  // reported by the chain
-    const int e = j - hb.blo[b];
-    const uint8_t* rej = hb.rej + static_cast<int64_t>(b) * R * kWMax + e;
-    int32_t* ent = last ? pack + h.off[GS_PK_POS] : hb.ent;
-    int m0 = 0, rej0 = 0;  // sampled nodes and their rejections before this chunk of nodes
+    uint32_t* w = wbuf[wave];
+    const int32_t v = hb.dst[r];
+    const uint32_t d = static_cast<uint32_t>(hb.deg[r]);
+    const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
+    int32_t* out = (last ? pack + h.off[GS_PK_POS] : hb.ent) + hb.pos_ptr[r];
+    const bool sampled = k > 0 && d >= static_cast<uint32_t>(k);
+    const int cnt = sampled ? k : static_cast<int>(d);
     bool over = false;
-    for (int q0 = 0; q0 < nr; q0 += 64) {
-        const int q = q0 + lane;
-        const bool on = q < nr;
-        const int r = r0 + q;
-        const int32_t v = on ? hb.dst[r] : 0;
-        const uint32_t d = on ? static_cast<uint32_t>(hb.deg[r]) : 0u;
-        const bool sampled = on && k > 0 && d >= static_cast<uint32_t>(k);
-        // this node's index among the block's sampled nodes, its rejections
-        const uint64_t sb = __ballot(sampled);
-        const int m = m0 + __popcll(sb & ((1ull << lane) - 1ull));
-        const int rj = sampled ? rej[static_cast<int64_t>(m) * kWMax] : 0;
-        int inc = rj;
+    if (!sampled) {
+        for (int t = lane; t < cnt; t += 64) out[t] = base + t;
+    } else {
+        // this node's index among the block's sampled nodes, and their rejections
+        const int e = j - hb.blo[b];
+        const int qn = r - r0;
+        int m = 0, rj = 0;
+        for (int q0 = 0; q0 < qn; q0 += 64) {
+            const int qq = q0 + lane;
+            const bool smp = qq < qn && hb.deg[r0 + qq] >= k;
+            const uint64_t bal = __ballot(smp);
+            const int mm = m + __popcll(bal & ((1ull << lane) - 1ull));
+            int x = smp ? hb.rej[(static_cast<int64_t>(b) * R + mm) * kWMax + e] : 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += t;
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            m += __popcll(bal);
+            rj += x;
         }
-        int u = m * k + rej0 + inc - rj;  // the node's first word on the true path
-        if (on) {
-            const int32_t base = static_cast<int32_t>(g.row_ptr[v]);
-            int32_t* out = ent + hb.pos_ptr[r];
-            const int cnt = sampled ? k : static_cast<int>(d);
-            if (!sampled) {
-                for (int t = 0; t < cnt; ++t) out[t] = base + t;
-            } else if (d <= static_cast<uint32_t>(setsize)) {
-                // pool branch: pool[x] for the accepted x, then pool[x] = pool[m - 1]
-                uint32_t mk[KMAX], mv[KMAX];
-                int nm = 0;
-                for (int i = 0; i < k; ++i) {
-                    const uint32_t mm = d - i;
-                    const int sh = __clz(mm);
-                    uint32_t x;
-                    for (;;) {
-                        if (u >= nvalid) {
-                            over = true;
-                            x = 0;
+        const int64_t gen = c->gen_end;
+        int64_t A = h.P0 + hb.dbase[b] + j + static_cast<int64_t>(m) * k + rj;  // the node's first word
+        auto stage = [&](int64_t from) {  // kEmitWords words from `from` into the wave's buffer
+            uint32_t t4[kEmitWords / 64];
+#pragma unroll
+            for (int u = 0; u < kEmitWords / 64; ++u) t4[u] = wr[(from + lane + 64 * u) & kRingMask];
+#pragma unroll
+            for (int u = 0; u < kEmitWords / 64; ++u) w[lane + 64 * u] = t4[u];
+        };
+        stage(A);
+        int u = 0;  // words of the buffer consumed
+        auto refill = [&]() {  // keep 64 words ahead of u in the buffer
+            if (u + 64 > kEmitWords) {
+                A += u;
+                u = 0;
+                stage(A);
+            }
+            if (A + u + 64 > gen) over = true;
+        };
+        if (d <= static_cast<uint32_t>(setsize)) {
+            uint32_t mk = 0, mv = 0;  // lane t < nm: pool slot mk holds mv
+            int nm = 0;
+            for (int i = 0; i < k && !over;) {
+                refill();
+                if (over) break;
+                const uint32_t mm = d - i;
+                const int sh = __clz(mm);
+                const uint32_t x = w[u + lane] >> sh;
+                const uint64_t acc = __ballot(x < mm);
+                if (!acc) {
+                    u += 64;
+                    continue;
+                }
+                const int p = __ffsll(static_cast<unsigned long long>(acc)) - 1;
+                const uint32_t xs = __shfl(x, p, 64);
+                u += p + 1;
+                const uint64_t hx = __ballot(lane < nm && mk == xs);
+                const uint64_t hl = __ballot(lane < nm && mk == mm - 1);
+                const uint32_t val = hx ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hx)) - 1, 64) : xs;
+                const uint32_t lastv = hl ? __shfl(mv, __ffsll(static_cast<unsigned long long>(hl)) - 1, 64) : mm - 1;
+                if (hx) {
+                    if (lane == __ffsll(static_cast<unsigned long long>(hx)) - 1) mv = lastv;
+                } else {
+                    if (lane == nm) {
+                        mk = xs;
+                        mv = lastv;
+                    }
+                    ++nm;
+                }
+                if (lane == 0) out[i] = base + static_cast<int32_t>(val);
+                ++i;
+            }
+        } else {
+            const int sh = __clz(d);
+            uint32_t selv = 0xFFFFFFFFu;  // lane t < n_sel: the t-th selected value
+            int n_sel = 0;
+            while (n_sel < k && !over) {
+                refill();
+                if (over) break;
+                const uint32_t x = w[u + lane] >> sh;
+                uint64_t cand = __ballot(x < d);
+                int consumed = 64;
+                while (cand) {
+                    const int p = __ffsll(static_cast<unsigned long long>(cand)) - 1;
+                    cand &= cand - 1;
+                    const uint32_t xs = __shfl(x, p, 64);
+                    if (!__ballot(lane < n_sel && selv == xs)) {
+                        if (lane == n_sel) selv = xs;
+                        if (lane == 0) out[n_sel] = base + static_cast<int32_t>(xs);
+                        ++n_sel;
+                        if (n_sel == k) {
+                            consumed = p + 1;
                             break;
                         }
-                        x = w[u++] >> sh;
-                        if (x < mm) break;
-                    }
-                    uint32_t val = x, lastv = mm - 1;
-                    bool found = false;
-#pragma unroll
-                    for (int t = 0; t < KMAX; ++t) {
-                        const bool live = t < nm;
-                        if (live && mk[t] == x) val = mv[t];
-                        if (live && mk[t] == mm - 1) lastv = mv[t];
-                    }
-#pragma unroll
-                    for (int t = 0; t < KMAX; ++t)
-                        if (t < nm && mk[t] == x) {
-                            mv[t] = lastv;
-                            found = true;
-                        }
-#pragma unroll
-                    for (int t = 0; t < KMAX; ++t)
-                        if (!found && t == nm) {
-                            mk[t] = x;
-                            mv[t] = lastv;
-                        }
-                    nm += found ? 0 : 1;
-                    out[i] = base + static_cast<int32_t>(val);
-                }
-            } else {
-                const int sh = __clz(d);
-                uint32_t sel[KMAX];
-                int n_sel = 0;
-                while (n_sel < k) {
-                    if (u >= nvalid) {
-                        over = true;
-                        break;
-                    }
-                    const uint32_t x = w[u++] >> sh;
-                    bool fresh = x < d;
-#pragma unroll
-                    for (int t = 0; t < KMAX; ++t) fresh &= !(t < n_sel && sel[t] == x);
-                    if (fresh) {
-#pragma unroll
-                        for (int t = 0; t < KMAX; ++t)
-                            if (t == n_sel) sel[t] = x;
-                        out[n_sel] = base + static_cast<int32_t>(x);
-                        ++n_sel;
                     }
                 }
-            }
-            // empty neighbourhood after the self rule (non-gcn): no entry, or
-            // a lone entry that is the node itself
-            if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
-            if (last) {
-                pack[h.off[GS_PK_DST_IDS] + r] = v;
-                pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
-                if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
+                u += consumed;
             }
         }
-        m0 += __popcll(sb);
-        rej0 += __shfl(inc, 63, 64);
     }
-    if (__ballot(over)) {
-        if (lane == 0) atomicOr(&c->status, kStWords);
+    if (lane == 0) {
+        // empty neighbourhood after the self rule (non-gcn): no entry, or a
+        // lone entry that is the node itself
+        if (!gcn && (cnt == 0 || (cnt == 1 && g.col[out[0]] == v))) atomicAdd(&h.n_empty, 1);
+        if (last) {
+            pack[h.off[GS_PK_DST_IDS] + r] = v;
+            pack[h.off[GS_PK_POS_PTR] + r] = hb.pos_ptr[r];
+            if (r == h.n_dst - 1) pack[h.off[GS_PK_POS_PTR] + h.n_dst] = hb.pos_ptr[h.n_dst];
+        }
+        if (over) atomicOr(&c->status, kStWords);
     }
 }
 
@@ -804,21 +846,8 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     gs::check_launch("draw_compose_kernel");
     draw_chain_kernel<<<1, 1024, kChainEntries * sizeof(uint16_t), st>>>(ds->ctl, hb, hop);
     gs::check_launch("draw_chain_kernel");
-    const size_t emit_lds = (4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
-#define GS_EMIT(KM)                                                                                               \
-    draw_emit_kernel<KM><<<nb_max, 64, emit_lds, st>>>(ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R, last ? 1 : 0, \
-                                                       gcn, ds->pack_cur)
-    if (k <= 8)
-        GS_EMIT(8);
-    else if (k <= 12)
-        GS_EMIT(12);
-    else if (k <= 16)
-        GS_EMIT(16);
-    else if (k <= 25)
-        GS_EMIT(25);
-    else
-        GS_EMIT(32);
-#undef GS_EMIT
+    draw_emit_kernel<<<static_cast<unsigned>((ds->nd_max[hop] + kEmitWaves - 1) / kEmitWaves), 64 * kEmitWaves, 0, st>>>(
+        ds->wr, ds->ctl, hb, ds->g, hop, k, setsize, R, last ? 1 : 0, gcn, ds->pack_cur);
     gs::check_launch("draw_emit_kernel");
 }
 
