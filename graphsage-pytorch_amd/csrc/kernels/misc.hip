@@ -58,7 +58,12 @@ constexpr int64_t kClsWcLds = 8 * 1024;
 // shorter per-block partial-slab phase: at B = 512 the kernel took 12.1 us
 // with 16 rows (32 blocks), 8.3 us with 8 or 4 (rocprof, in-step); the step
 // ran 81.5-82.3 us with 4 against 86.9-89.1 us with 16.
+// Large batches (Pubmed trains on B ~ 9.7k roots in one step) grow the rows
+// per block up to kClsRowsBig until about kClsSlabTarget slabs remain: at four
+// rows the slab sum read 2.4k slabs per element on 7 blocks (161 us).
 constexpr int kClsRowsMax = 4;
+constexpr int kClsRowsBig = 32;
+constexpr int64_t kClsSlabTarget = 384;
 
 struct ClsPlan {
     int rows;
@@ -66,7 +71,7 @@ struct ClsPlan {
     size_t smem;
 };
 
-inline ClsPlan cls_plan(int64_t C, int64_t D) {
+inline ClsPlan cls_plan(int64_t B, int64_t C, int64_t D) {
     ClsPlan p;
     p.wc_lds = C * (D + 1) <= kClsWcLds;
     const int64_t fixed = p.wc_lds ? C * (D + 1) : 0;
@@ -76,6 +81,10 @@ inline ClsPlan cls_plan(int64_t C, int64_t D) {
             p.rows = r;
             break;
         }
+    // keep the one-float4-per-thread E tile (FAST) while growing
+    while (p.rows >= kClsRowsMax && p.rows < kClsRowsBig && (B + p.rows - 1) / p.rows > kClsSlabTarget &&
+           fixed + 2 * p.rows * (C + D + 1) <= kClsLdsFloats && 2 * p.rows * D <= 4 * kClsThreads)
+        p.rows *= 2;
     p.smem = static_cast<size_t>(fixed + p.rows * (C + D + 1)) * sizeof(float);
     return p;
 }
@@ -374,7 +383,7 @@ int gs_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
 }
 
 int64_t gs_cls_nll_ws_floats(int64_t B, int64_t D, int64_t C) {
-    const int r = gs::cls_plan(C, D).rows;
+    const int r = gs::cls_plan(B, C, D).rows;
     const int64_t nb = (B + r - 1) / r;
     return nb * (C * (D + 1) + 1);
 }
@@ -390,7 +399,7 @@ int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float
     GS_REQUIRE(C + D + 1 <= kClsLdsFloats, GS_EINVAL, "classes + embedding dims too large");
     GS_REQUIRE(E && Wc && bc && labels && dE && ws, GS_EINVAL, "NULL device pointer");
     const int b = static_cast<int>(B), d = static_cast<int>(D), c = static_cast<int>(C);
-    const ClsPlan plan = cls_plan(C, D);
+    const ClsPlan plan = cls_plan(B, C, D);
     const int nb = (b + plan.rows - 1) / plan.rows;
     const bool fast = roots && D % 4 == 0 && plan.rows * D <= 4 * kClsThreads && C * D <= 4 * kClsThreads &&
                       aligned16(E) && aligned16(Wc);

@@ -200,6 +200,8 @@ def test_agg_bwd_matches_autograd(agg, F):
     (37, 64, 7, True, False),        # ragged last block, Cora-sized head
     (100, 256, 200, True, True),     # Wc too large for LDS -> read from global
     (1, 8, 1, False, False),
+    (9705, 128, 3, False, False),    # Pubmed's extended batch: 32 rows per block
+    (6001, 128, 3, True, True),      # grown rows on the FAST path, ragged last block
 ])
 def test_cls_nll_matches_torch(B, D, C, use_roots, mask):
     torch.manual_seed(0)
