@@ -24,7 +24,10 @@ namespace gs {
 
 class Team {
   public:
-    explicit Team(int helpers) {
+    // spin: pause rounds a helper polls for the next job before sleeping
+    // (0 for a caller whose jobs come once per step: idle helpers then leave
+    // the cores to the other host threads at once).
+    explicit Team(int helpers, int spin = 20000) : spin_(spin) {
         for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Team() {
@@ -86,7 +89,7 @@ class Team {
         uint64_t seen = gen_.load();
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
-            for (int spin = 0; g == seen && spin < 20000; ++spin) {
+            for (int spin = 0; g == seen && spin < spin_; ++spin) {
                 _mm_pause();
                 g = gen_.load(std::memory_order_acquire);
             }
@@ -112,6 +115,7 @@ class Team {
     std::mutex mu_;
     std::condition_variable cv_;
     bool stop_ = false;
+    int spin_;
 };
 
 }  // namespace gs

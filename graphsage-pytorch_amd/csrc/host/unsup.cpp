@@ -23,6 +23,8 @@
 //              one stream.
 //   unique     models.py:146  list(set(flat positives) | set(flat negatives)).
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,6 +35,7 @@
 #include "common.hpp"
 #include "graph.hpp"
 #include "pyset.hpp"
+#include "team.hpp"
 #include "rng.hpp"
 #include "unsup_dev.hpp"
 
@@ -120,8 +123,10 @@ struct gs_unsup {
     std::vector<int64_t> nodes, unique, pos, neg;  // pairs flattened (a, b)
     std::vector<int64_t> pos_cnt, neg_cnt;
     std::vector<uint8_t> has_pos;
+    std::vector<uint64_t> seen;         // [n_nodes / 64] scratch bitmap, all clear between calls
     int32_t subset_ok = 0;
     gs::UnsupDev* dev = nullptr;        // gs_unsup_attach_device: balls + far picks on the GPU
+    std::unique_ptr<gs::Team> team;     // persistent helpers (fresh-set orders beside the draws)
     ~gs_unsup();
 };
 
@@ -341,53 +346,83 @@ void negative_pairs_dev(gs_unsup& u, gs_rng* rng, int64_t num_neg, int32_t n_thr
     }
     std::vector<int32_t> host_far;
     gs::unsup_dev_far_lists(u.dev, k2, k2base, host_far);
-    // the fresh sets' orders are independent per node: emulate them on the
-    // worker threads, ahead of the draws
+    const auto t1a = clk::now();
+    // the fresh sets' orders are independent per node and the draws need only
+    // the lengths: emulate the orders on worker threads (a shared queue, the
+    // lists differ in length) while this thread draws and fetches the other
+    // nodes' picks, then helps with what is left
     std::vector<std::vector<int32_t>> fars(k2.size());
-    run_workers(std::max<int32_t>(1, n_threads), static_cast<int64_t>(k2.size()), [&](int64_t q, int32_t) {
+    const int helpers = std::min<int>(std::max<int32_t>(1, n_threads) - 1, static_cast<int>(k2.size()));
+    if (helpers > 0 && (!u.team || u.team->helpers() < helpers)) u.team = std::make_unique<gs::Team>(helpers, 0);
+    struct Waited {  // the job reads this frame: it has finished on every exit
+        gs::Team* t;
+        ~Waited() {
+            if (t) t->wait();
+        }
+    } job{helpers > 0 ? u.team.get() : nullptr};
+    auto emulate = [&](int q) {
         fars[static_cast<size_t>(q)].assign(host_far.begin() + k2base[q], host_far.begin() + k2base[q + 1]);
         fresh_set_order(fars[static_cast<size_t>(q)]);
-    });
-    size_t k2i = 0;
+    };
+    if (job.t) job.t->start(static_cast<int>(k2.size()), emulate);
+    // the draws, in node order on the one stream: positions into each far list
+    const int64_t kmax = std::max<int64_t>(num_neg, 1);
+    std::vector<int32_t> pick(static_cast<size_t>(n * kmax));
     std::vector<int32_t> pool;
-    std::vector<int64_t> picks(static_cast<size_t>(std::max<int64_t>(num_neg, 1)));
-    std::vector<int32_t> req_r, req_j;
-    std::vector<uint8_t> req_kind;
-    std::vector<int32_t> direct;      // ids picked on the host (fresh-set nodes), request order
-    std::vector<uint8_t> is_direct;   // per request
     for (int64_t i = 0; i < n; ++i) {
         const int64_t len = u.n_train_set - tib[i];
-        const std::vector<int32_t>* farp = kind[i] == 2 ? &fars[k2i++] : nullptr;
-        auto want = [&](int64_t j) {
-            req_r.push_back(static_cast<int32_t>(i));
-            req_j.push_back(static_cast<int32_t>(j));
-            req_kind.push_back(static_cast<uint8_t>(kind[i] == 1));
-            is_direct.push_back(kind[i] == 2);
-            if (kind[i] == 2) direct.push_back((*farp)[static_cast<size_t>(j)]);
-        };
+        int32_t* out = pick.data() + i * kmax;
         if (num_neg < len) {
             if (len <= setsize) pool.resize(static_cast<size_t>(len));
-            gs::sample_positions(rng->mt, len, num_neg, setsize, picks.data(), pool.data());
-            for (int64_t t = 0; t < num_neg; ++t) want(picks[t]);
+            gs::sample_positions(rng->mt, len, num_neg, setsize, out, pool.data());
             u.neg_cnt[i] = num_neg;
         } else {
-            for (int64_t t = 0; t < len; ++t) want(t);
+            for (int64_t t = 0; t < len; ++t) out[t] = static_cast<int32_t>(t);
             u.neg_cnt[i] = len;
         }
     }
+    const auto t1b = clk::now();
+    // copy-order and ascending-order picks: select queries on the device
+    std::vector<int32_t> req_r, req_j;
+    std::vector<uint8_t> req_kind;
+    for (int64_t i = 0; i < n; ++i)
+        if (kind[i] != 2)
+            for (int64_t t = 0; t < u.neg_cnt[i]; ++t) {
+                req_r.push_back(static_cast<int32_t>(i));
+                req_j.push_back(pick[static_cast<size_t>(i * kmax + t)]);
+                req_kind.push_back(static_cast<uint8_t>(kind[i] == 1));
+            }
     const auto t2 = clk::now();
     std::vector<int32_t> ids;
     gs::unsup_dev_select(u.dev, req_r, req_j, req_kind, ids);
-    size_t dq = 0;
-    u.neg.reserve(2 * req_r.size());
-    for (size_t q = 0; q < req_r.size(); ++q) {
-        u.neg.push_back(u.nodes[static_cast<size_t>(req_r[q])]);
-        u.neg.push_back(is_direct[q] ? direct[dq++] : ids[q]);
+    const auto t2a = clk::now();
+    if (job.t) {
+        job.t->wait();
+        job.t = nullptr;
+    } else {
+        for (int q = 0; q < static_cast<int>(k2.size()); ++q) emulate(q);
+    }
+    const auto t2b = clk::now();
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) total += u.neg_cnt[i];
+    u.neg.resize(static_cast<size_t>(2 * total));
+    size_t q = 0, k2i = 0, at = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t v = u.nodes[static_cast<size_t>(i)];
+        const int32_t* pk = pick.data() + i * kmax;
+        const std::vector<int32_t>* farp = kind[i] == 2 ? &fars[k2i++] : nullptr;
+        for (int64_t t = 0; t < u.neg_cnt[i]; ++t) {
+            u.neg[at++] = v;
+            u.neg[at++] = farp ? (*farp)[static_cast<size_t>(pk[t])] : ids[q++];
+        }
     }
     if (prof) {
         auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
-        std::fprintf(stderr, "[unsup dev] balls %.2f draws %.2f select %.2f ms (%zu picks)\n", ms(t0, t1), ms(t1, t2),
-                     ms(t2, clk::now()), req_r.size());
+        std::fprintf(stderr,
+                     "[unsup dev] balls %.2f far lists %.2f (%zu fresh sets, %lld ids) draws %.2f requests %.2f "
+                     "select %.2f (%zu picks) fresh-order wait %.2f compose %.2f ms\n",
+                     ms(t0, t1), ms(t1, t1a), k2.size(), static_cast<long long>(k2base.back()), ms(t1a, t1b),
+                     ms(t1b, t2), ms(t2, t2a), req_r.size(), ms(t2a, t2b), ms(t2b, clk::now()));
     }
 }
 #endif
@@ -464,11 +499,27 @@ int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, i
 
     const auto tu = clk::now();
     PySet a, b;  // models.py:146
-    for (int64_t x : u->pos) a.add(static_cast<int32_t>(x));
-    for (int64_t x : u->neg) b.add(static_cast<int32_t>(x));
+    // adding a present key leaves a set unchanged (no fill, no resize), so
+    // only first occurrences reach the emulator: a bitmap filters the repeats
+    // (a negatives list repeats its node once per pair)
+    u->seen.resize(static_cast<size_t>((g.n_nodes + 63) >> 6), 0);
+    auto add_distinct = [&](PySet& S, const std::vector<int64_t>& keys) {
+        for (int64_t x : keys) {
+            uint64_t& w = u->seen[static_cast<size_t>(x >> 6)];
+            const uint64_t bit = uint64_t(1) << (x & 63);
+            if (w & bit) continue;
+            w |= bit;
+            S.add(static_cast<int32_t>(x));
+        }
+        S.for_each([&](int32_t x) { u->seen[static_cast<size_t>(x >> 6)] = 0; });
+    };
+    add_distinct(a, u->pos);
+    add_distinct(b, u->neg);
+    const auto tu1 = clk::now();
     PySet r = gs::copy_of(a);
     r.merge(b);
     r.for_each([&](int32_t x) { u->unique.push_back(x); });
+    const auto tu2 = clk::now();
 
     // set(target) < set(unique) (models.py:147): every target present and the
     // union strictly larger than the distinct targets.
@@ -480,8 +531,9 @@ int gs_unsup_extend(gs_unsup* u, gs_rng* rng, const int64_t* nodes, int64_t n, i
 
     if (prof) {
         auto ms = [](clk::time_point x, clk::time_point y) { return std::chrono::duration<double>(y - x).count() * 1e3; };
-        std::fprintf(stderr, "[unsup] walks %.2f negatives %.2f unique+subset %.2f ms\n", ms(tw, tn), ms(tn, tu),
-                     ms(tu, clk::now()));
+        std::fprintf(stderr, "[unsup] walks %.2f negatives %.2f unique: sets %.2f union %.2f subset %.2f ms (%zu pos, %zu neg, %zu unique)\n",
+                     ms(tw, tn), ms(tn, tu), ms(tu, tu1), ms(tu1, tu2), ms(tu2, clk::now()), u->pos.size() / 2,
+                     u->neg.size() / 2, u->unique.size());
     }
     sizes[0] = static_cast<int64_t>(u->unique.size());
     sizes[1] = static_cast<int64_t>(u->pos.size() / 2);

@@ -968,6 +968,7 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
             u.ubef = ds->alloc<int32_t>(ndj + 1);
             u.fresh = ds->alloc<int32_t>(ds->npos_max[j] + ndj);
             u.tcnt = ds->alloc<int32_t>(ds->nd_max[j + 1] + 1);
+            u.longs = ds->alloc<int32_t>(ds->nd_max[j + 1] + 1);
             u.fmask = ds->alloc<uint64_t>(ndj);
             u.sched = ds->alloc<int32_t>(2 * (kMaxStages + 1));
             u.skeys = ds->alloc<int32_t>(2 * static_cast<int64_t>(kBigKeys));

@@ -87,6 +87,8 @@ struct UnionBufs {
     int32_t* sched;            // resize schedule (run, mask) of a big union, [2 * (kMaxStages + 1)]
     int32_t* skeys;            // a big union's stage keys by priority, two stages, [2 * kBigKeys]
     int32_t* lid;              // [n_nodes]: a union key's position in the next frontier (this hop's keys only)
+    int32_t* longs;            // [0] count, then the sources whose transposed list tsort_kernel leaves
+                               // to tlong_kernel, [nd_next_max + 1]
 };
 
 constexpr int kSmallSet = 128;      // table slots of one samp_neighs set (k <= 32)

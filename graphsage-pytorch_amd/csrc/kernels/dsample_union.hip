@@ -36,79 +36,7 @@ namespace ds {
 
 namespace {
 
-constexpr int kTmpSet = 40;                         // resize scratch per lane (ints)
-constexpr int kMaxK = 32;                           // fanouts of hops before the last
-// table + scratch + staged sample ids per lane; odd, so the lanes' tables
-// start in different LDS banks
-constexpr int kLaneSet = kSmallSet + kTmpSet + kMaxK + 1;
 constexpr int kMaxItems = 33;                       // |samp_neighs[r]| <= k + 1 <= 33
-
-__device__ __forceinline__ void ps_clear(int32_t* T, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i) T[i] = -1;
-}
-
-// set_insert_clean: key absent, room in the table.
-__device__ __forceinline__ void ps_insert_clean(int32_t* T, uint32_t mask, int32_t key) {
-    uint32_t perturb = static_cast<uint32_t>(key);
-    uint32_t i = static_cast<uint32_t>(key) & mask;
-    for (;;) {
-        if (T[i] == -1) {
-            T[i] = key;
-            return;
-        }
-        if (i + 9 <= mask) {
-            for (uint32_t j = 1; j <= 9; ++j)
-                if (T[i + j] == -1) {
-                    T[i + j] = key;
-                    return;
-                }
-        }
-        perturb >>= 5;
-        i = (i * 5 + 1 + perturb) & mask;
-    }
-}
-
-struct LSet {
-    int32_t* T;
-    int32_t* tmp;
-    uint32_t mask;
-    int used;
-};
-
-// set_table_resize: smallest power of two > minused, keys re-inserted in slot order.
-__device__ __forceinline__ void ls_resize(LSet& s, int minused) {
-    int n = 0;
-    for (uint32_t i = 0; i <= s.mask; ++i)
-        if (s.T[i] != -1) s.tmp[n++] = s.T[i];
-    uint32_t ns = 8;
-    while (ns <= static_cast<uint32_t>(minused)) ns <<= 1;
-    ps_clear(s.T, ns);
-    s.mask = ns - 1;
-    for (int q = 0; q < n; ++q) ps_insert_clean(s.T, s.mask, s.tmp[q]);
-}
-
-// set_add_entry.
-__device__ __forceinline__ void ls_add(LSet& s, int32_t key) {
-    uint32_t perturb = static_cast<uint32_t>(key);
-    uint32_t i = static_cast<uint32_t>(key) & s.mask;
-    uint32_t e;
-    for (;;) {
-        e = i;
-        uint32_t probes = (i + 9 <= s.mask) ? 9 : 0;
-        for (;;) {
-            if (s.T[e] == -1) goto found_unused;
-            if (s.T[e] == key) return;
-            if (probes-- == 0) break;
-            ++e;
-        }
-        perturb >>= 5;
-        i = (i * 5 + 1 + perturb) & s.mask;
-    }
-found_unused:
-    s.T[e] = key;
-    ++s.used;
-    if (static_cast<uint32_t>(s.used) * 5 >= s.mask * 3) ls_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4);
-}
 
 __device__ __forceinline__ uint32_t mask_for(int64_t minused) {
     uint32_t ns = 8;
@@ -308,78 +236,108 @@ __global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBuf
     if (lane == 0) ub.fmask[r] = m;
 }
 
-// Priority-displacement insertion of this thread's keys (t = tid + 1024 q <
-// nk, priority t) into the LDS table T (every slot EMPTY or holding a
-// priority); returns the rounds once every key sits in its final slot.  In a
-// round every unplaced key walks its probe sequence until it wins a slot — an
-// empty one, or one held by a lower priority (whose key notices below and
-// moves on); then every key checks it still holds its slot and, if not, steps
-// past it.  A slot's value only decreases, so no key revisits a slot it left,
-// and the assignment converges to the sequential one (the highest priority
-// always keeps its first free slot, and by induction every later key).
-__device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const int32_t (&key)[kKPT],
-                                      uint32_t (&ps)[kKPT], int64_t& first_round) {
-    const uint32_t tid = threadIdx.x;
+// Priority-displacement insertion of this thread's keys (t = t0 + tid + 1024 q
+// < t1, priority t) into the LDS table (every slot EMPTY or holding a
+// priority); returns the rounds once every key sits in its final slot.  A key
+// walks its probe sequence until it wins a slot — an empty one, or one held by
+// a lower priority (whose key notices and moves on).  A slot's value only
+// decreases, so no key revisits a slot it left, and the assignment converges
+// to the sequential one whatever the timing (the highest priority always
+// keeps its first free slot, and by induction every later key).
+//
+// Each thread runs to its own fixpoint (re-placing its displaced keys until a
+// pass finds all of them holding their slots) without waiting for the
+// others; a round ends at a barrier, after which a pass with no claims in
+// flight confirms every key.  (Displacement chains across waves still take a
+// round per link: 2-9 rounds at the headline's stages, as with a barrier per
+// step.  A lane-level queue over a thread's keys — one probe step per
+// iteration — measured slower at rmat2m and 15 % faster at Pubmed's 60 %-full
+// stage.)  claim(slot, t) -> t now holds the slot; held(slot) -> its priority.
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+
+template <typename Claim, typename Held>
+__device__ __forceinline__ int settle_keys(uint32_t mask, int t0, int t1, const int32_t (&key)[kKPT],
+                                           uint32_t (&ps)[kKPT], Claim claim, Held held, int64_t* first_round) {
+    const int base = t0 + static_cast<int>(threadIdx.x);
     bool placed[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) placed[q] = false;
     int rounds = 0;
     for (;; ++rounds) {
+        for (;;) {
+            bool moved = false;
 #pragma unroll
-        for (int q = 0; q < kKPT; ++q) {
-            const uint32_t t = tid + 1024u * q;
-            if (t < static_cast<uint32_t>(nk) && !placed[q])
-                for (;;) {
-                    const uint32_t old = atomicMin(&T[pr_slot(ps[q])], t);
-                    if (old > t) break;
-                    ps[q] = pr_next(ps[q], key[q], mask);
+            for (int q = 0; q < kKPT; ++q) {
+                const int t = base + 1024 * q;
+                if (t < t1) {
+                    if (placed[q] && held(pr_slot(ps[q])) != static_cast<uint32_t>(t)) {
+                        ps[q] = pr_next(ps[q], key[q], mask);
+                        placed[q] = false;
+                    }
+                    if (!placed[q]) {
+                        while (!claim(pr_slot(ps[q]), static_cast<uint32_t>(t))) ps[q] = pr_next(ps[q], key[q], mask);
+                        placed[q] = true;
+                        moved = true;
+                    }
                 }
+            }
+            if (!moved) break;
         }
         __syncthreads();
         int any = 0;
 #pragma unroll
         for (int q = 0; q < kKPT; ++q) {
-            const uint32_t t = tid + 1024u * q;
-            if (t < static_cast<uint32_t>(nk)) {
-                placed[q] = T[pr_slot(ps[q])] == t;
-                if (!placed[q]) {
-                    ps[q] = pr_next(ps[q], key[q], mask);
-                    any = 1;
-                }
-            }
+            const int t = base + 1024 * q;
+            if (t < t1) any |= held(pr_slot(ps[q])) != static_cast<uint32_t>(t);
         }
-        if (rounds == 0 && threadIdx.x == 0) first_round = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        if (rounds == 0 && threadIdx.x == 0 && first_round)
+            *first_round = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         if (!__syncthreads_or(any)) break;
     }
     return rounds + 1;
 }
 
+__device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const int32_t (&key)[kKPT],
+                                      uint32_t (&ps)[kKPT], int64_t& first_round) {
+    return settle_keys(
+        mask, 0, nk, key, ps, [&](uint32_t slot, uint32_t t) { return atomicMin(&T[slot], t) > t; },
+        [&](uint32_t slot) { return lds_load(&T[slot]); }, &first_round);
+}
+
 // The next frontier in the final table's slot order, each key's position in
 // it (lid), the pack layout of this hop, the transposed counts zeroed.
 // key_at(slot) -> key or -1.
-template <typename KeyAt>
+// occupied(slot) -> bool (no global read).  The write pass gathers the keys
+// of kGather slots before storing any (the stores could alias the gathered
+// array, so a plain loop waits out one gather per slot).
+constexpr int kGather = 16;
+template <typename KeyAt, typename Occ>
 __device__ __forceinline__ void finish_union(Ctl* c, const HopBufs& hb, const UnionBufs& ub, const HopBufs& next,
                                              int hop, int gcn, int32_t* __restrict__ pack, int nd_next_max,
-                                             uint32_t mf, int used0, int epoch, KeyAt key_at, int* shi) {
+                                             uint32_t mf, int used0, int epoch, KeyAt key_at, Occ occupied, int* shi) {
     HopCtl& h = c->hop[hop];
     const int tid = threadIdx.x;
     const int n = h.n_dst;
     const int sper = static_cast<int>((mf + 1 + 1023) / 1024);
     const uint32_t sa = min<uint32_t>(mf + 1, tid * sper), sb = min<uint32_t>(mf + 1, sa + sper);
     int my_keys = 0;
-    for (uint32_t i = sa; i < sb; ++i) my_keys += key_at(i) != -1;
+    for (uint32_t i = sa; i < sb; ++i) my_keys += occupied(i);
     int n_src;
     int rk = block_excl_scan(my_keys, shi, &n_src);
     if (n_src > nd_next_max) {
         if (tid == 0) c->status |= kStSize;
         return;
     }
-    for (uint32_t i = sa; i < sb; ++i) {
-        const int32_t key = key_at(i);
-        if (key != -1) {
-            ub.lid[key] = rk;
-            next.dst[rk++] = key;
-        }
+    for (uint32_t i0 = sa; i0 < sb; i0 += kGather) {
+        int32_t kk[kGather];
+#pragma unroll
+        for (int j = 0; j < kGather; ++j) kk[j] = i0 + j < sb ? key_at(i0 + j) : -1;
+#pragma unroll
+        for (int j = 0; j < kGather; ++j)
+            if (kk[j] != -1) {
+                ub.lid[kk[j]] = rk;
+                next.dst[rk++] = kk[j];
+            }
     }
     const int g1 = gcn ? 0 : 1;
     const int items_tot = ub.tpre[n];
@@ -435,34 +393,16 @@ __device__ __forceinline__ bool t16_claim(uint32_t* T, uint32_t slot, uint32_t t
     }
 }
 
+__device__ __forceinline__ uint32_t t16_load(const uint32_t* T, uint32_t slot) {
+    return (lds_load(T + (slot >> 1)) >> ((slot & 1) * 16)) & 0xFFFFu;
+}
+
+// settle() on the uint16 table, keys t0 .. t1-1.
 __device__ __forceinline__ void settle16(uint32_t* T, uint32_t mask, int t0, int t1, const int32_t (&key)[kKPT],
                                          uint32_t (&ps)[kKPT]) {
-    const uint32_t tid = threadIdx.x;
-    bool placed[kKPT];
-#pragma unroll
-    for (int q = 0; q < kKPT; ++q) placed[q] = false;
-    for (;;) {
-#pragma unroll
-        for (int q = 0; q < kKPT; ++q) {
-            const int t = t0 + static_cast<int>(tid) + 1024 * q;
-            if (t < t1 && !placed[q])
-                while (!t16_claim(T, pr_slot(ps[q]), static_cast<uint32_t>(t))) ps[q] = pr_next(ps[q], key[q], mask);
-        }
-        __syncthreads();
-        int any = 0;
-#pragma unroll
-        for (int q = 0; q < kKPT; ++q) {
-            const int t = t0 + static_cast<int>(tid) + 1024 * q;
-            if (t < t1) {
-                placed[q] = t16_get(T, pr_slot(ps[q])) == static_cast<uint32_t>(t);
-                if (!placed[q]) {
-                    ps[q] = pr_next(ps[q], key[q], mask);
-                    any = 1;
-                }
-            }
-        }
-        if (!__syncthreads_or(any)) break;
-    }
+    (void)settle_keys(
+        mask, t0, t1, key, ps, [&](uint32_t slot, uint32_t t) { return t16_claim(T, slot, t); },
+        [&](uint32_t slot) { return t16_load(T, slot); }, nullptr);
 }
 
 __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop, int gcn,
@@ -473,7 +413,6 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
     HopCtl& h = c->hop[hop];
     if (!h.big || (c->status & kStTable)) return;
     const int tid = threadIdx.x;
-    const int n = h.n_dst;
     const int used0 = ub.set_cnt[0];
     const uint32_t m_first = static_cast<uint32_t>(ub.first_meta[0]);
     const int nst = ub.sched[2 * kMaxStages + 1];
@@ -481,8 +420,13 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
     uint32_t prev_mask = m_first;
     int32_t key[kKPT];
     uint32_t ps[kKPT];
+    if (tid == 0) {
+        c->dbg[2] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        c->dbg[3] = nst;
+    }
     for (int s = 0; s < nst; ++s) {
         const uint32_t m = static_cast<uint32_t>(ub.sched[2 * s + 1]);
+        if (tid == 0 && s < 12) c->dbg[8 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         int32_t* sk = ub.skeys + (s & 1) * static_cast<int64_t>(kBigKeys);
         const int32_t* sk_prev = ub.skeys + ((s + 1) & 1) * static_cast<int64_t>(kBigKeys);
         // the previous table's keys in slot order, by priority into sk
@@ -496,15 +440,21 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
                 return p == 0xFFFFu ? -1 : sk_prev[p];
             };
             int mine = 0;
-            for (uint32_t i = a0; i < a1; ++i) mine += key_of(i) != -1;
+            for (uint32_t i = a0; i < a1; ++i) mine += s == 0 ? ub.first_tab[i] != -1 : t16_get(T, i) != 0xFFFFu;
             int at = block_excl_scan(mine, shi, &n_old);
-            for (uint32_t i = a0; i < a1; ++i) {
-                const int32_t kk = key_of(i);
-                if (kk != -1) {
-                    sk[at] = kk;
-                    if (s == 0) oldslot[at] = static_cast<int32_t>(i);
-                    ++at;
-                }
+            // kGather gathers in flight before the stores (sk may alias sk_prev
+            // for the compiler: a plain loop waits out one gather per slot)
+            for (uint32_t i0 = a0; i0 < a1; i0 += kGather) {
+                int32_t kk[kGather];
+#pragma unroll
+                for (int j = 0; j < kGather; ++j) kk[j] = i0 + j < a1 ? key_of(i0 + j) : -1;
+#pragma unroll
+                for (int j = 0; j < kGather; ++j)
+                    if (kk[j] != -1) {
+                        sk[at] = kk[j];
+                        if (s == 0) oldslot[at] = static_cast<int32_t>(i0 + j);
+                        ++at;
+                    }
             }
         }
         const int f0 = ub.ubef[ub.sched[2 * s]] - used0, f1 = ub.ubef[ub.sched[2 * (s + 1)]] - used0;
@@ -519,6 +469,10 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
         for (uint32_t i = tid; i <= m / 2; i += 1024) T[i] = 0xFFFFFFFFu;
         __syncthreads();
         const bool copy = s == 0 && m == m_first;
+        if (tid == 0 && s < 12) {
+            c->dbg[9 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+            c->dbg[11 + 4 * s] = (static_cast<int64_t>(nk) << 32) | m;
+        }
         for (int t0 = 0; t0 < nk; t0 += kStageKeys) {
             const int t1 = min(nk, t0 + kStageKeys);
 #pragma unroll
@@ -536,6 +490,7 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
             settle16(T, m, t0, t1, key, ps);
             __syncthreads();
         }
+        if (tid == 0 && s < 12) c->dbg[10 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         prev_mask = m;
     }
     const int32_t* sk_last = ub.skeys + ((nst - 1) & 1) * static_cast<int64_t>(kBigKeys);
@@ -544,7 +499,7 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
                      const uint32_t p = t16_get(T, i);
                      return p == 0xFFFFu ? -1 : sk_last[p];
                  },
-                 shi);
+                 [&](uint32_t i) { return t16_get(T, i) != 0xFFFFu; }, shi);
 }
 
 // The union's table (one block, LDS): the runs' new keys in merge order,
@@ -556,7 +511,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     __shared__ int shi[17];
     __shared__ int st_run[kMaxStages + 1];
     __shared__ uint32_t st_mask[kMaxStages];
-    __shared__ int s_nst, s_best, s_bad, s_epoch, s_big;
+    __shared__ int s_nst, s_bad, s_epoch, s_big;
     HopCtl& h = c->hop[hop];
     const int n = h.n_dst;
     const int tid = threadIdx.x;
@@ -655,6 +610,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         return;
     }
     const int nst = s_nst;
+    if (tid == 0) c->dbg[5] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     if (s_big) {  // the table needs uint16 priorities: ubig_kernel takes over from the schedule
         if (tid <= nst) {
             ub.sched[2 * tid] = st_run[tid];
@@ -739,7 +695,8 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     }
     // the next frontier: keys in slot order, each key's position (lid)
     finish_union(c, hb, ub, next, hop, gcn, pack, nd_next_max, prev_mask, used0, s_epoch,
-                 [&](uint32_t i) { return T[i] == 0xFFFFFFFFu ? -1 : static_cast<int32_t>(T[i]); }, shi);
+                 [&](uint32_t i) { return T[i] == 0xFFFFFFFFu ? -1 : static_cast<int32_t>(T[i]); },
+                 [&](uint32_t i) { return T[i] != 0xFFFFFFFFu; }, shi);
 }
 
 // Per run (one wave, lane q = item q): the destination's neighbourhood in
@@ -775,9 +732,11 @@ __global__ __launch_bounds__(64) void uout_kernel(Ctl* c, HopBufs hb, UnionBufs 
 
 // ---- transposed lists (GS_PK_TPTR / GS_PK_TIDX)
 
-__global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
+__global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt,
+                                                     int32_t* __restrict__ longs) {
     __shared__ int shi[17];
     const HopCtl& h = c->hop[hop];
+    if (threadIdx.x == 0) longs[0] = 0;  // tsort_kernel's queue of long lists
     const int ns = h.n_src;
     if (ns <= 0) return;
     const int per = (ns + 1023) / 1024;
@@ -810,24 +769,100 @@ __global__ __launch_bounds__(64) void tfill_kernel(Ctl* c, int hop, int32_t* __r
 }
 
 // per source: ascending destination, a destination's self entry before its
-// neighbour entry (host order: -(r+1) then r)
-__global__ void tsort_kernel(Ctl* c, int hop, int32_t* __restrict__ pack) {
+// neighbour entry (host order: -(r+1) then r).  Lists longer than kSortReg
+// (the hubs') go to tlong_kernel's queue.
+constexpr int kSortReg = 16;
+__device__ __forceinline__ int32_t tkey(int32_t v) { return v >= 0 ? 2 * v + 1 : -2 * v - 2; }
+__device__ __forceinline__ int32_t tval(int32_t k) { return (k & 1) ? (k - 1) / 2 : -(k + 2) / 2; }
+__global__ void tsort_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* __restrict__ longs) {
     const HopCtl& h = c->hop[hop];
     const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
     if (cidx >= h.n_src) return;
     const int32_t* tp = pack + h.off[GS_PK_TPTR];
     int32_t* x = pack + h.off[GS_PK_TIDX];
     const int lo = tp[cidx], hi = tp[cidx + 1];
-    auto kf = [](int32_t v) { return v >= 0 ? 2 * v + 1 : -2 * v - 2; };
-    for (int i = lo + 1; i < hi; ++i) {
-        const int32_t v = x[i];
-        const int kv = kf(v);
-        int j = i;
-        while (j > lo && kf(x[j - 1]) > kv) {
-            x[j] = x[j - 1];
-            --j;
+    if (hi - lo <= kSortReg) {
+        // short lists (the usual case): every load in flight at once, a
+        // bitonic network on the keys in registers, the keys mapped back
+        // (tkey is one-to-one: odd keys are neighbour entries, even ones self)
+        const int len = hi - lo;
+        if (len <= 1) return;
+        int32_t k[kSortReg];
+#pragma unroll
+        for (int j = 0; j < kSortReg; ++j) k[j] = j < len ? tkey(x[lo + j]) : INT_MAX;
+#pragma unroll
+        for (int kk = 2; kk <= kSortReg; kk <<= 1)
+#pragma unroll
+            for (int jj = kk >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+                for (int i = 0; i < kSortReg; ++i) {
+                    const int l = i ^ jj;
+                    if (l > i) {
+                        const int32_t a = k[i], b = k[l];
+                        const bool up = (i & kk) == 0;
+                        k[i] = up ? min(a, b) : max(a, b);
+                        k[l] = up ? max(a, b) : min(a, b);
+                    }
+                }
+#pragma unroll
+        for (int j = 0; j < kSortReg; ++j)
+            if (j < len) x[lo + j] = tval(k[j]);
+        return;
+    }
+    longs[1 + atomicAdd(&longs[0], 1)] = cidx;
+}
+
+// The long lists: a bitonic sort of the keys in LDS per list (a block per
+// list, grid-stride over the queue); the keys of a list are distinct.  A list
+// beyond kLongLds entries is sorted by one thread (never at the configs'
+// sizes: in-degree within one hop's lists).
+constexpr int kLongLds = 8192;
+constexpr int kLongThreads = 256;
+__global__ __launch_bounds__(kLongThreads) void tlong_kernel(Ctl* c, int hop, int32_t* __restrict__ pack,
+                                                             const int32_t* __restrict__ longs) {
+    __shared__ int32_t sk[kLongLds];
+    const HopCtl& h = c->hop[hop];
+    if (h.n_src <= 0) return;
+    const int n_long = longs[0];
+    const int32_t* tp = pack + h.off[GS_PK_TPTR];
+    int32_t* x = pack + h.off[GS_PK_TIDX];
+    for (int q = blockIdx.x; q < n_long; q += gridDim.x) {
+        const int src = longs[1 + q];
+        const int lo = tp[src], len = tp[src + 1] - lo;
+        if (len > kLongLds) {
+            if (threadIdx.x == 0)
+                for (int i = lo + 1; i < lo + len; ++i) {
+                    const int32_t v = x[i], kv = tkey(v);
+                    int j = i;
+                    while (j > lo && tkey(x[j - 1]) > kv) {
+                        x[j] = x[j - 1];
+                        --j;
+                    }
+                    x[j] = v;
+                }
+            continue;
         }
-        x[j] = v;
+        int P = 1;
+        while (P < len) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += kLongThreads) sk[i] = i < len ? tkey(x[lo + i]) : INT_MAX;
+        __syncthreads();
+        for (int kk = 2; kk <= P; kk <<= 1)
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (int i = threadIdx.x; i < P; i += kLongThreads) {
+                    const int l = i ^ jj;
+                    if (l > i) {
+                        const int32_t a = sk[i], b = sk[l];
+                        const bool up = (i & kk) == 0;
+                        if (up ? a > b : a < b) {
+                            sk[i] = b;
+                            sk[l] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (int i = threadIdx.x; i < len; i += kLongThreads) x[lo + i] = tval(sk[i]);
+        __syncthreads();  // sk is reused by the next list
     }
 }
 
@@ -858,12 +893,14 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     check_launch("ubig_kernel");
     uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);
     check_launch("uout_kernel");
-    tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt);
+    tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt, ub.longs);
     check_launch("tscan_kernel");
     tfill_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hop, pack, ub.tcnt);
     check_launch("tfill_kernel");
-    tsort_kernel<<<static_cast<unsigned>((nd_next_max + 255) / 256), 256, 0, st>>>(c, hop, pack);
+    tsort_kernel<<<static_cast<unsigned>((nd_next_max + 255) / 256), 256, 0, st>>>(c, hop, pack, ub.longs);
     check_launch("tsort_kernel");
+    tlong_kernel<<<256, kLongThreads, 0, st>>>(c, hop, pack, ub.longs);
+    check_launch("tlong_kernel");
 }
 
 }  // namespace ds
