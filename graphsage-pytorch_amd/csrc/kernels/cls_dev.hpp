@@ -61,6 +61,8 @@ struct Groups {
     int64_t off[9];
     int npart[8];
     int n, pstride;
+    bf16_t* sh = nullptr;  // bf16 shadow of params [sh_lo, sh_hi) (g_lowp_shadow), or none
+    int64_t sh_lo = 0, sh_hi = 0;
 };
 
 }  // namespace gs

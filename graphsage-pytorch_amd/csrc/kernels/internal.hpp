@@ -19,6 +19,8 @@ namespace gs {
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
 // Called on the step's stream right after the layer-1 forward launch of a training step.
 void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
+// Inside a runner loop: the SGD keeps the bf16 W1 current (no per-step cast).
+void trainer_keep_lowp(gs_trainer* t, bool keep);
 int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip

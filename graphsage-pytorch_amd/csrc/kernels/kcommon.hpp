@@ -129,6 +129,15 @@ struct DoneFlag {
 };
 inline thread_local DoneFlag g_done_flag;
 
+// bf16 copy of a parameter range the next SGD launch of this thread writes
+// beside the fp32 update (gs_trainer's W1 shadow for bf16 features: the next
+// forward reads it instead of casting W1 again), then clears.
+struct LowpShadow {
+    uint16_t* p = nullptr;  // element i of [lo, hi) goes to p[i - lo]
+    int64_t lo = 0, hi = 0;
+};
+inline thread_local LowpShadow g_lowp_shadow;
+
 template <typename... KArgs, typename... Args>
 inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
     LaunchEvents ev = g_launch_events;

@@ -311,7 +311,10 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         check_launch("gs_sage_linear_fwd(wres)");
         return GS_OK;
     }
-    if ((wide_on || wide32_on) && dt == GS_F32 && vload) {
+    // bf16 takes the wide tiles unless GS_LIN_FWD_BF16=chunked (A/B)
+    static const bool bf16_chunked = std::getenv("GS_LIN_FWD_BF16") &&
+                                     std::string(std::getenv("GS_LIN_FWD_BF16")) == "chunked";
+    if ((wide_on || wide32_on) && vload && (dt == GS_F32 || !bf16_chunked)) {
         const int R = wide32_on ? 32 : kWideRows;
         // XCD map (a 1-D grid, the kernel derives its tile): the column tiles of a row tile share
         // an XCD's L2; GS_FWD_NOXCD=1 restores the 2-D grid (A/B)
@@ -319,16 +322,20 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         const int64_t gx = (n + R - 1) / R, gy = (H + 63) / 64;
         const dim3 gw = (noxcd || gy == 1) ? dim3(static_cast<unsigned>(gx), static_cast<unsigned>(gy))
                                            : dim3(static_cast<unsigned>((gx + 7) / 8 * 8 * gy));
-        const float* xs = static_cast<const float*>(Xs);
-        const float* a = static_cast<const float*>(A);
-        const float* w = static_cast<const float*>(Wd);
-#define GS_LFWDW(RR, SELF, RELU_) \
-        launch_k(linear_fwd_wide_kernel<RR, SELF, RELU_>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K, xs, ldxs, sidx, a, lda, w, out, ldo)
-#define GS_LFWDW_R(RR) \
-        do { if (self) { if (relu) GS_LFWDW(RR, true, true); else GS_LFWDW(RR, true, false); } \
-             else { if (relu) GS_LFWDW(RR, false, true); else GS_LFWDW(RR, false, false); } } while (0)
-        if (R == 32) GS_LFWDW_R(32);
-        else GS_LFWDW_R(64);
+#define GS_LFWDW(TT, RR, SELF, RELU_)                                                                         \
+        launch_k(linear_fwd_wide_kernel<TT, RR, SELF, RELU_>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K,            \
+                 static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda, static_cast<const TT*>(Wd), \
+                 out, ldo)
+#define GS_LFWDW_R(TT, RR) \
+        do { if (self) { if (relu) GS_LFWDW(TT, RR, true, true); else GS_LFWDW(TT, RR, true, false); } \
+             else { if (relu) GS_LFWDW(TT, RR, false, true); else GS_LFWDW(TT, RR, false, false); } } while (0)
+        if (dt == GS_F32) {
+            if (R == 32) GS_LFWDW_R(float, 32);
+            else GS_LFWDW_R(float, 64);
+        } else {
+            if (R == 32) GS_LFWDW_R(bf16_t, 32);
+            else GS_LFWDW_R(bf16_t, 64);
+        }
 #undef GS_LFWDW_R
 #undef GS_LFWDW
         check_launch("gs_sage_linear_fwd(wide)");

@@ -254,10 +254,15 @@ constexpr int kWideRows = 64;
 #define GS_FWD_AHEAD 2
 #endif
 constexpr int kFwdAhead = GS_FWD_AHEAD;  // K chunks in flight ahead of the MFMAs (wide kernels)
-template <int ROWS, bool HAS_SELF, bool RELU>
+// T = bf16_t: the same tiles with 8 elements per slot (a chunk is 128 k) and
+// the 16x16x32 bf16 MFMA per slot pair — operands and order of the chunked
+// bf16 kernel (slots 4g + kq, chunks ascending), so bitwise its output.
+template <typename T, int ROWS, bool HAS_SELF, bool RELU>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
-    int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ W, float* __restrict__ out, int64_t ldo) {
+    int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo) {
+    constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
+    constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
     constexpr int RT = ROWS / 16;   // row tiles
     constexpr int WQ = 64 / ROWS;   // W slots per thread
@@ -280,20 +285,20 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     const int m0 = bx * ROWS, c0 = by * 64;
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
     const int arow_i = min(m0 + lr, n - 1);
-    const float* arow = A + static_cast<int64_t>(arow_i) * lda;
-    const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
-    const float* wrow[WQ];
+    const T* arow = A + static_cast<int64_t>(arow_i) * lda;
+    const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
+    const T* wrow[WQ];
 #pragma unroll
     for (int q = 0; q < WQ; ++q) wrow[q] = W + static_cast<int64_t>(min(c0 + lr + ROWS * q, H - 1)) * K;
-    const int nC = (K + 63) / 64;
+    const int nC = (K + BK - 1) / BK;
     // register ring of kFwdAhead chunks: slot u holds chunk c (c = u mod
     // kFwdAhead) once it is in LDS and is then refilled with chunk c + kFwdAhead
     uint4 ar[kFwdAhead], wr_[kFwdAhead][WQ];
     auto load = [&](int c, int u) {
-        const int kn = min(c, nC - 1) * 64;  // past the end: re-read the last chunk (never stored)
-        ar[u] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + ls * 4);
+        const int kn = min(c, nC - 1) * BK;  // past the end: re-read the last chunk (never stored)
+        ar[u] = concat_slot<T, HAS_SELF, true>(srow, arow, F, K, kn + ls * EPV);
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot<float, false, true>(nullptr, wrow[q], K, K, kn + ls * 4);
+        for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot<T, false, true>(nullptr, wrow[q], K, K, kn + ls * EPV);
     };
     auto stash = [&](int c, int u) {
         sA[c & 1][lr * SP + ls] = ar[u];
@@ -321,7 +326,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
                 wv[g] = tw[4 * g + kq];
             }
 #pragma unroll
-            for (int g = 0; g < 4; ++g) acc = mfma_slot<float>(av[g], wv[g], acc);
+            for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
             __builtin_amdgcn_sched_barrier(0);
             if (c + 1 < nC) stash(c + 1, (u + 1) % kFwdAhead);
         }

@@ -286,7 +286,9 @@ __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ 
         while (i >= G.off[grp + 1]) ++grp;
         const float gi = g[i] * mult[grp];
         g[i] = gi;
-        p[i] = p[i] - lr * gi;
+        const float pn = p[i] - lr * gi;
+        p[i] = pn;
+        if (G.sh && i >= G.sh_lo && i < G.sh_hi) G.sh[i - G.sh_lo] = f2bf(pn);
     }
 }
 
@@ -341,6 +343,12 @@ __global__ __launch_bounds__(kTb) void sgd4_kernel(Groups G, float* __restrict__
         pn.z = pv.z - lr * gi.z;
         pn.w = pv.w - lr * gi.w;
         p4[i] = pn;
+        if (G.sh && 4 * i >= G.sh_lo && 4 * i < G.sh_hi) {  // sh_lo, sh_hi multiples of 4
+            uint2 b;
+            b.x = static_cast<uint32_t>(f2bf(pn.x)) | (static_cast<uint32_t>(f2bf(pn.y)) << 16);
+            b.y = static_cast<uint32_t>(f2bf(pn.z)) | (static_cast<uint32_t>(f2bf(pn.w)) << 16);
+            *reinterpret_cast<uint2*>(G.sh + (4 * i - G.sh_lo)) = b;
+        }
     }
 }
 
@@ -422,8 +430,14 @@ void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart
     for (int i = 0; i < n_groups; ++i) G.npart[i] = npart[i];
     for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
     const int64_t total = G.off[n_groups];
+    const LowpShadow sh = g_lowp_shadow;
+    g_lowp_shadow = {};
+    G.sh = sh.p;
+    G.sh_lo = sh.lo;
+    G.sh_hi = sh.hi;
     bool vec = aligned16(params) && aligned16(grads) && std::getenv("GS_SGD_SCALAR") == nullptr;
     for (int i = 0; i <= n_groups; ++i) vec = vec && G.off[i] % 4 == 0;
+    vec = vec && (!sh.p || (sh.lo % 4 == 0 && sh.hi % 4 == 0 && reinterpret_cast<uintptr_t>(sh.p) % 8 == 0));
     if (vec) {  // 4.9 us -> see DESIGN §4 (rmat2m, ~100k parameters)
         const int64_t n4 = total / 4;
         const dim3 grid(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + kTb - 1) / kTb, 512))));
@@ -464,9 +478,14 @@ int gs_clip_sgd(int32_t n_groups, const int64_t* goff_host, float* params, float
     using namespace gs;
     GS_REQUIRE(n_groups >= 1 && n_groups <= 8 && goff_host, GS_EINVAL, "1..8 parameter groups");
     GS_REQUIRE(params && grads && ws, GS_EINVAL, "NULL device pointer");
+    const LowpShadow sh = g_lowp_shadow;
+    g_lowp_shadow = {};
     Groups G;
     G.n = n_groups;
     G.pstride = kNormBlocks;
+    G.sh = sh.p;
+    G.sh_lo = sh.lo;
+    G.sh_hi = sh.hi;
     for (int i = 0; i < n_groups; ++i) G.npart[i] = kNormBlocks;
     for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
     for (int i = 0; i < n_groups; ++i) GS_REQUIRE(G.off[i] <= G.off[i + 1], GS_EINVAL, "group offsets not sorted");

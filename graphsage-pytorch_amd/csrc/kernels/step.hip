@@ -58,8 +58,15 @@ struct gs_trainer {
     bool norm_ready = false;
     std::function<void(hipStream_t)> upper_hook;  // internal.hpp trainer_set_upper_hook
     std::function<void(hipStream_t)> fwd1_hook;   // after the layer-1 forward launch (trainer_set_fwd1_hook)
+    // bf16 features: W1 in bf16 for the layer-1 forward.  Cast from the fp32
+    // W1 before a forward, except inside a runner loop (lp_keep), where the
+    // SGD launch writes it beside W1 (g_lowp_shadow) and it stays valid from
+    // one step to the next: nothing else writes the parameters there.
+    uint16_t* w1_lp = nullptr;
+    bool lp_keep = false, lp_valid = false;
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
+        if (w1_lp) (void)hipFree(w1_lp);
         for (auto& tm : timer) {
             for (auto e : tm.ev0) (void)hipEventDestroy(e);
             for (auto e : tm.ev1) (void)hipEventDestroy(e);
@@ -227,7 +234,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         h[l - 1] = (embed_out && l == L) ? embed_out : cv.take<float>(rows[l - 1] * H);
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
     }
-    void* w1lp = lowp ? cv.take<uint16_t>(T.w_rows[0] * T.w_cols[0]) : nullptr;
     float* demb = cv.take<float>(B * H);
     float* cls_ws = cv.take<float>(gs_cls_nll_ws_floats(B, H, c.n_classes));
     int64_t dw_need = 0, dx_rows = 0, dprev_rows = 0;
@@ -250,9 +256,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     float* P = c.params;
     float* G = c.grads;
     // ---- forward (models.py:255-267)
-    if (lowp) ok(gs_cast_f32_bf16(P + T.w_off[0], w1lp, T.w_rows[0] * T.w_cols[0], st));
+    if (lowp && !(T.lp_keep && T.lp_valid)) {
+        ok(gs_cast_f32_bf16(P + T.w_off[0], T.w1_lp, T.w_rows[0] * T.w_cols[0], st));
+        T.lp_valid = T.lp_keep;
+    }
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
-    const void* W1 = lowp ? w1lp : static_cast<const void*>(P + T.w_off[0]);
+    const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
     if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
         const bool timed = timed_arm(T, 0);
@@ -445,6 +454,27 @@ int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols
 
 }  // namespace gs
 
+namespace {
+// The SGD launch that follows also writes the bf16 W1 (runner loops only).
+struct ShadowArm {
+    gs_trainer* t;
+    explicit ShadowArm(gs_trainer* t_) : t(t_) {
+        t->lp_valid = false;
+        if (t->lp_keep && t->w1_lp)
+            gs::g_lowp_shadow = {t->w1_lp, t->w_off[0], t->w_off[0] + t->w_rows[0] * t->w_cols[0]};
+    }
+    void done() { t->lp_valid = t->lp_keep && t->w1_lp; }
+    ~ShadowArm() { gs::g_lowp_shadow = {}; }
+};
+}  // namespace
+
+namespace gs {
+void trainer_keep_lowp(gs_trainer* t, bool keep) {
+    t->lp_keep = keep;
+    t->lp_valid = false;
+}
+}  // namespace gs
+
 extern "C" {
 
 int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
@@ -478,6 +508,11 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
         if (hipMalloc(&T->norm_part, 2 * T->pstride * sizeof(float)) != hipSuccess) {
             delete T;
             gs::fail(GS_ENOMEM, "hipMalloc(norm partials)");
+        }
+        if (cfg->feat_dtype == GS_BF16 &&
+            hipMalloc(&T->w1_lp, T->w_rows[0] * T->w_cols[0] * sizeof(uint16_t)) != hipSuccess) {
+            delete T;
+            gs::fail(GS_ENOMEM, "hipMalloc(bf16 W1)");
         }
     }
     T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
@@ -645,6 +680,7 @@ int gs_trainer_update_local(gs_trainer* t, void* stream) {
     GS_API_BEGIN
     GS_REQUIRE(t, GS_EINVAL, "NULL argument");
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
+    ShadowArm arm(t);
     if (t->norm_ready) {
         gs::sgd_with_parts(2, goff, t->npart, t->pstride, t->cfg.params, t->cfg.grads, t->norm_part, 1.0f,
                            t->cfg.max_norm, t->cfg.lr, gs::as_stream(stream));
@@ -653,6 +689,7 @@ int gs_trainer_update_local(gs_trainer* t, void* stream) {
                                    t->norm_part, stream);
         if (rc != GS_OK) return rc;
     }
+    arm.done();
     t->norm_ready = false;
     GS_API_END
 }
@@ -662,8 +699,10 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
     t->norm_ready = false;
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
+    ShadowArm arm(t);
     int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);
     if (rc != GS_OK) return rc;
+    arm.done();
     GS_API_END
 }
 

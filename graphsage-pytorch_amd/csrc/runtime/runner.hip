@@ -774,6 +774,15 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 }
         }
     } unwind{r, st};
+    struct KeepLowp {  // the SGD keeps the bf16 W1 current for this loop's steps only
+        gs_trainer* t;
+        explicit KeepLowp(gs_trainer* t_) : t(t_) {
+            if (t) gs::trainer_keep_lowp(t, true);
+        }
+        ~KeepLowp() {
+            if (t) gs::trainer_keep_lowp(t, false);
+        }
+    } keep_lowp{r->cfg.trainer};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();
