@@ -65,4 +65,75 @@ struct Groups {
     int64_t sh_lo = 0, sh_hi = 0;
 };
 
+// Host-visible step-completion flag (kcommon.hpp DoneFlag), stored by the
+// first thread of the launch.
+__device__ __forceinline__ void signal_done(int64_t* done, int64_t value) {
+    if (done && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Clip (per group, utils.py:186-187) + SGD (utils.py:187-190) on float4
+// (every group offset a multiple of 4, 16-B aligned arrays), block bx of
+// nblk: wave w folds group w's norm partials (lane-strided loads, then a
+// fixed xor-tree: the same order in every block and for any block size),
+// then each thread updates its quads; each thread's first g / p quads are
+// loaded before the fold, so the two dependent rounds overlap.  With G.sh the
+// new params of [sh_lo, sh_hi) also go to the bf16 shadow.
+__device__ __forceinline__ void sgd4_body(const Groups& G, float* __restrict__ p, float* __restrict__ g,
+                                          const float* __restrict__ part, float scale, float max_norm, float lr,
+                                          int bx, int nblk) {
+    __shared__ float mult[8];
+    const int nthr = static_cast<int>(blockDim.x);
+    const int64_t n4 = G.off[G.n] / 4;
+    const int64_t i0 = bx * int64_t(nthr) + threadIdx.x;
+    float4* g4 = reinterpret_cast<float4*>(g);
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), pv = gv;
+    if (i0 < n4) {
+        gv = g4[i0];
+        pv = p4[i0];
+    }
+    const int lane = threadIdx.x & 63;
+    for (int grp = threadIdx.x >> 6; grp < G.n; grp += nthr / 64) {
+        const float* pg = part + grp * G.pstride;
+        const int np = G.npart[grp];
+        float t = 0.f;
+#pragma unroll 4
+        for (int b = lane; b < np; b += 64) t += pg[b];
+        t = wave_sum(t);
+        if (lane == 0) {
+            const float norm = sqrtf(t) * scale;
+            mult[grp] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+        }
+    }
+    __syncthreads();
+    for (int64_t i = i0; i < n4; i += int64_t(nblk) * nthr) {
+        if (i != i0) {
+            gv = g4[i];
+            pv = p4[i];
+        }
+        int grp = 0;
+        while (4 * i >= G.off[grp + 1]) ++grp;
+        const float m = mult[grp];
+        float4 gi;
+        gi.x = gv.x * m;
+        gi.y = gv.y * m;
+        gi.z = gv.z * m;
+        gi.w = gv.w * m;
+        g4[i] = gi;
+        float4 pn;
+        pn.x = pv.x - lr * gi.x;
+        pn.y = pv.y - lr * gi.y;
+        pn.z = pv.z - lr * gi.z;
+        pn.w = pv.w - lr * gi.w;
+        p4[i] = pn;
+        if (G.sh && 4 * i >= G.sh_lo && 4 * i < G.sh_hi) {  // sh_lo, sh_hi multiples of 4
+            uint2 b;
+            b.x = static_cast<uint32_t>(f2bf(pn.x)) | (static_cast<uint32_t>(f2bf(pn.y)) << 16);
+            b.y = static_cast<uint32_t>(f2bf(pn.z)) | (static_cast<uint32_t>(f2bf(pn.w)) << 16);
+            *reinterpret_cast<uint2*>(G.sh + (4 * i - G.sh_lo)) = b;
+        }
+    }
+}
+
 }  // namespace gs

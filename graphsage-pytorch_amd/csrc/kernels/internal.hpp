@@ -21,6 +21,11 @@ void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook
 void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
 // Inside a runner loop: the SGD keeps the bf16 W1 current (no per-step cast).
 void trainer_keep_lowp(gs_trainer* t, bool keep);
+// Inside a runner loop without an all-reduce: the step's last launch runs the
+// clip + SGD too (gs_trainer_update_local is then a no-op for that step).
+void trainer_fuse_update(gs_trainer* t, bool fuse);
+// A fused SGD launch's grid barrier gave up waiting (never expected).
+bool trainer_barrier_failed(gs_trainer* t);
 int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip
@@ -40,6 +45,27 @@ struct SlabSum {
 // sum, S2 <= 1 = nothing to add); returns s1's partial count.
 bool sum_slabs_pair_ok(int64_t len1);
 int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st);
+// The clip + SGD that follows a step's last slab sum (no all-reduce between):
+// flat params / grads, group offsets and norm partials as sgd_with_parts
+// takes them, the bf16 W1 shadow (g_lowp_shadow) and the done flag
+// (g_done_flag) of the launching thread.
+struct FusedSgd {
+    int32_t n_groups;
+    const int64_t* goff_host;
+    const int* npart;
+    int pstride;
+    float* params;
+    float* grads;
+    const float* part;
+    float max_norm, lr;
+    unsigned long long* bar;     // grid-barrier counter (device, never reset)
+    unsigned long long* bar_gen; // host copy: arrivals so far
+    int* bar_err;                // set when a barrier wait gave up (device)
+};
+// sum_slabs_pair_launch, a grid barrier, then the clip + SGD in the same
+// launch (one dependent kernel boundary and the SGD's own launch fewer).
+int sum_slabs_pair_sgd_launch(const SlabSum& s1, const SlabSum& s2, int np_before, const FusedSgd& u,
+                              hipStream_t st);
 int sum_slabs_grid(int64_t len);
 
 // agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)

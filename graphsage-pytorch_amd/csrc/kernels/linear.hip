@@ -3,6 +3,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "cls_dev.hpp"
 #include "internal.hpp"
 #include "linear_dev.hpp"
 
@@ -70,6 +71,48 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum
         return;
     }
     sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+}
+
+// sum_slabs_pair_kernel, then every block waits at a grid barrier (all
+// gradients and norm partials written) and runs its share of the clip + SGD
+// (sgd4_body: the same fold and per-element arithmetic as sgd4_kernel, so
+// the parameters are bitwise those of the two-launch sequence).  The barrier
+// is a never-reset arrival counter: launch g waits for g · grid arrivals.
+// Every block of the grid is resident once earlier work drains (289 blocks
+// of 8 waves at the 2-layer step); a block that has waited ~1 s regardless
+// records it in *bar_err and goes on (the step is then wrong, never hung).
+struct SgdLaunch {
+    Groups G;
+    float* p;
+    float* g;
+    const float* part;
+    float max_norm, lr;
+    int64_t* done;
+    int64_t done_value;
+    unsigned long long* bar;
+    unsigned long long target;
+    int* bar_err;
+};
+__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_sgd_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2,
+                                                                             SgdLaunch u) {
+    signal_done(u.done, u.done_value);
+    const int bx = blockIdx.x;
+    if (bx < nb2) sum_slabs_body(bx, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
+    else sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+    __syncthreads();  // the block's sums and partials written; thread 0 publishes them
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(u.bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        while (__hip_atomic_load(u.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < u.target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                __hip_atomic_store(u.bar_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();  // thread 0's acquire covers the block (as a cooperative grid sync)
+    sgd4_body(u.G, u.p, u.g, u.part, 1.0f, u.max_norm, u.lr, bx, gridDim.x);
 }
 
 // ------------------------------------------------- W-stationary forward
@@ -455,6 +498,45 @@ int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st) 
     const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
     sum_slabs_pair_kernel<<<dim3(static_cast<unsigned>(nb1 + nb2)), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2);
     check_launch("sum_slabs_pair");
+    return nb1;
+}
+
+int sum_slabs_pair_sgd_launch(const SlabSum& s1, const SlabSum& s2, int np_before, const FusedSgd& u,
+                              hipStream_t st) {
+    GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1, GS_EINVAL, "slab pair: layer-1 sum not split");
+    GS_REQUIRE(u.n_groups >= 1 && u.n_groups <= 8, GS_EINVAL, "1..8 parameter groups");
+    const int nb1 = static_cast<int>(slab_split_blocks(s1.len));
+    const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
+    SgdLaunch a;
+    a.G.n = u.n_groups;
+    a.G.pstride = u.pstride;
+    for (int i = 0; i < u.n_groups; ++i) a.G.npart[i] = u.npart[i];
+    a.G.npart[0] = np_before + nb1;  // group 0: the partials before this launch and its layer-1 ones
+    for (int i = 0; i <= u.n_groups; ++i) a.G.off[i] = u.goff_host[i];
+    bool vec = aligned16(u.params) && aligned16(u.grads);
+    for (int i = 0; i <= u.n_groups; ++i) vec = vec && a.G.off[i] % 4 == 0;
+    const LowpShadow sh = g_lowp_shadow;
+    vec = vec && (!sh.p || (sh.lo % 4 == 0 && sh.hi % 4 == 0 && reinterpret_cast<uintptr_t>(sh.p) % 8 == 0));
+    GS_REQUIRE(vec, GS_EINVAL, "fused SGD needs 16-B aligned float4 groups");
+    g_lowp_shadow = {};
+    a.G.sh = sh.p;
+    a.G.sh_lo = sh.lo;
+    a.G.sh_hi = sh.hi;
+    a.p = u.params;
+    a.g = u.grads;
+    a.part = u.part;
+    a.max_norm = u.max_norm;
+    a.lr = u.lr;
+    a.done = g_done_flag.ptr;
+    a.done_value = g_done_flag.value;
+    g_done_flag = {};
+    const unsigned nb = static_cast<unsigned>(nb1 + nb2);
+    *u.bar_gen += nb;
+    a.bar = u.bar;
+    a.target = *u.bar_gen;
+    a.bar_err = u.bar_err;
+    sum_slabs_pair_sgd_kernel<<<dim3(nb), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2, a);
+    check_launch("sum_slabs_pair_sgd");
     return nb1;
 }
 

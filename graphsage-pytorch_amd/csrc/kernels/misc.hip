@@ -254,11 +254,6 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
 // every block) into clip_coef = max_norm / (||scale·g|| + 1e-6) clamped to 1,
 // then p -= lr · (scale · coef) · g and g is left scaled like torch's in-place
 // clip.
-__device__ __forceinline__ void signal_done(int64_t* done, int64_t value) {
-    if (done && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
                                                   const float* __restrict__ part, float scale, float max_norm,
                                                   float lr, int64_t* done, int64_t done_value) {
@@ -292,64 +287,12 @@ __global__ __launch_bounds__(kTb) void sgd_kernel(Groups G, float* __restrict__ 
     }
 }
 
-// sgd_kernel on float4 (every group offset a multiple of 4, 16-B aligned
-// arrays): each thread's first g / p quads are loaded before the partial fold,
-// so the two dependent rounds overlap; the same per-element arithmetic.
+// sgd_kernel on float4 (sgd4_body, cls_dev.hpp).
 __global__ __launch_bounds__(kTb) void sgd4_kernel(Groups G, float* __restrict__ p, float* __restrict__ g,
                                                    const float* __restrict__ part, float scale, float max_norm,
                                                    float lr, int64_t* done, int64_t done_value) {
     signal_done(done, done_value);
-    __shared__ float mult[8];
-    const int64_t n4 = G.off[G.n] / 4;
-    const int64_t i0 = blockIdx.x * int64_t(kTb) + threadIdx.x;
-    float4* g4 = reinterpret_cast<float4*>(g);
-    float4* p4 = reinterpret_cast<float4*>(p);
-    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f), pv = gv;
-    if (i0 < n4) {
-        gv = g4[i0];
-        pv = p4[i0];
-    }
-    const int lane = threadIdx.x & 63;
-    for (int grp = threadIdx.x >> 6; grp < G.n; grp += kTb / 64) {
-        const float* pg = part + grp * G.pstride;
-        const int np = G.npart[grp];
-        float t = 0.f;
-#pragma unroll 4
-        for (int b = lane; b < np; b += 64) t += pg[b];
-        t = wave_sum(t);
-        if (lane == 0) {
-            const float norm = sqrtf(t) * scale;
-            mult[grp] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
-        }
-    }
-    __syncthreads();
-    for (int64_t i = i0; i < n4; i += int64_t(gridDim.x) * kTb) {
-        if (i != i0) {
-            gv = g4[i];
-            pv = p4[i];
-        }
-        int grp = 0;
-        while (4 * i >= G.off[grp + 1]) ++grp;
-        const float m = mult[grp];
-        float4 gi;
-        gi.x = gv.x * m;
-        gi.y = gv.y * m;
-        gi.z = gv.z * m;
-        gi.w = gv.w * m;
-        g4[i] = gi;
-        float4 pn;
-        pn.x = pv.x - lr * gi.x;
-        pn.y = pv.y - lr * gi.y;
-        pn.z = pv.z - lr * gi.z;
-        pn.w = pv.w - lr * gi.w;
-        p4[i] = pn;
-        if (G.sh && 4 * i >= G.sh_lo && 4 * i < G.sh_hi) {  // sh_lo, sh_hi multiples of 4
-            uint2 b;
-            b.x = static_cast<uint32_t>(f2bf(pn.x)) | (static_cast<uint32_t>(f2bf(pn.y)) << 16);
-            b.y = static_cast<uint32_t>(f2bf(pn.z)) | (static_cast<uint32_t>(f2bf(pn.w)) << 16);
-            *reinterpret_cast<uint2*>(G.sh + (4 * i - G.sh_lo)) = b;
-        }
-    }
+    sgd4_body(G, p, g, part, scale, max_norm, lr, blockIdx.x, gridDim.x);
 }
 
 }  // namespace gs

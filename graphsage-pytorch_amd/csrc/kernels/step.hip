@@ -64,9 +64,17 @@ struct gs_trainer {
     // one step to the next: nothing else writes the parameters there.
     uint16_t* w1_lp = nullptr;
     bool lp_keep = false, lp_valid = false;
+    // Inside a runner loop without an all-reduce (fuse_update): the step's
+    // last slab sum also runs the clip + SGD (sum_slabs_pair_sgd_launch) and
+    // gs_trainer_update_local then has nothing left to do (update_done).
+    bool fuse_update = false, update_done = false;
+    unsigned long long* bar = nullptr;  // its grid-barrier counter (device) and arrivals so far
+    unsigned long long bar_gen = 0;
+    int* bar_err = nullptr;
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
         if (w1_lp) (void)hipFree(w1_lp);
+        if (bar) (void)hipFree(bar);
         for (auto& tm : timer) {
             for (auto e : tm.ev0) (void)hipEventDestroy(e);
             for (auto e : tm.ev1) (void)hipEventDestroy(e);
@@ -380,6 +388,27 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                                            dw_ws, dw_need, st);
             g_launch_events = {};
             timed_done(T, 2, armed);
+            const int n_cls = cls_reduce_grid(c.n_classes, H);
+            if (defer && S1 > 1 && T.fuse_update && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
+                n_cls <= T.pstride) {
+                // the clip + SGD in the same launch (gs_trainer_update_local's work)
+                d2.part = T.norm_part;
+                const int64_t goff[3] = {0, T.cls_w_off, T.total};
+                const int npart[2] = {0, n_cls};
+                const FusedSgd u{2, goff, npart, T.pstride, P, G, T.norm_part, c.max_norm, c.lr, T.bar, &T.bar_gen,
+                                 T.bar_err};
+                T.lp_valid = false;
+                if (T.lp_keep && T.w1_lp)
+                    g_lowp_shadow = {T.w1_lp, T.w_off[0], T.w_off[0] + T.w_rows[0] * T.w_cols[0]};
+                sum_slabs_pair_sgd_launch(SlabSum{reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0],
+                                                  T.norm_part + np},
+                                          d2, np, u, st);
+                g_lowp_shadow = {};
+                T.lp_valid = T.lp_keep && T.w1_lp;
+                T.update_done = true;
+                T.norm_ready = false;
+                return cv.at;
+            }
             if (defer && S1 > 1) {
                 d2.part = T.norm_part;
                 np += sum_slabs_pair_launch(SlabSum{reinterpret_cast<const float*>(dw_ws), S1, H * K1,
@@ -395,7 +424,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 parts = false;
             }
             T.npart[0] = np;
-            T.npart[1] = cls_reduce_grid(c.n_classes, H);
+            T.npart[1] = n_cls;
             T.norm_ready = parts && np <= T.pstride && T.npart[1] <= T.pstride;
             return cv.at;
         }
@@ -473,6 +502,18 @@ void trainer_keep_lowp(gs_trainer* t, bool keep) {
     t->lp_keep = keep;
     t->lp_valid = false;
 }
+
+void trainer_fuse_update(gs_trainer* t, bool fuse) {
+    t->fuse_update = fuse;
+    t->update_done = false;
+}
+
+bool trainer_barrier_failed(gs_trainer* t) {
+    int e = 0;
+    if (hipMemcpy(&e, t->bar_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        fail(GS_EHIP, "hipMemcpy(barrier flag)");
+    return e != 0;
+}
 }  // namespace gs
 
 extern "C" {
@@ -514,6 +555,11 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
             delete T;
             gs::fail(GS_ENOMEM, "hipMalloc(bf16 W1)");
         }
+        if (hipMalloc(&T->bar, 16) != hipSuccess || hipMemset(T->bar, 0, 16) != hipSuccess) {
+            delete T;
+            gs::fail(GS_ENOMEM, "hipMalloc(barrier)");
+        }
+        T->bar_err = reinterpret_cast<int*>(T->bar + 1);
     }
     T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
     T->use_top = std::getenv("GS_NO_TOP") == nullptr;
@@ -679,6 +725,11 @@ const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site) {
 int gs_trainer_update_local(gs_trainer* t, void* stream) {
     GS_API_BEGIN
     GS_REQUIRE(t, GS_EINVAL, "NULL argument");
+    if (t->update_done) {  // the step's last launch already ran the clip + SGD
+        t->update_done = false;
+        t->norm_ready = false;
+        return GS_OK;
+    }
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     ShadowArm arm(t);
     if (t->norm_ready) {
@@ -698,6 +749,7 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     GS_API_BEGIN
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
     t->norm_ready = false;
+    GS_REQUIRE(!t->update_done, GS_EINVAL, "the step's fused launch already applied the SGD");
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     ShadowArm arm(t);
     int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);

@@ -521,6 +521,14 @@ gs_runner::~gs_runner() {
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
     }
     if (cfg.trainer && comm_stream) gs::trainer_set_upper_hook(cfg.trainer, {});
+    if (cfg.trainer && !cfg.comm && !cfg.embed_out) {  // drained above; never expected
+        try {
+            if (gs::trainer_barrier_failed(cfg.trainer))
+                std::fprintf(stderr, "graphsage_amd: a fused SGD launch's grid barrier timed out; "
+                                     "the parameters of that step are not trustworthy\n");
+        } catch (...) {
+        }
+    }
     if (upper_ready) (void)hipEventDestroy(upper_ready);
     if (upper_reduced) (void)hipEventDestroy(upper_reduced);
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
@@ -766,6 +774,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         hipStream_t st;
         bool armed = true;
         ~Unwind() {
+            gs::g_done_flag = {};  // never left for a later SGD launch of this thread
             if (!armed) return;
             for (int k = 0; k < gs_runner::kDev; ++k)
                 if (r->flag_step[k] >= 0 && hipEventRecord(r->dev_done[k], st) == hipSuccess) {
@@ -783,6 +792,21 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             if (t) gs::trainer_keep_lowp(t, false);
         }
     } keep_lowp{r->cfg.trainer};
+    // GS_FUSED_SGD=1, no all-reduce: the step's last launch runs the clip + SGD
+    // behind a grid barrier.  Off: the barrier waits out the side stream's
+    // gather (blocks not yet resident), 88 us against 8.3 + 4.2 us for the
+    // two launches (rocprof, rmat2m).
+    struct FuseUpdate {
+        gs_trainer* t;
+        explicit FuseUpdate(gs_trainer* t_) : t(t_) {
+            if (t) gs::trainer_fuse_update(t, true);
+        }
+        ~FuseUpdate() {
+            if (t) gs::trainer_fuse_update(t, false);
+        }
+    } fuse_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && std::getenv("GS_FUSED_SGD")
+                      ? r->cfg.trainer
+                      : nullptr};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();
@@ -840,6 +864,9 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             t3 = Clock::now();
         } else {
             r->cur_k = k;
+            // the done flag goes to the step's SGD launch: the fused slab sum
+            // inside the step, or gs_trainer_update* below
+            if (r->use_flag) g_done_flag = {r->done_dev, b};
             int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, hop_sizes, offsets,
                                                           pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
                                                           st);
@@ -864,7 +891,6 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 rc = gs_comm_allreduce_sum(r->cfg.comm, grads, n_params, st);
                 if (rc != GS_OK) fail(rc, gs_last_error());
             }
-            if (r->use_flag) g_done_flag = {r->done_dev, b};
             rc = r->cfg.comm
                      ? gs_trainer_update(r->cfg.trainer, 1.0f / static_cast<float>(r->cfg.world), r->clip_ws, st)
                      : gs_trainer_update_local(r->cfg.trainer, st);
