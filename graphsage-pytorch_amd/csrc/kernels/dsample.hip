@@ -391,6 +391,9 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
     const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
+    // phase stamps of one workgroup of the last hop (gs_dsampler_debug slots 56..61)
+    const bool stamp = hop > 0 && b == h.n_blocks / 2 && blockIdx.y == 0 && tid == 0;
+    if (stamp) c->dbg[56] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     // masks: [node][draw][kMChunks] (pool: k draws, selected-set: 1), then the words
     uint64_t* masks = smem64;
     uint32_t* w = reinterpret_cast<uint32_t*>(masks + R * max(k, 1) * kMChunks);
@@ -427,6 +430,7 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     }
     __syncthreads();
     const int nsr = s_nsr;
+    if (stamp) c->dbg[57] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     // build: node m's window starts at word m * k (entry e0, no rejections yet)
     for (int t = wave; t < nsr * kMChunks; t += kMEntries / 64) {
         const int q = t / kMChunks, ch = t - q * kMChunks;
@@ -447,6 +451,7 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
         }
     }
     __syncthreads();
+    if (stamp) c->dbg[58] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     const int ent = e0 + tid;
     int u = ent < bw ? tid : -1;  // word index relative to e0
     uint8_t* rej = hb.rej + static_cast<int64_t>(b) * R * kWMax + ent;
@@ -464,6 +469,11 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
         }
     }
     if (rej_over) atomicOr(&c->status, kStWords);  // a node with > 254 rejections: never seen, reported
+    if (stamp) {
+        c->dbg[59] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
+        c->dbg[60] = nsr | (static_cast<int64_t>(bw) << 16) | (static_cast<int64_t>(h.n_blocks) << 32);
+        c->dbg[61] = gridDim.y | (static_cast<int64_t>(h.W) << 16) | (static_cast<int64_t>(ndr) << 32);
+    }
     if (ent < bw) {
         uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
         const int dr = u < 0 ? -1 : u - tid - ndr;
