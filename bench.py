@@ -261,14 +261,25 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 # rocprofv3 --kernel-trace --stats summaries of the bench command, per config
 # and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
 # the kernel beside the live event-timed one
-ROCPROF_STATS = {("rmat2m", 512): "profiles/r02_kernel_stats_rmat2m_steps300.csv",
-                 ("rmat2m-max-bf16", 512): "profiles/r02_kernel_stats_rmat2m_max_bf16_steps300.csv",
-                 ("rmat16m", 512): "profiles/r02_kernel_stats_rmat16m_steps300.csv"}
+# (newest round first: the first file present is used)
+ROCPROF_STATS = {("rmat2m", 512): ["profiles/r03_kernel_stats_rmat2m_steps300.csv",
+                                   "profiles/r02_kernel_stats_rmat2m_steps300.csv"],
+                 ("rmat2m-max-bf16", 512): ["profiles/r03_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                                            "profiles/r02_kernel_stats_rmat2m_max_bf16_steps300.csv"],
+                 ("rmat16m", 512): ["profiles/r03_kernel_stats_rmat16m_steps300.csv",
+                                    "profiles/r02_kernel_stats_rmat16m_steps300.csv"]}
+
+
+def rocprof_stats_file(config_name, batch):
+    for rel in ROCPROF_STATS.get((config_name, int(batch)), []):
+        if os.path.exists(os.path.join(ROOT, rel)):
+            return rel
+    return None
 
 
 def load_rocprof_avg(config_name, batch, kernel):
-    rel = ROCPROF_STATS.get((config_name, int(batch)))
-    if not rel or not os.path.exists(os.path.join(ROOT, rel)):
+    rel = rocprof_stats_file(config_name, batch)
+    if not rel:
         return None
     key = kernel.split("(")[0].strip()
     with open(os.path.join(ROOT, rel)) as f:
