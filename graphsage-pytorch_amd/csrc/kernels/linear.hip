@@ -531,12 +531,12 @@ int sum_slabs_pair_sgd_launch(const SlabSum& s1, const SlabSum& s2, int np_befor
     a.done_value = g_done_flag.value;
     g_done_flag = {};
     const unsigned nb = static_cast<unsigned>(nb1 + nb2);
-    *u.bar_gen += nb;
     a.bar = u.bar;
-    a.target = *u.bar_gen;
+    a.target = *u.bar_gen + nb;  // the host's count follows only a launch that went out
     a.bar_err = u.bar_err;
     sum_slabs_pair_sgd_kernel<<<dim3(nb), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2, a);
     check_launch("sum_slabs_pair_sgd");
+    *u.bar_gen = a.target;
     return nb1;
 }
 

@@ -219,3 +219,15 @@ def test_fullsize_device_sampler_runner_matches_host(wl, S_):
     for (mt_h, pos_h), (mt_d, pos_d) in zip(st_h, st_d):
         assert pos_h == pos_d
         np.testing.assert_array_equal(mt_h, mt_d)
+
+
+def test_fullsize_fused_sgd_matches_two_launches(wl, native, monkeypatch):
+    """The opt-in fused slab sum + clip + SGD launch (GS_FUSED_SGD=1: one
+    launch behind a grid barrier instead of the slab sum and the SGD) gives
+    the default runner's losses and parameters bit for bit."""
+    tr, losses, sizes = native
+    monkeypatch.setenv("GS_FUSED_SGD", "1")
+    tr2, losses2, sizes2 = _run(wl)
+    assert losses == losses2
+    assert torch.equal(tr.p.params, tr2.p.params)
+    np.testing.assert_array_equal(sizes, sizes2)
