@@ -98,8 +98,20 @@ __device__ __forceinline__ void sgd4_body(const Groups& G, float* __restrict__ p
         const float* pg = part + grp * G.pstride;
         const int np = G.npart[grp];
         float t = 0.f;
+        constexpr int kPre = 8;
+        if (np > 0 && np <= 64 * kPre) {
+            // every partial of the lane loaded before the first add (clamped
+            // addresses, the count tested after the loads): one memory round;
+            // adding +0 past the count leaves t unchanged
+            float v[kPre];
+#pragma unroll
+            for (int u = 0; u < kPre; ++u) v[u] = pg[min(lane + 64 * u, np - 1)];
+#pragma unroll
+            for (int u = 0; u < kPre; ++u) t += lane + 64 * u < np ? v[u] : 0.f;
+        } else {
 #pragma unroll 4
-        for (int b = lane; b < np; b += 64) t += pg[b];
+            for (int b = lane; b < np; b += 64) t += pg[b];
+        }
         t = wave_sum(t);
         if (lane == 0) {
             const float norm = sqrtf(t) * scale;

@@ -29,9 +29,22 @@ bool trainer_barrier_failed(gs_trainer* t);
 int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip
+// In-launch grouping of the weight-gradient slabs (linear_dw_grp_kernel):
+// cnt holds n_cnt zeroed ints (8 per 64x64 tile at least), gpart room for 8
+// slabs of H*K floats.  On return, slabs / S name what the slab sum must add
+// (the group partials and their count, or ws and the slab count unchanged).
+struct DwGroups {
+    int* cnt;
+    int64_t n_cnt;
+    float* gpart;
+    const float* slabs = nullptr;
+    int S = 0;
+};
+inline constexpr int kDwGroupParts = 8;
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
-                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st);
+                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
+                    DwGroups* grp = nullptr);
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 // One slab sum: out = Σ_s slabs[s] (S slabs of len floats), norm partials to part.
 struct SlabSum {

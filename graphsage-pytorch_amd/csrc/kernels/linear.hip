@@ -31,7 +31,18 @@ __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __rest
     const int per = (S + kSlabParts - 1) / kSlabParts;
     const int t0 = min(S, q * per), t1 = min(S, t0 + per);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < n4) {
+    constexpr int kPre = 8;
+    if (i < n4 && t1 - t0 <= kPre && t1 > t0) {
+        // the group's quads loaded before the first add (clamped addresses,
+        // the count tested after the loads): one memory round
+        float4 v[kPre];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u)
+            v[u] = *reinterpret_cast<const float4*>(slabs + min(t0 + u, t1 - 1) * len + 4 * i);
+#pragma unroll
+        for (int u = 0; u < kPre; ++u)
+            if (u < t1 - t0) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    } else if (i < n4) {
 #pragma unroll 8
         for (int t = t0; t < t1; ++t) {
             const float4 v = *reinterpret_cast<const float4*>(slabs + t * len + 4 * i);
@@ -419,8 +430,14 @@ namespace gs {
 // to add (sum_slabs_kernel, or a fused launch in bwd.hip).
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
-                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st) {
+                    int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
+                    DwGroups* grp) {
     GS_REQUIRE(dt == GS_F32 || dt == GS_BF16, GS_EINVAL, "dtype must be f32 or bf16");
+    static_assert(kDwGroupParts == kSlabParts && kDwGroupParts == kXcds, "group count = slab-sum parts = XCDs");
+    if (grp) {
+        grp->slabs = static_cast<const float*>(ws);
+        grp->S = 0;
+    }
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1 && H <= 4096, GS_EINVAL, "bad sizes");
     const bool self = Xs != nullptr;
     const int64_t K = self ? 2 * F : F;
@@ -444,11 +461,28 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
                     static_cast<unsigned>(S));
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H), kk = static_cast<int>(K);
     static const bool xcd_map = std::getenv("GS_DW_GRID3") == nullptr;
+    // opt-in (read per call): measured slower -- the writers' agent-scope releases
+    // took the launch from 13.9 to 24.2 us while the slab sum, now reading 2 MB
+    // instead of 8, stayed at 9.0 us (rocprof, rmat2m)
+    const bool no_group = std::getenv("GS_DW_GROUP") == nullptr;
     const int gx = static_cast<int>(grid.x), tiles = static_cast<int>(grid.x * grid.y);
     const dim3 grid_x(static_cast<unsigned>(kXcds * tiles * ((S + kXcds - 1) / kXcds)));
+    const int P = (S + kSlabParts - 1) / kSlabParts;  // slabs per group (the slab sum's grouping)
+    const bool grouped = grp && !no_group && P >= 2 && K % 4 == 0 && grp->cnt && grp->gpart &&
+                         grp->n_cnt >= static_cast<int64_t>(kXcds) * tiles;
+    if (grouped) {
+        grp->slabs = grp->gpart;
+        grp->S = (S + P - 1) / P;
+    } else if (grp) {
+        grp->S = S;
+    }
 #define GS_LDW1(TT, SELF, RELU, VL, ZV)                                                                  \
     do {                                                                                                 \
-        if (xcd_map)                                                                                     \
+        if (grouped)                                                                                     \
+            launch_k(linear_dw_grp_kernel<TT, SELF, RELU, VL, ZV>, grid_x, dim3(kThreads), 0, st,        \
+                nn, ff, hh, kk, rps, gx, tiles, S, P, static_cast<const TT*>(Xs), ldxs, sidx,            \
+                static_cast<const TT*>(A), lda, dout, out, ldo, target, H * K, grp->gpart, grp->cnt);    \
+        else if (xcd_map)                                                                                \
             launch_k(linear_dw_xcd_kernel<TT, SELF, RELU, VL, ZV>, grid_x, dim3(kThreads), 0, st,        \
                 nn, ff, hh, kk, rps, gx, tiles, S, static_cast<const TT*>(Xs), ldxs, sidx,               \
                 static_cast<const TT*>(A), lda, dout, out, ldo, target, H * K);                          \

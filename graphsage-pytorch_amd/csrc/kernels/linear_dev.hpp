@@ -678,6 +678,95 @@ __global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
                                                    lda, dout, out, ldo, dst, split_stride);
 }
 
+// The XCD-grouped row slabs.  The slab sum adds the S slabs in kSlabParts
+// groups of P = ceil(S / kSlabParts) consecutive slabs, each from zero in slab
+// order, then the group sums in group order (sum_slabs_body below).  Here the
+// groups are formed inside the launch: group q's slabs [qP, qP + P) are given
+// to workgroups w with w % 8 == q (one XCD under round-robin placement, so a
+// group's slabs are written and re-read in one L2), and of the P workgroups
+// of one tile the last to finish (an arrival counter per (group, tile),
+// agent-scope release by every writer, acquire by the last one) adds the
+// group's P slab tiles from zero in slab order into gpart[q].  The slab sum
+// then reads NG = ceil(S / P) <= 8 group partials instead of S slabs: with
+// one "slab" per group its order is exactly the two-level order above, so the
+// gradients are bitwise those of the ungrouped launch.  A different placement
+// changes only speed, never the result.  Counters start at zero (the trainer
+// zeroes them once) and the reducer resets its own.  Needs K % 4 == 0.
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
+__global__ __launch_bounds__(kThreads) void linear_dw_grp_kernel(
+    int n, int F, int H, int K, int rows_per_split, int gx, int tiles, int S, int P, const T* __restrict__ Xs,
+    int64_t ldxs, const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda,
+    const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo, float* __restrict__ dst,
+    int64_t split_stride, float* __restrict__ gpart, int* __restrict__ cnt) {
+    __shared__ int s_last;
+    const int w = blockIdx.x;
+    const int q = w % kXcds, j = w / kXcds;
+    const int m = j / tiles, t = j % tiles;
+    const int g0 = q * P;
+    const int z = g0 + m;
+    if (m >= P || z >= S) return;
+    linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx, A,
+                                                   lda, dout, out, ldo, dst, split_stride);
+    // publish this slab tile (guide recipe: drain, barrier, one release, ticket)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int gs = min(P, S - g0);
+    if (threadIdx.x == 0) {
+        int* c = cnt + q * tiles + t;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == gs - 1;
+        if (last) {
+            __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the group's tile: 64 rows x 16 float4 columns, 4 per thread; every
+    // slab's loads of a round issued before any add (clamped addresses, the
+    // selects after the loads)
+    const int k0 = (t % gx) * 64, h0 = (t / gx) * 64;
+    constexpr int kE = 64 * 16 / kThreads;
+    int64_t off[kE];
+    bool ok[kE];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) {
+        const int e = threadIdx.x + i * kThreads;
+        const int h = h0 + (e >> 4), k = k0 + (e & 15) * 4;
+        ok[i] = h < H && k < K;
+        off[i] = ok[i] ? static_cast<int64_t>(h) * K + k : 0;
+    }
+    float4 s[kE];
+#pragma unroll
+    for (int i = 0; i < kE; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int kU = 4;
+    for (int u0 = 0; u0 < gs; u0 += kU) {
+        float4 v[kU][kE];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const float* sl = dst + static_cast<int64_t>(g0 + min(u0 + u, gs - 1)) * split_stride;
+#pragma unroll
+            for (int i = 0; i < kE; ++i) v[u][i] = *reinterpret_cast<const float4*>(sl + off[i]);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (u0 + u >= gs) break;
+#pragma unroll
+            for (int i = 0; i < kE; ++i) {
+                s[i].x += v[u][i].x; s[i].y += v[u][i].y; s[i].z += v[u][i].z; s[i].w += v[u][i].w;
+            }
+        }
+    }
+    float* gp = gpart + static_cast<int64_t>(q) * split_stride;
+#pragma unroll
+    for (int i = 0; i < kE; ++i)
+        if (ok[i]) *reinterpret_cast<float4*>(gp + off[i]) = s[i];
+}
+
 // out[i] = Σ_s slabs[s][i] in one fixed order shared by every slab-sum
 // kernel: the S slabs fall into kSlabParts consecutive groups of
 // P = ceil(S / kSlabParts); each group is summed from zero in slab order, and
@@ -696,7 +785,37 @@ __device__ __forceinline__ void sum_slabs_body(int bx, int nblk, const float* __
     const int64_t n4 = active ? len / 4 : 0;
     const int per = (S + kSlabParts - 1) / kSlabParts;
     float sq = 0.f;
-    for (int64_t i = bx * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(nblk) * kThreads) {
+    constexpr int kPre = 16;
+    if (S <= kPre) {
+        // every slab's quad loaded before the first add (clamped addresses,
+        // the slab count tested after the loads): one memory round instead of
+        // one per group.  The adds are the loop below's, in its order: each
+        // group from zero in slab order, the group sums in group order (an
+        // empty trailing group adds +0 there, which leaves the sum unchanged).
+        for (int64_t i = bx * int64_t(kThreads) + threadIdx.x; i < n4; i += int64_t(nblk) * kThreads) {
+            float4 v[kPre];
+#pragma unroll
+            for (int t = 0; t < kPre; ++t)
+                v[t] = *reinterpret_cast<const float4*>(slabs + min(t, S - 1) * len + 4 * i);
+            float4 s = make_float4(0.f, 0.f, 0.f, 0.f), g = s;
+            bool first = true;
+#pragma unroll
+            for (int t = 0; t < kPre; ++t) {
+                if (t < S) {
+                    g.x += v[t].x; g.y += v[t].y; g.z += v[t].z; g.w += v[t].w;
+                    if ((t + 1) % per == 0 || t + 1 == S) {
+                        if (first) s = g;
+                        else { s.x += g.x; s.y += g.y; s.z += g.z; s.w += g.w; }
+                        first = false;
+                        g = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+            }
+            *reinterpret_cast<float4*>(out + 4 * i) = s;
+            sq = fmaf(s.x, s.x, sq); sq = fmaf(s.y, s.y, sq); sq = fmaf(s.z, s.z, sq); sq = fmaf(s.w, s.w, sq);
+        }
+    }
+    for (int64_t i = bx * int64_t(kThreads) + threadIdx.x; S > kPre && i < n4; i += int64_t(nblk) * kThreads) {
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < kSlabParts; ++q) {

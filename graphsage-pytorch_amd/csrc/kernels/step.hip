@@ -71,8 +71,13 @@ struct gs_trainer {
     unsigned long long* bar = nullptr;  // its grid-barrier counter (device) and arrivals so far
     unsigned long long bar_gen = 0;
     int* bar_err = nullptr;
+    // arrival counters of the grouped layer-1 weight-gradient launch (zeroed once;
+    // each group's reducer resets its own), kDwGroupParts per 64x64 tile of W1
+    int* dw_cnt = nullptr;
+    int64_t dw_n_cnt = 0;
     ~gs_trainer() {
         if (norm_part) (void)hipFree(norm_part);
+        if (dw_cnt) (void)hipFree(dw_cnt);
         if (w1_lp) (void)hipFree(w1_lp);
         if (bar) (void)hipFree(bar);
         for (auto& tm : timer) {
@@ -253,6 +258,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         }
     }
     char* dw_ws = cv.take<char>(dw_need);
+    // the layer-1 weight gradient's group partials (linear_dw_grp_kernel)
+    float* dw_gpart = cv.take<float>(kDwGroupParts * H * T.w_cols[0]);
     // the fused top path's dW_2 slabs outlive the layer-1 dW (their sum runs with layer 1's)
     const int64_t dw2_need = L == 2 ? gs_sage_linear_bwd_weight_ws(rows[1], T.w_cols[1], H) : 0;
     char* dw2_ws = dw2_need > 0 ? cv.take<char>(dw2_need) : nullptr;
@@ -383,11 +390,15 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 if (T.upper_hook) T.upper_hook(st);
             }
             const bool armed = timed_arm(T, 2);
+            DwGroups grp{T.dw_cnt, T.dw_n_cnt, dw_gpart};
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
                                            c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0],
-                                           dw_ws, dw_need, st);
+                                           dw_ws, dw_need, st, &grp);
             g_launch_events = {};
             timed_done(T, 2, armed);
+            // what the slab sum adds: the group partials (bitwise the same sums) or the slabs
+            const float* s1_src = S1 > 1 ? grp.slabs : nullptr;
+            const int s1_n = S1 > 1 ? grp.S : S1;
             const int n_cls = cls_reduce_grid(c.n_classes, H);
             if (defer && S1 > 1 && T.fuse_update && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
                 n_cls <= T.pstride) {
@@ -400,8 +411,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 T.lp_valid = false;
                 if (T.lp_keep && T.w1_lp)
                     g_lowp_shadow = {T.w1_lp, T.w_off[0], T.w_off[0] + T.w_rows[0] * T.w_cols[0]};
-                sum_slabs_pair_sgd_launch(SlabSum{reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0],
-                                                  T.norm_part + np},
+                sum_slabs_pair_sgd_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np},
                                           d2, np, u, st);
                 g_lowp_shadow = {};
                 T.lp_valid = T.lp_keep && T.w1_lp;
@@ -411,15 +421,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
             if (defer && S1 > 1) {
                 d2.part = T.norm_part;
-                np += sum_slabs_pair_launch(SlabSum{reinterpret_cast<const float*>(dw_ws), S1, H * K1,
-                                                    G + T.w_off[0], T.norm_part + np},
-                                            d2, st);
+                np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st);
             } else if (defer) {
                 if (d2.S > 1) sum_slabs_launch(d2.slabs, d2.S, d2.len, d2.out, nullptr, st);
                 parts = false;
             } else if (S1 > 1) {
-                np += sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), S1, H * K1, G + T.w_off[0],
-                                       T.norm_part + np, st);
+                np += sum_slabs_launch(s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np, st);
             } else {
                 parts = false;
             }
@@ -560,6 +567,12 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
             gs::fail(GS_ENOMEM, "hipMalloc(barrier)");
         }
         T->bar_err = reinterpret_cast<int*>(T->bar + 1);
+        T->dw_n_cnt = gs::kDwGroupParts * ((T->w_cols[0] + 63) / 64) * ((cfg->hidden + 63) / 64);
+        if (hipMalloc(&T->dw_cnt, T->dw_n_cnt * sizeof(int)) != hipSuccess ||
+            hipMemset(T->dw_cnt, 0, T->dw_n_cnt * sizeof(int)) != hipSuccess) {
+            delete T;
+            gs::fail(GS_ENOMEM, "hipMalloc(dW group counters)");
+        }
     }
     T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
     T->use_top = std::getenv("GS_NO_TOP") == nullptr;

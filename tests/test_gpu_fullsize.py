@@ -221,6 +221,19 @@ def test_fullsize_device_sampler_runner_matches_host(wl, S_):
         np.testing.assert_array_equal(mt_h, mt_d)
 
 
+def test_fullsize_grouped_dw_matches_slab_sum(wl, native, monkeypatch):
+    """The layer-1 weight gradient's slabs grouped inside the dW launch (one
+    partial per group of ceil(S/8) slabs, added by the group's last
+    workgroup; opt-in GS_DW_GROUP=1) give the losses and parameters of the
+    default slab sum over all S slabs bit for bit: the same two-level order."""
+    tr, losses, sizes = native
+    monkeypatch.setenv("GS_DW_GROUP", "1")
+    tr2, losses2, sizes2 = _run(wl)
+    assert losses == losses2
+    assert torch.equal(tr.p.params, tr2.p.params)
+    np.testing.assert_array_equal(sizes, sizes2)
+
+
 def test_fullsize_fused_sgd_matches_two_launches(wl, native, monkeypatch):
     """The opt-in fused slab sum + clip + SGD launch (GS_FUSED_SGD=1: one
     launch behind a grid barrier instead of the slab sum and the SGD) gives
