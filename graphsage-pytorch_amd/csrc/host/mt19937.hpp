@@ -203,6 +203,23 @@ inline void select_chunked(MT19937& rng, int64_t n, int64_t k, OutT* out) {
 // false, having consumed nothing, when fewer than k of the 32 words are in
 // range, a repeat occurs, or the block has fewer than 32 words left; the
 // caller then runs the general scan from the same stream position.
+// Left-packing permutations of an 8-lane vector: row m lists the lanes whose
+// bit is set in m, in lane order (the rest 0).
+struct PackLut {
+    int32_t idx[256][8];
+};
+constexpr PackLut make_pack_lut() {
+    PackLut t{};
+    for (int m = 0; m < 256; ++m) {
+        int j = 0;
+        for (int i = 0; i < 8; ++i)
+            if ((m >> i) & 1) t.idx[m][j++] = i;
+        for (; j < 8; ++j) t.idx[m][j] = 0;
+    }
+    return t;
+}
+alignas(32) inline constexpr PackLut kPackLut = make_pack_lut();
+
 template <class OutT>
 inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
     if (rng.index + 32 > MT19937::N) return false;
@@ -210,26 +227,35 @@ inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
     const __m128i shv = _mm_cvtsi32_si128(sh);
     const __m256i nv = _mm256_set1_epi32(static_cast<int32_t>(n));
     const __m256i* src = reinterpret_cast<const __m256i*>(rng.out + rng.index);
-    alignas(32) int32_t w[32];
+    __m256i v[4];
     uint32_t inr = 0;
 #pragma GCC unroll 4
     for (int q = 0; q < 4; ++q) {
-        const __m256i v = _mm256_srl_epi32(_mm256_loadu_si256(src + q), shv);
-        _mm256_store_si256(reinterpret_cast<__m256i*>(w) + q, v);
-        inr |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(nv, v)))) << (8 * q);
+        v[q] = _mm256_srl_epi32(_mm256_loadu_si256(src + q), shv);
+        inr |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(nv, v[q])))) << (8 * q);
     }
     if (__builtin_popcount(inr) < k) return false;
-    // compacted values, padded with distinct negatives (never equal to a value)
-    alignas(32) int32_t c[16] = {-1, -2, -3, -4, -5, -6, -7, -8, -9, -10, -11, -12, -13, -14, -15, -16};
-    uint32_t m = inr;
-    int last = 0;
-    for (int i = 0; i < k; ++i) {
-        last = __builtin_ctz(m);
-        c[i] = w[last];
-        m &= m - 1;
+    // The in-range values in stream order, left-packed 8 lanes at a time (a
+    // table permutation per chunk: no per-value dependency chain); only the
+    // first k are used.
+    alignas(32) int32_t c[40];
+    int at = 0;
+#pragma GCC unroll 4
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t m = (inr >> (8 * q)) & 0xFFu;
+        const __m256i perm = _mm256_load_si256(reinterpret_cast<const __m256i*>(kPackLut.idx[m]));
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(c + at), _mm256_permutevar8x32_epi32(v[q], perm));
+        at += __builtin_popcount(m);
     }
-    const __m256i a = _mm256_load_si256(reinterpret_cast<const __m256i*>(c));
-    const __m256i b = _mm256_load_si256(reinterpret_cast<const __m256i*>(c) + 1);
+    const int last = __builtin_ctz(_pdep_u32(1u << (k - 1), inr));  // the k-th in-range word
+    // lanes past k padded with distinct negatives (never equal to a value)
+    const __m256i kv = _mm256_set1_epi32(static_cast<int32_t>(k));
+    const __m256i a = _mm256_blendv_epi8(
+        _mm256_setr_epi32(-1, -2, -3, -4, -5, -6, -7, -8), _mm256_load_si256(reinterpret_cast<const __m256i*>(c)),
+        _mm256_cmpgt_epi32(kv, _mm256_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7)));
+    const __m256i b = _mm256_blendv_epi8(
+        _mm256_setr_epi32(-9, -10, -11, -12, -13, -14, -15, -16), _mm256_load_si256(reinterpret_cast<const __m256i*>(c) + 1),
+        _mm256_cmpgt_epi32(kv, _mm256_setr_epi32(8, 9, 10, 11, 12, 13, 14, 15)));
     __m256i dup = _mm256_setzero_si256();
 #pragma GCC unroll 4
     for (int r = 1; r <= 4; ++r) {  // rotations 1..4 cover every pair inside a vector

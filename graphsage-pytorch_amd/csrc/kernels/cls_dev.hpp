@@ -94,7 +94,9 @@ __device__ __forceinline__ void sgd4_body(const Groups& G, float* __restrict__ p
         pv = p4[i0];
     }
     const int lane = threadIdx.x & 63;
-    for (int grp = threadIdx.x >> 6; grp < G.n; grp += nthr / 64) {
+    // the group index wave-uniform in an SGPR: its npart is a scalar kernarg
+    // load, not a vector load whose wait would also drain the g / p loads above
+    for (int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); grp < G.n; grp += nthr / 64) {
         const float* pg = part + grp * G.pstride;
         const int np = G.npart[grp];
         float t = 0.f;
