@@ -61,33 +61,44 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 // the raw words the next launch and getstate need are the last 624, written
 // once at the end.
 constexpr int kGenThreads = 256;
+constexpr int kGenRing = 2048;  // LDS ring: reads reach back 624 words, a step writes 454 ahead
 __global__ __launch_bounds__(kGenThreads) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr,
                                                              Ctl* c, int64_t need_fixed, int need_hop) {
-    __shared__ uint32_t L[1024];
+    __shared__ uint32_t L[kGenRing];
+    constexpr int64_t M = kGenRing - 1;
     const int i = threadIdx.x;
     const int64_t g0 = c->gen_end;
     const int64_t need = need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
     if (g0 >= need) return;
     for (int q = i; q < 624; q += kGenThreads) {
         const int64_t A = g0 - 624 + q;
-        L[A & 1023] = xr[A & kRingMask];
+        L[A & M] = xr[A & kRingMask];
     }
     __syncthreads();
-    uint32_t prev = i < 227 ? L[(g0 - 227 + i) & 1023] : 0u;
+    uint32_t prev = i < 227 ? L[(g0 - 227 + i) & M] : 0u;
     int64_t g = g0;
+    // Two stages per barrier: word A = g + 227 + i reads x[A - 624] and
+    // x[A - 623] (<= g - 170, written before the barrier) and x[A - 227] =
+    // the thread's word of the first stage, a register.
     while (g < need) {
         if (i < 227) {
             const int64_t A = g + i;
-            const uint32_t a = L[(A - 624) & 1023], b = L[(A - 623) & 1023];
+            const uint32_t a = L[(A - 624) & M], b = L[(A - 623) & M];
+            const uint32_t a2 = L[(A - 397) & M], b2 = L[(A - 396) & M];
             const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
             const uint32_t x = prev ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
-            prev = x;
-            L[A & 1023] = x;
+            const uint32_t y2 = (a2 & 0x80000000u) | (b2 & 0x7fffffffu);
+            const uint32_t x2 = x ^ (y2 >> 1) ^ ((0u - (y2 & 1u)) & 0x9908b0dfu);
+            prev = x2;
+            L[A & M] = x;
+            L[(A + 227) & M] = x2;
             xr[A & kRingMask] = x;
+            xr[(A + 227) & kRingMask] = x2;
             wr[A & kRingMask] = temper(x);
+            wr[(A + 227) & kRingMask] = temper(x2);
         }
         __syncthreads();
-        g += 227;
+        g += 454;
     }
     if (i == 0) c->gen_end = g;
 }
@@ -212,6 +223,24 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
         hb.bw[nb] = 0;
     }
     __syncthreads();
+    // The table kernel's work list: the 256-entry parts of every block's
+    // window, blocks ascending.  Its grid is launched at the bound, and the
+    // items come first, so the workgroups with work are dispatched first and
+    // spread over the chip (the parts past a window no longer sit between them).
+    {
+        const int nb = (n + R - 1) / R;
+        const int pb = (nb + 1023) / 1024;
+        const int b0 = min(nb, static_cast<int>(threadIdx.x) * pb), b1 = min(nb, b0 + pb);
+        int cnt = 0;
+        for (int b = b0; b < b1; ++b) cnt += (min(hb.bw[b], kWMax) + kMEntries - 1) / kMEntries;
+        int tot;
+        int at = block_excl_scan(cnt, shi, &tot);
+        for (int b = b0; b < b1; ++b) {
+            const int parts = (min(hb.bw[b], kWMax) + kMEntries - 1) / kMEntries;
+            for (int y = 0; y < parts; ++y) hb.wg[at++] = b | (y << 16);
+        }
+        if (threadIdx.x == 0) h.n_wg = tot;
+    }
     if (threadIdx.x == 0) {
         int W = 64;
         while (W < s_maxw) W <<= 1;
@@ -285,7 +314,6 @@ __device__ __forceinline__ int load_words(const uint32_t* __restrict__ wr, const
 // window width times its draws, so wide blocks (late in the hop) are split
 // over several CUs, and each workgroup builds masks only over the words its
 // 256 entries can reach.
-constexpr int kMEntries = 256;                                    // entries per workgroup
 constexpr int kRejBudget = 192;                                   // mask-covered rejections per block
 constexpr int kMChunks = (kMEntries + kRejBudget + 63) / 64 + 1;  // mask words per draw (+1 for the 2-word window)
 
@@ -352,8 +380,14 @@ __device__ __forceinline__ int walk_masked(const uint32_t* __restrict__ M, int a
             rel += adv;
         }
     } else {
+        // The picks so far as a set: slots start at a sentinel no in-range
+        // value equals (values < d < 2^31) and a fresh value enters by a shift
+        // (membership is all the repeat test needs), so each word costs KMAX
+        // compares and KMAX selects, none of them on the pick count.
         const int sh = __clz(d);
         uint32_t sel[KMAX];
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t) sel[t] = 0xFFFFFFFFu;
         int cnt = 0;
         while (cnt < k && !bad) {
             const int j = min(rel >> 5, C32 - 2);
@@ -364,10 +398,10 @@ __device__ __forceinline__ int walk_masked(const uint32_t* __restrict__ M, int a
             const uint32_t val = w[a + max(rel - 1, 0)] >> sh;
             bool fresh = !bad;
 #pragma unroll
-            for (int t = 0; t < KMAX; ++t) fresh &= !(t < cnt && sel[t] == val);
+            for (int t = 0; t < KMAX; ++t) fresh &= sel[t] != val;
 #pragma unroll
-            for (int t = 0; t < KMAX; ++t)
-                if (t == cnt) sel[t] = val;
+            for (int t = KMAX - 1; t > 0; --t) sel[t] = fresh ? sel[t - 1] : sel[t];
+            sel[0] = fresh ? val : sel[0];
             cnt += fresh;
         }
     }
@@ -382,17 +416,18 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     __shared__ int s_d[256], s_moff[257];
     __shared__ int s_nsr;
     const HopCtl& h = c->hop[hop];
-    const int b = blockIdx.x;
-    if (b >= h.n_blocks) return;
+    if (static_cast<int>(blockIdx.x) >= h.n_wg) return;  // past the work list (hop_setup)
+    const int item = hb.wg[blockIdx.x];
+    const int b = item & 0xFFFF, part = item >> 16;
     const int Wst = h.W;
     const int bw = min(hb.bw[b], Wst);
-    const int e0 = blockIdx.y * kMEntries;
+    const int e0 = part * kMEntries;
     if (e0 >= bw) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r0 = b * R, nr = min(R, h.n_dst - r0);
     const int ndr = hb.dbase[min(b + 1, h.n_blocks)] - hb.dbase[b];
     // phase stamps of one workgroup of the last hop (gs_dsampler_debug slots 56..61)
-    const bool stamp = hop > 0 && b == h.n_blocks / 2 && blockIdx.y == 0 && tid == 0;
+    const bool stamp = hop > 0 && b == h.n_blocks / 2 && part == 0 && tid == 0;
     if (stamp) c->dbg[56] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
     // masks: [node][draw][kMChunks] (pool: k draws, selected-set: 1), then the words
     uint64_t* masks = smem64;
@@ -431,23 +466,37 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     __syncthreads();
     const int nsr = s_nsr;
     if (stamp) c->dbg[57] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
-    // build: node m's window starts at word m * k (entry e0, no rejections yet)
-    for (int t = wave; t < nsr * kMChunks; t += kMEntries / 64) {
-        const int q = t / kMChunks, ch = t - q * kMChunks;
+    // build: node m's window starts at word m * k (entry e0, no rejections
+    // yet).  One wave per node: its kMChunks words per lane read at once, then
+    // a ballot per (draw bound, chunk).
+    for (int q = wave; q < nsr; q += kMEntries / 64) {
         const uint32_t d = static_cast<uint32_t>(s_d[q]);
-        const int pos = q * k + 64 * ch + lane;
-        const bool ok = pos < nvalid;
-        const uint32_t x = ok ? w[pos] : 0u;
-        uint64_t* M = masks + s_moff[q] + ch;
+        uint64_t* M = masks + s_moff[q];
+        uint32_t x[kMChunks];
+        bool ok[kMChunks];
+#pragma unroll
+        for (int ch = 0; ch < kMChunks; ++ch) {
+            const int pos = q * k + 64 * ch + lane;
+            ok[ch] = pos < nvalid;
+            x[ch] = w[max(0, min(pos, nvalid - 1))];
+        }
         if (d <= static_cast<uint32_t>(setsize)) {
             for (int i = 0; i < k; ++i) {
                 const uint32_t m = d - i;
-                const uint64_t bal = __ballot(ok && (x >> __clz(m)) < m);
-                if (lane == 0) M[i * kMChunks] = bal;
+                const int sh = __clz(m);
+#pragma unroll
+                for (int ch = 0; ch < kMChunks; ++ch) {
+                    const uint64_t bal = __ballot(ok[ch] && (x[ch] >> sh) < m);
+                    if (lane == 0) M[i * kMChunks + ch] = bal;
+                }
             }
         } else {
-            const uint64_t bal = __ballot(ok && (x >> __clz(d)) < d);
-            if (lane == 0) M[0] = bal;
+            const int sh = __clz(d);
+#pragma unroll
+            for (int ch = 0; ch < kMChunks; ++ch) {
+                const uint64_t bal = __ballot(ok[ch] && (x[ch] >> sh) < d);
+                if (lane == 0) M[ch] = bal;
+            }
         }
     }
     __syncthreads();
@@ -472,7 +521,7 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
     if (stamp) {
         c->dbg[59] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         c->dbg[60] = nsr | (static_cast<int64_t>(bw) << 16) | (static_cast<int64_t>(h.n_blocks) << 32);
-        c->dbg[61] = gridDim.y | (static_cast<int64_t>(h.W) << 16) | (static_cast<int64_t>(ndr) << 32);
+        c->dbg[61] = h.n_wg | (static_cast<int64_t>(h.W) << 16) | (static_cast<int64_t>(ndr) << 32);
     }
     if (ent < bw) {
         uint16_t* E = hb.tab + static_cast<int64_t>(b) * Wst;
@@ -839,9 +888,11 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     const size_t mask_lds = static_cast<size_t>(R) * std::max(k, 1) * kMChunks * sizeof(uint64_t) +
                             (kMEntries + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
     // selected-set values in registers: the unrolled duplicate test costs KMAX per accepted word
-    const dim3 grid(static_cast<unsigned>(nb_max), kWMax / kMEntries);
+    const dim3 grid(static_cast<unsigned>(nb_max * (kWMax / kMEntries)));  // the work list's bound
     if (k <= 8)
         draw_masked_kernel<8><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
+    else if (k <= 10)  // the bench's and Pubmed's last hop
+        draw_masked_kernel<10><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 12)
         draw_masked_kernel<12><<<grid, kMEntries, mask_lds, st>>>(ds->wr, ds->ctl, hb, hop, k, setsize, R);
     else if (k <= 16)
@@ -966,6 +1017,7 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
         h.gexit_last = ds->alloc<int32_t>(kWMax);
         h.entry = ds->alloc<int32_t>(nb);
         h.rej = ds->alloc<uint8_t>(nb * r_of(k) * kWMax);
+        h.wg = ds->alloc<int32_t>(nb * (kWMax / kMEntries));
         h.ent = j + 1 < n_hops ? ds->alloc<int32_t>(ds->npos_max[j]) : nullptr;
         if (j + 1 < n_hops) {
             GS_REQUIRE(k >= 1, GS_EINVAL, "device sampler: hops before the last need a fanout >= 1");

@@ -14,6 +14,7 @@ constexpr int kComposeEntries = 30720;       // G * W entries a compose block st
 constexpr int kMinG = kComposeEntries / kWMax;
 constexpr int kChainEntries = 30720;         // group exits the chain block stages in LDS (uint16)
 constexpr int kMaxGroups = 1024;
+constexpr int kMEntries = 256;               // window entries per table-kernel workgroup
 
 // status bits (Ctl::status)
 constexpr int kStWindow = 1;   // a true entry fell outside its block window
@@ -39,6 +40,7 @@ struct HopCtl {
     int32_t n_empty;
     int32_t n_src, n_nbr;      // hops before the last (union, lists)
     int32_t big;               // the union's table outgrew LDS uint32 slots: ubig_kernel builds it
+    int32_t n_wg;              // table-kernel work items (HopBufs::wg)
     int64_t P0;                // absolute stream position at the hop's first draw
     int64_t need_end;          // words the hop may read (exclusive)
     int32_t off[GS_PK_NFIELDS];
@@ -71,6 +73,7 @@ struct HopBufs {
     int32_t* entry;            // true entry per block [nb_max]
     int32_t* ent;              // absolute CSR entries of the hop's samples (hops before the last)
     uint8_t* rej;              // rejections of sampled node m of block b from entry e: [(b * R + m) * kWMax + e]
+    int32_t* wg;               // table-kernel work items b | part << 16, blocks ascending, [nb_max * kWMax / kMEntries]
 };
 
 struct UnionBufs {

@@ -20,5 +20,5 @@ for b in range(6):
     us = lambda a, b_: (d[b_] - d[a]) / 100.0
     x, y = int(d[60]), int(d[61])
     print(f"batch {b}: load {us(56, 57):.1f} us, masks {us(57, 58):.1f} us, walks {us(58, 59):.1f} us; "
-          f"nodes {x & 0xffff}, entries {(x >> 16) & 0xffff}, blocks {x >> 32}, grid.y {y & 0xffff}, "
+          f"nodes {x & 0xffff}, entries {(x >> 16) & 0xffff}, blocks {x >> 32}, work items {y & 0xffff}, "
           f"W {(y >> 16) & 0xffff}, draws {y >> 32}", flush=True)
