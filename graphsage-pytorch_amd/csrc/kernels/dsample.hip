@@ -535,7 +535,7 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
 // window (uint16; 0xFFFF outside it), or absolute for the last group.  The
 // group's block maps are staged in LDS.
 __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, int hop) {
-    extern __shared__ uint16_t tabs[];
+    extern __shared__ __attribute__((aligned(16))) uint16_t tabs[];
     __shared__ int los[kComposeEntries / 64 + 1], wid[kComposeEntries / 64 + 1];
     const HopCtl& h = c->hop[hop];
     const int gi = blockIdx.x;
@@ -548,21 +548,20 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
         wid[i] = i < nbk ? min(hb.bw[b0 + i], W) : W;
     }
     __syncthreads();
-    // widths are multiples of 64: 16-byte loads, all of a block's in flight
-    // before its LDS stores
-    for (int q = 0; q < nbk; ++q) {
-        const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0 + q) * W);
-        uint4* dst = reinterpret_cast<uint4*>(tabs + q * W);
-        const int n16 = wid[q] / 8;
-        constexpr int kB = kWMax / 8 / 256;
-        uint4 v[kB];
+    // The group's block maps are nbk consecutive rows of W entries in hb.tab
+    // (an entry past a row's width is never read): one flat copy of 16-byte
+    // chunks, every load of the thread in flight before its LDS stores (one
+    // memory round instead of one per block).
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(hb.tab + static_cast<int64_t>(b0) * W);
+        uint4* dst = reinterpret_cast<uint4*>(tabs);
+        const int n16 = nbk * W / 8;  // <= kComposeEntries / 8
+        constexpr int kU = kComposeEntries / 8 / 256;
+        uint4 v[kU];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
-            const int i = threadIdx.x + 256 * u;
-            if (i < n16) v[u] = src[i];
-        }
+        for (int u = 0; u < kU; ++u) v[u] = src[min(static_cast<int>(threadIdx.x) + 256 * u, n16 - 1)];
 #pragma unroll
-        for (int u = 0; u < kB; ++u) {
+        for (int u = 0; u < kU; ++u) {
             const int i = threadIdx.x + 256 * u;
             if (i < n16) dst[i] = v[u];
         }
@@ -596,7 +595,7 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
 // then every block's true entry (a lookup in its group's path) and the hop's
 // end position.
 __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, int hop) {
-    extern __shared__ uint16_t gx[];
+    extern __shared__ __attribute__((aligned(16))) uint16_t gx[];
     __shared__ int gentry[kMaxGroups + 1];
     HopCtl& h = c->hop[hop];
     const int W = h.W, G = h.G, ng = h.n_groups;
@@ -606,8 +605,20 @@ __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, in
     }
     const int64_t n16 = static_cast<int64_t>(ng - 1) * W;
     const bool staged = n16 <= kChainEntries;
-    if (staged)
-        for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) gx[i] = hb.gexit[i];
+    if (staged) {  // W % 64 == 0: whole 16-byte chunks, every load of a thread before its stores
+        const uint4* src = reinterpret_cast<const uint4*>(hb.gexit);
+        uint4* dst = reinterpret_cast<uint4*>(gx);
+        const int n8 = static_cast<int>(n16 / 8);
+        constexpr int kU = (kChainEntries / 8 + 1023) / 1024;
+        uint4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = src[max(0, min(static_cast<int>(threadIdx.x) + 1024 * u, n8 - 1))];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i = threadIdx.x + 1024 * u;
+            if (i < n8) dst[i] = v[u];
+        }
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         int j = 0;
