@@ -161,32 +161,64 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
     const int r0 = min(n, static_cast<int>(threadIdx.x) * per), r1 = min(n, r0 + per);
     int cnt_sum = 0, draw_sum = 0;
     float mean_sum = 0.f, var_sum = 0.f;
-    // degrees, kSetupBatch nodes at a time: every id, then every row_ptr pair,
-    // loaded before any is used (independent loads in flight together)
-    for (int rb = r0; rb < r1; rb += kSetupBatch) {
-        int32_t vv[kSetupBatch];
-        int64_t lo[kSetupBatch], hi[kSetupBatch];
-#pragma unroll
-        for (int q = 0; q < kSetupBatch; ++q) vv[q] = rb + q < r1 ? hb.dst[rb + q] : 0;
-#pragma unroll
-        for (int q = 0; q < kSetupBatch; ++q) {
-            lo[q] = rb + q < r1 ? g.row_ptr[vv[q]] : 0;
-            hi[q] = rb + q < r1 ? g.row_ptr[vv[q] + 1] : 0;
-        }
-#pragma unroll
-        for (int q = 0; q < kSetupBatch; ++q)
-            if (rb + q < r1) hb.deg[rb + q] = static_cast<int32_t>(hi[q] - lo[q]);
-    }
-    for (int r = r0; r < r1; ++r) {
-        const int32_t d = hb.deg[r];
+    // Up to kSetupRows rows per thread (n <= 16 Ki) stay in registers between
+    // the passes: every id, then every row_ptr pair loaded at once, and no
+    // pass re-reads what an earlier one stored (a store-then-load per row
+    // costs a memory round each).  Larger frontiers take the global passes.
+    constexpr int kSetupRows = 16;
+    const bool cached = per <= kSetupRows;
+    int32_t dc[kSetupRows];
+    float2 mc[kSetupRows];
+    auto moments = [&](int r, int32_t d, float2& mv) {
         const bool sampled = k > 0 && d >= k;
         cnt_sum += sampled ? k : d;
         draw_sum += sampled ? k : 0;
         float mu, va;
         rejection_moments(static_cast<uint32_t>(d), k, setsize, mu, va);
-        hb.mv[r] = make_float2(mu, va);
+        mv = make_float2(mu, va);
+        hb.mv[r] = mv;
         mean_sum += mu;
         var_sum += va;
+    };
+    if (cached) {
+        int32_t vv[kSetupRows];
+        int64_t lo[kSetupRows], hi[kSetupRows];
+#pragma unroll
+        for (int q = 0; q < kSetupRows; ++q) vv[q] = r0 + q < r1 ? hb.dst[r0 + q] : 0;
+#pragma unroll
+        for (int q = 0; q < kSetupRows; ++q) {
+            lo[q] = r0 + q < r1 ? g.row_ptr[vv[q]] : 0;
+            hi[q] = r0 + q < r1 ? g.row_ptr[vv[q] + 1] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < kSetupRows; ++q) {
+            dc[q] = static_cast<int32_t>(hi[q] - lo[q]);
+            if (r0 + q < r1) {
+                hb.deg[r0 + q] = dc[q];
+                moments(r0 + q, dc[q], mc[q]);
+            }
+        }
+    } else {
+        // degrees, kSetupBatch nodes at a time: every id, then every row_ptr
+        // pair, loaded before any is used (independent loads in flight together)
+        for (int rb = r0; rb < r1; rb += kSetupBatch) {
+            int32_t vv[kSetupBatch];
+            int64_t lo[kSetupBatch], hi[kSetupBatch];
+#pragma unroll
+            for (int q = 0; q < kSetupBatch; ++q) vv[q] = rb + q < r1 ? hb.dst[rb + q] : 0;
+#pragma unroll
+            for (int q = 0; q < kSetupBatch; ++q) {
+                lo[q] = rb + q < r1 ? g.row_ptr[vv[q]] : 0;
+                hi[q] = rb + q < r1 ? g.row_ptr[vv[q] + 1] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kSetupBatch; ++q)
+                if (rb + q < r1) hb.deg[rb + q] = static_cast<int32_t>(hi[q] - lo[q]);
+        }
+        for (int r = r0; r < r1; ++r) {
+            float2 mv;
+            moments(r, hb.deg[r], mv);
+        }
     }
     int cnt_tot, draw_tot;
     float mean_tot, var_tot;
@@ -194,8 +226,7 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
     int draw_pre = block_excl_scan(draw_sum, shi, &draw_tot);
     float mean_pre = block_excl_scan(mean_sum, shf, &mean_tot);
     float var_pre = block_excl_scan(var_sum, shf, &var_tot);
-    for (int r = r0; r < r1; ++r) {
-        const int32_t d = hb.deg[r];
+    auto place = [&](int r, int32_t d, float2 mv) {
         const bool sampled = k > 0 && d >= k;
         hb.pos_ptr[r] = cnt_pre;
         if (r % R == 0) {
@@ -211,9 +242,15 @@ __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, Hop
         }
         cnt_pre += sampled ? k : d;
         draw_pre += sampled ? k : 0;
-        const float2 mv = hb.mv[r];
         mean_pre += mv.x;
         var_pre += mv.y;
+    };
+    if (cached) {
+#pragma unroll
+        for (int q = 0; q < kSetupRows; ++q)
+            if (r0 + q < r1) place(r0 + q, dc[q], mc[q]);
+    } else {
+        for (int r = r0; r < r1; ++r) place(r, hb.deg[r], hb.mv[r]);
     }
     if (threadIdx.x == 0) {
         hb.pos_ptr[n] = cnt_tot;
@@ -568,25 +605,38 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
     }
     __syncthreads();
     int32_t* path = hb.path + static_cast<int64_t>(b0) * W;
-    for (int e = threadIdx.x; e < wid[0]; e += blockDim.x) {
-        int j = los[0] + e;
+    // kPathIlp entries per thread walk their block chains together (each chain
+    // is a dependent LDS lookup per block)
+    constexpr int kPathIlp = 4;
+    const int w0 = wid[0];
+    const int bw_next = last_group ? 0 : hb.bw[b0 + nbk];
+    for (int e0 = threadIdx.x; e0 < w0; e0 += kPathIlp * blockDim.x) {
+        int j[kPathIlp];
+#pragma unroll
+        for (int u = 0; u < kPathIlp; ++u) j[u] = los[0] + e0 + u * static_cast<int>(blockDim.x);
         for (int q = 0; q < nbk; ++q) {
-            path[q * W + e] = j;
-            if (j < 0) continue;
-            const int t = j - los[q];
-            if (t < 0 || t >= wid[q]) {
-                j = -1;
-                continue;
+            const int lq = los[q], wq = wid[q];
+#pragma unroll
+            for (int u = 0; u < kPathIlp; ++u) {
+                const int e = e0 + u * static_cast<int>(blockDim.x);
+                if (e < w0) path[q * W + e] = j[u];
+                const int t = j[u] - lq;
+                const bool in = j[u] >= 0 && t >= 0 && t < wq;
+                const uint16_t d = tabs[q * W + (in ? t : 0)];
+                j[u] = (in && d != 0xFFFF) ? j[u] + d : -1;
             }
-            const uint16_t d = tabs[q * W + t];
-            j = d == 0xFFFF ? -1 : j + d;
         }
-        if (last_group) {
-            hb.gexit_last[e] = j;
-        } else {
-            const int t = j - los[nbk];
-            hb.gexit[static_cast<int64_t>(gi) * W + e] =
-                (j < 0 || t < 0 || t >= hb.bw[b0 + nbk]) ? 0xFFFF : static_cast<uint16_t>(t);
+#pragma unroll
+        for (int u = 0; u < kPathIlp; ++u) {
+            const int e = e0 + u * static_cast<int>(blockDim.x);
+            if (e >= w0) break;
+            if (last_group) {
+                hb.gexit_last[e] = j[u];
+            } else {
+                const int t = j[u] - los[nbk];
+                hb.gexit[static_cast<int64_t>(gi) * W + e] =
+                    (j[u] < 0 || t < 0 || t >= bw_next) ? 0xFFFF : static_cast<uint16_t>(t);
+            }
         }
     }
 }
