@@ -27,6 +27,7 @@ struct MT19937 {
     int index = N + 1;
 
     void init_genrand(uint32_t s) {
+        ext = false;
         mt[0] = s;
         for (int i = 1; i < N; ++i)
             mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + static_cast<uint32_t>(i);
@@ -64,7 +65,12 @@ struct MT19937 {
 
     // Output words of the current block, tempered once per block (the block's
     // raw state stays in mt[], exactly what random.getstate() exposes).
-    alignas(64) uint32_t out[N];
+    // out[N .. N + kExt): the next block's first words, valid while `ext`
+    // (extend()), so a fast path can read across the block end; mt[] and the
+    // stream position stay CPython's (settle() twists once they are consumed).
+    static constexpr int kExt = 32;
+    alignas(64) uint32_t out[N + kExt];
+    bool ext = false;
 
     static inline uint32_t temper(uint32_t y) {
         y ^= (y >> 11);
@@ -77,6 +83,30 @@ struct MT19937 {
     // Recompute out[] from mt[] (after setstate).
     void refresh() {
         for (int i = 0; i < N; ++i) out[i] = temper(mt[i]);
+        ext = false;
+    }
+
+    // The next block's first kExt tempered words from the current mt[]
+    // (new mt[kk] = mt[kk + M] ^ twist(mt[kk], mt[kk + 1]) for kk < N - M),
+    // mt[] untouched: twist() later produces the same words.
+    void extend() {
+        constexpr uint32_t A = 0x9908b0dfu;
+        for (int kk = 0; kk < kExt; ++kk) {
+            const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+            out[N + kk] = temper(mt[kk + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A));
+        }
+        ext = true;
+    }
+
+    // After a fast path consumed words past the block end: the twist that
+    // genrand_uint32 would have done, the position carried into the new block
+    // (index == N stays as is: CPython twists lazily on the next draw).
+    void settle() {
+        if (index > N) {
+            const int over = index - N;
+            twist();
+            index = over;
+        }
     }
 
     // genrand_uint32's block regeneration, written as three branch-free loops
@@ -222,7 +252,9 @@ alignas(32) inline constexpr PackLut kPackLut = make_pack_lut();
 
 template <class OutT>
 inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
-    if (rng.index + 32 > MT19937::N) return false;
+    static_assert(MT19937::kExt >= 32, "the fast path reads 32 words");
+    if (rng.index >= MT19937::N) rng.twist();  // genrand_uint32's lazy twist, before the first word
+    if (rng.index + 32 > MT19937::N && !rng.ext) rng.extend();  // words across the block end
     const int sh = 32 - (64 - __builtin_clzll(static_cast<uint64_t>(n)));
     const __m128i shv = _mm_cvtsi32_si128(sh);
     const __m256i nv = _mm256_set1_epi32(static_cast<int32_t>(n));
@@ -272,9 +304,30 @@ inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
             dup = _mm256_or_si256(dup, _mm256_cmpeq_epi32(a, _mm256_permutevar8x32_epi32(b, rot)));
         }
     }
-    if (!_mm256_testz_si256(dup, dup)) return false;
+    if (!_mm256_testz_si256(dup, dup)) {
+        // A repeat among the first k in-range values: the picks are the first
+        // k values of the packed in-range run that repeat no earlier pick (a
+        // value repeating an earlier in-range word repeats a pick), and the
+        // stream advances past the word of the k-th.  Fewer than k such values
+        // in the 32 words: the general scan from the same position.
+        int32_t sel[16];
+        int cnt = 0, idx = 0;
+        for (; idx < at && cnt < k; ++idx) {
+            const int32_t v = c[idx];
+            bool fresh = true;
+            for (int t = 0; t < cnt; ++t) fresh &= sel[t] != v;
+            sel[cnt] = v;
+            cnt += fresh;
+        }
+        if (cnt < k) return false;
+        for (int i = 0; i < k; ++i) out[i] = static_cast<OutT>(sel[i]);
+        rng.index += __builtin_ctz(_pdep_u32(1u << (idx - 1), inr)) + 1;
+        rng.settle();
+        return true;
+    }
     for (int i = 0; i < k; ++i) out[i] = static_cast<OutT>(c[i]);
     rng.index += last + 1;
+    rng.settle();
     return true;
 }
 
