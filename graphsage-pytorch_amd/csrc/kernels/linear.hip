@@ -369,7 +369,26 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     static const bool bf16_chunked = std::getenv("GS_LIN_FWD_BF16") &&
                                      std::string(std::getenv("GS_LIN_FWD_BF16")) == "chunked";
     if ((wide_on || wide32_on) && vload && (dt == GS_F32 || !bf16_chunked)) {
-        const int R = wide32_on ? 32 : kWideRows;
+        // Rows per tile: 32, or 48 when 32-row tiles would need more than one
+        // workgroup per CU (a second round on some CUs: layer 1 at rmat2m
+        // measured 10.5 us at 256 workgroups against 15.0 us at 264-300) and
+        // 48-row tiles fit one (GS_FWD_ROWS=32 keeps 32: A/B).  Every row tile
+        // runs the same MFMA chain, so the output is bitwise the same.
+        const char* rows_env = std::getenv("GS_FWD_ROWS");  // read per call (tests switch it)
+        const bool rows32 = rows_env && std::string(rows_env) == "32";
+        int R = wide32_on ? 32 : kWideRows;
+        {
+            static const int ncu = [] {
+                int d = 0, c = 256;
+                if (hipGetDevice(&d) != hipSuccess ||
+                    hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+                    c = 256;
+                return c;
+            }();
+            const int64_t gyy = (H + 63) / 64;
+            auto blocks = [&](int64_t rr) { return ((n + rr - 1) / rr + 7) / 8 * 8 * gyy; };
+            if (wide32_on && !rows32 && blocks(32) > ncu && blocks(48) <= ncu) R = 48;
+        }
         // XCD map (a 1-D grid, the kernel derives its tile): the column tiles of a row tile share
         // an XCD's L2; GS_FWD_NOXCD=1 restores the 2-D grid (A/B)
         static const bool noxcd = std::getenv("GS_FWD_NOXCD") != nullptr;
@@ -385,9 +404,11 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
              else { if (relu) GS_LFWDW(TT, RR, false, true); else GS_LFWDW(TT, RR, false, false); } } while (0)
         if (dt == GS_F32) {
             if (R == 32) GS_LFWDW_R(float, 32);
+            else if (R == 48) GS_LFWDW_R(float, 48);
             else GS_LFWDW_R(float, 64);
         } else {
             if (R == 32) GS_LFWDW_R(bf16_t, 32);
+            else if (R == 48) GS_LFWDW_R(bf16_t, 48);
             else GS_LFWDW_R(bf16_t, 64);
         }
 #undef GS_LFWDW_R

@@ -265,7 +265,8 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
     constexpr int RT = ROWS / 16;   // row tiles
-    constexpr int WQ = 64 / ROWS;   // W slots per thread
+    constexpr int WQ = (64 + ROWS - 1) / ROWS;  // W slots per thread (ROWS = 48: the second only for lr < 16)
+    static_assert(ROWS % 16 == 0 && ROWS <= 64, "row tiles of 16, at most 64 rows");
     __shared__ uint4 sA[2][ROWS * SP];
     __shared__ uint4 sW[2][64 * SP];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
     const T* wrow[WQ];
 #pragma unroll
-    for (int q = 0; q < WQ; ++q) wrow[q] = W + static_cast<int64_t>(min(c0 + lr + ROWS * q, H - 1)) * K;
+    for (int q = 0; q < WQ; ++q) wrow[q] = W + static_cast<int64_t>(min(c0 + min(lr + ROWS * q, 63), H - 1)) * K;
     const int nC = (K + BK - 1) / BK;
     // register ring of kFwdAhead chunks: slot u holds chunk c (c = u mod
     // kFwdAhead) once it is in LDS and is then refilled with chunk c + kFwdAhead
@@ -303,7 +304,8 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     auto stash = [&](int c, int u) {
         sA[c & 1][lr * SP + ls] = ar[u];
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) sW[c & 1][(lr + ROWS * q) * SP + ls] = wr_[u][q];
+        for (int q = 0; q < WQ; ++q)
+            if (64 % ROWS == 0 || lr + ROWS * q < 64) sW[c & 1][(lr + ROWS * q) * SP + ls] = wr_[u][q];
     };
 #pragma unroll
     for (int u = 0; u < kFwdAhead; ++u) load(u, u);

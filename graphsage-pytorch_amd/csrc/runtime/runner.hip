@@ -180,6 +180,13 @@ struct gs_runner {
     // so the side stream's work lands under that step's latency-bound launches
     // rather than under its forward (A/B switch)
     bool gate_fwd = false;
+    // GS_SIDE_GATE_STEP: the lookahead's side-stream work waits on the GPU for
+    // the previous step's last launch (an event recorded on the step stream
+    // just before this step's launches), so it starts under this step's
+    // forward and its gather lands under the top launch (A/B switch)
+    bool gate_step = false;
+    hipEvent_t gate_ev = nullptr;
+    hipEvent_t side_gate = nullptr;        // set around the lookahead issue
     int64_t pull_blocks = 1 << 30;  // GS_PULL_BLOCKS: cap on the pull kernel's grid (grid-stride)
     bool pull_copy = false;  // GS_PULL_COPY=1: the pack pull as a runtime copy (copy engine) instead of a kernel
     hipEvent_t fwd_done[kDev] = {};
@@ -438,6 +445,7 @@ bool gs_runner::issue(int64_t b, bool block) {
         if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
     }
     stats.wait_ring_s += secs(tr, Clock::now());
+    if (side_gate) hip_ok(hipStreamWaitEvent(side, side_gate, 0), "hipStreamWaitEvent");
     if (devmode) {
         const DevResult& R = dres[b % n_dpack];
         const int rc = gs_trainer_gather(cfg.trainer, dpack[b % n_dpack], R.hop_sizes, R.offsets, k, side);
@@ -529,6 +537,7 @@ gs_runner::~gs_runner() {
         } catch (...) {
         }
     }
+    if (gate_ev) (void)hipEventDestroy(gate_ev);
     if (upper_ready) (void)hipEventDestroy(upper_ready);
     if (upper_reduced) (void)hipEventDestroy(upper_reduced);
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
@@ -729,6 +738,8 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         });
     }
     r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
+    r->gate_step = std::getenv("GS_SIDE_GATE_STEP") != nullptr && !cfg->embed_out;
+    if (r->gate_step) hip_ok(hipEventCreateWithFlags(&r->gate_ev, hipEventDisableTiming), "hipEventCreate");
     r->pull_copy = std::getenv("GS_PULL_COPY") != nullptr;
     r->pull_ahead = std::getenv("GS_PULL_AHEAD") != nullptr;
     if (const char* e = std::getenv("GS_PULL_BLOCKS")) r->pull_blocks = std::max(1, std::atoi(e));
@@ -817,7 +828,14 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         // look ahead: batch b+1's pull + gather run on the side stream under
         // this step (never block here: with a slow sampler that would idle the GPU)
-        if (b + 1 < r->n_units && r->issued == b + 1) r->issue(b + 1, false);
+        if (b + 1 < r->n_units && r->issued == b + 1) {
+            if (r->gate_step) {
+                hip_ok(hipEventRecord(r->gate_ev, st), "hipEventRecord");
+                r->side_gate = r->gate_ev;
+            }
+            r->issue(b + 1, false);
+            r->side_gate = nullptr;
+        }
         const int k = static_cast<int>(b % gs_runner::kDev);
         const auto tg = Clock::now();
         hip_ok(hipEventSynchronize(r->gathered[k]), "hipEventSynchronize");  // normally long done
