@@ -62,14 +62,25 @@ __device__ __forceinline__ uint32_t temper(uint32_t y) {
 // once at the end.
 constexpr int kGenThreads = 256;
 constexpr int kGenRing = 2048;  // LDS ring: reads reach back 624 words, a step writes 454 ahead
+// spec = 1 (the sampler's aux stream, beside the last hop's draws): extend
+// the stream to `need_fixed` words past hop need_hop's first draw, into
+// gen_spec, never touching gen_end or any word below it (the draws in flight
+// read only words below gen_end).  The main stream's next launch, ordered
+// after the aux stream by an event, takes gen_spec over as its gen_end.  The
+// lead stays bounded by need_fixed, far inside the ring.
+constexpr int64_t kGenAhead = int64_t(1) << 18;  // a rmat2m batch reads ~75k words
 __global__ __launch_bounds__(kGenThreads) void mt_gen_kernel(uint32_t* __restrict__ xr, uint32_t* __restrict__ wr,
-                                                             Ctl* c, int64_t need_fixed, int need_hop) {
+                                                             Ctl* c, int64_t need_fixed, int need_hop, int spec = 0) {
     __shared__ uint32_t L[kGenRing];
     constexpr int64_t M = kGenRing - 1;
     const int i = threadIdx.x;
-    const int64_t g0 = c->gen_end;
-    const int64_t need = need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
-    if (g0 >= need) return;
+    const int64_t ge = c->gen_end;
+    const int64_t g0 = max(ge, c->gen_spec);
+    const int64_t need = spec ? c->hop[need_hop].P0 + need_fixed : need_hop >= 0 ? c->hop[need_hop].need_end : need_fixed;
+    if (g0 >= need) {
+        if (!spec && i == 0 && g0 != ge) c->gen_end = g0;
+        return;
+    }
     for (int q = i; q < 624; q += kGenThreads) {
         const int64_t A = g0 - 624 + q;
         L[A & M] = xr[A & kRingMask];
@@ -100,7 +111,10 @@ __global__ __launch_bounds__(kGenThreads) void mt_gen_kernel(uint32_t* __restric
         __syncthreads();
         g += 454;
     }
-    if (i == 0) c->gen_end = g;
+    if (i == 0) {
+        if (spec) c->gen_spec = g;
+        else c->gen_end = g;
+    }
 }
 
 // Seed the stream from random.setstate's (mt[624], pos): block 0 = mt, the
@@ -113,6 +127,7 @@ __global__ void mt_seed_kernel(const uint32_t* __restrict__ mt, int64_t pos, uin
     }
     if (threadIdx.x == 0) {
         c->gen_end = 624;
+        c->gen_spec = 0;
         c->pos_cur = pos;
         c->status = 0;
     }
@@ -916,6 +931,10 @@ struct gs_dsampler {
     int32_t* lid = nullptr;    // union key -> frontier position (shared by the hops)
     hipEvent_t done = nullptr;
     hipStream_t last_stream = nullptr;
+    // aux stream: the union's lists and the next run's words beside the
+    // draws (GS_DS_AUX=0: everything on the caller's stream)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_gen = nullptr, ev_join = nullptr;
     bool ran = false;
 
     template <typename T>
@@ -927,6 +946,10 @@ struct gs_dsampler {
     }
     ~gs_dsampler() {
         if (done) (void)hipEventSynchronize(done);
+        if (aux) (void)hipStreamSynchronize(aux);
+        for (hipEvent_t e : {ev_gen, ev_join})
+            if (e) (void)hipEventDestroy(e);
+        if (aux) (void)hipStreamDestroy(aux);
         for (void* p : owned) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
         if (done) (void)hipEventDestroy(done);
@@ -945,6 +968,15 @@ void launch_hop_draws(gs_dsampler* ds, int hop, bool last, int n_roots, hipStrea
     gs::check_launch("hop_setup_kernel");
     mt_gen_kernel<<<1, kGenThreads, 0, st>>>(ds->xr, ds->wr, ds->ctl, 0, hop);
     gs::check_launch("mt_gen_kernel");
+    if (last && ds->aux) {  // the previous hop's lists and the next run's words, beside this hop's draws
+        hip_ok(hipEventRecord(ds->ev_gen, st), "hipEventRecord(dsampler fork)");
+        hip_ok(hipStreamWaitEvent(ds->aux, ds->ev_gen, 0), "hipStreamWaitEvent(dsampler fork)");
+        if (hop > 0)
+            gs::ds::launch_hop_lists(ds->ctl, ds->hb[hop - 1], ds->ub[hop - 1], hop - 1, ds->nd_max[hop - 1],
+                                     ds->nd_max[hop], ds->flags, ds->pack_cur, ds->aux);
+        mt_gen_kernel<<<1, kGenThreads, 0, ds->aux>>>(ds->xr, ds->wr, ds->ctl, kGenAhead, hop, 1);
+        gs::check_launch("mt_gen_kernel(ahead)");
+    }
     const int nb_max = static_cast<int>((ds->nd_max[hop] + R - 1) / R);
     const size_t mask_lds = static_cast<size_t>(R) * std::max(k, 1) * kMChunks * sizeof(uint64_t) +
                             (kMEntries + 4 * R * std::max(k, 1) + 64) * sizeof(uint32_t);
@@ -1105,6 +1137,12 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
         }
     }
     hip_ok(hipEventCreateWithFlags(&ds->done, hipEventDisableTiming), "hipEventCreate");
+    const char* aux_env = std::getenv("GS_DS_AUX");
+    if (!(aux_env && std::string(aux_env) == "0")) {
+        hip_ok(hipStreamCreateWithFlags(&ds->aux, hipStreamNonBlocking), "hipStreamCreate(dsampler aux)");
+        for (hipEvent_t* e : {&ds->ev_gen, &ds->ev_join})
+            hip_ok(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+    }
     // the stream starts as random.seed(0) would leave it; callers set it
     gs::MT19937 mt;
     const uint32_t zero = 0;
@@ -1186,7 +1224,12 @@ int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int3
         const bool last = j == ds->n_hops - 1;
         launch_hop_draws(ds, j, last, static_cast<int>(n_roots), st);
         if (!last) gs::ds::launch_hop_union(ds->g, ds->ctl, ds->hb[j], ds->ub[j], ds->hb[j + 1], j, ds->fanouts[j],
-                                            ds->nd_max[j], ds->nd_max[j + 1], ds->flags, pack, st);
+                                            ds->nd_max[j], ds->nd_max[j + 1], ds->flags, pack, st,
+                                            !(ds->aux && j + 2 == ds->n_hops));
+    }
+    if (ds->aux) {  // join: the lists are in the pack, the words ahead are in the ring
+        hip_ok(hipEventRecord(ds->ev_join, ds->aux), "hipEventRecord(dsampler join)");
+        hip_ok(hipStreamWaitEvent(st, ds->ev_join, 0), "hipStreamWaitEvent(dsampler join)");
     }
     finish_kernel<<<8, 256, 0, st>>>(ds->ctl, roots, static_cast<int>(n_roots), pack,
                                      (ds->flags & GS_SAMPLE_FAIL_EMPTY) ? 1 : 0, ds->n_hops);

@@ -48,6 +48,7 @@ struct HopCtl {
 
 struct Ctl {
     int64_t gen_end;           // raw/tempered words valid below this absolute index
+    int64_t gen_spec;          // words the aux stream generated ahead (valid below it once joined)
     int64_t pos_cur;           // next word of the stream
     int64_t pos_batch;         // stream position at the start of the last run
     int32_t status;
@@ -152,7 +153,15 @@ namespace ds {
 // dsample_union.hip: for hop `hop` (not the last): per-node sets, the frontier
 // union (next.dst, n_src), the neighbour / self / transposed lists into the
 // pack.  Buffers in `ub` are allocated on first use.
+// with_lists = false: the caller launches the lists (launch_hop_lists) itself
+// later, e.g. on another stream beside the next hop's draws (nothing of the
+// next hop reads them; it needs next.dst only).
 void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& ub, const HopBufs& next, int hop,
-                      int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st);
+                      int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st,
+                      bool with_lists);
+// The neighbour / self / transposed lists of hop `hop` into the pack (reads
+// the union's lid, so before any later union).
+void launch_hop_lists(Ctl* c, const HopBufs& hb, UnionBufs& ub, int hop, int64_t nd_max, int64_t nd_next_max,
+                      int flags, int32_t* pack, hipStream_t st);
 }  // namespace ds
 }  // namespace gs

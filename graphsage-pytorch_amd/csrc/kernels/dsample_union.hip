@@ -867,7 +867,8 @@ __global__ __launch_bounds__(kLongThreads) void tlong_kernel(Ctl* c, int hop, in
 }
 
 void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& ub, const HopBufs& next, int hop,
-                      int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st) {
+                      int k, int64_t nd_max, int64_t nd_next_max, int flags, int32_t* pack, hipStream_t st,
+                      bool with_lists) {
     static const bool attr = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(ublock_kernel),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -891,6 +892,12 @@ void launch_hop_union(const DevGraph& g, Ctl* c, const HopBufs& hb, UnionBufs& u
     ubig_kernel<<<1, 1024, kUnionBig * sizeof(uint16_t), st>>>(c, hb, ub, next, hop, gcn, pack,
                                                                static_cast<int>(nd_next_max));
     check_launch("ubig_kernel");
+    if (with_lists) launch_hop_lists(c, hb, ub, hop, nd_max, nd_next_max, flags, pack, st);
+}
+
+void launch_hop_lists(Ctl* c, const HopBufs& hb, UnionBufs& ub, int hop, int64_t nd_max, int64_t nd_next_max,
+                      int flags, int32_t* pack, hipStream_t st) {
+    const int gcn = (flags & GS_SAMPLE_GCN) ? 1 : 0;
     uout_kernel<<<static_cast<unsigned>(nd_max), 64, 0, st>>>(c, hb, ub, hop, gcn, pack);
     check_launch("uout_kernel");
     tscan_kernel<<<1, 1024, 0, st>>>(c, hop, pack, ub.tcnt, ub.longs);

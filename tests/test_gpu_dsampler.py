@@ -174,6 +174,39 @@ def test_device_multi_hop_matches_host(graph, fan, gcn):
         np.testing.assert_array_equal(mt_d, mt_h)
 
 
+@pytest.mark.parametrize("fan", [[25, 10], [5, 4, 3], [10]])
+def test_device_aux_stream_back_to_back(graph, fan, monkeypatch):
+    """The aux stream (the last union's lists and the next run's words beside
+    the last hop's draws, joined before the run ends) against GS_DS_AUX=0:
+    runs issued back to back with no host sync between them give the host
+    sampler's packs, and the stream ends where the host's does."""
+    fan = np.array(fan, np.int32)
+    rs = np.random.RandomState(11)
+    roots = [rs.choice(graph.n_nodes, 512, replace=True).astype(np.int32) for _ in range(12)]
+    out = {}
+    for aux in ("1", "0"):
+        monkeypatch.setenv("GS_DS_AUX", aux)
+        ds = gs.sampler.DeviceSampler(graph, fan, 512)
+        ds.set_rng(gs.RNG(5))
+        bound = ds.pack_bound(512)
+        packs = torch.zeros((len(roots), bound), dtype=torch.int32, device="cuda")
+        dev_roots = [torch.from_numpy(r).cuda() for r in roots]
+        torch.cuda.synchronize()
+        for i, r in enumerate(dev_roots):
+            L.check(L.lib().gs_dsampler_run(ds._h, r.data_ptr(), 512, packs[i].data_ptr(), bound, L.stream_ptr()))
+        torch.cuda.synchronize()
+        out[aux] = (packs.cpu().numpy(), ds.get_rng())
+    rng_h = gs.RNG(5)
+    for i, r in enumerate(roots):
+        ref, sizes, offs, used = host_pack(graph, rng_h, r.astype(np.int64), fan, 0)
+        for aux in ("1", "0"):
+            assert_packs_equal(out[aux][0][i][:used], ref, sizes, offs, 512, f"aux {aux} batch {i}")
+    mt_h, pos_h = rng_h.getstate()
+    for aux in ("1", "0"):
+        assert out[aux][1][1] == pos_h
+        np.testing.assert_array_equal(out[aux][1][0], mt_h)
+
+
 # ---------------------------------------------------------------------------
 # Straight against the reference: the vectors captured by importing the
 # reference (tests/golden/make_golden.py: per-hop unions, sets and the
