@@ -437,10 +437,58 @@ __device__ __forceinline__ int walk_masked(const uint32_t* __restrict__ M, int a
         // (membership is all the repeat test needs), so each word costs KMAX
         // compares and KMAX selects, none of them on the pick count.
         const int sh = __clz(d);
+        // Speculative pass: the first k accepted words by their masks alone
+        // (one dependent LDS read per draw), then their values all at once.
+        // Without a repeat among them they are exactly the k picks; at the
+        // first repeat l the exact loop below resumes with picks 0..l-1 and
+        // the walk just past word l.
+        // (KMAX <= 16 only: at the root hop's KMAX = 25 the pairwise repeat
+        // test and its registers cost more than the chain saves, measured)
+        constexpr int KS = KMAX <= 16 ? KMAX : 1;
+        int rels[KS];
+        uint32_t vals[KS];
+        if constexpr (KMAX <= 16) {
+            int r = rel;
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) {
+                if (i < k) {
+                    const int j = min(r >> 5, C32 - 2);
+                    const uint32_t win = __builtin_amdgcn_alignbit(M[j + 1], M[j], r & 31) & (0u - (r < lim));
+                    const int adv = __ffs(win);
+                    bad |= adv == 0;
+                    r += adv;
+                }
+                rels[i] = r;
+            }
+#pragma unroll
+            for (int i = 0; i < KMAX; ++i) vals[i] = i < k ? w[a + max(rels[i] - 1, 0)] >> sh : 0xFFFFFFFFu - i;
+        }
+        int keep = 0;  // picks the speculative pass settled
+        if constexpr (KMAX <= 16) {
+            int first = k;  // the first pick index whose value repeats an earlier one
+#pragma unroll
+            for (int l = KMAX - 1; l > 0; --l) {
+                bool rep = false;
+#pragma unroll
+                for (int i = 0; i < l; ++i) rep |= vals[i] == vals[l];
+                first = (rep && l < k) ? l : first;
+            }
+            if (!bad && first == k) return a + rels[KMAX - 1];  // rels[i >= k] hold the walk after draw k-1
+            // resume just past the repeated word with picks 0..first-1; a
+            // speculative walk that left its masks restarts from the node's start
+            keep = bad ? 0 : first;
+#pragma unroll
+            for (int t = 1; t < KMAX; ++t)
+                if (t == keep) rel = rels[t];
+        }
         uint32_t sel[KMAX];
 #pragma unroll
-        for (int t = 0; t < KMAX; ++t) sel[t] = 0xFFFFFFFFu;
-        int cnt = 0;
+        for (int t = 0; t < KMAX; ++t) {
+            sel[t] = 0xFFFFFFFFu;
+            if constexpr (KMAX <= 16) sel[t] = t < keep ? vals[t] : 0xFFFFFFFFu;
+        }
+        int cnt = keep;
+        bad = false;
         while (cnt < k && !bad) {
             const int j = min(rel >> 5, C32 - 2);
             const uint32_t win = __builtin_amdgcn_alignbit(M[j + 1], M[j], rel & 31) & (0u - (rel < lim));
