@@ -25,6 +25,7 @@ GS_OK, GS_EINVAL, GS_ENOMEM, GS_EHIP, GS_ERANGE, GS_EEMPTY = range(6)
 GS_F32, GS_BF16 = 0, 1
 GS_AGG_MEAN, GS_AGG_MAX = 0, 1
 GS_SAMPLE_GCN, GS_SAMPLE_FULL = 1, 2
+GS_DSAMPLER_NO_AUX = 8  # gs_dsampler_create: every kernel on the caller's stream
 GS_MAX_HOPS = 8
 (GS_PK_POS_PTR, GS_PK_POS, GS_PK_DST_IDS, GS_PK_NBR_PTR, GS_PK_NBR, GS_PK_SELF,
  GS_PK_TPTR, GS_PK_TIDX, GS_PK_NFIELDS) = range(9)
@@ -159,6 +160,8 @@ _SIGS = {
     "gs_dsampler_pack_bound": (_i64, [_vp, _i64]),
     "gs_dsampler_run": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
     "gs_dsampler_result": (_i32, [_vp, _vp, _vp, _p(_i64)]),
+    "gs_dsampler_runs": (_i64, [_vp]),
+    "gs_dsampler_result_of": (_i32, [_vp, _i64, _vp, _vp, _p(_i64)]),
     "gs_dsampler_debug": (_i32, [_vp, _vp, _i32]),
 }
 

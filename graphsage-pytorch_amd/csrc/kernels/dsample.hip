@@ -971,7 +971,9 @@ struct gs_dsampler {
     uint32_t* tmp = nullptr;  // small transfer buffer (state block, words)
     int64_t tmp_n = 0;
     Ctl* ctl = nullptr;       // device control block
-    Ctl* ctl_host = nullptr;  // pinned mirror, copied at the end of every run
+    Ctl* ctl_host = nullptr;  // pinned mirrors, run i's copied into slot i % kResSlots at its end
+    hipEvent_t run_done[kResSlots] = {};  // per slot: its run's end
+    int64_t n_runs = 0;
     HopBufs hb[GS_MAX_HOPS];
     UnionBufs ub[GS_MAX_HOPS];
     int32_t* pack_cur = nullptr;
@@ -1000,6 +1002,8 @@ struct gs_dsampler {
         if (aux) (void)hipStreamDestroy(aux);
         for (void* p : owned) (void)hipFree(p);
         if (ctl_host) (void)hipHostFree(ctl_host);
+        for (hipEvent_t e : run_done)
+            if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
     }
 };
@@ -1081,6 +1085,14 @@ void check_status(int status) {
 }  // namespace
 
 namespace gs {
+bool dsampler_run_ready(gs_dsampler* ds, int64_t run) {
+    if (!ds || run < ds->n_runs - kResSlots) return true;
+    if (run >= ds->n_runs) return false;
+    const hipError_t e = hipEventQuery(ds->run_done[run % kResSlots]);
+    if (e == hipErrorNotReady) return false;
+    hip_ok(e, "hipEventQuery(dsampler run)");
+    return true;
+}
 bool dsampler_ready(gs_dsampler* ds) {
     if (!ds || !ds->ran) return true;
     const hipError_t e = hipEventQuery(ds->done);
@@ -1137,8 +1149,10 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
     ds->wr = ds->alloc<uint32_t>(kRing);
     ds->ctl = ds->alloc<Ctl>(1);
     hip_ok(hipMemset(ds->ctl, 0, sizeof(Ctl)), "hipMemset");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&ds->ctl_host), sizeof(Ctl), hipHostMallocDefault), "hipHostMalloc");
-    std::memset(ds->ctl_host, 0, sizeof(Ctl));
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&ds->ctl_host), kResSlots * sizeof(Ctl), hipHostMallocDefault),
+           "hipHostMalloc");
+    std::memset(ds->ctl_host, 0, kResSlots * sizeof(Ctl));
+    for (hipEvent_t& e : ds->run_done) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     for (int32_t j = 0; j < n_hops; ++j) {
         const int k = ds->fanouts[j];
         const int64_t ndj = ds->nd_max[j];
@@ -1186,7 +1200,7 @@ int gs_dsampler_create(const gs_graph* gp, const int32_t* fanouts, int32_t n_hop
     }
     hip_ok(hipEventCreateWithFlags(&ds->done, hipEventDisableTiming), "hipEventCreate");
     const char* aux_env = std::getenv("GS_DS_AUX");
-    if (!(aux_env && std::string(aux_env) == "0")) {
+    if (!(flags & GS_DSAMPLER_NO_AUX) && !(aux_env && std::string(aux_env) == "0")) {
         hip_ok(hipStreamCreateWithFlags(&ds->aux, hipStreamNonBlocking), "hipStreamCreate(dsampler aux)");
         for (hipEvent_t* e : {&ds->ev_gen, &ds->ev_join})
             hip_ok(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
@@ -1282,9 +1296,12 @@ int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int3
     finish_kernel<<<8, 256, 0, st>>>(ds->ctl, roots, static_cast<int>(n_roots), pack,
                                      (ds->flags & GS_SAMPLE_FAIL_EMPTY) ? 1 : 0, ds->n_hops);
     gs::check_launch("finish_kernel");
-    hip_ok(hipMemcpyAsync(ds->ctl_host, ds->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st), "hipMemcpyAsync(ctl)");
+    const int slot = static_cast<int>(ds->n_runs % kResSlots);
+    hip_ok(hipMemcpyAsync(ds->ctl_host + slot, ds->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, st), "hipMemcpyAsync(ctl)");
+    hip_ok(hipEventRecord(ds->run_done[slot], st), "hipEventRecord");
     hip_ok(hipEventRecord(ds->done, st), "hipEventRecord");
     ds->ran = true;
+    ++ds->n_runs;
     GS_API_END
 }
 
@@ -1292,15 +1309,13 @@ int gs_dsampler_debug(gs_dsampler* ds, int64_t* out, int32_t n) {
     GS_API_BEGIN
     GS_REQUIRE(ds && ds->ran && out && n >= 0 && n <= 64, GS_EINVAL, "bad arguments");
     hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
-    std::memcpy(out, ds->ctl_host->dbg, n * sizeof(int64_t));
+    std::memcpy(out, ds->ctl_host[(ds->n_runs - 1) % kResSlots].dbg, n * sizeof(int64_t));
     GS_API_END
 }
 
-int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
-    GS_API_BEGIN
-    GS_REQUIRE(ds && ds->ran, GS_EINVAL, "no run to report");
-    hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
-    const Ctl& c = *ds->ctl_host;
+namespace {
+// The layout of the run whose Ctl mirror is `c`, as the host sampler reports it.
+void report(const gs_dsampler* ds, const Ctl& c, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
     check_status(c.status);
     for (int32_t j = 0; j < GS_MAX_HOPS; ++j) {
         const bool on = j < ds->n_hops;
@@ -1319,6 +1334,28 @@ int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, in
             }
     }
     if (used) *used = c.used;
+}
+}  // namespace
+
+int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds && ds->ran, GS_EINVAL, "no run to report");
+    hip_ok(hipEventSynchronize(ds->done), "hipEventSynchronize");
+    report(ds, ds->ctl_host[(ds->n_runs - 1) % kResSlots], hop_sizes, offsets, used);
+    GS_API_END
+}
+
+int64_t gs_dsampler_runs(const gs_dsampler* ds) { return ds ? ds->n_runs : -1; }
+
+int gs_dsampler_result_of(gs_dsampler* ds, int64_t run, int64_t* hop_sizes, int64_t* offsets, int64_t* used) {
+    GS_API_BEGIN
+    GS_REQUIRE(ds, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(run >= 0 && run < ds->n_runs && run >= ds->n_runs - kResSlots, GS_ERANGE,
+               "device sampler: run not issued or no longer kept (the last " + std::to_string(kResSlots) +
+                   " runs are)");
+    const int slot = static_cast<int>(run % kResSlots);
+    hip_ok(hipEventSynchronize(ds->run_done[slot]), "hipEventSynchronize");
+    report(ds, ds->ctl_host[slot], hop_sizes, offsets, used);
     GS_API_END
 }
 

@@ -15,6 +15,7 @@ constexpr int kMinG = kComposeEntries / kWMax;
 constexpr int kChainEntries = 30720;         // group exits the chain block stages in LDS (uint16)
 constexpr int kMaxGroups = 1024;
 constexpr int kMEntries = 256;               // window entries per table-kernel workgroup
+constexpr int kResSlots = 4;                 // runs whose results are kept (gs_dsampler_result_of)
 
 // status bits (Ctl::status)
 constexpr int kStWindow = 1;   // a true entry fell outside its block window

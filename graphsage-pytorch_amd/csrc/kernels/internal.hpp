@@ -165,5 +165,6 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
 
 // dsample.hip: whether the last gs_dsampler_run has completed (no wait).
 bool dsampler_ready(gs_dsampler* ds);
+bool dsampler_run_ready(gs_dsampler* ds, int64_t run);  // run number `run` has finished
 
 }  // namespace gs

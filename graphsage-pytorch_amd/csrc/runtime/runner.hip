@@ -202,17 +202,25 @@ struct gs_runner {
     gs_runner_stats stats{};
 
     // cfg.device_sampler: one gs_dsampler per stream, each on its own HIP
-    // stream; packs are written straight into a device ring of S + 3 entries
-    // (batch b's entry was last read by step b - S - 3, which issue() has
-    // waited for before enqueuing b).
+    // stream, up to dev_depth runs queued per stream (the sampler keeps each
+    // run's result: gs_dsampler_result_of), so a stream's next run is already
+    // on the GPU when its current one finishes; packs are written straight into
+    // a device ring of dev_depth * S + 3 entries (batch b's entry was last read
+    // by step b - dev_depth * S - 3, which issue() has waited for before
+    // enqueuing b).
+    static constexpr int kDevDepthMax = 2;
     struct DevStream {
         gs_dsampler* ds = nullptr;
         hipStream_t st = nullptr;
-        hipEvent_t t0 = nullptr, t1 = nullptr;  // around the run: its device time
+        // queued runs, oldest first: batch, sampler run number, events around
+        // the run (its device time), already counted in `sampled`
+        int nq = 0;
+        int64_t qb[kDevDepthMax] = {}, qrun[kDevDepthMax] = {};
+        hipEvent_t t0[kDevDepthMax] = {}, t1[kDevDepthMax] = {};
+        bool counted[kDevDepthMax] = {};
         int64_t next = 0;                       // next batch to enqueue (w, w + S, ...)
-        int64_t inflight = -1;                  // enqueued, result not read yet
-        bool counted = false;                   // inflight already counted in `sampled`
     };
+    int dev_depth = kDevDepthMax;
     struct DevResult {
         int64_t hop_sizes[4 * GS_MAX_HOPS];
         int64_t offsets[GS_MAX_HOPS * GS_PK_NFIELDS];
@@ -361,21 +369,24 @@ void gs_runner::pull(int64_t b, int slot_id) {
     pulled = b + 1;
 }
 
-// Device sampler: enqueue stream w's next batch (one in flight per stream:
-// its result must be read before the sampler's next run overwrites it).
+// Device sampler: enqueue stream w's next batches, up to dev_depth queued.
 void gs_runner::dev_enqueue(int w) {
     using namespace gs;
     DevStream& d = dstreams[w];
-    if (d.inflight >= 0) return;
-    const int64_t b = d.next;
-    if (b >= n_units || b >= release_mark.load()) return;
-    hip_ok(hipEventRecord(d.t0, d.st), "hipEventRecord");
-    const int rc = gs_dsampler_run(d.ds, roots_dev + b * cfg.batch, cfg.batch, dpack[b % n_dpack], dcap, d.st);
-    if (rc != GS_OK) fail(rc, gs_last_error());
-    hip_ok(hipEventRecord(d.t1, d.st), "hipEventRecord");
-    d.inflight = b;
-    d.counted = false;
-    d.next = b + cfg.n_streams;
+    while (d.nq < dev_depth) {
+        const int64_t b = d.next;
+        if (b >= n_units || b >= release_mark.load()) return;
+        const int q = d.nq;
+        hip_ok(hipEventRecord(d.t0[q], d.st), "hipEventRecord");
+        const int rc = gs_dsampler_run(d.ds, roots_dev + b * cfg.batch, cfg.batch, dpack[b % n_dpack], dcap, d.st);
+        if (rc != GS_OK) fail(rc, gs_last_error());
+        hip_ok(hipEventRecord(d.t1[q], d.st), "hipEventRecord");
+        d.qb[q] = b;
+        d.qrun[q] = gs_dsampler_runs(d.ds) - 1;
+        d.counted[q] = false;
+        d.nq = q + 1;
+        d.next = b + cfg.n_streams;
+    }
 }
 
 // Device sampler: batch b's result (hop sizes, layout) into dres[b % ring];
@@ -383,30 +394,42 @@ void gs_runner::dev_enqueue(int w) {
 bool gs_runner::dev_take(int64_t b, bool block) {
     using namespace gs;
     DevStream& d = dstreams[b % cfg.n_streams];
-    if (!block && (d.inflight != b || !dsampler_ready(d.ds))) return false;  // not enqueued yet (held) or running
-    GS_REQUIRE(d.inflight == b, GS_EINVAL, "device sampler: batch not enqueued (past the release mark?)");
+    const bool queued = d.nq > 0 && d.qb[0] == b;
+    if (!block && (!queued || !dsampler_run_ready(d.ds, d.qrun[0]))) return false;  // not enqueued yet (held) or running
+    GS_REQUIRE(queued, GS_EINVAL, "device sampler: batch not enqueued (past the release mark?)");
     const auto tw = Clock::now();
     DevResult& R = dres[b % n_dpack];
-    const int rc = gs_dsampler_result(d.ds, R.hop_sizes, R.offsets, &R.used);
+    const int rc = gs_dsampler_result_of(d.ds, d.qrun[0], R.hop_sizes, R.offsets, &R.used);
     if (rc != GS_OK) fail(rc, gs_last_error());
-    hip_ok(hipEventSynchronize(d.t1), "hipEventSynchronize");
+    hip_ok(hipEventSynchronize(d.t1[0]), "hipEventSynchronize");
     float ms = 0.f;
-    hip_ok(hipEventElapsedTime(&ms, d.t0, d.t1), "hipEventElapsedTime");
+    hip_ok(hipEventElapsedTime(&ms, d.t0[0], d.t1[0]), "hipEventElapsedTime");
     R.sample_s = 1e-3 * ms;
     stats.wait_sample_s += secs(tw, Clock::now());
-    if (!d.counted) sampled.fetch_add(1);
-    d.inflight = -1;
-    d.counted = false;
+    if (!d.counted[0]) sampled.fetch_add(1);
+    // pop the front: every slot moves up one, the freed events to the back
+    const hipEvent_t e0 = d.t0[0], e1 = d.t1[0];
+    for (int q = 1; q < kDevDepthMax; ++q) {
+        d.qb[q - 1] = d.qb[q];
+        d.qrun[q - 1] = d.qrun[q];
+        d.t0[q - 1] = d.t0[q];
+        d.t1[q - 1] = d.t1[q];
+        d.counted[q - 1] = d.counted[q];
+    }
+    d.t0[kDevDepthMax - 1] = e0;
+    d.t1[kDevDepthMax - 1] = e1;
+    --d.nq;
     return true;
 }
 
 // Device sampler: count finished sampling runs (progress()).
 void gs_runner::dev_poll() {
     for (auto& d : dstreams)
-        if (d.inflight >= 0 && !d.counted && gs::dsampler_ready(d.ds)) {
-            d.counted = true;
-            sampled.fetch_add(1);
-        }
+        for (int q = 0; q < d.nq; ++q)
+            if (!d.counted[q] && gs::dsampler_run_ready(d.ds, d.qrun[q])) {
+                d.counted[q] = true;
+                sampled.fetch_add(1);
+            }
 }
 
 // Device sampler: every stream's state back into its rng (waits for the
@@ -484,8 +507,10 @@ gs_runner::~gs_runner() {
         }
         for (auto& d : dstreams) {
             if (d.ds) gs_dsampler_destroy(d.ds);
-            if (d.t0) (void)hipEventDestroy(d.t0);
-            if (d.t1) (void)hipEventDestroy(d.t1);
+            for (int q = 0; q < kDevDepthMax; ++q) {
+                if (d.t0[q]) (void)hipEventDestroy(d.t0[q]);
+                if (d.t1[q]) (void)hipEventDestroy(d.t1[q]);
+            }
             if (d.st) (void)hipStreamDestroy(d.st);
         }
     }
@@ -686,10 +711,14 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         for (int32_t w = 0; w < S; ++w) {
             gs_runner::DevStream& d = r->dstreams[w];
             hip_ok(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking), "hipStreamCreate(dsampler)");
-            hip_ok(hipEventCreate(&d.t0), "hipEventCreate");
-            hip_ok(hipEventCreate(&d.t1), "hipEventCreate");
+            for (int q = 0; q < gs_runner::kDevDepthMax; ++q) {
+                hip_ok(hipEventCreate(&d.t0[q]), "hipEventCreate");
+                hip_ok(hipEventCreate(&d.t1[q]), "hipEventCreate");
+            }
             int rc = gs_dsampler_create(cfg->graph, r->fanouts.data(), cfg->n_hops, cfg->batch,
-                                        cfg->flags & (GS_SAMPLE_GCN | GS_SAMPLE_FAIL_EMPTY), &d.ds);
+                                        (cfg->flags & (GS_SAMPLE_GCN | GS_SAMPLE_FAIL_EMPTY)) |
+                                            (S > 1 ? GS_DSAMPLER_NO_AUX : 0),
+                                        &d.ds);
             if (rc != GS_OK) fail(rc, gs_last_error());
             uint32_t mt[624];
             int64_t pos = 0;
@@ -700,7 +729,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             d.next = w;
         }
         r->dcap = std::max<int64_t>(r->cap, gs_dsampler_pack_bound(r->dstreams[0].ds, cfg->batch));
-        r->n_dpack = S + 3;
+        const char* depth_env = std::getenv("GS_DS_DEPTH");  // runs queued per device stream (1 or 2)
+        r->dev_depth = depth_env && std::atoi(depth_env) == 1 ? 1 : gs_runner::kDevDepthMax;
+        r->n_dpack = r->dev_depth * S + 3;
         r->dpack.assign(r->n_dpack, nullptr);
         for (auto& p : r->dpack) hip_ok(hipMalloc(&p, r->dcap * sizeof(int32_t)), "hipMalloc(pack)");
         r->dres.resize(r->n_dpack);

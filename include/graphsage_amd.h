@@ -230,6 +230,12 @@ int gs_sample_pack_run_multi_team(const gs_graph* g, gs_rng* rng, const int64_t*
  * exactly as the reference's `random` would.  One handle is one
  * stream; its calls are ordered on the caller's stream.  Fanouts <= 32. */
 typedef struct gs_dsampler gs_dsampler;
+/* gs_dsampler_create flag: every kernel on the caller's stream.  By default a
+ * sampler owns an aux stream that runs the union lists of the hop before the
+ * last and the next run's MT19937 words beside the last hop's draws (one
+ * fork, one join per run) — it pays for one sampler alone on the GPU, not for
+ * several sharing it (the runner sets this flag for S > 1). */
+#define GS_DSAMPLER_NO_AUX 8
 int gs_dsampler_create(const gs_graph* g, const int32_t* fanouts, int32_t n_hops,
                        int64_t max_roots, int32_t flags, gs_dsampler** out);
 void gs_dsampler_destroy(gs_dsampler* ds);
@@ -247,6 +253,12 @@ int64_t gs_dsampler_pack_bound(const gs_dsampler* ds, int64_t n_roots);
 int gs_dsampler_run(gs_dsampler* ds, const int32_t* roots, int64_t n_roots, int32_t* pack,
                     int64_t cap, void* stream);
 int gs_dsampler_result(gs_dsampler* ds, int64_t* hop_sizes, int64_t* offsets, int64_t* used);
+/* Runs issued so far on this sampler; run i (0-based) is gs_dsampler_run's
+ * i-th call.  gs_dsampler_result_of(ds, i, ...) reports run i's layout (waits
+ * for that run only), so a caller may keep a second run queued behind the one
+ * it reads; the last 4 runs are kept (GS_ERANGE for older ones). */
+int64_t gs_dsampler_runs(const gs_dsampler* ds);
+int gs_dsampler_result_of(gs_dsampler* ds, int64_t run, int64_t* hop_sizes, int64_t* offsets, int64_t* used);
 /* Diagnostics of the last run (waits for it): n <= 64 words — per-phase
  * device timestamps (100 MHz) and round counts of the frontier union's
  * stages; the layout is documented in kernels/dsample_union.hip. */
