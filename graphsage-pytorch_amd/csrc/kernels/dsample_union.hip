@@ -97,6 +97,39 @@ __device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_
     }
 }
 
+// One table stage of distinct keys: the table is cleared to mask m and lane
+// t < nk inserts `key` with priority t — every key takes the first free slot
+// of its probe sequence in priority order, exactly as nk sequential
+// set_add_entry calls (distinct keys: every add is fresh).  Computed by
+// priority displacement inside the wave (the frontier union's method,
+// settle_keys): a key claims its probe slot with an LDS atomicMin of its
+// priority and moves on when a higher priority holds it or later takes it;
+// after the divergent claims reconverge, every lane re-reads its slot, so a
+// round needs no barrier.  Then each slot gets its key.
+__device__ __forceinline__ void w_stage(volatile int32_t* T, uint32_t m, int nk, int32_t key) {
+    const int lane = wlane();
+    w_clear(T, m + 1);  // -1 = priority 0xFFFFFFFF: empty
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the clear before the claims (one wave: LDS keeps its order)
+    uint32_t* U = const_cast<uint32_t*>(reinterpret_cast<volatile uint32_t*>(T));
+    const bool act = lane < nk;
+    const uint32_t t = static_cast<uint32_t>(lane);
+    uint32_t ps = act ? pr_init(key, m) : 0u;
+    bool placed = !act;
+    for (;;) {
+        if (!placed) {
+            while (atomicMin(&U[pr_slot(ps)], t) < t) ps = pr_next(ps, key, m);
+            placed = true;
+        }
+        const uint32_t h = act ? reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps)] : t;
+        if (h != t) {
+            ps = pr_next(ps, key, m);
+            placed = false;
+        }
+        if (!__ballot(!placed)) break;
+    }
+    if (act) T[pr_slot(ps)] = key;
+}
+
 // The keys of T (mask + 1 <= 128 slots) in slot order into K; returns their count.
 __device__ __forceinline__ int w_compact(const volatile int32_t* T, uint32_t mask, volatile int32_t* K) {
     const int lane = wlane();
@@ -116,8 +149,7 @@ __device__ __forceinline__ uint32_t w_resize(volatile int32_t* T, uint32_t mask,
     const int n = w_compact(T, mask, K);
     uint32_t ns = 8;
     while (ns <= static_cast<uint32_t>(minused)) ns <<= 1;
-    w_clear(T, ns);
-    for (int q = 0; q < n; ++q) (void)w_add(T, ns - 1, K[q]);
+    w_stage(T, ns - 1, n, K[min(wlane(), kSmallSet - 1)]);
     return ns - 1;
 }
 
@@ -146,10 +178,29 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
         // set(list): set_add_key per item in result order, resizing to used * 4
         const int32_t e = lane < k ? hb.ent[hb.pos_ptr[r] + lane] : 0;
         const int32_t mine = lane < k ? g.col[e] : 0;
-        for (int i = 0; i < k; ++i) {
-            if (w_add(T, mask, __shfl(mine, i, 64))) {
-                ++used;
-                if (static_cast<uint32_t>(used) * 5 >= mask * 3) mask = w_resize(T, mask, used * 4, K);
+        // The k sampled keys are distinct (distinct entries of one adjacency
+        // set), so every add is fresh and `used` after key i is i + 1: the
+        // resizes (to used * 4 once used * 5 >= mask * 3) fall at known keys.
+        // Each stage — the previous table's keys in slot order, then the keys
+        // up to the next resize — is one w_stage.
+        int i0 = 0, n_old = 0;
+        while (i0 < k || n_old > 0) {
+            int i1 = i0;
+            while (i1 < k) {
+                ++i1;
+                if (static_cast<uint32_t>(i1) * 5 >= mask * 3) break;
+            }
+            const int src = min(max(i0 + lane - n_old, 0), 63);
+            const int32_t fresh = __shfl(mine, src, 64);
+            w_stage(T, mask, n_old + (i1 - i0), lane < n_old ? K[min(lane, kSmallSet - 1)] : fresh);
+            used = i1;
+            n_old = 0;
+            i0 = i1;
+            if (static_cast<uint32_t>(used) * 5 >= mask * 3) {  // set_table_resize(used * 4)
+                n_old = w_compact(T, mask, K);
+                uint32_t ns = 8;
+                while (ns <= static_cast<uint32_t>(used * 4)) ns <<= 1;
+                mask = ns - 1;
             }
         }
         // the copy `|` makes: resized to 2 * used when used * 5 >= 21, else
@@ -158,8 +209,7 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
         if (used * 5 >= 21) nm = mask_for(2 * used);
         if (nm != mask) {
             const int m = w_compact(T, mask, K);
-            w_clear(T, nm + 1);
-            for (int q = 0; q < m; ++q) (void)w_add(T, nm, K[q]);
+            w_stage(T, nm, m, K[min(lane, kSmallSet - 1)]);
             mask = nm;
         }
     } else {
@@ -177,8 +227,8 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
         if (mask == m0 && !dirty) {
             if (lane < d) T[g.slot[rs + lane]] = g.col[rs + lane];
         } else {
-            const int32_t mine = lane < d ? g.col[rs + lane] : 0;
-            for (int t = 0; t < d; ++t) (void)w_add(T, mask, __shfl(mine, t, 64));
+            // the set's keys in its iteration order, all distinct: one stage
+            w_stage(T, mask, d, lane < d ? g.col[rs + lane] : 0);
         }
     }
     // | set([node]): set_merge with a one-element set
