@@ -682,6 +682,24 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     uint32_t prev_mask = m_first;
     for (int s = 0; s < nst; ++s) {
         const uint32_t m = st_mask[s];
+        // A stage of at most 64 keys (the first two or three) in one wave: the
+        // previous table compacted in slot order, then w_stage (the per-node
+        // sets' wave-level insert) — no block barrier inside the stage.
+        const int nk_w = ub.ubef[st_run[s + 1]];  // the union's size after the stage
+        if (nk_w <= 64 && !(s == 0 && m == m_first)) {  // uniform
+            if (tid < 64) {
+                const volatile int32_t* P = s == 0 ? reinterpret_cast<const volatile int32_t*>(ub.first_tab)
+                                                   : reinterpret_cast<const volatile int32_t*>(T);
+                volatile int32_t* K = need;
+                const int n_old = w_compact(P, prev_mask, K);
+                const int f0 = ub.ubef[st_run[s]] - used0;
+                const int32_t kk = tid < n_old ? K[tid] : (tid < nk_w ? ub.fresh[f0 + tid - n_old] : 0);
+                w_stage(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk);
+            }
+            __syncthreads();
+            prev_mask = m;
+            continue;
+        }
         // compaction of the previous table
         int n_old;
         {
