@@ -130,6 +130,48 @@ __device__ __forceinline__ void w_stage(volatile int32_t* T, uint32_t m, int nk,
     if (act) T[pr_slot(ps)] = key;
 }
 
+// w_stage with up to 64 * KPL keys: lane l's q-th key has priority l + 64 q
+// (the frontier union's small stages).  A lane's later key may displace its
+// earlier one within a claim pass; the re-read after the pass sees it.
+template <int KPL>
+__device__ __forceinline__ void w_stage_n(volatile int32_t* T, uint32_t m, int nk, const int32_t (&key)[KPL]) {
+    const int lane = wlane();
+    w_clear(T, m + 1);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    uint32_t* U = const_cast<uint32_t*>(reinterpret_cast<volatile uint32_t*>(T));
+    uint32_t ps[KPL];
+    bool placed[KPL];
+#pragma unroll
+    for (int q = 0; q < KPL; ++q) {
+        const bool act = lane + 64 * q < nk;
+        ps[q] = act ? pr_init(key[q], m) : 0u;
+        placed[q] = !act;
+    }
+    for (;;) {
+#pragma unroll
+        for (int q = 0; q < KPL; ++q)
+            if (!placed[q]) {
+                const uint32_t t = static_cast<uint32_t>(lane + 64 * q);
+                while (atomicMin(&U[pr_slot(ps[q])], t) < t) ps[q] = pr_next(ps[q], key[q], m);
+                placed[q] = true;
+            }
+        bool moved = false;
+#pragma unroll
+        for (int q = 0; q < KPL; ++q) {
+            const uint32_t t = static_cast<uint32_t>(lane + 64 * q);
+            if (static_cast<int>(t) < nk && reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps[q])] != t) {
+                ps[q] = pr_next(ps[q], key[q], m);
+                placed[q] = false;
+                moved = true;
+            }
+        }
+        if (!__ballot(moved)) break;
+    }
+#pragma unroll
+    for (int q = 0; q < KPL; ++q)
+        if (lane + 64 * q < nk) T[pr_slot(ps[q])] = key[q];
+}
+
 // The keys of T (mask + 1 <= 128 slots) in slot order into K; returns their count.
 __device__ __forceinline__ int w_compact(const volatile int32_t* T, uint32_t mask, volatile int32_t* K) {
     const int lane = wlane();
@@ -682,19 +724,25 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
     uint32_t prev_mask = m_first;
     for (int s = 0; s < nst; ++s) {
         const uint32_t m = st_mask[s];
-        // A stage of at most 64 keys (the first two or three) in one wave: the
-        // previous table compacted in slot order, then w_stage (the per-node
-        // sets' wave-level insert) — no block barrier inside the stage.
+        // A stage of at most 256 keys (the first three or four) in one wave:
+        // the previous table compacted in slot order, then w_stage_n (the
+        // per-node sets' wave-level insert, four keys per lane) — no block
+        // barrier inside the stage.
         const int nk_w = ub.ubef[st_run[s + 1]];  // the union's size after the stage
-        if (nk_w <= 64 && !(s == 0 && m == m_first)) {  // uniform
+        if (nk_w <= 256 && !(s == 0 && m == m_first)) {  // uniform
             if (tid < 64) {
                 const volatile int32_t* P = s == 0 ? reinterpret_cast<const volatile int32_t*>(ub.first_tab)
                                                    : reinterpret_cast<const volatile int32_t*>(T);
                 volatile int32_t* K = need;
                 const int n_old = w_compact(P, prev_mask, K);
                 const int f0 = ub.ubef[st_run[s]] - used0;
-                const int32_t kk = tid < n_old ? K[tid] : (tid < nk_w ? ub.fresh[f0 + tid - n_old] : 0);
-                w_stage(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk);
+                int32_t kk[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = tid + 64 * q;
+                    kk[q] = t < n_old ? K[t] : (t < nk_w ? ub.fresh[f0 + t - n_old] : 0);
+                }
+                w_stage_n<4>(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk);
             }
             __syncthreads();
             prev_mask = m;
