@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _ASAN_LIB = os.environ.get("GS_HOST_ASAN_LIB")
 LIB_PATH = _ASAN_LIB or os.path.join(_HERE, "libgraphsage_amd.so")
 
-GS_OK, GS_EINVAL, GS_ENOMEM, GS_EHIP, GS_ERANGE, GS_EEMPTY = range(6)
+GS_OK, GS_EINVAL, GS_ENOMEM, GS_EHIP, GS_ERANGE, GS_EEMPTY, GS_ELIMIT = range(7)
 GS_F32, GS_BF16 = 0, 1
 GS_AGG_MEAN, GS_AGG_MAX = 0, 1
 GS_SAMPLE_GCN, GS_SAMPLE_FULL = 1, 2
@@ -202,6 +202,13 @@ class LibraryMissing(RuntimeError):
     pass
 
 
+class DeviceLimit(RuntimeError):
+    """GS_ELIMIT: a device-path capacity (the device sampler's rejection
+    windows, walks or frontier tables) was too small for this batch.  The
+    batch itself is valid and the caller's stream state is untouched, so the
+    host path computes the same result."""
+
+
 def lib():
     """Load (once) and return the configured ctypes library."""
     global _lib
@@ -239,6 +246,8 @@ def check(rc, what=""):
         raise IndexError(msg)
     if rc == GS_ENOMEM:
         raise MemoryError(msg)
+    if rc == GS_ELIMIT:
+        raise DeviceLimit(msg)
     raise RuntimeError(msg)
 
 

@@ -14,7 +14,11 @@
 #include <immintrin.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -59,10 +63,36 @@ class Team {
     }
 
     // The caller takes the job's remaining tasks too, then waits for the rest
-    // (all of them have returned when this does).
+    // (all of them have returned when this does).  A task that threw counts
+    // as returned; the first such exception is rethrown here, once every task
+    // is done (nothing of the job is still running when the caller unwinds).
+    // A job whose tasks make no progress for kStallSeconds is a bug (a task
+    // that never returns): it is reported on stderr and the process aborts,
+    // rather than hanging silently or unwinding while helpers still run.
+    static constexpr int kStallSeconds = 120;
     void wait() {
         work();
-        while (done_.load(std::memory_order_acquire) < n_) _mm_pause();
+        int seen = done_.load(std::memory_order_acquire);
+        auto t_seen = std::chrono::steady_clock::now();
+        for (uint64_t spin = 0; seen < n_; ++spin) {
+            _mm_pause();
+            const int now = done_.load(std::memory_order_acquire);
+            if (now != seen) {
+                seen = now;
+                t_seen = std::chrono::steady_clock::now();
+            } else if ((spin & 0xFFFFF) == 0xFFFFF &&
+                       std::chrono::steady_clock::now() - t_seen > std::chrono::seconds(kStallSeconds)) {
+                std::fprintf(stderr, "graphsage_amd: sampler helper team stalled: %d of %d tasks done, no progress "
+                                     "for %d s; aborting\n", seen, n_, kStallSeconds);
+                std::abort();
+            }
+        }
+        std::exception_ptr e;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            std::swap(e, err_);
+        }
+        if (e) std::rethrow_exception(e);
     }
 
     // start() + wait(): the caller is one more worker.
@@ -80,7 +110,12 @@ class Team {
                 if (next_ >= n_) return;
                 i = next_++;
             }
-            fn_(i);  // fn_ is replaced only after every task has returned
+            try {
+                fn_(i);  // fn_ is replaced only after every task has returned
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!err_) err_ = std::current_exception();
+            }
             done_.fetch_add(1, std::memory_order_release);
         }
     }
@@ -109,6 +144,7 @@ class Team {
 
     std::vector<std::thread> th_;
     std::function<void(int)> fn_;
+    std::exception_ptr err_;  // the job's first task exception (guarded by mu_)
     int n_ = 0, next_ = 0;  // guarded by mu_
     std::atomic<int> done_{0};
     std::atomic<uint64_t> gen_{0};

@@ -1073,12 +1073,17 @@ int64_t pos_now(gs_dsampler* ds, hipStream_t st) {
 void check_status(int status) {
     if (!status) return;
     if (status & kStEmpty) gs::fail(GS_EEMPTY, "empty neighbourhood");
+    // invariant breaks: loud, never retried
+    if (status & kStOrder) gs::fail(GS_EINVAL, "device sampler: block states out of order");
+    if (status & kStSpin)
+        gs::fail(GS_EINVAL, "device sampler: a set-table insert exceeded its probe bound (table invariant broken)");
+    // capacities of the device path (the batch is valid; the host sampler takes it)
     if (status & kStWindow)
-        gs::fail(GS_ERANGE, "device sampler: a rejection count fell outside its block window (resample on the host)");
-    if (status & kStWords) gs::fail(GS_ERANGE, "device sampler: a walk ran past its loaded words");
-    if (status & kStTable) gs::fail(GS_ERANGE, "device sampler: frontier union outgrew the device table");
-    if (status & kStOrder) gs::fail(GS_ERANGE, "device sampler: block states out of order");
-    if (status & kStSize) gs::fail(GS_ERANGE, "device sampler: frontier outgrew its bound");
+        gs::fail(GS_ELIMIT, "device sampler: a rejection count fell outside its block window (batch too large "
+                            "for the device windows; sample it on the host)");
+    if (status & kStWords) gs::fail(GS_ELIMIT, "device sampler: a walk ran past its loaded words");
+    if (status & kStTable) gs::fail(GS_ELIMIT, "device sampler: frontier union outgrew the device table");
+    if (status & kStSize) gs::fail(GS_ELIMIT, "device sampler: frontier outgrew its bound");
     gs::fail(GS_EINVAL, "device sampler: status " + std::to_string(status));
 }
 

@@ -24,6 +24,15 @@ constexpr int kStTable = 4;    // a frontier union outgrew the device table
 constexpr int kStEmpty = 8;    // empty neighbourhood with GS_SAMPLE_FAIL_EMPTY
 constexpr int kStSize = 16;    // a frontier outgrew its preallocated bound
 constexpr int kStOrder = 32;   // block states lost their order (never expected)
+constexpr int kStSpin = 64;    // a table insert exceeded its probe / displacement bound (never expected)
+
+// Probe steps one key may take in a table of mask + 1 slots before the insert
+// gives up (kStSpin): CPython's probe sequence (10 linear slots, then
+// i = 5 i + 1 + perturb, full period once perturb is 0) reaches every slot
+// within (mask + 1) + 7 * 10 steps, so a table that is at most 3/5 full never
+// gets near this; only a broken invariant (more keys than free slots) does,
+// and it then fails loudly instead of spinning the kernel forever.
+__host__ __device__ constexpr uint32_t probe_cap(uint32_t mask) { return 2u * (mask + 1u) + 256u; }
 
 struct DevGraph {
     const int64_t* row_ptr;

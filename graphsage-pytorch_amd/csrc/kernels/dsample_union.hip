@@ -77,11 +77,13 @@ __device__ __forceinline__ void w_clear(volatile int32_t* T, uint32_t nslots) {
 
 // set_add_entry (no dummies): the first slot of the probe sequence holding
 // the key (already present: false) or empty (the key goes there: true).
-__device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_t key) {
+// More than probe_cap(mask) probe groups (a full table: never expected) set
+// `bad` and return false.
+__device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_t key, bool& bad) {
     const int lane = wlane();
     uint32_t i = static_cast<uint32_t>(key) & mask;
     uint32_t perturb = static_cast<uint32_t>(key);
-    for (;;) {
+    for (uint32_t step = 0; step < probe_cap(mask); ++step) {
         const uint32_t probes = (i + 9 <= mask) ? 9u : 0u;
         const bool in = static_cast<uint32_t>(lane) <= probes;
         const int32_t x = in ? T[i + lane] : 0;
@@ -95,6 +97,8 @@ __device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_
         perturb >>= 5;
         i = (i * 5 + 1 + perturb) & mask;
     }
+    bad = true;
+    return false;
 }
 
 // One table stage of distinct keys: the table is cleared to mask m and lane
@@ -106,70 +110,98 @@ __device__ __forceinline__ bool w_add(volatile int32_t* T, uint32_t mask, int32_
 // priority and moves on when a higher priority holds it or later takes it;
 // after the divergent claims reconverge, every lane re-reads its slot, so a
 // round needs no barrier.  Then each slot gets its key.
-__device__ __forceinline__ void w_stage(volatile int32_t* T, uint32_t m, int nk, int32_t key) {
+//
+// Termination: a slot's value only decreases and a key only moves forward,
+// so the stage ends once every key has a slot — provided the table has a
+// free slot for each (nk <= 3/5 (m + 1) by the callers' resize rules).  Each
+// key's probe steps are bounded by probe_cap(m) anyway: past it the key
+// stops (its lane's `bad` is set, its slot left unwritten) and the stage
+// ends, so a broken invariant surfaces as a status bit, never as a hang.
+__device__ __forceinline__ void w_stage(volatile int32_t* T, uint32_t m, int nk, int32_t key, bool& bad) {
     const int lane = wlane();
     w_clear(T, m + 1);  // -1 = priority 0xFFFFFFFF: empty
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the clear before the claims (one wave: LDS keeps its order)
     uint32_t* U = const_cast<uint32_t*>(reinterpret_cast<volatile uint32_t*>(T));
     const bool act = lane < nk;
     const uint32_t t = static_cast<uint32_t>(lane);
+    const uint32_t cap = probe_cap(m);
     uint32_t ps = act ? pr_init(key, m) : 0u;
-    bool placed = !act;
+    uint32_t steps = 0;
+    bool placed = !act, stop = !act;
     for (;;) {
         if (!placed) {
-            while (atomicMin(&U[pr_slot(ps)], t) < t) ps = pr_next(ps, key, m);
+            while (atomicMin(&U[pr_slot(ps)], t) < t && ++steps < cap) ps = pr_next(ps, key, m);
             placed = true;
+            if (steps >= cap) stop = true;
         }
-        const uint32_t h = act ? reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps)] : t;
+        const uint32_t h = stop ? t : reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps)];
         if (h != t) {
             ps = pr_next(ps, key, m);
             placed = false;
+            if (++steps >= cap) {
+                stop = true;
+                placed = true;
+            }
         }
         if (!__ballot(!placed)) break;
     }
-    if (act) T[pr_slot(ps)] = key;
+    if (act && stop) bad = true;
+    if (act && !stop) T[pr_slot(ps)] = key;
 }
 
 // w_stage with up to 64 * KPL keys: lane l's q-th key has priority l + 64 q
 // (the frontier union's small stages).  A lane's later key may displace its
-// earlier one within a claim pass; the re-read after the pass sees it.
+// earlier one within a claim pass; the re-read after the pass sees it.  The
+// probe bound is per key, as in w_stage.
 template <int KPL>
-__device__ __forceinline__ void w_stage_n(volatile int32_t* T, uint32_t m, int nk, const int32_t (&key)[KPL]) {
+__device__ __forceinline__ void w_stage_n(volatile int32_t* T, uint32_t m, int nk, const int32_t (&key)[KPL],
+                                          bool& bad) {
     const int lane = wlane();
     w_clear(T, m + 1);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     uint32_t* U = const_cast<uint32_t*>(reinterpret_cast<volatile uint32_t*>(T));
-    uint32_t ps[KPL];
-    bool placed[KPL];
+    const uint32_t cap = probe_cap(m);
+    uint32_t ps[KPL], steps[KPL];
+    bool placed[KPL], stop[KPL];
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
         const bool act = lane + 64 * q < nk;
         ps[q] = act ? pr_init(key[q], m) : 0u;
         placed[q] = !act;
+        stop[q] = !act;
+        steps[q] = 0;
     }
     for (;;) {
 #pragma unroll
         for (int q = 0; q < KPL; ++q)
             if (!placed[q]) {
                 const uint32_t t = static_cast<uint32_t>(lane + 64 * q);
-                while (atomicMin(&U[pr_slot(ps[q])], t) < t) ps[q] = pr_next(ps[q], key[q], m);
+                while (atomicMin(&U[pr_slot(ps[q])], t) < t && ++steps[q] < cap) ps[q] = pr_next(ps[q], key[q], m);
                 placed[q] = true;
+                if (steps[q] >= cap) stop[q] = true;
             }
         bool moved = false;
 #pragma unroll
         for (int q = 0; q < KPL; ++q) {
             const uint32_t t = static_cast<uint32_t>(lane + 64 * q);
-            if (static_cast<int>(t) < nk && reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps[q])] != t) {
+            if (!stop[q] && reinterpret_cast<volatile uint32_t*>(T)[pr_slot(ps[q])] != t) {
                 ps[q] = pr_next(ps[q], key[q], m);
-                placed[q] = false;
-                moved = true;
+                if (++steps[q] >= cap) {
+                    stop[q] = true;
+                } else {
+                    placed[q] = false;
+                    moved = true;
+                }
             }
         }
         if (!__ballot(moved)) break;
     }
 #pragma unroll
     for (int q = 0; q < KPL; ++q)
-        if (lane + 64 * q < nk) T[pr_slot(ps[q])] = key[q];
+        if (lane + 64 * q < nk) {
+            if (stop[q]) bad = true;
+            else T[pr_slot(ps[q])] = key[q];
+        }
 }
 
 // The keys of T (mask + 1 <= 128 slots) in slot order into K; returns their count.
@@ -187,11 +219,12 @@ __device__ __forceinline__ int w_compact(const volatile int32_t* T, uint32_t mas
 }
 
 // set_table_resize: smallest power of two > minused, keys re-inserted in slot order.
-__device__ __forceinline__ uint32_t w_resize(volatile int32_t* T, uint32_t mask, int minused, volatile int32_t* K) {
+__device__ __forceinline__ uint32_t w_resize(volatile int32_t* T, uint32_t mask, int minused, volatile int32_t* K,
+                                             bool& bad) {
     const int n = w_compact(T, mask, K);
     uint32_t ns = 8;
     while (ns <= static_cast<uint32_t>(minused)) ns <<= 1;
-    w_stage(T, ns - 1, n, K[min(wlane(), kSmallSet - 1)]);
+    w_stage(T, ns - 1, n, K[min(wlane(), kSmallSet - 1)], bad);
     return ns - 1;
 }
 
@@ -215,6 +248,7 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
     const int d = hb.deg[r];
     uint32_t mask = 7;
     int used = 0;
+    bool bad = false;  // a stage or add past its probe bound (kStSpin)
     w_clear(T, 8);
     if (k > 0 && d >= k) {
         // set(list): set_add_key per item in result order, resizing to used * 4
@@ -234,7 +268,7 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
             }
             const int src = min(max(i0 + lane - n_old, 0), 63);
             const int32_t fresh = __shfl(mine, src, 64);
-            w_stage(T, mask, n_old + (i1 - i0), lane < n_old ? K[min(lane, kSmallSet - 1)] : fresh);
+            w_stage(T, mask, n_old + (i1 - i0), lane < n_old ? K[min(lane, kSmallSet - 1)] : fresh, bad);
             used = i1;
             n_old = 0;
             i0 = i1;
@@ -251,7 +285,7 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
         if (used * 5 >= 21) nm = mask_for(2 * used);
         if (nm != mask) {
             const int m = w_compact(T, mask, K);
-            w_stage(T, nm, m, K[min(lane, kSmallSet - 1)]);
+            w_stage(T, nm, m, K[min(lane, kSmallSet - 1)], bad);
             mask = nm;
         }
     } else {
@@ -270,18 +304,23 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
             if (lane < d) T[g.slot[rs + lane]] = g.col[rs + lane];
         } else {
             // the set's keys in its iteration order, all distinct: one stage
-            w_stage(T, mask, d, lane < d ? g.col[rs + lane] : 0);
+            w_stage(T, mask, d, lane < d ? g.col[rs + lane] : 0, bad);
         }
     }
     // | set([node]): set_merge with a one-element set
-    if (static_cast<uint32_t>(used + 1) * 5 >= mask * 3) mask = w_resize(T, mask, (used + 1) * 2, K);
+    if (static_cast<uint32_t>(used + 1) * 5 >= mask * 3) mask = w_resize(T, mask, (used + 1) * 2, K, bad);
     if (used == 0 && mask == 7) {
         w_clear(T, 8);
         if (lane == 0) T[v & 7] = v;
         used = 1;
-    } else if (w_add(T, mask, v)) {
+    } else if (w_add(T, mask, v, bad)) {
         ++used;
-        if (static_cast<uint32_t>(used) * 5 >= mask * 3) mask = w_resize(T, mask, used > 50000 ? used * 2 : used * 4, K);
+        if (static_cast<uint32_t>(used) * 5 >= mask * 3)
+            mask = w_resize(T, mask, used > 50000 ? used * 2 : used * 4, K, bad);
+    }
+    if (__ballot(bad)) {  // a broken table invariant: report it, never spin
+        if (lane == 0) atomicOr(&c->status, kStSpin);
+        return;
     }
     // iteration order, marks
     const uint64_t E = static_cast<uint64_t>(static_cast<uint32_t>(c->epoch + 1)) << 32;
@@ -349,8 +388,15 @@ __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) { return __atomi
 
 template <typename Claim, typename Held>
 __device__ __forceinline__ int settle_keys(uint32_t mask, int t0, int t1, const int32_t (&key)[kKPT],
-                                           uint32_t (&ps)[kKPT], Claim claim, Held held, int64_t* first_round) {
+                                           uint32_t (&ps)[kKPT], Claim claim, Held held, int64_t* first_round,
+                                           bool& bad) {
     const int base = t0 + static_cast<int>(threadIdx.x);
+    // probe steps of this thread's keys together: past the bound (a table
+    // with fewer free slots than keys — never expected) the thread stops
+    // claiming and reports itself settled, so the block leaves the loop and
+    // the caller raises kStSpin instead of spinning forever
+    const uint32_t cap = kKPT * probe_cap(mask);
+    uint32_t steps = 0;
     bool placed[kKPT];
 #pragma unroll
     for (int q = 0; q < kKPT; ++q) placed[q] = false;
@@ -361,15 +407,17 @@ __device__ __forceinline__ int settle_keys(uint32_t mask, int t0, int t1, const 
 #pragma unroll
             for (int q = 0; q < kKPT; ++q) {
                 const int t = base + 1024 * q;
-                if (t < t1) {
+                if (t < t1 && !bad) {
                     if (placed[q] && held(pr_slot(ps[q])) != static_cast<uint32_t>(t)) {
                         ps[q] = pr_next(ps[q], key[q], mask);
                         placed[q] = false;
                     }
                     if (!placed[q]) {
-                        while (!claim(pr_slot(ps[q]), static_cast<uint32_t>(t))) ps[q] = pr_next(ps[q], key[q], mask);
+                        while (!claim(pr_slot(ps[q]), static_cast<uint32_t>(t)) && ++steps < cap)
+                            ps[q] = pr_next(ps[q], key[q], mask);
                         placed[q] = true;
                         moved = true;
+                        if (++steps >= cap) bad = true;
                     }
                 }
             }
@@ -380,7 +428,7 @@ __device__ __forceinline__ int settle_keys(uint32_t mask, int t0, int t1, const 
 #pragma unroll
         for (int q = 0; q < kKPT; ++q) {
             const int t = base + 1024 * q;
-            if (t < t1) any |= held(pr_slot(ps[q])) != static_cast<uint32_t>(t);
+            if (t < t1 && !bad) any |= held(pr_slot(ps[q])) != static_cast<uint32_t>(t);
         }
         if (rounds == 0 && threadIdx.x == 0 && first_round)
             *first_round = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
@@ -390,10 +438,10 @@ __device__ __forceinline__ int settle_keys(uint32_t mask, int t0, int t1, const 
 }
 
 __device__ __forceinline__ int settle(uint32_t* T, uint32_t mask, int nk, const int32_t (&key)[kKPT],
-                                      uint32_t (&ps)[kKPT], int64_t& first_round) {
+                                      uint32_t (&ps)[kKPT], int64_t& first_round, bool& bad) {
     return settle_keys(
         mask, 0, nk, key, ps, [&](uint32_t slot, uint32_t t) { return atomicMin(&T[slot], t) > t; },
-        [&](uint32_t slot) { return lds_load(&T[slot]); }, &first_round);
+        [&](uint32_t slot) { return lds_load(&T[slot]); }, &first_round, bad);
 }
 
 // The next frontier in the final table's slot order, each key's position in
@@ -491,10 +539,10 @@ __device__ __forceinline__ uint32_t t16_load(const uint32_t* T, uint32_t slot) {
 
 // settle() on the uint16 table, keys t0 .. t1-1.
 __device__ __forceinline__ void settle16(uint32_t* T, uint32_t mask, int t0, int t1, const int32_t (&key)[kKPT],
-                                         uint32_t (&ps)[kKPT]) {
+                                         uint32_t (&ps)[kKPT], bool& bad) {
     (void)settle_keys(
         mask, t0, t1, key, ps, [&](uint32_t slot, uint32_t t) { return t16_claim(T, slot, t); },
-        [&](uint32_t slot) { return t16_load(T, slot); }, nullptr);
+        [&](uint32_t slot) { return t16_load(T, slot); }, nullptr, bad);
 }
 
 __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop, int gcn,
@@ -579,8 +627,12 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
                 key[q] = kk;
                 ps[q] = p0;
             }
-            settle16(T, m, t0, t1, key, ps);
-            __syncthreads();
+            bool bad = false;
+            settle16(T, m, t0, t1, key, ps, bad);
+            if (__syncthreads_or(bad)) {
+                if (tid == 0) atomicOr(&c->status, kStSpin);
+                return;
+            }
         }
         if (tid == 0 && s < 12) c->dbg[10 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
         prev_mask = m;
@@ -742,9 +794,15 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
                     const int t = tid + 64 * q;
                     kk[q] = t < n_old ? K[t] : (t < nk_w ? ub.fresh[f0 + t - n_old] : 0);
                 }
-                w_stage_n<4>(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk);
+                bool bad = false;
+                w_stage_n<4>(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk, bad);
+                if (__ballot(bad) && tid == 0) s_bad = 2;
             }
             __syncthreads();
+            if (s_bad) {  // uniform
+                if (tid == 0) atomicOr(&c->status, kStSpin);
+                return;
+            }
             prev_mask = m;
             continue;
         }
@@ -796,7 +854,12 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         __syncthreads();
         int64_t first_round = 0;
         if (tid == 0 && s < 12) c->dbg[8 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());
-        const int rounds = settle(T, m, nk, key, ps, first_round);
+        bool bad = false;
+        const int rounds = settle(T, m, nk, key, ps, first_round, bad);
+        if (__syncthreads_or(bad)) {
+            if (tid == 0) atomicOr(&c->status, kStSpin);
+            return;
+        }
         if (tid == 0 && s < 12) {
             c->dbg[9 + 4 * s] = first_round;
             c->dbg[10 + 4 * s] = static_cast<int64_t>(__builtin_amdgcn_s_memrealtime());

@@ -228,6 +228,9 @@ struct gs_runner {
         double sample_s = 0;
     };
     bool devmode = false;
+    // guards dstreams' queues (nq, qb, next, counted): gs_runner_release and
+    // gs_runner_progress may be called from another thread than gs_runner_run
+    std::recursive_mutex dev_mu;
     std::vector<DevStream> dstreams;
     int32_t* roots_dev = nullptr;
     int64_t n_dpack = 0, dcap = 0;
@@ -372,6 +375,7 @@ void gs_runner::pull(int64_t b, int slot_id) {
 // Device sampler: enqueue stream w's next batches, up to dev_depth queued.
 void gs_runner::dev_enqueue(int w) {
     using namespace gs;
+    std::lock_guard<std::recursive_mutex> lk(dev_mu);
     DevStream& d = dstreams[w];
     while (d.nq < dev_depth) {
         const int64_t b = d.next;
@@ -393,6 +397,7 @@ void gs_runner::dev_enqueue(int w) {
 // block == false: false while its sampling is still running.
 bool gs_runner::dev_take(int64_t b, bool block) {
     using namespace gs;
+    std::lock_guard<std::recursive_mutex> lk(dev_mu);
     DevStream& d = dstreams[b % cfg.n_streams];
     const bool queued = d.nq > 0 && d.qb[0] == b;
     if (!block && (!queued || !dsampler_run_ready(d.ds, d.qrun[0]))) return false;  // not enqueued yet (held) or running
@@ -424,6 +429,7 @@ bool gs_runner::dev_take(int64_t b, bool block) {
 
 // Device sampler: count finished sampling runs (progress()).
 void gs_runner::dev_poll() {
+    std::lock_guard<std::recursive_mutex> lk(dev_mu);
     for (auto& d : dstreams)
         for (int q = 0; q < d.nq; ++q)
             if (!d.counted[q] && gs::dsampler_run_ready(d.ds, d.qrun[q])) {
@@ -968,6 +974,15 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         r->stats.max_step_s = std::max(r->stats.max_step_s, secs(t0, t4));
     }
     unwind.armed = false;
+    // GS_FUSED_SGD: a grid barrier that gave up ran its SGD on partial sums;
+    // the run fails here (after its steps drained) instead of training on
+    // with corrupted parameters
+    if (fuse_update.t && n_steps > 0) {
+        hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+        if (trainer_barrier_failed(r->cfg.trainer))
+            fail(GS_EHIP, "runner: a fused clip+SGD launch's grid barrier timed out (GS_FUSED_SGD); the parameters "
+                          "of that step are not trustworthy");
+    }
     GS_API_END
 }
 

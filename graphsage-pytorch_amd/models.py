@@ -382,6 +382,11 @@ class GraphSage(nn.Module):
         ds.set_rng(rng)
         try:
             pack, sizes, offs, used = ds.run(roots)
+        except _lib.DeviceLimit:
+            # the batch outgrew a device capacity (its rejection windows widen
+            # with the frontier): `rng` is untouched, so the host sampler
+            # draws the same sample from the same state
+            return None
         except IndexError:
             # MAX over an empty neighbourhood: the reference raises after its
             # sampling consumed the stream (models.py:321-325)
@@ -415,11 +420,11 @@ class GraphSage(nn.Module):
                                "cuda tensor (the reference's --cuda path, main.py:52)")
         if self.agg_func not in ("MEAN", "MAX"):
             raise ValueError(f"agg_func must be 'MEAN' or 'MAX', got {self.agg_func!r}")
-        if self.device_sampler:
-            ds = self._draw_device(roots, X.device)
-        elif self.sampler_helpers > 0 and self.agg_func == "MEAN":
+        # the device sampler returns None for a batch past its capacities
+        ds = self._draw_device(roots, X.device) if self.device_sampler else None
+        if ds is None and self.sampler_helpers > 0 and self.agg_func == "MEAN":
             ds = self._draw_pack(roots, X.device)
-        else:
+        elif ds is None:
             s = self._draw(roots, self.fanouts)
             if self.agg_func == "MAX":
                 for j in range(1, s.n_hops + 1):

@@ -30,6 +30,10 @@ extern "C" {
 #define GS_ERANGE 4  /* "Sample larger than population" / id out of range          */
 #define GS_EEMPTY 5  /* MAX over an empty neighbourhood (reference: IndexError,
                         models.py:321-325)                                       */
+#define GS_ELIMIT 6  /* a device-path capacity was exceeded (device sampler: a
+                        rejection window, walk or frontier table too small for
+                        this batch); the host path computes the same result, and
+                        the stream state the caller holds is untouched            */
 
 const char* gs_last_error(void);
 const char* gs_version(void);

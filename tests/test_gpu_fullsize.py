@@ -33,6 +33,7 @@ import pytest
 import torch
 
 import oracle
+from tests.fullsize_parity import check_embeddings_vs_oracle, check_pack_vs_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -104,6 +105,43 @@ def test_fullsize_runner_vs_oracle_train_steps(wl, adj, native):
         torch.testing.assert_close(sd[f"sage_layer{i}.weight"].cpu(), W[i - 1].detach(), atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(sd["layer.0.weight"].cpu(), cw.detach(), atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(sd["layer.0.bias"].cpu(), cb.detach(), atol=1e-4, rtol=1e-4)
+
+
+def test_fullsize_first_batch_indices_and_embeddings_vs_oracle(wl, adj):
+    """North_star's parity bar at the headline size, per root of the first
+    batch: the runner's pack (its sampler threads' gs_sample_pack_run_multi_team)
+    holds exactly the oracle's sampled sets at both hops, the |L1| frontier in
+    its CPython set order and the oracle's |L0| (tests/fullsize_parity.py);
+    the drop-in module's forward on the same stream equals
+    oracle.forward_dense within 1e-5 (fp32)."""
+    roots = wl["batches"][0]
+    seed = train.rank_seed(SEED, 0, 0)
+    hops = check_pack_vs_oracle(wl["graph"], adj, roots, FAN, seed)
+    W = [w.to(DEV) for w in train.reference_init(2, F, H, C, False, SEED)[0]]
+    check_embeddings_vs_oracle(models, wl["graph"], wl["X"], wl["X"].cpu(), hops, roots, FAN, W, seed, DEV)
+
+
+def test_fullsize_device_sampler_past_capacity_falls_back(wl):
+    """A forward batch too large for the device sampler's windows / tables
+    (16 Ki roots at fanouts 25, 10: the hop-1 union alone outgrows the
+    device table) raises DeviceLimit inside GraphSage(device_sampler=True),
+    which then samples on the host from the untouched stream: the same
+    embeddings and `random` state as the host-sampler module."""
+    roots = np.arange(16384, dtype=np.int64) * 127 % wl["n"]
+    roots = roots[wl["graph"].degrees()[roots] > 0]
+    W = [w.to(DEV) for w in train.reference_init(2, F, H, C, False, SEED)[0]]
+    out = []
+    for dev_s in (False, True):
+        rng = sampler.RNG(11)
+        m = models.GraphSage(2, F, H, wl["X"], wl["graph"], DEV, fanouts=FAN, rng=rng, device_sampler=dev_s)
+        with torch.no_grad():
+            for i in (1, 2):
+                getattr(m, f"sage_layer{i}").weight.copy_(W[i - 1])
+            out.append((m(roots).cpu(), rng.getstate()))
+    (e0, (mt0, p0)), (e1, (mt1, p1)) = out
+    assert torch.equal(e0, e1)
+    assert p0 == p1
+    np.testing.assert_array_equal(mt0, mt1)
 
 
 def test_fullsize_runner_is_deterministic(wl, native):

@@ -28,10 +28,12 @@ import pytest
 import torch
 
 import oracle
+from tests.fullsize_parity import check_embeddings_vs_oracle, check_pack_vs_oracle
 
 pytestmark = pytest.mark.gpu
 
 train = importlib.import_module("graphsage-pytorch_amd.train")
+models = importlib.import_module("graphsage-pytorch_amd.models")
 ops = importlib.import_module("graphsage-pytorch_amd.hip_ops")
 DEV = torch.device("cuda", 0)
 SEED, F, H, C, B, FAN, S, SCALE, PAIRS = 824, 128, 128, 16, 512, [25, 10], 2, 24, 160_000_000
@@ -89,11 +91,28 @@ def native(wl):
     return _run(wl)
 
 
-def test_rmat16m_runner_vs_oracle_train_steps(wl, native):
-    tr, losses, sizes = native
+@pytest.fixture(scope="module")
+def adj(wl):
     t0 = time.time()
-    adj = oracle.Adjacency(wl["src"], wl["dst"], wl["n"], sort_device=DEV)
+    a = oracle.Adjacency(wl["src"], wl["dst"], wl["n"], sort_device=DEV)
     print(f"[rmat16m] oracle adjacency index {time.time() - t0:.1f} s", flush=True)
+    return a
+
+
+def test_rmat16m_first_batch_indices_and_embeddings_vs_oracle(wl, adj):
+    """Per root of the first batch at the 16M size: the runner's pack holds
+    exactly the oracle's sampled sets at both hops, the |L1| frontier in its
+    CPython set order and the oracle's |L0|; the module forward on the same
+    stream equals oracle.forward_dense within 1e-5 (tests/fullsize_parity.py)."""
+    roots = wl["batches"][0]
+    seed = train.rank_seed(SEED, 0, 0)
+    hops = check_pack_vs_oracle(wl["graph"], adj, roots, FAN, seed)
+    W = [w.to(DEV) for w in train.reference_init(2, F, H, C, False, SEED)[0]]
+    check_embeddings_vs_oracle(models, wl["graph"], wl["X"], _Rows(wl["X"]), hops, roots, FAN, W, seed, DEV)
+
+
+def test_rmat16m_runner_vs_oracle_train_steps(wl, native, adj):
+    tr, losses, sizes = native
     X = _Rows(wl["X"])
     labels = wl["labels"].cpu().long()
     sage_w, cw, cb = train.reference_init(2, F, H, C, False, SEED)

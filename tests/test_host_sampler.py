@@ -421,3 +421,19 @@ def test_team_pack_equals_single_thread(gs, helpers, fan, group):
             assert r1.getstate()[0].tolist() == r2.getstate()[0].tolist() and r1.getstate()[1] == r2.getstate()[1]
     finally:
         L.lib().gs_team_destroy(team)
+
+
+@pytest.mark.parametrize("scale,pairs,batch", [(12, 40_000, 64), (16, 600_000, 512)])
+def test_runner_pack_matches_oracle_per_root(gs, scale, pairs, batch):
+    """The pack the runner's sampler threads write (gs_sample_pack_run_multi_team
+    with a helper team) decoded per root and per hop against
+    oracle.sample_layers on the same stream — the check the GPU suite runs at
+    the rmat2m / rmat16m sizes (tests/fullsize_parity.py)."""
+    from tests.fullsize_parity import check_pack_vs_oracle
+    src, dst = gs.rmat_pairs(scale, pairs, seed=5)
+    n = 1 << scale
+    graph = gs.CSRGraph.from_pairs(src, dst, n)
+    adj = Adjacency(src, dst, n)
+    cands = np.nonzero(graph.degrees() > 0)[0]
+    roots = cands[np.random.default_rng(3).permutation(len(cands))[:batch]]
+    check_pack_vs_oracle(graph, adj, roots, [25, 10], seed=77)
