@@ -80,9 +80,20 @@ struct MT19937 {
         return y;
     }
 
-    // Recompute out[] from mt[] (after setstate).
+    // Recompute out[] from mt[] (after setstate and every twist): the
+    // tempering of 8 words per AVX2 instruction sequence.
     void refresh() {
-        for (int i = 0; i < N; ++i) out[i] = temper(mt[i]);
+        const __m256i b = _mm256_set1_epi32(static_cast<int32_t>(0x9d2c5680u));
+        const __m256i c = _mm256_set1_epi32(static_cast<int32_t>(0xefc60000u));
+        static_assert(N % 8 == 0, "whole vectors");
+        for (int i = 0; i < N; i += 8) {
+            __m256i y = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(mt + i));
+            y = _mm256_xor_si256(y, _mm256_srli_epi32(y, 11));
+            y = _mm256_xor_si256(y, _mm256_and_si256(_mm256_slli_epi32(y, 7), b));
+            y = _mm256_xor_si256(y, _mm256_and_si256(_mm256_slli_epi32(y, 15), c));
+            y = _mm256_xor_si256(y, _mm256_srli_epi32(y, 18));
+            _mm256_store_si256(reinterpret_cast<__m256i*>(out + i), y);
+        }
         ext = false;
     }
 
@@ -109,20 +120,35 @@ struct MT19937 {
         }
     }
 
-    // genrand_uint32's block regeneration, written as three branch-free loops
-    // the compiler vectorises (the recurrence distances 1, 397 and 227 allow it).
-    void twist() {
+    // genrand_uint32's block regeneration, eight words per AVX2 step: the
+    // recurrence distances (1 ahead, 397 ahead, then 227 behind) all exceed
+    // or precede the 8-word vector, so each vector reads only words that are
+    // final for this twist (old mt[kk + 1 ..], new mt[kk - 227 ..]).
+    static inline __m256i twist8(__m256i cur, __m256i nxt, __m256i far) {
+        const __m256i up = _mm256_set1_epi32(static_cast<int32_t>(0x80000000u));
+        const __m256i lo = _mm256_set1_epi32(0x7fffffff);
+        const __m256i a = _mm256_set1_epi32(static_cast<int32_t>(0x9908b0dfu));
+        const __m256i one = _mm256_set1_epi32(1);
+        const __m256i y = _mm256_or_si256(_mm256_and_si256(cur, up), _mm256_and_si256(nxt, lo));
+        const __m256i mag = _mm256_and_si256(_mm256_cmpeq_epi32(_mm256_and_si256(y, one), one), a);
+        return _mm256_xor_si256(_mm256_xor_si256(far, _mm256_srli_epi32(y, 1)), mag);
+    }
+    static inline uint32_t twist1(uint32_t cur, uint32_t nxt, uint32_t far) {
         constexpr uint32_t A = 0x9908b0dfu;
-        for (int kk = 0; kk < N - M; ++kk) {
-            const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + M] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
-        }
-        for (int kk = N - M; kk < N - 1; ++kk) {
-            const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
-            mt[kk] = mt[kk + (M - N)] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
-        }
-        const uint32_t y = (mt[N - 1] & 0x80000000u) | (mt[0] & 0x7fffffffu);
-        mt[N - 1] = mt[M - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+        const uint32_t y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+        return far ^ (y >> 1) ^ ((0u - (y & 1u)) & A);
+    }
+    void twist() {
+        auto ld = [&](int i) { return _mm256_loadu_si256(reinterpret_cast<const __m256i*>(mt + i)); };
+        int kk = 0;
+        for (; kk + 8 <= N - M; kk += 8)  // 0 .. 223
+            _mm256_storeu_si256(reinterpret_cast<__m256i*>(mt + kk), twist8(ld(kk), ld(kk + 1), ld(kk + M)));
+        for (; kk < N - M; ++kk) mt[kk] = twist1(mt[kk], mt[kk + 1], mt[kk + M]);
+        for (; kk + 8 <= N - 1; kk += 8)  // 227 .. 618
+            _mm256_storeu_si256(reinterpret_cast<__m256i*>(mt + kk),
+                                twist8(ld(kk), ld(kk + 1), ld(kk + (M - N))));
+        for (; kk < N - 1; ++kk) mt[kk] = twist1(mt[kk], mt[kk + 1], mt[kk + (M - N)]);
+        mt[N - 1] = twist1(mt[N - 1], mt[0], mt[M - 1]);
         refresh();
         index = 0;
     }
@@ -372,6 +398,54 @@ inline bool pool_fast(MT19937& rng, int64_t n, int64_t k, OutT* out, int32_t* po
     return true;
 }
 
+// Pool branch for k <= 16 from a 32-word window: the accepted word of draw i
+// is the first word at or after the previous draw's whose top bits,
+// (w >> clz(n - i)), fall below n - i.  Each draw's accept mask over the 32
+// words is a few vector shifts and compares, independent of the other draws,
+// so the only serial chain left is one tzcnt per draw (the per-word loop of
+// pool_fast carries i -> bound -> shift -> compare through every word).
+// Returns false, having consumed nothing, when the 32 words run out.
+template <class OutT>
+inline bool pool_fast_window(MT19937& rng, int64_t n, int64_t k, OutT* out, int32_t* pool) {
+    static_assert(MT19937::kExt >= 32, "the window reads 32 words");
+    if (k > 16) return false;
+    if (rng.index >= MT19937::N) rng.twist();
+    if (rng.index + 32 > MT19937::N && !rng.ext) rng.extend();
+    const uint32_t nn = static_cast<uint32_t>(n);
+    const uint32_t* wp = rng.out + rng.index;
+    __m256i w[4];
+#pragma GCC unroll 4
+    for (int q = 0; q < 4; ++q) w[q] = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(wp) + q);
+    uint32_t r[16];
+    uint64_t p = 0;  // words consumed so far
+    for (int i = 0; i < k; ++i) {
+        const uint32_t m = nn - static_cast<uint32_t>(i);
+        const int sh = __builtin_clz(m);
+        const __m128i shv = _mm_cvtsi32_si128(sh);
+        const __m256i mv = _mm256_set1_epi32(static_cast<int32_t>(m));
+        uint32_t acc = 0;
+#pragma GCC unroll 4
+        for (int q = 0; q < 4; ++q)  // w >> sh < m, as signed: both below 2^31 (sh >= 1)
+            acc |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(
+                       _mm256_cmpgt_epi32(mv, _mm256_srl_epi32(w[q], shv)))))
+                   << (8 * q);
+        const uint64_t live = static_cast<uint64_t>(acc) & (~uint64_t(0) << p);
+        if (!live) return false;
+        const int j = __builtin_ctzll(live);
+        r[i] = wp[j] >> sh;
+        p = static_cast<uint64_t>(j) + 1;
+    }
+    for (int64_t t = 0; t < n; ++t) pool[t] = static_cast<int32_t>(t);
+    for (int64_t q = 0; q < k; ++q) {
+        const uint32_t j = r[q];
+        out[q] = static_cast<OutT>(pool[j]);
+        pool[j] = pool[n - q - 1];
+    }
+    rng.index += static_cast<int>(p);
+    rng.settle();
+    return true;
+}
+
 // random.sample(population, k) expressed on positions 0..n-1 of the
 // population: writes the k chosen positions in result order.  `pool` must
 // hold setsize entries.  Requires 0 <= k <= n.
@@ -379,6 +453,7 @@ template <class OutT>
 inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize, OutT* out,
                              int32_t* pool) {
     if (n <= setsize) {
+        if (GS_SELECT_SMALL && k <= 16 && n < (int64_t(1) << 31) && pool_fast_window(rng, n, k, out, pool)) return;
         if (GS_SELECT_SMALL && k <= 32 && pool_fast(rng, n, k, out, pool)) return;
         // pool branch: pool = list(population); j = randbelow(n-i);
         // result[i] = pool[j]; pool[j] = pool[n-i-1]   (positions stand in

@@ -10,6 +10,7 @@
 // only orders the rows of a gather, so by default it is skipped and the
 // device expands the sampled positions through the CSR itself.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -23,8 +24,8 @@
 #include "rng.hpp"
 #include "team.hpp"
 
-#ifndef GS_PHASE  // phase marks for tools/sampler_prof.cpp; no-ops in the library
-#define GS_PHASE(i)
+#ifndef GS_PHASE  // phase marks of the sampler thread for tools/sampler_bench.cpp; no-ops in the library
+#define GS_PHASE(i)  // 1 draws (hops before the last), 2 sets + union, 3 frontier list, 4 last-hop draws, 5 join
 #endif
 
 namespace gs {
@@ -41,6 +42,25 @@ struct Hop {
     std::vector<int64_t> set_items;
     std::vector<int32_t> tptr, tidx;  // transposed (src -> dst) incl. self edges as -(r+1)
     int64_t n_empty = 0;              // empty neighbourhoods after the self rule
+    int64_t n_pos = 0;                // sampled entries (== pos.size() unless drawn into a pack)
+};
+
+// A pack written while sampling (gs_sample_pack_run's path): the last hop's
+// pos_ptr / entries / dst_ids go straight into the caller's buffer from the
+// draws, and each earlier hop's lists are copied in by whoever built them (a
+// helper, beside the next hop's draws), so the sampler thread never copies
+// the pack afterwards.  `off` follows layout_of's field order and alignment.
+struct PackOut {
+    int32_t* buf = nullptr;
+    int64_t cap = 0;
+    int64_t at = 0;  // next free element
+    int64_t off[GS_MAX_HOPS][GS_PK_NFIELDS];
+    int64_t put(int32_t hop, int field, int64_t n) {
+        off[hop][field] = at;
+        at += (n + 3) & ~int64_t(3);  // every array 16-byte aligned
+        GS_REQUIRE(at <= cap, GS_EINVAL, "pack exceeds its bound");
+        return off[hop][field];
+    }
 };
 
 struct Sample {
@@ -50,9 +70,21 @@ struct Sample {
 };
 
 // Draw the sampled row positions of every frontier node, in frontier order.
-static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
+// With `po` (the last hop of a pack run) the absolute CSR entries, pos_ptr
+// and dst_ids go straight into the pack, h.pos / h.ent stay empty, and the
+// destinations left empty by the self rule are counted on the way (only a
+// lone entry can be self: one col read for those).
+static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = nullptr, int32_t hop = 0,
+                           bool gcn = false) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    h.pos_ptr.assign(n + 1, 0);
+    int32_t* pptr;
+    if (po) {
+        pptr = po->buf + po->put(hop, GS_PK_POS_PTR, n + 1);
+    } else {
+        h.pos_ptr.resize(n + 1);
+        pptr = h.pos_ptr.data();
+    }
+    pptr[0] = 0;
     thread_local std::vector<int64_t> deg;
     deg.resize(n);
     int64_t total = 0;
@@ -66,26 +98,44 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h) {
         deg[r] = d;
         total += (h.k > 0 && d >= h.k) ? h.k : d;
         GS_REQUIRE(total < (int64_t(1) << 31), GS_ERANGE, "sampled entries exceed int32");
-        h.pos_ptr[r + 1] = static_cast<int32_t>(total);
+        pptr[r + 1] = static_cast<int32_t>(total);
     }
-    h.pos.resize(total);
-    h.ent.resize(total);
+    h.n_pos = total;
+    int32_t* ent;
+    int32_t* posv = nullptr;
+    if (po) {
+        ent = po->buf + po->put(hop, GS_PK_POS, total);
+        int32_t* d = po->buf + po->put(hop, GS_PK_DST_IDS, n);
+        for (int64_t r = 0; r < n; ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
+        h.pos.clear();
+        h.ent.clear();
+    } else {
+        h.pos.resize(total);
+        h.ent.resize(total);
+        ent = h.ent.data();
+        posv = h.pos.data();
+    }
     const int64_t setsize = sample_setsize(h.k);
-    thread_local std::vector<int32_t> pool;
+    thread_local std::vector<int32_t> pool, tmp;
     pool.resize(std::max<int64_t>(setsize, 1));
+    int64_t empty = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t d = deg[r];
-        int32_t* dstp = h.pos.data() + h.pos_ptr[r];
-        const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
-        if (h.k > 0 && d >= h.k) {
-            sample_positions(rng, d, h.k, setsize, dstp, pool.data());
-        } else {
-            for (int64_t t = 0; t < d; ++t) dstp[t] = static_cast<int32_t>(t);
-        }
+        const int64_t cnt = pptr[r + 1] - pptr[r];
         const int32_t rs = static_cast<int32_t>(rp[h.dst_ids[r]]);  // < 2^31 (checked in run_sample)
-        int32_t* ep = h.ent.data() + h.pos_ptr[r];
-        for (int64_t t = 0; t < cnt; ++t) ep[t] = rs + dstp[t];
+        int32_t* ep = ent + pptr[r];
+        if (h.k > 0 && d >= h.k) {
+            int32_t* dstp = posv ? posv + pptr[r] : ep;  // positions, then entries in place
+            sample_positions(rng, d, h.k, setsize, dstp, pool.data());
+            for (int64_t t = 0; t < cnt; ++t) ep[t] = rs + dstp[t];
+        } else {
+            if (posv)
+                for (int64_t t = 0; t < d; ++t) posv[pptr[r] + t] = static_cast<int32_t>(t);
+            for (int64_t t = 0; t < d; ++t) ep[t] = rs + static_cast<int32_t>(t);
+        }
+        if (po && !gcn) empty += cnt == 0 || (cnt == 1 && g.col[ep[0]] == h.dst_ids[r]);
     }
+    if (po) h.n_empty = empty;
 }
 
 // Destinations left without neighbours once self is removed (non-gcn): the
@@ -114,7 +164,11 @@ static int64_t count_empty(const Graph& g, const Hop& h, bool gcn) {
 struct HopScratch {
     PySet first, u;                   // samp_neighs[0]; the union
     std::vector<int32_t> slot_local;  // union slot -> rank in iteration order
-    std::vector<std::vector<int64_t>> part_items;  // per helper part of build_sets
+    std::vector<std::vector<int64_t>> part_items;  // per chunk of sets_union (per part of build_sets)
+    std::unique_ptr<std::atomic<int>[]> chunk_done;  // sets_union: chunk c's sets are built
+    int64_t n_chunk_cap = 0;
+    std::atomic<int64_t> next_chunk{0};  // sets_union: the next chunk to build
+    int64_t n_items = 0;              // items of all sets of the hop (before gather_sets)
     std::vector<int32_t> tmp, cur;    // lists()
 };
 
@@ -170,17 +224,88 @@ static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::
     }
 }
 
-static void union_map(Hop& h, HopScratch& sc) {
+// The frontier union list(set.union(*samp_neighs)) (:286) merged in set
+// order while the sets are still being built: the sets are cut into chunks
+// of kChunk destinations, taken in order from a shared counter by the
+// helpers and by this thread; this thread merges chunk c into the union as
+// soon as it is complete (set 0's full table first), and builds the next
+// unclaimed chunk itself whenever the one it needs is still in progress.
+// The union sees exactly the sequential merge order; only the set builds
+// overlap it.  Leaves each chunk's items in sc.part_items and per-set counts
+// in h.set_ptr[1 + r] (gather_sets makes set_ptr / set_items from them).
+static constexpr int64_t kChunk = 32;
+
+static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    const int64_t nch = (n + kChunk - 1) / kChunk;
+    h.set_ptr.assign(n + 1, 0);
+    if (static_cast<int64_t>(sc.part_items.size()) < nch) sc.part_items.resize(nch);
+    if (sc.n_chunk_cap < nch) {
+        sc.chunk_done.reset(new std::atomic<int>[nch]);
+        sc.n_chunk_cap = nch;
+    }
+    for (int64_t c = 0; c < nch; ++c) sc.chunk_done[c].store(0, std::memory_order_relaxed);
+    sc.next_chunk.store(0, std::memory_order_relaxed);
+    int32_t* counts = h.set_ptr.data() + 1;
+    auto build = [&](int64_t c) {
+        const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
+        auto& items = sc.part_items[c];
+        items.clear();
+        sets_range(g, h, a, b, items, counts, c == 0 ? &sc.first : nullptr);
+        sc.chunk_done[c].store(1, std::memory_order_release);
+    };
+    const bool helped = team && nch > 1;
+    if (helped)
+        team->start(team->helpers(), [&](int) {
+            for (int64_t c; (c = sc.next_chunk.fetch_add(1, std::memory_order_relaxed)) < nch;) build(c);
+        });
     PySet& u = sc.u;
     u.reset();
-    if (n > 0) {
-        copy_into(u, sc.first);  // non-empty: merge_runs never sees fill == 0
-        u.merge_runs(h.set_items.data(), h.set_ptr.data() + 1, n - 1);
+    int64_t n_items = 0;
+    for (int64_t c = 0; c < nch; ++c) {
+        while (!sc.chunk_done[c].load(std::memory_order_acquire)) {
+            const int64_t m = sc.next_chunk.fetch_add(1, std::memory_order_relaxed);
+            if (m < nch) build(m);  // m >= c: everything before c was claimed already
+            else _mm_pause();
+        }
+        const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
+        const auto& items = sc.part_items[c];
+        n_items += static_cast<int64_t>(items.size());
+        // this chunk's runs: set_ptr-style offsets into `items`
+        int32_t ptr[kChunk + 1];
+        ptr[0] = 0;
+        for (int64_t r = a; r < b; ++r) ptr[r - a + 1] = ptr[r - a] + counts[r];
+        if (c == 0) {
+            copy_into(u, sc.first);  // non-empty: merge_runs never sees fill == 0
+            u.merge_runs(items.data(), ptr + 1, b - a - 1);
+        } else {
+            u.merge_runs(items.data(), ptr, b - a);
+        }
     }
+    if (helped) team->wait();  // every helper is out of the chunk loop
+    sc.n_items = n_items;
+    GS_PHASE(2);
+}
+
+// h.set_ptr (a scan of the per-set counts) and h.set_items (the chunks'
+// items concatenated) for lists() and the Sample view.
+static void gather_sets(Hop& h, HopScratch& sc) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    const int64_t nch = (n + kChunk - 1) / kChunk;
+    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] += h.set_ptr[r];
+    h.set_items.resize(static_cast<size_t>(sc.n_items));
+    size_t at = 0;
+    for (int64_t c = 0; c < nch; ++c) {
+        const auto& v = sc.part_items[c];
+        if (!v.empty()) std::memcpy(h.set_items.data() + at, v.data(), v.size() * sizeof(int64_t));
+        at += v.size();
+    }
+}
+
+static void union_map(Hop& h, HopScratch& sc) {
+    PySet& u = sc.u;
     // The next frontier: the union's keys in slot order (a vector compaction
     // of the table).  The slot -> rank map the lists need is built by lists().
-    GS_PHASE(2);
     h.src_ids.resize(static_cast<size_t>(u.used));
     int64_t* dst = h.src_ids.data();
     const __m256i empty = _mm256_set1_epi32(PySet::EMPTY);
@@ -214,7 +339,6 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
     };
     // Neighbourhoods in union-local ids, ascending (= the dense mask's column
     // order, :305-308); non-gcn removes self (:297-298).
-    GS_PHASE(3);
     h.nbr_ptr.assign(n + 1, 0);
     h.nbr.clear();
     h.self_local.resize(n);
@@ -241,7 +365,6 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
     }
     // Transposed lists over Fj: for source c, the destinations reading it
     // (r >= 0) and the destinations whose self row it is (-(r+1)), r ascending.
-    GS_PHASE(4);
     const int64_t ns = static_cast<int64_t>(h.src_ids.size());
     h.tptr.assign(ns + 1, 0);
     for (int32_t c : h.nbr) ++h.tptr[c + 1];
@@ -256,41 +379,6 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
             h.tidx[cur[h.nbr[e]]++] = static_cast<int32_t>(r);
     }
     h.materialised = true;
-    GS_PHASE(5);
-}
-
-// sets_range over the whole hop (split across the team's helpers when there
-// are any), then set_ptr and the concatenated set_items.
-static void build_sets(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
-    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    GS_PHASE(0);
-    h.set_ptr.assign(n + 1, 0);
-    h.set_items.clear();
-    const int parts = team ? static_cast<int>(std::min<int64_t>(team->helpers() + 1, std::max<int64_t>(n / 64, 1))) : 1;
-    if (parts <= 1) {
-        h.set_items.reserve(h.pos.size() + n);
-        sets_range(g, h, 0, n, h.set_items, h.set_ptr.data() + 1, &sc.first);
-    } else {
-        auto& part_items = sc.part_items;
-        if (static_cast<int>(part_items.size()) < parts) part_items.resize(parts);
-        for (int p = 0; p < parts; ++p) part_items[p].clear();
-        team->parallel_for(parts, [&](int p) {
-            const int64_t a = n * p / parts, b = n * (p + 1) / parts;
-            part_items[p].reserve(static_cast<size_t>(h.pos_ptr[b] - h.pos_ptr[a] + (b - a)));
-            sets_range(g, h, a, b, part_items[p], h.set_ptr.data() + 1, p == 0 ? &sc.first : nullptr);
-        });
-        size_t total = 0;
-        for (int p = 0; p < parts; ++p) total += part_items[p].size();
-        h.set_items.resize(total);
-        size_t at = 0;
-        for (int p = 0; p < parts; ++p) {
-            const auto& v = part_items[p];
-            std::memcpy(h.set_items.data() + at, v.data(), v.size() * sizeof(int64_t));
-            at += v.size();
-        }
-    }
-    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] += h.set_ptr[r];
-    GS_PHASE(1);
 }
 
 // Sampling state reused from batch to batch by one thread (the runner's
@@ -302,11 +390,28 @@ struct SampleCtx {
     std::vector<int64_t> frontier;
 };
 
+// count_empties: fill Hop::n_empty (the Sample view reports it; a pack run
+// needs it only to fail MAX batches, GS_SAMPLE_FAIL_EMPTY — its scan re-reads
+// a row entry of every single-sample destination, ~2-3 % of a batch).
+// po: write the pack while sampling (PackOut; not with GS_SAMPLE_FULL).
+static void copy_lists(const Hop& h, PackOut& po, int32_t j) {
+    auto cpy = [&](int f, const std::vector<int32_t>& v) {
+        if (!v.empty()) std::memcpy(po.buf + po.off[j][f], v.data(), v.size() * sizeof(int32_t));
+    };
+    cpy(GS_PK_NBR_PTR, h.nbr_ptr);
+    cpy(GS_PK_NBR, h.nbr);
+    cpy(GS_PK_SELF, h.self_local);
+    cpy(GS_PK_TPTR, h.tptr);
+    cpy(GS_PK_TIDX, h.tidx);
+}
+
 static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
-                            const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team) {
+                            const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team,
+                            bool count_empties = true, PackOut* po = nullptr) {
     GS_REQUIRE(n_hops >= 1 && n_hops <= GS_MAX_HOPS, GS_EINVAL, "n_hops out of [1, 8]");
     GS_REQUIRE(n_roots >= 1 && roots, GS_EINVAL, "empty nodes_batch");
     GS_REQUIRE(g.n_entries < (int64_t(1) << 31), GS_ERANGE, "graph has >= 2^31 CSR entries (int32 pack entries)");
+    GS_REQUIRE(!po || !(flags & GS_SAMPLE_FULL), GS_EINVAL, "pack output with GS_SAMPLE_FULL");
     for (int64_t i = 0; i < n_roots; ++i)
         GS_REQUIRE(roots[i] >= 0 && roots[i] < g.n_nodes, GS_ERANGE, "node id out of range");
     if (team && team->helpers() == 0) team = nullptr;
@@ -325,30 +430,59 @@ static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const in
             if (p) t->wait();
         }
     } join{team, pending};
+    GS_PHASE(0);
     for (int32_t j = 0; j < n_hops; ++j) {
         Hop& h = s->hops[j];
         h.k = fanouts ? fanouts[j] : 10;
         h.dst_ids.swap(frontier);
-        draw_positions(g, rng, h);
-        h.n_empty = count_empty(g, h, gcn);
         const bool last = (j == n_hops - 1);
+        if (last && po) {
+            draw_positions(g, rng, h, po, j, gcn);  // pos_ptr, entries, dst_ids into the pack; n_empty
+            if (!count_empties) h.n_empty = 0;
+            GS_PHASE(4);
+            continue;
+        }
+        draw_positions(g, rng, h);
+        h.n_empty = count_empties ? count_empty(g, h, gcn) : 0;
+        GS_PHASE(last ? 4 : 1);
         if (!last || (flags & GS_SAMPLE_FULL)) {
             HopScratch& sc = c.scratch[j & 1];
             if (pending) {  // the team is needed for the sets below
                 team->wait();
                 pending = false;
             }
-            build_sets(g, h, sc, team);
+            sets_union(g, h, sc, team);
             union_map(h, sc);
             frontier.assign(h.src_ids.begin(), h.src_ids.end());
-            if (team) {  // lists + transpose on a helper, under the next hop's draws
-                team->start(1, [&h, &sc, gcn](int) { lists(h, sc, gcn); });
+            GS_PHASE(3);
+            if (po) {  // this hop's list fields: sizes are known from the sets and the union
+                const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+                const int64_t n_nbr = sc.n_items - (gcn ? 0 : n);
+                po->put(j, GS_PK_NBR_PTR, n + 1);
+                po->put(j, GS_PK_NBR, n_nbr);
+                po->put(j, GS_PK_SELF, n);
+                po->put(j, GS_PK_TPTR, static_cast<int64_t>(h.src_ids.size()) + 1);
+                po->put(j, GS_PK_TIDX, n_nbr + n);
+            }
+            if (team) {  // lists + transpose (+ their pack copy) on a helper, under the next hop's draws
+                team->start(1, [&h, &sc, gcn, po, j](int) {
+                    gather_sets(h, sc);
+                    lists(h, sc, gcn);
+                    if (po) copy_lists(h, *po, j);
+                });
                 pending = true;
             } else {
+                gather_sets(h, sc);
                 lists(h, sc, gcn);
+                if (po) copy_lists(h, *po, j);
             }
         }
     }
+    if (pending) {
+        team->wait();
+        pending = false;
+    }
+    GS_PHASE(5);
 }
 
 static Sample* run_sample(const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
@@ -572,15 +706,28 @@ static int pack_run(const gs_graph* gp, gs_rng* rng, const int64_t* roots, int64
     const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
     thread_local std::unique_ptr<gs::SampleCtx> ctx;  // reused batch to batch by this thread
     if (!ctx) ctx.reset(new gs::SampleCtx());
-    gs::run_sample_into(*ctx, g, rng->mt, roots, n_roots, fanouts, n_hops, flags, team);
+    const bool direct = !(flags & GS_SAMPLE_FULL);  // the pack written while sampling
+    gs::PackOut po;
+    for (auto& row : po.off)
+        for (auto& o : row) o = -1;
+    po.buf = buf;
+    po.cap = cap - n_roots;
+    gs::run_sample_into(*ctx, g, rng->mt, roots, n_roots, fanouts, n_hops, flags, team,
+                        (flags & GS_SAMPLE_FAIL_EMPTY) != 0, direct ? &po : nullptr);
     const Sample* s = &ctx->s;
     gs_pack_layout L;
-    layout_of(*s, &L);
-    gs_sample_pack(reinterpret_cast<const gs_sample*>(s), buf, cap);
+    if (direct) {
+        for (int32_t j = 0; j < GS_MAX_HOPS; ++j)
+            for (int f = 0; f < GS_PK_NFIELDS; ++f) L.off[j][f] = po.off[j][f];
+        L.total = po.at;
+    } else {
+        layout_of(*s, &L);
+        gs_sample_pack(reinterpret_cast<const gs_sample*>(s), buf, cap);
+    }
     for (int32_t j = 0; j < n_hops; ++j) {
         const Hop& h = s->hops[j];
         hop_sizes[4 * j] = static_cast<int64_t>(h.dst_ids.size());
-        hop_sizes[4 * j + 1] = static_cast<int64_t>(h.pos.size());
+        hop_sizes[4 * j + 1] = h.n_pos;
         hop_sizes[4 * j + 2] = h.materialised ? static_cast<int64_t>(h.src_ids.size()) : -1;
         hop_sizes[4 * j + 3] = h.materialised ? static_cast<int64_t>(h.nbr.size()) : -1;
         if (h.n_empty && (flags & GS_SAMPLE_FAIL_EMPTY)) gs::fail(GS_EEMPTY, "empty neighbourhood");

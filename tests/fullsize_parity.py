@@ -116,7 +116,8 @@ def check_embeddings_vs_oracle(gs_models, graph, X, X_rows, hops, roots, fanouts
     view of the device table)."""
     import torch
     H = weights[0].shape[0]
-    m = gs_models.GraphSage(2, X.shape[1], H, X, graph, device, fanouts=list(fanouts), rng=sampler.RNG(seed))
+    m = gs_models.GraphSage(2, X.shape[1], H, X, graph, device, fanouts=list(fanouts),
+                            rng=sampler.RNG(seed)).to(device)
     with torch.no_grad():
         for i in (1, 2):
             getattr(m, f"sage_layer{i}").weight.copy_(weights[i - 1])

@@ -133,7 +133,8 @@ def test_fullsize_device_sampler_past_capacity_falls_back(wl):
     out = []
     for dev_s in (False, True):
         rng = sampler.RNG(11)
-        m = models.GraphSage(2, F, H, wl["X"], wl["graph"], DEV, fanouts=FAN, rng=rng, device_sampler=dev_s)
+        m = models.GraphSage(2, F, H, wl["X"], wl["graph"], DEV, fanouts=FAN, rng=rng,
+                             device_sampler=dev_s).to(DEV)
         with torch.no_grad():
             for i in (1, 2):
                 getattr(m, f"sage_layer{i}").weight.copy_(W[i - 1])

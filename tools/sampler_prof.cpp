@@ -22,8 +22,9 @@ static clk::time_point g_last;
 namespace gs {
 static void materialise(const Graph& g, Hop& h, bool gcn) {
     HopScratch sc;
-    build_sets(g, h, sc, nullptr);
+    sets_union(g, h, sc, nullptr);
     union_map(h, sc);
+    gather_sets(h, sc);
     lists(h, sc, gcn);
 }
 }  // namespace gs
