@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-4 pass B: host sampler A/B on the box's CPU (round-3 host code vs the
+# current one, one stream + one helper, alternating; then 7 streams), the
+# -m gpu suite, smoke(), the driver's default bench command.
+set -o pipefail
+export TMPDIR=/tmp
+ROOT=${GRAFT_REPO_ROOT:-$PWD}
+OUT=$ROOT/gpurun_out/r04b
+mkdir -p "$OUT"; cd "$ROOT"
+for i in 1 2 3; do
+  timeout -k 10 120 tools/bin/sampler_bench_r03 1 300 1 >> "$OUT/sampler_ab.txt" 2>&1 || exit $?
+  timeout -k 10 120 tools/bin/sampler_bench_new 1 300 1 >> "$OUT/sampler_ab.txt" 2>&1 || exit $?
+done
+timeout -k 10 200 tools/bin/sampler_bench_r03 1 200 7 >> "$OUT/sampler_ab.txt" 2>&1 || exit $?
+timeout -k 10 200 tools/bin/sampler_bench_new 1 200 7 >> "$OUT/sampler_ab.txt" 2>&1 || exit $?
+grep -E "helpers|windows" "$OUT/sampler_ab.txt"
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > "$OUT/gpu_tests.log" 2>&1
+rc=$?; tail -3 "$OUT/gpu_tests.log"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit $?
+echo smoke ok
+timeout -k 10 400 python3 bench.py > "$OUT/bench_rmat2m_steps20.json" 2> "$OUT/bench_rmat2m_steps20.err" || exit $?
+echo "default: $(grep -o '"value": [0-9.]*' "$OUT/bench_rmat2m_steps20.json" | head -1)"
