@@ -539,6 +539,37 @@ def run_embed(args, cfg):
         dist.destroy_process_group()
 
 
+def reference_stream_window(trainer, wl, cfg, args, batches):
+    """The reference's own sampling trajectory, driver-timed: ONE sampler
+    stream seeded exactly as random.seed(seed) (stream 0 of rank 0,
+    models.py:281-282, main.py:40) — every batch's draws are the reference's
+    words in order, bit for bit — with helper threads building its sets and
+    lists (the same draws).  Steps run back to back after a short warmup; the
+    single stream is sequential on its `random` state, so this window is
+    sampler-bound by construction and reports the sampler's per-batch time."""
+    helpers = max(1, min(7, args.per_gpu - 2))
+    K, W = args.ref_stream_steps, 5
+    rb = batches[:W + K]
+    runner = train.Runner(trainer, wl["graph"], rb, [train.make_rng(args.seed, 0, 0)], cfg["fanouts"], gcn=False,
+                          fail_empty=cfg["agg"] == "MAX", helpers=helpers, warm=not args.no_warm,
+                          sampler=args.sampler)
+    runner.run(W)
+    torch.cuda.synchronize()
+    runner.stats(reset=True)
+    t0 = time.perf_counter()
+    runner.run(K)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = runner.stats()
+    runner.close()
+    n = max(1, st["steps"])
+    return {"value": round(cfg["batch"] * K / el, 1), "unit": "root nodes/s", "steps": K, "warmup": W,
+            "ms_per_step": round(el / K * 1e3, 4),
+            "stream": f"random.seed({args.seed}) (stream 0 of rank 0: the reference's single global stream)",
+            "sampler": {"streams": 1, "helpers": helpers, "ms_per_batch": round(1e3 * st["sample_s"] / n, 4)},
+            "lookahead_misses": st["lookahead_misses"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -554,8 +585,13 @@ def main():
                     help="rmat2m-embed: reference batches per device launch (1 = one batch per launch)")
     ap.add_argument("--sustain", type=int, default=200,
                     help="steady-state steps after the measured ones (samplers running ahead), reported as `sustained`")
-    ap.add_argument("--ar-buckets", type=int, default=1, choices=(1, 2),
-                    help="N > 1: gradient all-reduce buckets (2 = upper layers + classifier under the layer-1 dW GEMM)")
+    ap.add_argument("--ar-buckets", type=int, default=None, choices=(1, 2),
+                    help="N > 1: gradient all-reduce buckets (2, the default at N > 1: upper layers + classifier "
+                         "under the layer-1 dW GEMM, then W1 in the row chunks its chunked dW GEMM completes, "
+                         "GS_AR_W1_CHUNKS=2; 1: one all-reduce after the backward)")
+    ap.add_argument("--ref-stream-steps", type=int, default=60,
+                    help="N = 1: steps of the `reference_stream` window (the reference's single seed-824 random "
+                         "stream, S = 1 with helper threads; 0 = skip)")
     ap.add_argument("--sampler-streams", type=int, default=None,
                     help="independent bit-exact sampler streams per GPU (1 = the reference's single stream; "
                          "default with helpers: min(8, (host cores per GPU - 2) / 2), two cores left for the "
@@ -603,6 +639,8 @@ def main():
     if cfg.get("loop") == "embed":
         return run_embed(args, cfg)
     rank, world = train.init_distributed()
+    if args.ar_buckets is None:
+        args.ar_buckets = 2 if world > 1 else 1
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -755,6 +793,11 @@ def main():
                "cgroup_throttled_ms": (round((sthr1 - sthr0) / 1e3, 3) if sthr0 is not None else None)}
     value = cfg["batch"] * args.steps * world / elapsed
     sizes = st["hop_sizes_sum"] / max(1, st["steps"])  # mean (n_dst, n_pos, n_src, n_nbr) per hop
+    ref_stream = None
+    if world == 1 and args.ref_stream_steps > 0 and args.sampler == "host":
+        runner.close()  # its sampler threads are done (the batch list is consumed)
+        runner = None
+        ref_stream = reference_stream_window(trainer, wl, cfg, args, batches)
     n_edges = float(sizes[:L, 1].sum()) * args.steps
     fused1 = bool(lib.gs_trainer_layer1_fused(trainer._h))
     n1, e1 = float(sizes[L - 1, 0]), float(sizes[L - 1, 1])
@@ -843,6 +886,8 @@ def main():
                        "cold_start": {"value": round(cfg["batch"] * args.steps * world / cold_elapsed, 1),
                                       "ms_per_step": round(cold_elapsed / args.steps * 1e3, 4), **cold_proof},
                        "allreduce_buckets": args.ar_buckets if world > 1 else 0,
+                       "allreduce_w1_chunks": (int(os.environ.get("GS_AR_W1_CHUNKS", "2"))
+                                               if world > 1 and args.ar_buckets == 2 else 0),
                        "sampled_edges_per_s": round(n_edges * world / elapsed, 1),
                        "graph_build_s": round(wl["t_graph"], 2), "final_loss": round(loss, 5),
                        "host_csr": "one per node, /dev/shm image mapped by every rank" if wl["csr_shared"]
@@ -861,10 +906,12 @@ def main():
             "roofline": roof,
             "roofline_kernels": rooflines,
             "sustained": sus,
+            "reference_stream": ref_stream,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    runner.close()
+    if runner is not None:
+        runner.close()
     if comm is not None:
         comm.close()
     if world > 1:

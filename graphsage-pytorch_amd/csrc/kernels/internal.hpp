@@ -17,6 +17,13 @@ namespace gs {
 // so a caller can all-reduce the finished gradients [w1_floats, n_params)
 // under that GEMM (the runner's bucketed all-reduce).  Empty: no hook.
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
+// Layer-1 weight gradient in `chunks` row chunks (2-layer top path with an
+// upper hook): after each chunk's slab sum, hook(stream, float offset into the
+// gradient buffer, float count) — the runner all-reduces the chunk there, so
+// only the last chunk's collective follows the step's last GEMM.  The chunks
+// use the whole gradient's row slabs: the same sums bit for bit.
+void trainer_set_w1_chunk_hook(gs_trainer* t, int chunks,
+                               std::function<void(hipStream_t, int64_t, int64_t)> hook);
 // Called on the step's stream right after the layer-1 forward launch of a training step.
 void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
 // Inside a runner loop: the SGD keeps the bf16 W1 current (no per-step cast).
@@ -44,7 +51,7 @@ inline constexpr int kDwGroupParts = 8;
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
-                    DwGroups* grp = nullptr);
+                    DwGroups* grp = nullptr, int64_t H_split = -1);
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 // One slab sum: out = Σ_s slabs[s] (S slabs of len floats), norm partials to part.
 struct SlabSum {

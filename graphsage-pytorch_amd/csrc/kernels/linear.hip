@@ -452,7 +452,7 @@ namespace gs {
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
-                    DwGroups* grp) {
+                    DwGroups* grp, int64_t H_split) {
     GS_REQUIRE(dt == GS_F32 || dt == GS_BF16, GS_EINVAL, "dtype must be f32 or bf16");
     static_assert(kDwGroupParts == kSlabParts && kDwGroupParts == kXcds, "group count = slab-sum parts = XCDs");
     if (grp) {
@@ -467,9 +467,12 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
         return 1;
     }
     GS_REQUIRE(A && dout && dW && (out || !relu), GS_EINVAL, "NULL device pointer");
-    const int S = dw_splits(n, K, H);
-    const int rps = dw_rows_per_split(n, K, H);
-    const int64_t need = gs_sage_linear_bwd_weight_ws(n, K, H);
+    // H_split: the row slabs of an H_split-row gradient (a chunk of its rows
+    // then has the whole gradient's slabs, hence its sums bit for bit)
+    const int64_t Hs = H_split > 0 ? H_split : H;
+    const int S = dw_splits(n, K, Hs);
+    const int rps = dw_rows_per_split(n, K, Hs);
+    const int64_t need = static_cast<int64_t>(S > 1 ? S : 0) * K * H * 4;
     GS_REQUIRE(ws_bytes >= need && (need == 0 || ws), GS_EINVAL, "workspace too small");
     float* target = (S > 1) ? static_cast<float*>(ws) : dW;
     // 4-element input reads: 16 B (fp32) / 8 B (bf16) aligned

@@ -57,6 +57,8 @@ struct gs_trainer {
     int npart[2] = {0, 0};
     bool norm_ready = false;
     std::function<void(hipStream_t)> upper_hook;  // internal.hpp trainer_set_upper_hook
+    std::function<void(hipStream_t, int64_t, int64_t)> w1_chunk_hook;  // trainer_set_w1_chunk_hook
+    int w1_chunks = 1;
     std::function<void(hipStream_t)> fwd1_hook;   // after the layer-1 forward launch (trainer_set_fwd1_hook)
     // bf16 features: W1 in bf16 for the layer-1 forward.  Cast from the fp32
     // W1 before a forward, except inside a runner loop (lp_keep), where the
@@ -389,6 +391,28 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 }
                 if (T.upper_hook) T.upper_hook(st);
             }
+            if (!defer && T.w1_chunk_hook && T.w1_chunks > 1 && H % (64 * T.w1_chunks) == 0) {
+                // dW1 in row chunks, each summed and handed to the hook (its
+                // all-reduce then runs under the next chunk's GEMM); the clip
+                // of the communicator path recomputes the norm from the
+                // reduced gradient, so no norm partials are kept
+                const int64_t Hc = H / T.w1_chunks;
+                for (int q = 0; q < T.w1_chunks; ++q) {
+                    const int64_t h0 = q * Hc;
+                    float* dWq = G + T.w_off[0] + h0 * K1;
+                    const int Sq = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, Hc,
+                                                   c.gcn ? nullptr : c.X, c.feat_ld, dst_L, agg[0], F,
+                                                   lb.back().dH + h0, h[0] + h0, H, 0, dWq, dw_ws, dw_need, st,
+                                                   nullptr, H);
+                    if (Sq > 1) sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), Sq, Hc * K1, dWq, nullptr, st);
+                    T.w1_chunk_hook(st, T.w_off[0] + h0 * K1, Hc * K1);
+                }
+                g_launch_events = {};
+                T.npart[0] = 0;
+                T.npart[1] = 0;
+                T.norm_ready = false;
+                return cv.at;
+            }
             const bool armed = timed_arm(T, 2);
             DwGroups grp{T.dw_cnt, T.dw_n_cnt, dw_gpart};
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
@@ -470,6 +494,10 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
 }
 
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->upper_hook = std::move(hook); }
+void trainer_set_w1_chunk_hook(gs_trainer* t, int chunks, std::function<void(hipStream_t, int64_t, int64_t)> hook) {
+    t->w1_chunks = hook ? std::max(1, chunks) : 1;
+    t->w1_chunk_hook = std::move(hook);
+}
 
 void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk) {
     if (t->cfg.n_layers != 2 || t->cfg.gcn || tk < 1 || tk > 31 || B < 1) return;

@@ -127,6 +127,12 @@ struct gs_runner {
     // cfg.ar_buckets == 2: the upper gradients' all-reduce on its own stream
     hipStream_t comm_stream = nullptr;
     hipEvent_t upper_ready = nullptr, upper_reduced = nullptr;
+    // GS_AR_W1_CHUNKS (default 2): W1's gradient all-reduced in row chunks as
+    // the trainer's chunked dW1 produces them (trainer_set_w1_chunk_hook);
+    // w1_issued counts the chunks the current step handed over (0: the
+    // trainer took the one-piece path, so the runner reduces W1 itself)
+    hipEvent_t w1_ready = nullptr;
+    int w1_issued = 0;
     // Ring of 3 per batch in flight (b % 3): device pack buffer, trainer
     // gather slot, events.  The side stream pulls batch b's pack and gathers
     // its layer 1 (reads only X and the pack) while the main stream runs
@@ -559,7 +565,11 @@ gs_runner::~gs_runner() {
         }
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
     }
-    if (cfg.trainer && comm_stream) gs::trainer_set_upper_hook(cfg.trainer, {});
+    if (cfg.trainer && comm_stream) {
+        gs::trainer_set_upper_hook(cfg.trainer, {});
+        gs::trainer_set_w1_chunk_hook(cfg.trainer, 1, {});
+    }
+    if (w1_ready) (void)hipEventDestroy(w1_ready);
     if (cfg.trainer && !cfg.comm && !cfg.embed_out) {  // drained above; never expected
         try {
             if (gs::trainer_barrier_failed(cfg.trainer))
@@ -773,6 +783,21 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
                                                  rp->comm_stream);
             if (rc != GS_OK) fail(rc, gs_last_error());
         });
+        const char* ch_env = std::getenv("GS_AR_W1_CHUNKS");
+        const int chunks = ch_env ? std::atoi(ch_env) : 2;
+        if (chunks > 1) {
+            hip_ok(hipEventCreateWithFlags(&r->w1_ready, hipEventDisableTiming), "hipEventCreate");
+            trainer_set_w1_chunk_hook(cfg->trainer, chunks, [rp](hipStream_t st, int64_t off, int64_t n) {
+                // same comm stream, after the upper bucket: every rank issues
+                // the collectives on one communicator in one stream order
+                hip_ok(hipEventRecord(rp->w1_ready, st), "hipEventRecord");
+                hip_ok(hipStreamWaitEvent(rp->comm_stream, rp->w1_ready, 0), "hipStreamWaitEvent");
+                const int rc = gs_comm_allreduce_sum(rp->cfg.comm, gs_trainer_grads(rp->cfg.trainer) + off, n,
+                                                     rp->comm_stream);
+                if (rc != GS_OK) fail(rc, gs_last_error());
+                ++rp->w1_issued;
+            });
+        }
     }
     r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
     r->gate_step = std::getenv("GS_SIDE_GATE_STEP") != nullptr && !cfg->embed_out;
@@ -922,6 +947,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             // the done flag goes to the step's SGD launch: the fused slab sum
             // inside the step, or gs_trainer_update* below
             if (r->use_flag) g_done_flag = {r->done_dev, b};
+            r->w1_issued = 0;
             int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, hop_sizes, offsets,
                                                           pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
                                                           st);
@@ -936,10 +962,12 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 // layer-1 dW GEMM; W1's collective follows them on the SAME stream,
                 // so every rank issues the two collectives on one communicator in
                 // one stream order (not by host issue order across two streams)
-                hip_ok(hipEventRecord(r->upper_ready, st), "hipEventRecord");  // dW1 final
-                hip_ok(hipStreamWaitEvent(r->comm_stream, r->upper_ready, 0), "hipStreamWaitEvent");
-                rc = gs_comm_allreduce_sum(r->cfg.comm, grads, trainer_w1_floats(r->cfg.trainer), r->comm_stream);
-                if (rc != GS_OK) fail(rc, gs_last_error());
+                if (r->w1_issued == 0) {  // W1 in one piece (the trainer's unchunked path)
+                    hip_ok(hipEventRecord(r->upper_ready, st), "hipEventRecord");  // dW1 final
+                    hip_ok(hipStreamWaitEvent(r->comm_stream, r->upper_ready, 0), "hipStreamWaitEvent");
+                    rc = gs_comm_allreduce_sum(r->cfg.comm, grads, trainer_w1_floats(r->cfg.trainer), r->comm_stream);
+                    if (rc != GS_OK) fail(rc, gs_last_error());
+                }
                 hip_ok(hipEventRecord(r->upper_reduced, r->comm_stream), "hipEventRecord");
                 hip_ok(hipStreamWaitEvent(st, r->upper_reduced, 0), "hipStreamWaitEvent");
             } else if (r->cfg.comm) {

@@ -99,16 +99,21 @@ def test_two_rank_step_arithmetic_on_one_gpu(gs):
         torch.testing.assert_close(a.cpu(), b, atol=1e-6, rtol=1e-6)
 
 
-@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
-def test_bucketed_allreduce_equals_single(gs, agg):
+@pytest.mark.parametrize("agg,batch", [("MEAN", 48), ("MAX", 48), ("MEAN", 200)])
+def test_bucketed_allreduce_equals_single(gs, agg, batch, monkeypatch):
     """ar_buckets = 2 (upper gradients all-reduced on a comm stream under the
-    layer-1 dW GEMM, then W1) against one all-reduce, one rank: bitwise."""
+    layer-1 dW GEMM, then W1 — in one piece, or in the row chunks the trainer
+    hands over as its chunked dW1 completes them, GS_AR_W1_CHUNKS = 2, the
+    default) against one all-reduce, one rank: bitwise.  Every batch gives the
+    layer-1 gradient several row slabs (4-6 at these frontiers), so the
+    chunks' slab sums are exercised."""
     graph, adj, X, labels, cands = _setup(gs)
     Xd = torch.from_numpy(uniform_features(5, X.shape[0], 256)).to(DEV)
-    batches = list(train.rank_batches(cands, 48, 0, 1, 9))[:5]
+    batches = list(train.rank_batches(cands, batch, 0, 1, 9))[:5]
     out = []
     comm = train.Communicator(0, 1, DEV)
-    for buckets in (1, 2):
+    for buckets, chunks in ((1, "1"), (2, "1"), (2, "2")):
+        monkeypatch.setenv("GS_AR_W1_CHUNKS", chunks)
         tr = train.NativeTrainer(graph, Xd, labels.to(DEV), 16, fanouts=(25, 10), agg_func=agg, seed=SEED)
         r = train.Runner(tr, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
                          fail_empty=agg == "MAX", depth=2, comm=comm, ar_buckets=buckets)
@@ -117,8 +122,9 @@ def test_bucketed_allreduce_equals_single(gs, agg):
         out.append((tr.p.params.clone(), float(tr.loss)))
         r.close()
     comm.close()
-    assert torch.equal(out[0][0], out[1][0])
-    assert out[0][1] == out[1][1]
+    for p, loss in out[1:]:
+        assert torch.equal(out[0][0], p)
+        assert out[0][1] == loss
 
 
 def test_held_runner_samples_nothing_before_release(gs):

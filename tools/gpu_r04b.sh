@@ -20,3 +20,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 echo smoke ok
 timeout -k 10 400 python3 bench.py > "$OUT/bench_rmat2m_steps20.json" 2> "$OUT/bench_rmat2m_steps20.err" || exit $?
 echo "default: $(grep -o '"value": [0-9.]*' "$OUT/bench_rmat2m_steps20.json" | head -1)"
+python3 - "$OUT/bench_rmat2m_steps20.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+c = d["config"]
+print("value", d["value"], "ms", d["ms_per_step"], "sampler", c["sampler"], "sustained", {k: d["sustained"][k] for k in ("value", "lookahead_misses", "max_step_ms")})
+print("reference_stream", d.get("reference_stream"))
+PY
