@@ -163,6 +163,7 @@ constexpr int kSetupBatch = 8;
 // the blocks, the word need of the hop, and (last hop) the pack offsets.
 __global__ __launch_bounds__(1024) void hop_setup_kernel(DevGraph g, Ctl* c, HopBufs hb, int hop, int k, int setsize,
                                                          int R, int last, int n_roots, int gcn) {
+    GS_DS_BAIL(c);
     __shared__ int shi[17];
     __shared__ float shf[17];
     __shared__ int s_maxw, s_maxlo;
@@ -512,6 +513,7 @@ __device__ __forceinline__ int walk_masked(const uint32_t* __restrict__ M, int a
 template <int KMAX>
 __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
                                                                 int hop, int k, int setsize, int R) {
+    GS_DS_BAIL(c);
     extern __shared__ uint64_t smem64[];
     __shared__ int s_d[256], s_moff[257];
     __shared__ int s_nsr;
@@ -635,6 +637,7 @@ __global__ __launch_bounds__(kMEntries) void draw_masked_kernel(const uint32_t* 
 // window (uint16; 0xFFFF outside it), or absolute for the last group.  The
 // group's block maps are staged in LDS.
 __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, int hop) {
+    GS_DS_BAIL(c);
     extern __shared__ __attribute__((aligned(16))) uint16_t tabs[];
     __shared__ int los[kComposeEntries / 64 + 1], wid[kComposeEntries / 64 + 1];
     const HopCtl& h = c->hop[hop];
@@ -708,6 +711,7 @@ __global__ __launch_bounds__(256) void draw_compose_kernel(Ctl* c, HopBufs hb, i
 // then every block's true entry (a lookup in its group's path) and the hop's
 // end position.
 __global__ __launch_bounds__(1024) void draw_chain_kernel(Ctl* c, HopBufs hb, int hop) {
+    GS_DS_BAIL(c);
     extern __shared__ __attribute__((aligned(16))) uint16_t gx[];
     __shared__ int gentry[kMaxGroups + 1];
     HopCtl& h = c->hop[hop];
@@ -779,6 +783,7 @@ constexpr int kEmitWords = 256;
 __global__ __launch_bounds__(64 * kEmitWaves) void draw_emit_kernel(const uint32_t* __restrict__ wr, Ctl* c, HopBufs hb,
                                                                     DevGraph g, int hop, int k, int setsize, int R,
                                                                     int last, int gcn, int32_t* __restrict__ pack) {
+    GS_DS_BAIL(c);
     __shared__ uint32_t wbuf[kEmitWaves][kEmitWords];
     HopCtl& h = c->hop[hop];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -909,6 +914,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void draw_emit_kernel(const uint32
 // Roots after the pack (the host sampler's layout), totals for the host.
 __global__ void finish_kernel(Ctl* c, const int32_t* __restrict__ roots, int n_roots, int32_t* __restrict__ pack,
                               int fail_empty, int n_hops) {
+    GS_DS_BAIL(c);
     const int at = c->total;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_roots; i += gridDim.x * blockDim.x)
         pack[at + i] = roots[i];

@@ -25,6 +25,21 @@ constexpr int kStEmpty = 8;    // empty neighbourhood with GS_SAMPLE_FAIL_EMPTY
 constexpr int kStSize = 16;    // a frontier outgrew its preallocated bound
 constexpr int kStOrder = 32;   // block states lost their order (never expected)
 constexpr int kStSpin = 64;    // a table insert exceeded its probe / displacement bound (never expected)
+// Statuses after which the run's later kernels have nothing valid to read
+// (unwritten sample entries, a frontier never built, stale hop sizes): every
+// kernel after begin_kernel returns at once once one is set (GS_DS_BAIL), so a
+// failed run reports its status instead of reading garbage indices.
+constexpr int kStFail = kStWindow | kStWords | kStTable | kStSize | kStOrder | kStSpin;
+// Block-uniform early return on a failed run: thread 0 reads the status once
+// (another block of the same launch may set it meanwhile) and the block
+// follows that one reading.
+#define GS_DS_BAIL(c)                                               \
+    do {                                                            \
+        __shared__ int s_bail_;                                     \
+        if (threadIdx.x == 0) s_bail_ = (c)->status & kStFail;      \
+        __syncthreads();                                            \
+        if (s_bail_) return;                                        \
+    } while (0)
 
 // Probe steps one key may take in a table of mask + 1 slots before the insert
 // gives up (kStSpin): CPython's probe sequence (10 linear slots, then

@@ -237,6 +237,7 @@ __device__ __forceinline__ uint32_t w_resize(volatile int32_t* T, uint32_t mask,
 constexpr int kSetWaves = 4;
 __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c, HopBufs hb, UnionBufs ub, int hop,
                                                               int k) {
+    GS_DS_BAIL(c);
     __shared__ int32_t tabs[kSetWaves][kSmallSet], keys[kSetWaves][kSmallSet];
     const int wave = static_cast<int>(threadIdx.x >> 6), lane = wlane();
     const int r = blockIdx.x * kSetWaves + wave;
@@ -352,6 +353,7 @@ __global__ __launch_bounds__(64 * kSetWaves) void sets_kernel(DevGraph g, Ctl* c
 // Per run r >= 1 (one wave, lane q = item q): the items new to the union —
 // those whose mark is their own (the union's first occurrence of the key).
 __global__ __launch_bounds__(64) void ufresh_kernel(Ctl* c, HopBufs hb, UnionBufs ub, int hop) {
+    GS_DS_BAIL(c);
     const int r = blockIdx.x, lane = threadIdx.x;
     if (r >= c->hop[hop].n_dst) return;
     const uint64_t E = static_cast<uint64_t>(static_cast<uint32_t>(c->epoch + 1)) << 32;
@@ -547,6 +549,7 @@ __device__ __forceinline__ void settle16(uint32_t* T, uint32_t mask, int t0, int
 
 __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop, int gcn,
                                                     int32_t* __restrict__ pack, int nd_next_max) {
+    GS_DS_BAIL(c);
     extern __shared__ uint32_t T[];  // kUnionBig uint16 slots
     __shared__ int shi[17];
     __shared__ int32_t oldslot[kSmallSet];
@@ -651,6 +654,7 @@ __global__ __launch_bounds__(1024) void ubig_kernel(Ctl* c, HopBufs hb, UnionBuf
 // each key's position in it (lid), the pack layout of this hop.
 __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionBufs ub, HopBufs next, int hop,
                                                       int gcn, int32_t* __restrict__ pack, int nd_next_max) {
+    GS_DS_BAIL(c);
     extern __shared__ uint32_t T[];
     __shared__ int shi[17];
     __shared__ int st_run[kMaxStages + 1];
@@ -883,6 +887,7 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
 // models.py:305-308; non-gcn drops self, :297-298), and its self id.
 __global__ __launch_bounds__(64) void uout_kernel(Ctl* c, HopBufs hb, UnionBufs ub, int hop, int gcn,
                                                   int32_t* __restrict__ pack) {
+    GS_DS_BAIL(c);
     const HopCtl& h = c->hop[hop];
     const int r = blockIdx.x, lane = threadIdx.x;
     if (r >= h.n_dst || h.n_src < 0 || (c->status & (kStTable | kStSize))) return;
@@ -913,6 +918,7 @@ __global__ __launch_bounds__(64) void uout_kernel(Ctl* c, HopBufs hb, UnionBufs 
 
 __global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt,
                                                      int32_t* __restrict__ longs) {
+    GS_DS_BAIL(c);
     __shared__ int shi[17];
     const HopCtl& h = c->hop[hop];
     if (threadIdx.x == 0) longs[0] = 0;  // tsort_kernel's queue of long lists
@@ -937,6 +943,7 @@ __global__ __launch_bounds__(1024) void tscan_kernel(Ctl* c, int hop, int32_t* _
 // One wave per destination r: its self entry -(r+1) and its neighbour
 // entries r at the sources' cursors (order fixed by tsort_kernel).
 __global__ __launch_bounds__(64) void tfill_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* tcnt) {
+    GS_DS_BAIL(c);
     const HopCtl& h = c->hop[hop];
     const int r = blockIdx.x, lane = threadIdx.x;
     if (r >= h.n_dst || h.n_src <= 0) return;
@@ -954,6 +961,7 @@ constexpr int kSortReg = 16;
 __device__ __forceinline__ int32_t tkey(int32_t v) { return v >= 0 ? 2 * v + 1 : -2 * v - 2; }
 __device__ __forceinline__ int32_t tval(int32_t k) { return (k & 1) ? (k - 1) / 2 : -(k + 2) / 2; }
 __global__ void tsort_kernel(Ctl* c, int hop, int32_t* __restrict__ pack, int32_t* __restrict__ longs) {
+    GS_DS_BAIL(c);
     const HopCtl& h = c->hop[hop];
     const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
     if (cidx >= h.n_src) return;
@@ -999,6 +1007,7 @@ constexpr int kLongLds = 8192;
 constexpr int kLongThreads = 256;
 __global__ __launch_bounds__(kLongThreads) void tlong_kernel(Ctl* c, int hop, int32_t* __restrict__ pack,
                                                              const int32_t* __restrict__ longs) {
+    GS_DS_BAIL(c);
     __shared__ int32_t sk[kLongLds];
     const HopCtl& h = c->hop[hop];
     if (h.n_src <= 0) return;
