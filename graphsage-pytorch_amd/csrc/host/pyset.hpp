@@ -159,6 +159,16 @@ struct PySet {
         return true;
     }
 
+    // add() of a key known to be absent (set(random.sample(...)): distinct
+    // sampled entries of one row): the same slot and resizes as add(), without
+    // comparing against the keys on the probe path.
+    void add_absent(int32_t key) {
+        insert_clean(tab, mask, key);
+        ++fill;
+        ++used;
+        if (static_cast<size_t>(fill) * 5 >= mask * 3) resize(used > 50000 ? used * 2 : used * 4);
+    }
+
     // Slot of a present key (same probe walk as add), or -1.
     int64_t find_slot(int32_t key) const {
         size_t perturb = static_cast<size_t>(key);

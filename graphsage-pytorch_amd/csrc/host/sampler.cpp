@@ -72,10 +72,10 @@ struct Sample {
 // Draw the sampled row positions of every frontier node, in frontier order.
 // With `po` (the last hop of a pack run) the absolute CSR entries, pos_ptr
 // and dst_ids go straight into the pack, h.pos / h.ent stay empty, and the
-// destinations left empty by the self rule are counted on the way (only a
-// lone entry can be self: one col read for those).
+// destinations left empty by the self rule are counted on the way when asked
+// (only a lone entry can be self: one col read — a cache miss — for those).
 static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = nullptr, int32_t hop = 0,
-                           bool gcn = false) {
+                           bool gcn = false, bool count_empties = false) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
     int32_t* pptr;
     if (po) {
@@ -133,9 +133,9 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = n
                 for (int64_t t = 0; t < d; ++t) posv[pptr[r] + t] = static_cast<int32_t>(t);
             for (int64_t t = 0; t < d; ++t) ep[t] = rs + static_cast<int32_t>(t);
         }
-        if (po && !gcn) empty += cnt == 0 || (cnt == 1 && g.col[ep[0]] == h.dst_ids[r]);
+        if (count_empties && !gcn) empty += cnt == 0 || (cnt == 1 && g.col[ep[0]] == h.dst_ids[r]);
     }
-    if (po) h.n_empty = empty;
+    if (po) h.n_empty = empty;  // 0 unless counted
 }
 
 // Destinations left without neighbours once self is removed (non-gcn): the
@@ -207,8 +207,8 @@ static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::
         const int64_t cnt = h.pos_ptr[r + 1] - h.pos_ptr[r];
         if (h.k > 0 && d >= h.k) {
             // set(random.sample(adj, k)) : adds in result order
-            s.reset();
-            for (int64_t q = 0; q < cnt; ++q) s.add(g.col[rs + h.pos[h.pos_ptr[r] + q]]);
+            s.reset();  // the sampled entries are distinct positions of one row: distinct keys
+            for (int64_t q = 0; q < cnt; ++q) s.add_absent(g.col[rs + h.pos[h.pos_ptr[r] + q]]);
             copy_into(t, s);  // samp_neigh | set([v])  (:285)
         } else {
             // the adjacency set object itself (its own table layout; dummies
@@ -437,8 +437,7 @@ static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const in
         h.dst_ids.swap(frontier);
         const bool last = (j == n_hops - 1);
         if (last && po) {
-            draw_positions(g, rng, h, po, j, gcn);  // pos_ptr, entries, dst_ids into the pack; n_empty
-            if (!count_empties) h.n_empty = 0;
+            draw_positions(g, rng, h, po, j, gcn, count_empties);  // pos_ptr, entries, dst_ids into the pack
             GS_PHASE(4);
             continue;
         }
