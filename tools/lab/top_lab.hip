@@ -74,6 +74,16 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     std::printf("top kernel: %.2f us per launch (back to back, %d launches)\n", ms * 1e3 / reps, reps);
+    {  // outputs' bit pattern (variants must agree bit for bit)
+        std::vector<uint32_t> hE(B * H), hI(B * K), hZ(B * H);
+        CK(hipMemcpy(hE.data(), E, B * H * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hI.data(), dIn, B * K * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hZ.data(), dZ, B * H * 4, hipMemcpyDeviceToHost));
+        unsigned long long hsh = 1469598103934665603ull;
+        for (auto* v : {&hE, &hZ, &hI})
+            for (uint32_t x : *v) hsh = (hsh ^ x) * 1099511628211ull;
+        std::printf("  outputs hash %016llx\n", hsh);
+    }
     // stamps of one launch
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
     CK(hipMemset(st, 0, nb * 64));
