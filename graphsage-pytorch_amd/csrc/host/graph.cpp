@@ -2,6 +2,7 @@
 // (dataCenter.py:33-41 / :77-86 semantics) and the synthetic R-MAT pair
 // generator used for the 2M/16M configs.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -216,6 +217,42 @@ Graph* graph_from_image(const void* img, int64_t bytes) {
     if (hdr[5]) g->dirty.view(b + L.dirty, n_nodes);
     GS_REQUIRE(g->row_ptr.data()[0] == 0 && g->row_ptr.data()[n_nodes] == n_entries, GS_EINVAL,
                "image row_ptr inconsistent with its entry count");
+    // Everything the samplers index memory with, checked once (a truncated or
+    // stale /dev/shm image must fail here, not read out of bounds later):
+    // row_ptr monotone, every col in [0, n_nodes), each row's table size
+    // a power of two above its degree, every slot inside its row's table,
+    // and the header's max degree.
+    std::atomic<int> bad{0};
+    std::atomic<int64_t> maxd{0};
+    const int64_t* rp = g->row_ptr.data();
+    const int32_t* col = g->col.data();
+    const uint32_t* sl = g->slot.data();
+    const uint8_t* l2 = g->log2size.data();
+    const int32_t nthr = static_cast<int32_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    parallel_chunks(n_nodes, nthr, [&](int64_t lo, int64_t hi, int32_t) {
+        int local = 0;
+        int64_t md = 0;
+        for (int64_t v = lo; v < hi && !local; ++v) {
+            const int64_t a = rp[v], e = rp[v + 1], d = e - a;
+            if (d < 0 || a < 0 || e > n_entries || l2[v] > 31 || (d > 0 && (int64_t(1) << l2[v]) <= d)) {
+                local = 1;
+                break;
+            }
+            md = std::max(md, d);
+            const uint32_t tsz = uint32_t(1) << l2[v];
+            for (int64_t t = a; t < e; ++t)
+                if (col[t] < 0 || col[t] >= n_nodes || sl[t] >= tsz) {
+                    local = 1;
+                    break;
+                }
+        }
+        if (local) bad.store(1);
+        int64_t cur = maxd.load();
+        while (md > cur && !maxd.compare_exchange_weak(cur, md)) {
+        }
+    });
+    GS_REQUIRE(!bad.load(), GS_EINVAL, "graph image corrupt: row_ptr, col, table sizes or slots out of range");
+    GS_REQUIRE(maxd.load() == g->max_degree, GS_EINVAL, "graph image corrupt: max degree differs from its rows");
     return g.release();
 }
 

@@ -109,3 +109,33 @@ def test_image_rejects_garbage(tmp_path):
     import pytest
     with pytest.raises(Exception):
         gs.CSRGraph.from_image(str(p))
+
+
+def test_image_rejects_corrupt_rows(tmp_path):
+    """A well-formed header over corrupt arrays (a stale or half-written
+    /dev/shm file) fails at load: a col entry out of range, then a row_ptr
+    that is not monotone — never an out-of-bounds read in the samplers."""
+    import numpy as np
+    import pytest
+    src, dst = gs.rmat_pairs(10, 5000, seed=3)
+    g = gs.CSRGraph.from_pairs(src, dst, 1 << 10)
+    path = tmp_path / "g.img"
+    g.write_image(str(path))
+    assert gs.CSRGraph.from_image(str(path)).n_entries == g.n_entries  # the intact image loads
+    raw = bytearray(path.read_bytes())
+    n, e = g.n_nodes, g.n_entries
+    al = lambda x: (x + 63) // 64 * 64  # noqa: E731
+    off_rp = 64
+    off_col = al(off_rp + 8 * (n + 1))
+    bad = bytearray(raw)
+    bad[off_col:off_col + 4] = np.array([n + 5], np.int32).tobytes()  # col[0] past n_nodes
+    p1 = tmp_path / "bad_col.img"
+    p1.write_bytes(bytes(bad))
+    with pytest.raises(ValueError, match="corrupt"):
+        gs.CSRGraph.from_image(str(p1))
+    bad = bytearray(raw)
+    bad[off_rp + 8:off_rp + 16] = np.array([e + 1], np.int64).tobytes()  # row_ptr[1] > row_ptr[n]
+    p2 = tmp_path / "bad_rp.img"
+    p2.write_bytes(bytes(bad))
+    with pytest.raises(ValueError, match="corrupt"):
+        gs.CSRGraph.from_image(str(p2))
