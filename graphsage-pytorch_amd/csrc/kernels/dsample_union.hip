@@ -64,6 +64,13 @@ constexpr int kKPT = (kUnionMax * 3 / 5) / 1024 + 1;
 constexpr int kStageKeys = kKPT * 1024;
 constexpr size_t kUnionLds = (kUnionMax + kStageKeys) * sizeof(uint32_t);  // table + a stage's old keys
 
+// Keys per lane of ublock's one-wave stages (stages of at most 64 * KPL keys;
+// A/B build switch: -DGS_UNION_KPL=8 takes stages up to 512 keys in one wave).
+#ifndef GS_UNION_KPL
+#define GS_UNION_KPL 4
+#endif
+constexpr int kUnionKpl = GS_UNION_KPL;
+
 }  // namespace
 
 // ---- one wave per set: CPython's set operations on a 128-slot LDS table,
@@ -785,21 +792,21 @@ __global__ __launch_bounds__(1024) void ublock_kernel(Ctl* c, HopBufs hb, UnionB
         // per-node sets' wave-level insert, four keys per lane) — no block
         // barrier inside the stage.
         const int nk_w = ub.ubef[st_run[s + 1]];  // the union's size after the stage
-        if (nk_w <= 256 && !(s == 0 && m == m_first)) {  // uniform
+        if (nk_w <= 64 * kUnionKpl && !(s == 0 && m == m_first)) {  // uniform
             if (tid < 64) {
                 const volatile int32_t* P = s == 0 ? reinterpret_cast<const volatile int32_t*>(ub.first_tab)
                                                    : reinterpret_cast<const volatile int32_t*>(T);
                 volatile int32_t* K = need;
                 const int n_old = w_compact(P, prev_mask, K);
                 const int f0 = ub.ubef[st_run[s]] - used0;
-                int32_t kk[4];
+                int32_t kk[kUnionKpl];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < kUnionKpl; ++q) {
                     const int t = tid + 64 * q;
                     kk[q] = t < n_old ? K[t] : (t < nk_w ? ub.fresh[f0 + t - n_old] : 0);
                 }
                 bool bad = false;
-                w_stage_n<4>(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk, bad);
+                w_stage_n<kUnionKpl>(reinterpret_cast<volatile int32_t*>(T), m, nk_w, kk, bad);
                 if (__ballot(bad) && tid == 0) s_bad = 2;
             }
             __syncthreads();
