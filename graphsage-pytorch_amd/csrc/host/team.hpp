@@ -28,10 +28,14 @@ namespace gs {
 
 class Team {
   public:
-    // spin: pause rounds a helper polls for the next job before sleeping
-    // (0 for a caller whose jobs come once per step: idle helpers then leave
-    // the cores to the other host threads at once).
-    explicit Team(int helpers, int spin = 20000) : spin_(spin) {
+    // spin_us: how long a helper polls for the next job before sleeping on
+    // the condition variable, in microseconds of wall time (a pause count
+    // spans 4-10x different times on different CPUs).  A sampler stream's
+    // jobs come every ~0.1-0.3 ms, so its helpers stay awake between them
+    // (a futex wake-up at each batch's set builds cost tens of microseconds);
+    // 0 for a caller whose jobs come once per step: idle helpers then leave
+    // the cores to the other host threads at once.
+    explicit Team(int helpers, int spin_us = 500) : spin_us_(spin_us) {
         for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
     }
     ~Team() {
@@ -124,9 +128,13 @@ class Team {
         uint64_t seen = gen_.load();
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
-            for (int spin = 0; g == seen && spin < spin_; ++spin) {
-                _mm_pause();
-                g = gen_.load(std::memory_order_acquire);
+            if (g == seen && spin_us_ > 0) {
+                const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+                for (uint32_t spin = 1; g == seen; ++spin) {
+                    _mm_pause();
+                    g = gen_.load(std::memory_order_acquire);
+                    if ((spin & 255) == 0 && std::chrono::steady_clock::now() > until) break;
+                }
             }
             if (g == seen) {
                 std::unique_lock<std::mutex> lk(mu_);
@@ -151,7 +159,7 @@ class Team {
     std::mutex mu_;
     std::condition_variable cv_;
     bool stop_ = false;
-    int spin_;
+    int spin_us_;
 };
 
 }  // namespace gs
