@@ -86,6 +86,7 @@ _SIGS = {
     "gs_sample_pack_run_multi": (_i32, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp, _vp,
                                         _p(_i64)]),
     "gs_team_create": (_i32, [_i32, _p(_vp)]),
+    "gs_team_create_shared": (_i32, [_vp, _p(_vp)]),
     "gs_team_destroy": (None, [_vp]),
     "gs_sample_pack_run_multi_team": (_i32, [_vp, _vp, _vp, _i64, _i64, _vp, _i32, _i32, _vp, _i64, _vp,
                                              _vp, _p(_i64), _vp]),

@@ -256,7 +256,7 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     };
     const bool helped = team && nch > 1;
     if (helped)
-        team->start(team->helpers(), [&](int) {
+        team->start(static_cast<int>(std::min<int64_t>(team->helpers(), nch - 1)), [&](int) {
             for (int64_t c; (c = sc.next_chunk.fetch_add(1, std::memory_order_relaxed)) < nch;) build(c);
         });
     PySet& u = sc.u;
@@ -787,6 +787,13 @@ int gs_team_create(int32_t helpers, gs_team** out) {
     GS_API_BEGIN
     GS_REQUIRE(out && helpers >= 0 && helpers <= 64, GS_EINVAL, "helpers out of [0, 64]");
     *out = reinterpret_cast<gs_team*>(new gs::Team(helpers));
+    GS_API_END
+}
+
+int gs_team_create_shared(const gs_team* peer, gs_team** out) {
+    GS_API_BEGIN
+    GS_REQUIRE(out && peer, GS_EINVAL, "null team");
+    *out = reinterpret_cast<gs_team*>(new gs::Team(reinterpret_cast<const gs::Team*>(peer)->pool()));
     GS_API_END
 }
 

@@ -752,10 +752,20 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         for (auto& p : r->dpack) hip_ok(hipMalloc(&p, r->dcap * sizeof(int32_t)), "hipMalloc(pack)");
         r->dres.resize(r->n_dpack);
     }
+    // GS_SHARED_HELPERS=1: one pool of S x helpers threads behind all the
+    // streams' teams (a stream's set builds take the helpers the others leave
+    // idle) instead of helpers private to each stream.
+    const char* shared_env = std::getenv("GS_SHARED_HELPERS");
+    const bool shared_helpers = shared_env && std::atoi(shared_env) == 1;
     for (int32_t w = 0; w < S && !r->devmode; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
-        if (cfg->helpers > 0 && gs_team_create(cfg->helpers, &s->team) != GS_OK) fail(GS_EINVAL, gs_last_error());
+        if (cfg->helpers > 0) {
+            const int rc = shared_helpers && w > 0 ? gs_team_create_shared(r->streams[0]->team, &s->team)
+                                                   : gs_team_create(shared_helpers ? cfg->helpers * S : cfg->helpers,
+                                                                    &s->team);
+            if (rc != GS_OK) fail(GS_EINVAL, gs_last_error());
+        }
         for (int64_t b = w; b < r->n_units; b += S) s->batches.push_back(b);
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {

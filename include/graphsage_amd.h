@@ -218,6 +218,11 @@ int gs_sample_pack_run_multi(const gs_graph* g, gs_rng* rng, const int64_t* root
  * calling thread at a time. */
 typedef struct gs_team gs_team;
 int gs_team_create(int32_t helpers, gs_team** out);
+/* A second handle on peer's helper threads (one pool for several sampling
+ * streams: a stream's set builds take whatever helpers the others leave
+ * idle).  Each handle still serves one calling thread; the threads live
+ * until the last handle on them is destroyed. */
+int gs_team_create_shared(const gs_team* peer, gs_team** out);
 void gs_team_destroy(gs_team* team);
 /* gs_sample_pack_run_multi with a team (NULL: none). */
 int gs_sample_pack_run_multi_team(const gs_graph* g, gs_rng* rng, const int64_t* roots,

@@ -423,6 +423,66 @@ def test_team_pack_equals_single_thread(gs, helpers, fan, group):
         L.lib().gs_team_destroy(team)
 
 
+def test_shared_team_streams_equal_single_thread(gs):
+    """Three sampling streams on three threads whose teams share one pool of
+    helpers (gs_team_create_shared, the runner's GS_SHARED_HELPERS layout):
+    a helper builds whichever stream's sets are posted, and every stream's
+    packs must still equal its team-less run's bit for bit."""
+    import threading
+    L = gs._lib
+    G_, _ = _graph(gs, "rmat")
+    fan = np.array((25, 10), np.int32)
+    nh = len(fan)
+    cand = np.nonzero(G_.degrees())[0]
+    n_streams, n_batches = 3, 5
+    roots = [[np.random.RandomState(10 * w + b).choice(cand, 300).astype(np.int64) for b in range(n_batches)]
+             for w in range(n_streams)]
+    want = []
+    for w in range(n_streams):
+        r = gs.RNG(100 + w)
+        want.append([_pack_run(gs, G_, r, roots[w][b], fan, None) for b in range(n_batches)])
+    first = ctypes.c_void_p()
+    L.check(L.lib().gs_team_create(2 * n_streams, ctypes.byref(first)))
+    teams = [first]
+    for _ in range(n_streams - 1):
+        t = ctypes.c_void_p()
+        L.check(L.lib().gs_team_create_shared(first, ctypes.byref(t)))
+        teams.append(t)
+    got = [[None] * n_batches for _ in range(n_streams)]
+    errors = []
+
+    def stream(w):
+        try:
+            r = gs.RNG(100 + w)
+            bound = int(L.lib().gs_sample_pack_bound_multi(G_.handle, 300, 300, fan.ctypes.data, nh))
+            for b in range(n_batches):
+                buf = np.full(bound, -7, np.int32)
+                sizes = np.empty(4 * nh, np.int64)
+                offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+                used = ctypes.c_int64()
+                L.check(L.lib().gs_sample_pack_run_multi_team(
+                    G_.handle, r._h, roots[w][b].ctypes.data, 300, 300, fan.ctypes.data, nh, 0, buf.ctypes.data,
+                    bound, sizes.ctypes.data, offs.ctypes.data, ctypes.byref(used), teams[w]))
+                got[w][b] = (buf[:used.value].copy(), sizes.reshape(nh, 4).copy())
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    try:
+        th = [threading.Thread(target=stream, args=(w,)) for w in range(n_streams)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        for t in reversed(teams):
+            L.lib().gs_team_destroy(t)
+    assert not errors, errors
+    for w in range(n_streams):
+        for b in range(n_batches):
+            assert np.array_equal(got[w][b][0], want[w][b][0]), (w, b)
+            assert np.array_equal(got[w][b][1], want[w][b][1]), (w, b)
+
+
 @pytest.mark.parametrize("scale,pairs,batch", [(12, 40_000, 64), (16, 600_000, 512)])
 def test_runner_pack_matches_oracle_per_root(gs, scale, pairs, batch):
     """The pack the runner's sampler threads write (gs_sample_pack_run_multi_team

@@ -5,9 +5,10 @@
 //   g++ -O3 -march=x86-64-v3 -std=c++17 -pthread -I include -I graphsage-pytorch_amd/csrc/host \
 //       tools/sampler_bench.cpp graphsage-pytorch_amd/csrc/host/graph.cpp \
 //       graphsage-pytorch_amd/csrc/host/errors.cpp -o /tmp/sampler_bench
-//   /tmp/sampler_bench [helpers=1] [batches=300] [streams=1]
+//   /tmp/sampler_bench [helpers=1] [batches=300] [streams=1] [shared=0]
 // With streams > 1, that many independent streams run on their own threads
-// (each with its own team), as the runner's layout does.
+// (each with its own team), as the runner's layout does; shared=1 gives them
+// one pool of helpers x streams threads (GS_SHARED_HELPERS=1 in the runner).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -35,6 +36,7 @@ int main(int argc, char** argv) {
     const int helpers = argc > 1 ? std::atoi(argv[1]) : 1;
     const int batches = argc > 2 ? std::atoi(argv[2]) : 300;
     const int streams = argc > 3 ? std::atoi(argv[3]) : 1;
+    const bool shared = argc > 4 && std::atoi(argv[4]) == 1;
     const int scale = 21;
     const int64_t pairs = 20000000, n = int64_t(1) << scale;
     std::vector<int64_t> src(pairs), dst(pairs);
@@ -50,6 +52,8 @@ int main(int argc, char** argv) {
     const int64_t B = 512;
     std::vector<double> per(streams, 0.0);
     std::vector<uint64_t> check(streams, 0);
+    gs_team* pool = nullptr;  // shared mode: the handle the streams' teams share threads with
+    if (shared && helpers > 0) gs_team_create(helpers * streams, &pool);
     auto body = [&](int w) {
         t_main = w == 0;
         gs_rng* rng = nullptr;
@@ -57,7 +61,8 @@ int main(int argc, char** argv) {
         const uint32_t key = 824 + 64 * w;
         gs_rng_seed_words(rng, &key, 1);
         gs_team* team = nullptr;
-        if (helpers > 0) gs_team_create(helpers, &team);
+        if (pool) gs_team_create_shared(pool, &team);
+        else if (helpers > 0) gs_team_create(helpers, &team);
         const int64_t cap = gs_sample_pack_bound(gp, B, fan, 2) + B;
         std::vector<int32_t> buf(cap);
         int64_t hs[4 * GS_MAX_HOPS], off[GS_MAX_HOPS * GS_PK_NFIELDS], used = 0;
@@ -108,8 +113,9 @@ int main(int argc, char** argv) {
     std::printf("stream 0 phases (us per batch): draws hop 1 %.1f, sets + union %.1f, frontier %.1f, last-hop draws %.1f, "
                 "join %.1f\n", g_phase[1] / batches, g_phase[2] / batches, g_phase[3] / batches, g_phase[4] / batches,
                 g_phase[5] / batches);
-    std::printf("helpers %d streams %d: %.1f us per batch per stream, %.0f batches/s total; pack hash %016llx\n",
-                helpers, streams, mean, streams * batches / wall, static_cast<unsigned long long>(check[0]));
+    gs_team_destroy(pool);
+    std::printf("helpers %d streams %d%s: %.1f us per batch per stream, %.0f batches/s total; pack hash %016llx\n",
+                helpers, streams, shared ? " shared" : "", mean, streams * batches / wall, static_cast<unsigned long long>(check[0]));
     gs_graph_destroy(gp);
     return 0;
 }
