@@ -72,6 +72,41 @@ __device__ __forceinline__ void signal_done(int64_t* done, int64_t value) {
         __hip_atomic_store(done, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One group's squared norm from its np partials, as every clip of this
+// library folds them (lane-strided, then a fixed xor tree; identical on every
+// lane, in every kernel, for any block size).
+__device__ __forceinline__ float clip_fold(const float* __restrict__ pg, int np, int lane) {
+    float t = 0.f;
+    constexpr int kPre = 8;
+    if (np > 0 && np <= 64 * kPre) {
+        // every partial of the lane loaded before the first add (clamped
+        // addresses, the count tested after the loads): one memory round;
+        // adding +0 past the count leaves t unchanged
+        float v[kPre];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) v[u] = pg[min(lane + 64 * u, np - 1)];
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) t += lane + 64 * u < np ? v[u] : 0.f;
+    } else {
+#pragma unroll 4
+        for (int b = lane; b < np; b += 64) t += pg[b];
+    }
+    return wave_sum(t);
+}
+
+// clip_grad_norm_'s coefficient (utils.py:186), times the gradient scale.
+__device__ __forceinline__ float clip_mult(float sumsq, float scale, float max_norm) {
+    const float norm = sqrtf(sumsq) * scale;
+    return scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
+}
+
+// One parameter's clip + SGD step: the clipped gradient to gi, the new value
+// returned (p.add_(g, alpha=-lr), utils.py:190; one rounding, as contracted).
+__device__ __forceinline__ float sgd_elem(float p, float g, float m, float lr, float& gi) {
+    gi = g * m;
+    return fmaf(-lr, gi, p);
+}
+
 // Clip (per group, utils.py:186-187) + SGD (utils.py:187-190) on float4
 // (every group offset a multiple of 4, 16-B aligned arrays), block bx of
 // nblk: wave w folds group w's norm partials (lane-strided loads, then a
@@ -97,28 +132,8 @@ __device__ __forceinline__ void sgd4_body(const Groups& G, float* __restrict__ p
     // the group index wave-uniform in an SGPR: its npart is a scalar kernarg
     // load, not a vector load whose wait would also drain the g / p loads above
     for (int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); grp < G.n; grp += nthr / 64) {
-        const float* pg = part + grp * G.pstride;
-        const int np = G.npart[grp];
-        float t = 0.f;
-        constexpr int kPre = 8;
-        if (np > 0 && np <= 64 * kPre) {
-            // every partial of the lane loaded before the first add (clamped
-            // addresses, the count tested after the loads): one memory round;
-            // adding +0 past the count leaves t unchanged
-            float v[kPre];
-#pragma unroll
-            for (int u = 0; u < kPre; ++u) v[u] = pg[min(lane + 64 * u, np - 1)];
-#pragma unroll
-            for (int u = 0; u < kPre; ++u) t += lane + 64 * u < np ? v[u] : 0.f;
-        } else {
-#pragma unroll 4
-            for (int b = lane; b < np; b += 64) t += pg[b];
-        }
-        t = wave_sum(t);
-        if (lane == 0) {
-            const float norm = sqrtf(t) * scale;
-            mult[grp] = scale * fminf(max_norm / (norm + 1e-6f), 1.0f);
-        }
+        const float t = clip_fold(part + grp * G.pstride, G.npart[grp], lane);
+        if (lane == 0) mult[grp] = clip_mult(t, scale, max_norm);
     }
     __syncthreads();
     for (int64_t i = i0; i < n4; i += int64_t(nblk) * nthr) {
@@ -129,17 +144,12 @@ __device__ __forceinline__ void sgd4_body(const Groups& G, float* __restrict__ p
         int grp = 0;
         while (4 * i >= G.off[grp + 1]) ++grp;
         const float m = mult[grp];
-        float4 gi;
-        gi.x = gv.x * m;
-        gi.y = gv.y * m;
-        gi.z = gv.z * m;
-        gi.w = gv.w * m;
+        float4 gi, pn;
+        pn.x = sgd_elem(pv.x, gv.x, m, lr, gi.x);
+        pn.y = sgd_elem(pv.y, gv.y, m, lr, gi.y);
+        pn.z = sgd_elem(pv.z, gv.z, m, lr, gi.z);
+        pn.w = sgd_elem(pv.w, gv.w, m, lr, gi.w);
         g4[i] = gi;
-        float4 pn;
-        pn.x = pv.x - lr * gi.x;
-        pn.y = pv.y - lr * gi.y;
-        pn.z = pv.z - lr * gi.z;
-        pn.w = pv.w - lr * gi.w;
         p4[i] = pn;
         if (G.sh && 4 * i >= G.sh_lo && 4 * i < G.sh_hi) {  // sh_lo, sh_hi multiples of 4
             uint2 b;

@@ -31,6 +31,12 @@ void trainer_keep_lowp(gs_trainer* t, bool keep);
 // Inside a runner loop without an all-reduce: the step's last launch runs the
 // clip + SGD too (gs_trainer_update_local is then a no-op for that step).
 void trainer_fuse_update(gs_trainer* t, bool fuse);
+// Inside a runner loop without an all-reduce (fp32 2-layer steps): defer each
+// step's clip + SGD into the next step's launches (gs_trainer fields defer /
+// pending).  Returns whether deferral is on; off (at the end of the loop)
+// applies the last pending update, so the flat parameters and gradients are
+// those of the separate update launch.
+bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st);
 // A fused SGD launch's grid barrier gave up waiting (never expected).
 bool trainer_barrier_failed(gs_trainer* t);
 int64_t trainer_w1_floats(const gs_trainer* t);
@@ -64,7 +70,14 @@ struct SlabSum {
 // Both sums in one launch (s1 the split layer-1 sum, s2 a deferred layer-2
 // sum, S2 <= 1 = nothing to add); returns s1's partial count.
 bool sum_slabs_pair_ok(int64_t len1);
-int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st);
+// spec_S: also W1's speculative update spec_S = spec_P - lr·(layer-1 sum) (the
+// trainer's deferred update), and the launch takes the done flag (g_done_flag).
+int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P = nullptr,
+                          float* spec_S = nullptr, float lr = 0.f);
+// The pending update's tail at the end of a deferred-update run: the flat
+// parameters and gradients become what the separate clip + SGD launch would
+// have left (W1 from sp.S or recomputed into w1_out, the others updated).
+void spec_finalize_launch(const FwdSpec& sp, float* w1_out, int64_t w1_floats, hipStream_t st);
 // The clip + SGD that follows a step's last slab sum (no all-reduce between):
 // flat params / grads, group offsets and norm partials as sgd_with_parts
 // takes them, the bf16 W1 shadow (g_lowp_shadow) and the done flag

@@ -138,6 +138,30 @@ struct LowpShadow {
 };
 inline thread_local LowpShadow g_lowp_shadow;
 
+// A clip + SGD left pending by the previous step (gs_trainer in deferred-update
+// mode, step.hip), applied by the next layer-1 forward launch of this thread
+// (the fp32 wide kernel), then cleared.  The step's last slab sum wrote
+// S = W1 - lr·G1, W1's update when the clip coefficient of its group is 1;
+// every workgroup of the forward folds the norm partials itself and reads S
+// as W1 when it is, else writes W1 - lr·(coef·G1) into S's buffer first.  The
+// forward's grid also applies the pending update to the flat parameters
+// [up_lo, up_hi) (W2, Wc, bc: read only after the forward).
+struct FwdSpec {
+    int on = 0;
+    const float* S = nullptr;    // W1 - lr·G1 (clip coefficient 1)
+    const float* P = nullptr;    // W1 before the update
+    float* Wn = nullptr;         // S's buffer: the updated W1 when the coefficient is not 1
+    const float* G1 = nullptr;   // W1's gradient
+    const float* part0 = nullptr;  // norm partials, group 0 (the sage weights) and 1 (the classifier)
+    const float* part1 = nullptr;
+    int np0 = 0, np1 = 0;
+    float lr = 0.f, max_norm = 0.f;
+    float* p = nullptr;          // flat params / grads
+    float* g = nullptr;
+    int64_t up_lo = 0, up_hi = 0, grp1_lo = 0;  // the other parameters; group 1 from grp1_lo
+};
+inline thread_local FwdSpec g_fwd_spec;
+
 template <typename... KArgs, typename... Args>
 inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
     LaunchEvents ev = g_launch_events;

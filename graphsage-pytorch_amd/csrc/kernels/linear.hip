@@ -22,12 +22,22 @@ __global__ __launch_bounds__(kThreads) void sum_slabs_kernel(const float* __rest
 // loads instead of S: at the layer-1 dW (31 slabs of 64 Ki floats) and 8
 // waves, one round of 4 loads instead of eight rounds, over 256 blocks
 // instead of 65.  len % 4 == 0.
+// With spec (the trainer's deferred update): also S = P - lr·sum, W1's SGD
+// step when its clip coefficient turns out to be 1 (sgd_elem with m = 1).
+struct SlabSpec {
+    const float* P = nullptr;
+    float* S = nullptr;
+    float lr = 0.f;
+};
 __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __restrict__ slabs, int S, int64_t len,
-                                                     float* __restrict__ out, float* __restrict__ part) {
+                                                     float* __restrict__ out, float* __restrict__ part,
+                                                     SlabSpec spec = {}) {
     __shared__ float4 red[kSlabParts - 1][64];
     const int q = threadIdx.x >> 6, c = threadIdx.x & 63;
     const int64_t n4 = len / 4;
     const int64_t i = bx * int64_t(64) + c;
+    float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (spec.S && q == 0 && i < n4) pv = reinterpret_cast<const float4*>(spec.P)[i];  // with the slab loads
     const int per = (S + kSlabParts - 1) / kSlabParts;
     const int t0 = min(S, q * per), t1 = min(S, t0 + per);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -60,6 +70,14 @@ __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __rest
         }
         *reinterpret_cast<float4*>(out + 4 * i) = s;
         sq = fmaf(s.x, s.x, sq); sq = fmaf(s.y, s.y, sq); sq = fmaf(s.z, s.z, sq); sq = fmaf(s.w, s.w, sq);
+        if (spec.S) {
+            float4 pn, gi;
+            pn.x = sgd_elem(pv.x, s.x, 1.0f, spec.lr, gi.x);
+            pn.y = sgd_elem(pv.y, s.y, 1.0f, spec.lr, gi.y);
+            pn.z = sgd_elem(pv.z, s.z, 1.0f, spec.lr, gi.z);
+            pn.w = sgd_elem(pv.w, s.w, 1.0f, spec.lr, gi.w);
+            reinterpret_cast<float4*>(spec.S)[i] = pn;
+        }
     }
     if (part) block_sum_to(sq, part + bx);
 }
@@ -75,13 +93,19 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const 
 // blocks [0, nb2) the layer-2 dW slabs as sum_slabs_body over nb2 blocks of
 // kThreads (the other threads of these wider blocks only join the partial's
 // reduction) -- each bitwise its standalone kernel, partials where those write.
-__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2) {
+// With spec.S (the trainer's deferred update) the layer-1 sum also writes W1's
+// speculative update, and the launch stores the step's done flag (the
+// runner's completion signal, otherwise stored by the SGD launch).
+__global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2,
+                                                                         SlabSpec spec, int64_t* done,
+                                                                         int64_t done_value) {
+    signal_done(done, done_value);
     const int bx = blockIdx.x;
     if (bx < nb2) {  // the longer per-block chains first
         sum_slabs_body(bx, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
         return;
     }
-    sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part);
+    sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part, spec);
 }
 
 // sum_slabs_pair_kernel, then every block waits at a grid barrier (all
@@ -296,6 +320,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && F < (1 << 28), GS_EINVAL, "bad sizes");
     GS_REQUIRE(H >= 16 && H <= 256 && H % 16 == 0, GS_EINVAL, "out_size must be a multiple of 16 in [16, 256]");
     GS_REQUIRE(lda >= F && ldo >= H && (!Xs || ldxs >= F), GS_EINVAL, "leading dimension too small");
+    GS_REQUIRE(n > 0 || !g_fwd_spec.on, GS_EINVAL, "pending update with no rows");
     if (n == 0) return GS_OK;
     GS_REQUIRE(A && Wd && out, GS_EINVAL, "NULL device pointer");
     const bool self = Xs != nullptr;
@@ -305,8 +330,14 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                        aligned16(A) && aligned16(Wd);
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
+    // a pending clip + SGD (the trainer's deferred update): the fp32 wide kernel applies it
+    const FwdSpec sp = g_fwd_spec;
+    g_fwd_spec = {};
+    GS_REQUIRE(!sp.on || (dt == GS_F32 && Wd == sp.S && K % 4 == 0), GS_EINVAL, "pending update: bad forward");
     // read per call (tests switch it between launches): wres | wide32 | wide | sk | chunked
     const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
+    GS_REQUIRE(!sp.on || fwd_mode.empty() || fwd_mode == "wide" || fwd_mode == "wide32", GS_EINVAL,
+               "pending update needs the wide forward");
     // fp32 default: 32-row W-in-LDS tiles (bitwise the chunked kernel's sums:
     // same MFMA operands in the same order).  In-step at rmat2m the step ran
     // 80.2-80.7 us against 82.3-82.4 us with the 16-row chunked kernel, which
@@ -398,7 +429,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
 #define GS_LFWDW(TT, RR, SELF, RELU_)                                                                         \
         launch_k(linear_fwd_wide_kernel<TT, RR, SELF, RELU_>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K,            \
                  static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda, static_cast<const TT*>(Wd), \
-                 out, ldo)
+                 out, ldo, sp)
 #define GS_LFWDW_R(TT, RR) \
         do { if (self) { if (relu) GS_LFWDW(TT, RR, true, true); else GS_LFWDW(TT, RR, true, false); } \
              else { if (relu) GS_LFWDW(TT, RR, false, true); else GS_LFWDW(TT, RR, false, false); } } while (0)
@@ -416,6 +447,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
         check_launch("gs_sage_linear_fwd(wide)");
         return GS_OK;
     }
+    GS_REQUIRE(!sp.on, GS_EINVAL, "pending update needs the wide forward (16-B aligned operands)");
     const dim3 grid(static_cast<unsigned>((n + 15) / 16), static_cast<unsigned>((H + 63) / 64));
 #define GS_LFWD1(TT, SELF, RELU, VL)                                                                     \
     launch_k(linear_fwd_kernel<TT, SELF, RELU, VL>, grid, dim3(kThreads), 0, st,                        \
@@ -550,13 +582,72 @@ int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* 
 
 bool sum_slabs_pair_ok(int64_t len1) { return slab_split_on(len1); }
 
-int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st) {
+int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P, float* spec_S,
+                          float lr) {
     GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1, GS_EINVAL, "slab pair: layer-1 sum not split");
     const int nb1 = static_cast<int>(slab_split_blocks(s1.len));
     const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
-    sum_slabs_pair_kernel<<<dim3(static_cast<unsigned>(nb1 + nb2)), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2);
+    SlabSpec spec;
+    DoneFlag done;
+    if (spec_S) {  // the step's last launch: it carries the done flag
+        GS_REQUIRE(spec_P && aligned16(spec_P) && aligned16(spec_S), GS_EINVAL, "slab pair: bad update buffers");
+        spec = SlabSpec{spec_P, spec_S, lr};
+        done = g_done_flag;
+        g_done_flag = {};
+    }
+    sum_slabs_pair_kernel<<<dim3(static_cast<unsigned>(nb1 + nb2)), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2, spec,
+                                                                                              done.ptr, done.value);
     check_launch("sum_slabs_pair");
     return nb1;
+}
+
+// The deferred update's last step (spec_finalize_launch): the groups' clip
+// coefficients from the norm partials (clip_fold, as every clip here), W1 =
+// S (coefficient 1) or P - lr·coef·G1 into w1_out with G1 scaled, and the
+// clip + SGD of the other parameters: what sgd4_kernel would have left.
+__global__ __launch_bounds__(kThreads) void spec_finalize_kernel(FwdSpec sp, float* __restrict__ w1_out,
+                                                                 int64_t w1_floats) {
+    const int lane = threadIdx.x & 63;
+    const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), 1.0f, sp.max_norm);
+    const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), 1.0f, sp.max_norm);
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x, t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    float4* G1 = reinterpret_cast<float4*>(const_cast<float*>(sp.G1));
+    const float4* S4 = reinterpret_cast<const float4*>(sp.S);
+    const float4* P4 = reinterpret_cast<const float4*>(sp.P);
+    float4* O4 = reinterpret_cast<float4*>(w1_out);
+    for (int64_t i = t; i < w1_floats / 4; i += stride) {
+        const float4 gv = G1[i];
+        const float4 pv = m0 == 1.0f ? S4[i] : P4[i];
+        float4 gi, pn;
+        pn.x = sgd_elem(pv.x, gv.x, m0, sp.lr, gi.x);
+        pn.y = sgd_elem(pv.y, gv.y, m0, sp.lr, gi.y);
+        pn.z = sgd_elem(pv.z, gv.z, m0, sp.lr, gi.z);
+        pn.w = sgd_elem(pv.w, gv.w, m0, sp.lr, gi.w);
+        G1[i] = gi;
+        O4[i] = m0 == 1.0f ? pv : pn;
+    }
+    float4* p4 = reinterpret_cast<float4*>(sp.p);
+    float4* g4 = reinterpret_cast<float4*>(sp.g);
+    for (int64_t i = sp.up_lo / 4 + t; i < sp.up_hi / 4; i += stride) {
+        const float m = 4 * i >= sp.grp1_lo ? m1 : m0;
+        const float4 pv = p4[i], gv = g4[i];
+        float4 gi, pn;
+        pn.x = sgd_elem(pv.x, gv.x, m, sp.lr, gi.x);
+        pn.y = sgd_elem(pv.y, gv.y, m, sp.lr, gi.y);
+        pn.z = sgd_elem(pv.z, gv.z, m, sp.lr, gi.z);
+        pn.w = sgd_elem(pv.w, gv.w, m, sp.lr, gi.w);
+        g4[i] = gi;
+        p4[i] = pn;
+    }
+}
+
+void spec_finalize_launch(const FwdSpec& sp, float* w1_out, int64_t w1_floats, hipStream_t st) {
+    GS_REQUIRE(sp.on && w1_floats % 4 == 0 && sp.up_lo % 4 == 0 && sp.up_hi % 4 == 0 && sp.grp1_lo % 4 == 0,
+               GS_EINVAL, "spec finalize: bad layout");
+    const int64_t n4 = std::max(w1_floats, sp.up_hi - sp.up_lo) / 4;
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + kThreads - 1) / kThreads, 256)));
+    spec_finalize_kernel<<<dim3(grid), kThreads, 0, st>>>(sp, w1_out, w1_floats);
+    check_launch("spec_finalize");
 }
 
 int sum_slabs_pair_sgd_launch(const SlabSum& s1, const SlabSum& s2, int np_before, const FusedSgd& u,

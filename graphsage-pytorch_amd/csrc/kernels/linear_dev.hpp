@@ -17,6 +17,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
+
+#include "cls_dev.hpp"
 
 #include "kcommon.hpp"
 
@@ -257,10 +260,62 @@ constexpr int kFwdAhead = GS_FWD_AHEAD;  // K chunks in flight ahead of the MFMA
 // T = bf16_t: the same tiles with 8 elements per slot (a chunk is 128 k) and
 // the 16x16x32 bf16 MFMA per slot pair — operands and order of the chunked
 // bf16 kernel (slots 4g + kq, chunks ascending), so bitwise its output.
+// The pending clip + SGD of the previous step (sp.on, fp32 only; FwdSpec in
+// kcommon.hpp), run in the forward's prologue: the flat parameters past W1
+// updated grid-stride (their readers come after this launch), and W1 read
+// from sp.S when its group's clip coefficient is 1 (W == sp.S then).  Else
+// the workgroup writes its own 64-row slice of the update into sp.Wn (= S's
+// buffer; every workgroup of a column tile writes the same values there) and
+// reads it back: the same W1 the separate SGD launch would have left, so the
+// same output bit for bit.  Returns whether the loads issued from W must be
+// issued again (they read the speculative update).
+__device__ __forceinline__ bool fwd_pending_update(const FwdSpec& sp, int H, int K, int c0) {
+    const int lane = threadIdx.x & 63;
+    const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), 1.0f, sp.max_norm);
+    const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), 1.0f, sp.max_norm);
+    {
+        const int64_t nthr = int64_t(gridDim.x) * gridDim.y * blockDim.x;
+        const int64_t t = (int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        float4* p4 = reinterpret_cast<float4*>(sp.p);
+        float4* g4 = reinterpret_cast<float4*>(sp.g);
+        for (int64_t i = sp.up_lo / 4 + t; i < sp.up_hi / 4; i += nthr) {
+            const float m = 4 * i >= sp.grp1_lo ? m1 : m0;
+            const float4 pv = p4[i], gv = g4[i];
+            float4 gi, pn;
+            pn.x = sgd_elem(pv.x, gv.x, m, sp.lr, gi.x);
+            pn.y = sgd_elem(pv.y, gv.y, m, sp.lr, gi.y);
+            pn.z = sgd_elem(pv.z, gv.z, m, sp.lr, gi.z);
+            pn.w = sgd_elem(pv.w, gv.w, m, sp.lr, gi.w);
+            g4[i] = gi;
+            p4[i] = pn;
+        }
+    }
+    if (m0 == 1.0f) return false;
+    // this column tile's rows of the update, then visible to the workgroup's own loads
+    const int k4 = K / 4, rows = min(64, H - c0);
+    const float4* P4 = reinterpret_cast<const float4*>(sp.P) + int64_t(c0) * k4;
+    const float4* G4 = reinterpret_cast<const float4*>(sp.G1) + int64_t(c0) * k4;
+    float4* N4 = reinterpret_cast<float4*>(sp.Wn) + int64_t(c0) * k4;
+    for (int i = threadIdx.x; i < rows * k4; i += blockDim.x) {
+        const float4 pv = P4[i], gv = G4[i];
+        float4 gi, pn;
+        pn.x = sgd_elem(pv.x, gv.x, m0, sp.lr, gi.x);
+        pn.y = sgd_elem(pv.y, gv.y, m0, sp.lr, gi.y);
+        pn.z = sgd_elem(pv.z, gv.z, m0, sp.lr, gi.z);
+        pn.w = sgd_elem(pv.w, gv.w, m0, sp.lr, gi.w);
+        N4[i] = pn;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale L1 lines of the speculative S
+    return true;
+}
+
 template <typename T, int ROWS, bool HAS_SELF, bool RELU>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
-    const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo) {
+    const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo,
+    FwdSpec sp) {
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
@@ -281,9 +336,14 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         const int gy = (H + 63) / 64, b = blockIdx.x;
         bx = (b / (8 * gy)) * 8 + (b & 7);
         by = (b >> 3) % gy;
-        if (bx * ROWS >= n) return;  // spare blocks of the last group of 8
     }
     const int m0 = bx * ROWS, c0 = by * 64;
+    bool pending = false;
+    if constexpr (std::is_same<T, float>::value) pending = sp.on != 0;
+    if (m0 >= n) {  // spare blocks of the last group of 8 (they still take their share of the update)
+        if (pending) fwd_pending_update(sp, H, K, c0);
+        return;
+    }
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
     const int arow_i = min(m0 + lr, n - 1);
     const T* arow = A + static_cast<int64_t>(arow_i) * lda;
@@ -309,6 +369,12 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     };
 #pragma unroll
     for (int u = 0; u < kFwdAhead; ++u) load(u, u);
+    // the pending update after the first loads (its fold then waits on the same round)
+    if (pending && fwd_pending_update(sp, H, K, c0)) {
+        // W1 is not the speculative update: read the one written above
+#pragma unroll
+        for (int u = 0; u < kFwdAhead; ++u) load(u, u);
+    }
     stash(0, 0);
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int c0 = 0; c0 < nC; c0 += kFwdAhead) {

@@ -77,7 +77,21 @@ struct gs_trainer {
     // each group's reducer resets its own), kDwGroupParts per 64x64 tile of W1
     int* dw_cnt = nullptr;
     int64_t dw_n_cnt = 0;
+    // Deferred update (trainer_defer_update, runner loops without an
+    // all-reduce): a step's clip + SGD is not a launch of its own.  The step's
+    // last slab sum writes W1's update for clip coefficient 1 into the other
+    // W1 buffer, and the next step's layer-1 forward applies the pending
+    // update (FwdSpec, kcommon.hpp): W1 from that buffer (or recomputed there
+    // when the coefficient is not 1), the other parameters in its prologue.
+    // The current W1 lives in w1_buf(w1_cur): buffer 0 is its place in the
+    // flat params, buffer 1 w1_alt; trainer_defer_update(false) puts the
+    // result of the last pending update back into the flat params.
+    bool defer = false, pending = false;
+    float* w1_alt = nullptr;
+    int w1_cur = 0;
+    float* w1_buf(int i) { return i == 0 ? cfg.params + w_off[0] : w1_alt; }
     ~gs_trainer() {
+        if (w1_alt) (void)hipFree(w1_alt);
         if (norm_part) (void)hipFree(norm_part);
         if (dw_cnt) (void)hipFree(dw_cnt);
         if (w1_lp) (void)hipFree(w1_lp);
@@ -280,6 +294,31 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
     const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
+    GS_REQUIRE(!T.defer || (!lowp && !fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
+    const bool pend = T.defer && T.pending;
+    if (T.defer) {
+        W1 = T.w1_buf(pend ? T.w1_cur ^ 1 : T.w1_cur);
+        if (pend) {  // the previous step's clip + SGD, applied by this forward launch
+            FwdSpec sp;
+            sp.on = 1;
+            sp.S = T.w1_buf(T.w1_cur ^ 1);
+            sp.P = T.w1_buf(T.w1_cur);
+            sp.Wn = T.w1_buf(T.w1_cur ^ 1);
+            sp.G1 = G + T.w_off[0];
+            sp.part0 = T.norm_part;
+            sp.part1 = T.norm_part + T.pstride;
+            sp.np0 = T.npart[0];
+            sp.np1 = T.npart[1];
+            sp.lr = c.lr;
+            sp.max_norm = c.max_norm;
+            sp.p = P;
+            sp.g = G;
+            sp.up_lo = T.w_off[0] + T.w_rows[0] * T.w_cols[0];
+            sp.up_hi = T.total;
+            sp.grp1_lo = T.cls_w_off;
+            g_fwd_spec = sp;
+        }
+    }
     if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
         const bool timed = timed_arm(T, 0);
         ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
@@ -295,6 +334,11 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                               dst_L, agg[0], F, W1, h[0], H, 1, st));
         g_launch_events = {};  // an alternative kernel that does not time leaves it armed
         timed_done(T, 1, armed);
+        if (pend) {  // the launch took the pending update: W1 is now the other buffer
+            GS_REQUIRE(!g_fwd_spec.on, GS_EINVAL, "the forward launch did not take the pending update");
+            T.w1_cur ^= 1;
+            T.pending = false;
+        }
         if (T.fwd1_hook && !embed_out) T.fwd1_hook(st);
     }
     // a 2-layer training step runs layer 2, the loss head and layer 2's dIn in
@@ -445,7 +489,15 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
             if (defer && S1 > 1) {
                 d2.part = T.norm_part;
-                np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st);
+                // deferred update: this launch also writes W1's update for clip
+                // coefficient 1 (and carries the done flag); the clip + SGD
+                // itself is left to the next forward
+                const bool spec = T.defer && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
+                                  n_cls <= T.pstride;
+                np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st,
+                                            spec ? T.w1_buf(T.w1_cur) : nullptr,
+                                            spec ? T.w1_buf(T.w1_cur ^ 1) : nullptr, c.lr);
+                T.pending = spec;
             } else if (defer) {
                 if (d2.S > 1) sum_slabs_launch(d2.slabs, d2.S, d2.len, d2.out, nullptr, st);
                 parts = false;
@@ -541,6 +593,59 @@ void trainer_keep_lowp(gs_trainer* t, bool keep) {
 void trainer_fuse_update(gs_trainer* t, bool fuse) {
     t->fuse_update = fuse;
     t->update_done = false;
+}
+
+// W1 back in the flat params (a pending update stays pending: its S and P
+// buffers are then the flat W1 and w1_alt, or it is finalised by the caller).
+static void w1_home(gs_trainer* t, hipStream_t st) {
+    if (t->w1_cur == 0) return;
+    GS_REQUIRE(!t->pending, GS_EINVAL, "W1 moved with an update pending");
+    const int64_t n = t->w_rows[0] * t->w_cols[0];
+    GS_REQUIRE(hipMemcpyAsync(t->w1_buf(0), t->w1_alt, n * sizeof(float), hipMemcpyDeviceToDevice, st) == hipSuccess,
+               GS_EHIP, "hipMemcpyAsync(W1)");
+    t->w1_cur = 0;
+}
+
+bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
+    if (!on) {
+        if (t->pending) {  // the last step's clip + SGD: the flat params become what sgd4 would leave
+            FwdSpec sp;
+            sp.on = 1;
+            sp.S = t->w1_buf(t->w1_cur ^ 1);
+            sp.P = t->w1_buf(t->w1_cur);
+            sp.G1 = t->cfg.grads + t->w_off[0];
+            sp.part0 = t->norm_part;
+            sp.part1 = t->norm_part + t->pstride;
+            sp.np0 = t->npart[0];
+            sp.np1 = t->npart[1];
+            sp.lr = t->cfg.lr;
+            sp.max_norm = t->cfg.max_norm;
+            sp.p = t->cfg.params;
+            sp.g = t->cfg.grads;
+            sp.up_lo = t->w_off[0] + t->w_rows[0] * t->w_cols[0];
+            sp.up_hi = t->total;
+            sp.grp1_lo = t->cls_w_off;
+            spec_finalize_launch(sp, t->w1_buf(0), t->w_rows[0] * t->w_cols[0], st);
+            t->pending = false;
+            t->w1_cur = 0;
+        }
+        w1_home(t, st);
+        t->defer = false;
+        t->norm_ready = false;
+        return false;
+    }
+    const gs_trainer_config& c = t->cfg;
+    const int64_t n1 = t->w_rows[0] * t->w_cols[0];
+    const bool ok = c.feat_dtype == GS_F32 && !t->fused1 && t->fuse_bwd && t->use_top && c.n_layers == 2 && !c.gcn &&
+                    !t->fuse_update && !t->upper_hook && !t->w1_chunk_hook && n1 % 4 == 0 &&
+                    t->cls_w_off % 4 == 0 && t->total % 4 == 0 && aligned16(c.params) && aligned16(c.grads);
+    if (!ok) return false;
+    if (!t->w1_alt)
+        GS_REQUIRE(hipMalloc(&t->w1_alt, n1 * sizeof(float)) == hipSuccess, GS_ENOMEM, "hipMalloc(W1 buffer)");
+    t->defer = true;
+    t->pending = false;
+    t->w1_cur = 0;
+    return true;
 }
 
 bool trainer_barrier_failed(gs_trainer* t) {
@@ -771,6 +876,11 @@ int gs_trainer_update_local(gs_trainer* t, void* stream) {
         t->norm_ready = false;
         return GS_OK;
     }
+    if (t->pending) {  // deferred update: the next forward (or trainer_defer_update(false)) applies it
+        t->norm_ready = false;
+        return GS_OK;
+    }
+    gs::w1_home(t, gs::as_stream(stream));  // a deferred-update step that could not defer
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     ShadowArm arm(t);
     if (t->norm_ready) {
@@ -791,6 +901,8 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
     t->norm_ready = false;
     GS_REQUIRE(!t->update_done, GS_EINVAL, "the step's fused launch already applied the SGD");
+    GS_REQUIRE(!t->pending, GS_EINVAL, "a deferred update is pending (all-reduce paths do not defer)");
+    gs::w1_home(t, gs::as_stream(stream));
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     ShadowArm arm(t);
     int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);

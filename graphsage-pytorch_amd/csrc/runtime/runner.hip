@@ -21,6 +21,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -153,7 +154,7 @@ struct gs_runner {
     hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
     // Step completion without an event between steps: the step's SGD launch
-    // stores its batch index into done_host (fine-grained pinned memory) when
+    // (with a deferred update: its last slab sum) stores its batch index into done_host (fine-grained pinned memory) when
     // it starts, i.e. once every launch that reads the step's ring entry has
     // completed (stream order); the host polls it.  dev_done events remain for
     // the last step of each gs_runner_run call (teardown) and as the
@@ -890,6 +891,30 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     } fuse_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && std::getenv("GS_FUSED_SGD")
                       ? r->cfg.trainer
                       : nullptr};
+    // No all-reduce: each step's clip + SGD is deferred into the next step's
+    // launches (the last slab sum writes W1's update for clip coefficient 1,
+    // the next layer-1 forward applies the update) instead of a launch between
+    // the steps; the loop's end applies the last one (GS_DEFER_SGD=0: off).
+    struct DeferUpdate {
+        gs_trainer* t;
+        hipStream_t st;
+        bool on = false;
+        DeferUpdate(gs_trainer* t_, hipStream_t s) : t(t_), st(s) {
+            if (t) on = gs::trainer_defer_update(t, true, st);
+        }
+        ~DeferUpdate() {
+            if (!on) return;
+            try {
+                gs::trainer_defer_update(t, false, st);
+            } catch (const gs::Error& e) {
+                std::fprintf(stderr, "graphsage_amd: runner: applying the last deferred update failed: %s\n", e.what());
+            }
+        }
+    } defer_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && !fuse_update.t &&
+                           !(std::getenv("GS_DEFER_SGD") && std::string(std::getenv("GS_DEFER_SGD")) == "0")
+                       ? r->cfg.trainer
+                       : nullptr,
+                   st};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();
@@ -1010,6 +1035,10 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         r->stats.fwd_bwd_s += secs(t2, t3);
         r->stats.update_s += secs(t3, t4);
         r->stats.max_step_s = std::max(r->stats.max_step_s, secs(t0, t4));
+    }
+    if (defer_update.on) {  // the last step's update, errors reported here (the destructor covers unwinding)
+        defer_update.on = false;
+        gs::trainer_defer_update(defer_update.t, false, st);
     }
     unwind.armed = false;
     // GS_FUSED_SGD: a grid barrier that gave up ran its SGD on partial sums;

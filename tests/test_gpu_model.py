@@ -307,6 +307,71 @@ def test_native_runner_matches_python_loop(gs, S, agg, gcn):
     runner.close()
 
 
+@pytest.mark.parametrize("max_norm", [5.0, 1e-3, 0.05])
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_runner_deferred_update_matches_python_loop(gs, agg, max_norm):
+    """The runner's deferred update (each step's clip + SGD applied by the next
+    step's launches: W1's update for clip coefficient 1 written by the slab
+    sum and read by the next forward, recomputed there when the gradients
+    were clipped; the other parameters updated in the forward's prologue; the
+    last update at the end of each run call) leaves the parameters and the
+    clipped gradients of the Python loop's separate update launches, bit for
+    bit: no clipping (5.0), clipping at every step (1e-3), and a mix (0.05),
+    over runs of 1, 2 and 4 steps."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:7]
+    a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=max_norm, seed=824)
+    b = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=max_norm, seed=824)
+    pf = train.Prefetcher(graph, None, batches, [25, 10], False, DEV,
+                          rngs=[train.make_rng(11, 0, w) for w in range(2)], fail_empty=agg == "MAX")
+    norms = []
+    for _ in batches:
+        ds, roots_dev, _info = pf.next()
+        a.forward_backward(ds, roots_dev)
+        g_off = a.p.group_off
+        norms.append(float(torch.linalg.vector_norm(a.p.grads[int(g_off[0]):int(g_off[1])])))
+        a.apply_update()
+    pf.close()
+    runner = train.Runner(b, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
+                          fail_empty=agg == "MAX", depth=2)
+    for k in (1, 2, 4):
+        runner.run(k)
+    torch.cuda.synchronize()
+    assert torch.equal(a.p.params, b.p.params)
+    assert torch.equal(a.p.grads, b.p.grads)
+    assert float(a.loss) == float(b.loss)
+    runner.close()
+    clipped = sum(x > max_norm for x in norms)
+    if max_norm == 5.0:
+        assert clipped == 0, norms
+    if max_norm == 1e-3:
+        assert clipped == len(norms), norms
+
+
+def test_runner_deferred_update_switch(gs, monkeypatch):
+    """GS_DEFER_SGD=0 (a separate update launch per step) and the default
+    deferred update leave the same parameters bit for bit."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:6]
+    out = []
+    for env in ("0", None):
+        if env is None:
+            monkeypatch.delenv("GS_DEFER_SGD", raising=False)
+        else:
+            monkeypatch.setenv("GS_DEFER_SGD", env)
+        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), max_norm=0.05, seed=824)
+        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10], depth=2)
+        r.run(len(batches))
+        torch.cuda.synchronize()
+        out.append(t.p.params.clone())
+        r.close()
+    assert torch.equal(out[0], out[1])
+
+
 @pytest.mark.parametrize("agg,gcn,layers,name,B", [
     ("MEAN", False, 2, "rmat", 96), ("MAX", False, 2, "rmat", 96), ("MEAN", True, 2, "rmat", 96),
     ("MEAN", False, 3, "rmat", 96),

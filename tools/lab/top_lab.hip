@@ -4,11 +4,13 @@
 // launches, and per-stage s_memrealtime stamps (100 MHz) of every block.
 // Developer tool, not part of the library:
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/lab/top_lab.hip -o tools/bin/top_lab
+//   tools/bin/top_lab [tids]    (tids: the runner's padded list records, as in the step)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <random>
+#include <string>
 #include <vector>
 
 __device__ unsigned long long* g_stamps;
@@ -51,6 +53,16 @@ int main(int argc, char** argv) {
     int *dptr, *dnbr, *dself, *dlab, *droots;
     up(h1, &dh1); up(W, &dW); up(Wc, &dWc); up(bc, &dbc);
     up(ptr, &dptr); up(nbr, &dnbr); up(self, &dself); up(labels, &dlab); up(roots, &droots);
+    // argv[1] == "tids": the runner's padded records [self | list padded to 25 with -1]
+    const bool use_tids = argc > 1 && std::string(argv[1]) == "tids";
+    const int tk = 25;
+    std::vector<int> tids(size_t(B) * (tk + 1), -1);
+    for (int r = 0; r < B; ++r) {
+        tids[size_t(r) * (tk + 1)] = self[r];
+        for (int e = ptr[r]; e < ptr[r + 1]; ++e) tids[size_t(r) * (tk + 1) + 1 + (e - ptr[r])] = nbr[e];
+    }
+    int* dtids;
+    up(tids, &dtids);
     CK(hipMalloc(&agg, B * H * 4)); CK(hipMalloc(&E, B * H * 4)); CK(hipMalloc(&dZ, B * H * 4));
     CK(hipMalloc(&dIn, B * K * 4)); CK(hipMalloc(&slab, (B / 4 + 1) * (C * (H + 1) + 1) * 4));
     unsigned long long* st;
@@ -61,7 +73,7 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
     auto launch = [&] {
         gs::top_fwd_bwd(GS_AGG_MEAN, B, C, dh1, dptr, dnbr, dself, dW, dWc, dbc, dlab, droots, agg, nullptr, E, dZ,
-                        dIn, slab, s);
+                        dIn, slab, s, use_tids ? dtids : nullptr, use_tids ? tk : 0);
     };
     for (int i = 0; i < 20; ++i) launch();
     hipEvent_t e0, e1;
