@@ -164,7 +164,41 @@ struct ClsReduce {
 // classifier reduce and the agg backward to dH_1; the dW_2 slab sum is left
 // in *deferred (S <= 1: dW_2 written directly) for sum_slabs_pair_launch.
 // Returns the norm partials that sum will write (placed first, as layer_bwd's).
-int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st);
+// Roles of the fused layer-2 backward launches (bwd.hip).
+struct BwdA {
+    int n, F, H, K, rps;
+    const float* Xs;
+    int64_t ldxs;
+    const int* sidx;
+    const float* A;
+    const float* dZ;
+    float* target;  // dW slabs (or dW itself when S == 1)
+    int dw_gx, dw_gy, dw_nb;
+    const float* W;
+    float* dSelf;
+    float* dA;
+    int dx_gx, dx_nb;
+    // classifier reduce (top layer only)
+    int B, D, C, cls_rows;
+    const float* cls_slab;
+    float* dWc;
+    float* dbc;
+    float* loss;
+    float* cls_part;
+};
+struct BwdMoved {
+    BwdA a;
+    int cls_nb = 0;
+};
+int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st,
+                  BwdMoved* moved = nullptr);
+// With `moved` (GS_DW_PLUS=1) layer_bwd_top launches only the agg backward and
+// leaves its dW_2 slab and classifier-reduce roles here, for the layer-1 dW
+// launch (dw1_plus_launch: fp32, self rows, 16-B aligned; -1 = not taken,
+// else the slab count; the slabs go to ws).
+int dw1_plus_launch(int64_t n, int64_t F, int64_t H, const float* Xs, int64_t ldxs, const int32_t* sidx,
+                    const float* A, int64_t lda, const float* dout, int64_t ldo, float* dW, void* ws,
+                    int64_t ws_bytes, const BwdMoved& mv, hipStream_t st);
 
 bool layer_bwd_fusable(const LayerBwd& a);
 int cls_reduce_grid(int64_t C, int64_t D);

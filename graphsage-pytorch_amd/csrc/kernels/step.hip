@@ -422,10 +422,16 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             int np = 0;
             bool parts = true;
             SlabSum d2{};
+            // GS_DW_PLUS=1 (A/B): the dW_2 slabs and the classifier reduce move from
+            // the layer-2 backward launch into the layer-1 dW launch (dw1_plus_launch)
+            const char* dw_plus_s = std::getenv("GS_DW_PLUS");  // read per step (tests switch it)
+            const bool dw_plus_env = dw_plus_s && std::string(dw_plus_s) == "1";
+            const bool dw_plus = defer && dw_plus_env && !lowp && !c.gcn && !T.w1_chunk_hook;
+            BwdMoved moved{};
             if (defer) {
                 lb[0].slabs = reinterpret_cast<float*>(dw2_ws);
                 lb[0].slab_bytes = dw2_need;
-                np = layer_bwd_top(lb[0], cr, &d2, st);
+                np = layer_bwd_top(lb[0], cr, &d2, st, dw_plus ? &moved : nullptr);
                 parts = np > 0;
             } else {
                 for (size_t i = 0; i < lb.size(); ++i) {
@@ -459,9 +465,19 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
             const bool armed = timed_arm(T, 2);
             DwGroups grp{T.dw_cnt, T.dw_n_cnt, dw_gpart};
-            const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
-                                           c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0],
-                                           dw_ws, dw_need, st, &grp);
+            int S1 = -1;
+            if (dw_plus) {
+                S1 = dw1_plus_launch(rows[0], F, H, static_cast<const float*>(c.X), c.feat_ld, dst_L,
+                                     static_cast<const float*>(agg[0]), F, lb.back().dH, H, G + T.w_off[0], dw_ws,
+                                     dw_need, moved, st);
+                GS_REQUIRE(S1 > 1, GS_EINVAL, "GS_DW_PLUS: the layer-1 dW launch could not take the moved roles");
+                grp.slabs = reinterpret_cast<const float*>(dw_ws);
+                grp.S = S1;
+            } else {
+                S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
+                                     c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws,
+                                     dw_need, st, &grp);
+            }
             g_launch_events = {};
             timed_done(T, 2, armed);
             // what the slab sum adds: the group partials (bitwise the same sums) or the slabs

@@ -372,6 +372,33 @@ def test_runner_deferred_update_switch(gs, monkeypatch):
     assert torch.equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
+def test_dw_plus_matches_default(gs, monkeypatch, agg):
+    """GS_DW_PLUS=1 (the top path's dW_2 slabs and classifier reduce launched
+    beside the layer-1 dW instead of in the layer-2 backward launch) runs the
+    same bodies: loss, gradients and parameters bitwise the default's."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 9))[:5]
+    out = []
+    for env in (None, "1"):
+        if env is None:
+            monkeypatch.delenv("GS_DW_PLUS", raising=False)
+        else:
+            monkeypatch.setenv("GS_DW_PLUS", env)
+        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=0.05, seed=824)
+        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
+                         fail_empty=agg == "MAX", depth=2)
+        r.run(len(batches))
+        torch.cuda.synchronize()
+        out.append((t.p.params.clone(), t.p.grads.clone(), float(t.loss)))
+        r.close()
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
+
+
 @pytest.mark.parametrize("agg,gcn,layers,name,B", [
     ("MEAN", False, 2, "rmat", 96), ("MAX", False, 2, "rmat", 96), ("MEAN", True, 2, "rmat", 96),
     ("MEAN", False, 3, "rmat", 96),

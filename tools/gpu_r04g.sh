@@ -9,7 +9,7 @@ ROOT=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$ROOT/gpurun_out/r04g
 mkdir -p "$OUT"; cd "$ROOT"
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-    tests/test_gpu_model.py tests/test_gpu_fullsize.py -k "deferred or runner or top_launch or fused_backward" \
+    tests/test_gpu_model.py tests/test_gpu_fullsize.py -k "deferred or runner or top_launch or fused_backward or dw_plus" \
     > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
 tail -1 "$OUT/gpu_tests.log"
 for i in 1 2; do
@@ -22,11 +22,11 @@ for i in 1 2; do
 done
 grep -A1 "==" "$OUT/top_lab_ab.txt" | grep -v "^--"
 for i in 1 2; do
-  for C in "0 0" "1 0" "1 1"; do
+  for C in "0 0 0" "1 0 0" "1 1 0" "1 0 1"; do
     set -- $C
-    GS_DEFER_SGD=$1 GS_SHARED_HELPERS=$2 timeout -k 10 300 python3 bench.py --no-cpu-baseline --ref-stream-steps 0 \
-        > "$OUT/bench_d$1_s$2_$i.json" 2> "$OUT/bench_d$1_s$2_$i.err" || exit $?
-    python3 - "$OUT/bench_d$1_s$2_$i.json" "defer $1 shared $2" <<'PY'
+    GS_DEFER_SGD=$1 GS_SHARED_HELPERS=$2 GS_DW_PLUS=$3 timeout -k 10 300 python3 bench.py --no-cpu-baseline \
+        --ref-stream-steps 0 > "$OUT/bench_d$1_s$2_p$3_$i.json" 2> "$OUT/bench_d$1_s$2_p$3_$i.err" || exit $?
+    python3 - "$OUT/bench_d$1_s$2_p$3_$i.json" "defer $1 shared $2 dwplus $3" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 c = d["config"]
