@@ -316,8 +316,9 @@ def test_runner_deferred_update_matches_python_loop(gs, agg, max_norm):
     were clipped; the other parameters updated in the forward's prologue; the
     last update at the end of each run call) leaves the parameters and the
     clipped gradients of the Python loop's separate update launches, bit for
-    bit: no clipping (5.0), clipping at every step (1e-3), and a mix (0.05),
-    over runs of 1, 2 and 4 steps."""
+    bit: the reference's max_norm (5.0: the first steps clip, the later ones
+    do not), clipping at every step (1e-3), and a mix (0.05), over runs of
+    1, 2 and 4 steps."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
@@ -343,11 +344,8 @@ def test_runner_deferred_update_matches_python_loop(gs, agg, max_norm):
     assert torch.equal(a.p.grads, b.p.grads)
     assert float(a.loss) == float(b.loss)
     runner.close()
-    clipped = sum(x > max_norm for x in norms)
-    if max_norm == 5.0:
-        assert clipped == 0, norms
-    if max_norm == 1e-3:
-        assert clipped == len(norms), norms
+    if max_norm == 1e-3:  # every step took the recompute path
+        assert all(x > max_norm for x in norms), norms
 
 
 def test_runner_deferred_update_switch(gs, monkeypatch):
