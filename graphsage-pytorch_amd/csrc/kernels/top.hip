@@ -74,7 +74,7 @@ __device__ __forceinline__ constexpr int mfma_k(int i) { return 4 * (i & 3) + (i
 template <int OP>
 __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     constexpr int H = kTopH, K = kTopK, D = kTopH;
-    // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, Wc, dlogits, loss, labels
+    // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, Wc, dlogits, loss
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW2 = smem;                                        // [H][K]
     float (*sX)[K] = reinterpret_cast<float (*)[K]>(sW2 + H * K);
@@ -89,27 +89,28 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     const int nr = min(kTopRows, a.B - r0);
 
     GS_TOP_STAMP(0);
-    const int cl = lane & 15, dq = lane >> 4;
-    int* sy = reinterpret_cast<int*>(sloss + kTopRows);  // the rows' labels
     // ---- W2 -> LDS by DMA (no registers), issued before anything else so its
     // latency hides under the gather.  Row c is one wave instruction of 64
     // 16-byte quads; quad q of the row lands in slot q ^ (c & 15), which keeps
     // both later access patterns free of bank conflicts: a column read by
     // lanes = rows (ds_read_b128, 16 rows per quarter-wave on 16 distinct
     // slots) and a row read by lanes = k.
-    // Waves 2 and 3 issue it, and stage the loss head's operands (Wc, the
-    // labels): the gather below runs on waves 0 and 1 alone, two dependent
-    // load rounds (record, rows) with nothing queued in front of them (vmcnt
-    // retires in order, and Wc's LDS stores and the roots -> labels pair are
-    // dependent rounds of their own).
-    if (w >= 2) {
-        const int wl = tid - 128;
+    // Waves 2 and 3 issue it: the gather below runs on waves 0 and 1, whose
+    // dependent load rounds would otherwise queue behind the DMA (vmcnt
+    // retires in order).
+    if (w >= 2)
         for (int c = w - 2; c < H; c += 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
                                              0, 0);
-        const int root = wl < nr ? a.roots[r0 + wl] : 0;
+
+    // ---- stage 0: loss-head operands (independent of the rest, issued first)
+    const int cl = lane & 15, dq = lane >> 4;
+    const int wr_ = min(w, nr - 1);
+    const int root = a.roots[r0 + wr_];
+    const float b_lane = a.bc[min(cl, C - 1)];
+    {
         const int nW4 = C * D / 4;
-        for (int q = wl; q < nW4; q += 128) {
+        for (int q = tid; q < nW4; q += kTopThreads) {
             const float4 v = reinterpret_cast<const float4*>(a.Wc)[q];
             const int t = 4 * q;
             float* d = sW + t + t / D;  // row pitch D + 1 (D % 4 == 0: a quad stays in one row)
@@ -118,9 +119,8 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             d[2] = v.z;
             d[3] = v.w;
         }
-        if (wl < nr) sy[wl] = a.labels[root];
     }
-    const float b_lane = a.bc[min(cl, C - 1)];
+    const int y_w = a.labels[root];
 
     // ---- stage 1: the aggregate (agg_fwd_kernel<OP, float, 4, 32, explicit>)
     // and the self row, one 32-lane group per row.  With the padded records
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     if (w < nr) {
         const int ii = w;
         const float* e = sE[ii];
-        const int y = sy[ii];
+        const int y = y_w;
         static_assert(D % 4 == 0, "whole D quarters");
         constexpr int DQ = D / 4;  // whole quarters: a straight-line chain
         const int d_lo = dq * DQ;
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 
 static size_t top_smem_bytes(int64_t C) {
     return sizeof(float) * (static_cast<size_t>(kTopH) * kTopK + kTopRows * (kTopK + 2 * kTopH) + C * (kTopH + 1) +
-                            kTopRows * C + 2 * kTopRows);
+                            kTopRows * C + kTopRows);
 }
 
 // The kernel keeps W2 in LDS (~146 KiB at 16 classes): raise the launch limit

@@ -25,7 +25,7 @@ def main():
     wl = bench.build_workload(cfg, device, 824, 1)
     trainer = train.NativeTrainer(wl["graph"], wl["X"], wl["labels"], cfg["classes"], num_layers=2, hidden=128,
                                   fanouts=cfg["fanouts"], agg_func=cfg["agg"], seed=824)
-    batches = train.rank_batches(wl["candidates"], cfg["batch"], 0, 1, 824 + 1000)[:steps]
+    batches = list(train.rank_batches(wl["candidates"], cfg["batch"], 0, 1, 824 + 1000))[:steps]
     runner = train.Runner(trainer, wl["graph"], batches, [train.make_rng(824, 0, w) for w in range(4)],
                           cfg["fanouts"], gcn=False, fail_empty=cfg["agg"] == "MAX")
     g_off = trainer.p.group_off

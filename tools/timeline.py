@@ -1,5 +1,6 @@
 """Median step timeline from a rocprofv3 kernel trace of bench.py: for each
-main-stream kernel of a step (sgd to sgd), its start offset, duration and the
+main-stream kernel of a step (its last launch to the next step's: the sgd,
+or the slab sum with the deferred update), its start offset, duration and the
 idle gap before it, plus which side-stream kernels overlapped it.  Steps from
 the middle third of the run (calibration-free when --sustain covers it).
 Developer tool:  python3 tools/timeline.py gpurun_out/<dir>/run_kernel_trace.csv [first_frac last_frac]"""
@@ -15,16 +16,17 @@ ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"
 queues = {}
 for e in ev:
     queues.setdefault(e[3], []).append(e)
-main_q = max(queues, key=lambda q: sum(1 for e in queues[q] if "sgd" in e[2]))
+last = "sgd" if any("sgd" in e[2] for e in ev) else "sum_slabs_pair"
+main_q = max(queues, key=lambda q: sum(1 for e in queues[q] if last in e[2]))
 main = queues[main_q]
 side = [e for q, v in queues.items() if q != main_q for e in v]
-sgd = [i for i, e in enumerate(main) if "sgd" in e[2]]
+sgd = [i for i, e in enumerate(main) if last in e[2]]
 steps = []
 for a, b in zip(sgd, sgd[1:]):
     steps.append(main[a + 1:b + 1])
 steps = steps[int(len(steps) * lo):int(len(steps) * hi)]
 period = [s[-1][1] - s[0][0] for s in steps]
-print(f"{len(steps)} steps; first-kernel start to sgd end: median {np.median(period)/1e3:.2f} us")
+print(f"{len(steps)} steps; first-kernel start to {last} end: median {np.median(period)/1e3:.2f} us")
 n = min(len(s) for s in steps)
 for i in range(n):
     name = steps[0][i][2]
