@@ -271,24 +271,31 @@ constexpr int kFwdAhead = GS_FWD_AHEAD;  // K chunks in flight ahead of the MFMA
 // issued again (they read the speculative update).
 __device__ __forceinline__ bool fwd_pending_update(const FwdSpec& sp, int H, int K, int c0) {
     const int lane = threadIdx.x & 63;
+    // the other parameters' update, spread over every workgroup (thread t of
+    // block b takes quad b + nblk·t, so a block holds at most a few): its
+    // loads issued with the fold's, one memory round for both
+    const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
+    const int64_t b = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
+    float4* p4 = reinterpret_cast<float4*>(sp.p);
+    float4* g4 = reinterpret_cast<float4*>(sp.g);
+    const int64_t i0 = sp.up_lo / 4 + b + nblk * threadIdx.x, iend = sp.up_hi / 4;
+    float4 pv0 = make_float4(0.f, 0.f, 0.f, 0.f), gv0 = pv0;
+    if (i0 < iend) {
+        pv0 = p4[i0];
+        gv0 = g4[i0];
+    }
     const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), 1.0f, sp.max_norm);
     const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), 1.0f, sp.max_norm);
-    {
-        const int64_t nthr = int64_t(gridDim.x) * gridDim.y * blockDim.x;
-        const int64_t t = (int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
-        float4* p4 = reinterpret_cast<float4*>(sp.p);
-        float4* g4 = reinterpret_cast<float4*>(sp.g);
-        for (int64_t i = sp.up_lo / 4 + t; i < sp.up_hi / 4; i += nthr) {
-            const float m = 4 * i >= sp.grp1_lo ? m1 : m0;
-            const float4 pv = p4[i], gv = g4[i];
-            float4 gi, pn;
-            pn.x = sgd_elem(pv.x, gv.x, m, sp.lr, gi.x);
-            pn.y = sgd_elem(pv.y, gv.y, m, sp.lr, gi.y);
-            pn.z = sgd_elem(pv.z, gv.z, m, sp.lr, gi.z);
-            pn.w = sgd_elem(pv.w, gv.w, m, sp.lr, gi.w);
-            g4[i] = gi;
-            p4[i] = pn;
-        }
+    for (int64_t i = i0; i < iend; i += nblk * blockDim.x) {
+        const float m = 4 * i >= sp.grp1_lo ? m1 : m0;
+        const float4 pv = i == i0 ? pv0 : p4[i], gv = i == i0 ? gv0 : g4[i];
+        float4 gi, pn;
+        pn.x = sgd_elem(pv.x, gv.x, m, sp.lr, gi.x);
+        pn.y = sgd_elem(pv.y, gv.y, m, sp.lr, gi.y);
+        pn.z = sgd_elem(pv.z, gv.z, m, sp.lr, gi.z);
+        pn.w = sgd_elem(pv.w, gv.w, m, sp.lr, gi.w);
+        g4[i] = gi;
+        p4[i] = pn;
     }
     if (m0 == 1.0f) return false;
     // this column tile's rows of the update, then visible to the workgroup's own loads
