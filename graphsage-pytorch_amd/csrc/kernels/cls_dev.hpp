@@ -94,6 +94,22 @@ __device__ __forceinline__ float clip_fold(const float* __restrict__ pg, int np,
     return wave_sum(t);
 }
 
+// clip_fold in two halves, for a kernel that issues the partials' loads
+// ahead of its own (np <= 512: one load per lane and u; clip_fold's sums).
+struct FoldLoads {
+    float v[8];
+};
+__device__ __forceinline__ void clip_fold_issue(const float* __restrict__ pg, int np, int lane, FoldLoads& f) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) f.v[u] = pg[min(lane + 64 * u, max(np, 1) - 1)];  // np >= 1 (the caller's)
+}
+__device__ __forceinline__ float clip_fold_finish(int np, int lane, const FoldLoads& f) {
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += lane + 64 * u < np ? f.v[u] : 0.f;
+    return wave_sum(t);
+}
+
 // clip_grad_norm_'s coefficient (utils.py:186), times the gradient scale.
 __device__ __forceinline__ float clip_mult(float sumsq, float scale, float max_norm) {
     const float norm = sqrtf(sumsq) * scale;

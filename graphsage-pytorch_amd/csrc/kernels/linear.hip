@@ -333,7 +333,9 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     // a pending clip + SGD (the trainer's deferred update): the fp32 wide kernel applies it
     const FwdSpec sp = g_fwd_spec;
     g_fwd_spec = {};
-    GS_REQUIRE(!sp.on || (dt == GS_F32 && Wd == sp.S && K % 4 == 0), GS_EINVAL, "pending update: bad forward");
+    GS_REQUIRE(!sp.on || (dt == GS_F32 && Wd == sp.S && K % 4 == 0 && self && relu && sp.np0 >= 1 &&
+                          sp.np0 <= 512 && sp.np1 >= 1 && sp.np1 <= 512 && sp.up_hi > sp.up_lo),
+               GS_EINVAL, "pending update: bad forward");
     // read per call (tests switch it between launches): wres | wide32 | wide | sk | chunked
     const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
     GS_REQUIRE(!sp.on || fwd_mode.empty() || fwd_mode == "wide" || fwd_mode == "wide32", GS_EINVAL,
@@ -433,7 +435,16 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
 #define GS_LFWDW_R(TT, RR) \
         do { if (self) { if (relu) GS_LFWDW(TT, RR, true, true); else GS_LFWDW(TT, RR, true, false); } \
              else { if (relu) GS_LFWDW(TT, RR, false, true); else GS_LFWDW(TT, RR, false, false); } } while (0)
-        if (dt == GS_F32) {
+        if (dt == GS_F32 && sp.on) {  // self rows and relu (checked above): the pending-update instances
+#define GS_LFWDP(RR)                                                                                          \
+            launch_k(linear_fwd_wide_kernel<float, RR, true, true, true>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K, \
+                     static_cast<const float*>(Xs), ldxs, sidx, static_cast<const float*>(A), lda,            \
+                     static_cast<const float*>(Wd), out, ldo, sp)
+            if (R == 32) GS_LFWDP(32);
+            else if (R == 48) GS_LFWDP(48);
+            else GS_LFWDP(64);
+#undef GS_LFWDP
+        } else if (dt == GS_F32) {
             if (R == 32) GS_LFWDW_R(float, 32);
             else if (R == 48) GS_LFWDW_R(float, 48);
             else GS_LFWDW_R(float, 64);

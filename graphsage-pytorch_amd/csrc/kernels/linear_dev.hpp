@@ -261,44 +261,42 @@ constexpr int kFwdAhead = GS_FWD_AHEAD;  // K chunks in flight ahead of the MFMA
 // the 16x16x32 bf16 MFMA per slot pair — operands and order of the chunked
 // bf16 kernel (slots 4g + kq, chunks ascending), so bitwise its output.
 // The pending clip + SGD of the previous step (sp.on, fp32 only; FwdSpec in
-// kcommon.hpp), run in the forward's prologue: the flat parameters past W1
-// updated grid-stride (their readers come after this launch), and W1 read
-// from sp.S when its group's clip coefficient is 1 (W == sp.S then).  Else
-// the workgroup writes its own 64-row slice of the update into sp.Wn (= S's
-// buffer; every workgroup of a column tile writes the same values there) and
-// reads it back: the same W1 the separate SGD launch would have left, so the
-// same output bit for bit.  Returns whether the loads issued from W must be
-// issued again (they read the speculative update).
-__device__ __forceinline__ bool fwd_pending_update(const FwdSpec& sp, int H, int K, int c0) {
-    const int lane = threadIdx.x & 63;
-    // the other parameters' update, spread over every workgroup (thread t of
-    // block b takes quad b + nblk·t, so a block holds at most a few): its
-    // loads issued with the fold's, one memory round for both
-    const int64_t nblk = int64_t(gridDim.x) * gridDim.y;
-    const int64_t b = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
+// kcommon.hpp), run in the forward's prologue.  fwd_pending_issue loads the
+// norm partials and this thread's share of the other parameters (W2, Wc, bc:
+// thread t of block b takes quad b + nblk·t) before the forward's own first
+// loads, so waiting for them (vmcnt retires in order) never waits for a K
+// chunk; fwd_pending_apply then folds the partials (clip_fold's sums: the
+// coefficients sgd4 would compute), updates those parameters (their readers
+// come after this launch) and returns whether W1 is not the speculative
+// update sp.S (the coefficient of its group is not 1).  In that case the
+// workgroup writes its own 64-row slice of the update into sp.Wn (= S's
+// buffer; every workgroup of a column tile writes the same values there),
+// releases it, and the caller reloads its first chunks: the same W1 the
+// separate SGD launch would have left, so the same output bit for bit.
+// One quad of the other parameters' update (clip coefficient m).
+__device__ __forceinline__ void sgd_quad(float4* p4, float4* g4, int64_t i, float4 pv, float4 gv, float m, float lr) {
+    float4 gi, pn;
+    pn.x = sgd_elem(pv.x, gv.x, m, lr, gi.x);
+    pn.y = sgd_elem(pv.y, gv.y, m, lr, gi.y);
+    pn.z = sgd_elem(pv.z, gv.z, m, lr, gi.z);
+    pn.w = sgd_elem(pv.w, gv.w, m, lr, gi.w);
+    g4[i] = gi;
+    p4[i] = pn;
+}
+
+// The rest of the pending update once the coefficients are known: the other
+// parameters' quads past the first (only for grids of fewer threads than
+// quads), then, if W1's coefficient is not 1, this column tile's rows of W1's
+// update into sp.Wn, released and visible to the workgroup.  Returns whether
+// it wrote them (the caller reloads its first chunks).
+__device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, float m0, float m1, int H, int K,
+                                                 int c0) {
+    const int64_t stride = int64_t(gridDim.x) * gridDim.y * blockDim.x;
     float4* p4 = reinterpret_cast<float4*>(sp.p);
     float4* g4 = reinterpret_cast<float4*>(sp.g);
-    const int64_t i0 = sp.up_lo / 4 + b + nblk * threadIdx.x, iend = sp.up_hi / 4;
-    float4 pv0 = make_float4(0.f, 0.f, 0.f, 0.f), gv0 = pv0;
-    if (i0 < iend) {
-        pv0 = p4[i0];
-        gv0 = g4[i0];
-    }
-    const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), 1.0f, sp.max_norm);
-    const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), 1.0f, sp.max_norm);
-    for (int64_t i = i0; i < iend; i += nblk * blockDim.x) {
-        const float m = 4 * i >= sp.grp1_lo ? m1 : m0;
-        const float4 pv = i == i0 ? pv0 : p4[i], gv = i == i0 ? gv0 : g4[i];
-        float4 gi, pn;
-        pn.x = sgd_elem(pv.x, gv.x, m, sp.lr, gi.x);
-        pn.y = sgd_elem(pv.y, gv.y, m, sp.lr, gi.y);
-        pn.z = sgd_elem(pv.z, gv.z, m, sp.lr, gi.z);
-        pn.w = sgd_elem(pv.w, gv.w, m, sp.lr, gi.w);
-        g4[i] = gi;
-        p4[i] = pn;
-    }
+    for (int64_t i = i0 + stride; i < sp.up_hi / 4; i += stride)
+        sgd_quad(p4, g4, i, p4[i], g4[i], 4 * i >= sp.grp1_lo ? m1 : m0, sp.lr);
     if (m0 == 1.0f) return false;
-    // this column tile's rows of the update, then visible to the workgroup's own loads
     const int k4 = K / 4, rows = min(64, H - c0);
     const float4* P4 = reinterpret_cast<const float4*>(sp.P) + int64_t(c0) * k4;
     const float4* G4 = reinterpret_cast<const float4*>(sp.G1) + int64_t(c0) * k4;
@@ -318,11 +316,12 @@ __device__ __forceinline__ bool fwd_pending_update(const FwdSpec& sp, int H, int
     return true;
 }
 
-template <typename T, int ROWS, bool HAS_SELF, bool RELU>
+template <typename T, int ROWS, bool HAS_SELF, bool RELU, bool PEND = false>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo,
     FwdSpec sp) {
+    static_assert(!PEND || std::is_same<T, float>::value, "the pending update is fp32");
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
@@ -345,10 +344,33 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         by = (b >> 3) % gy;
     }
     const int m0 = bx * ROWS, c0 = by * 64;
-    bool pending = false;
-    if constexpr (std::is_same<T, float>::value) pending = sp.on != 0;
+    // PEND: the pending update's loads before the first chunk's, branch-free
+    // (the launcher guarantees 1 <= np0, np1 <= 512: clip_fold's one round),
+    // so the fold's waits count past the K chunks' loads: the norm partials
+    // and this thread's quad of the other parameters (thread t of block b:
+    // quad b + nblk·t; a thread past them reads the last one and stores nothing)
+    FoldLoads f0, f1;
+    float4 upv, ugv;
+    const int64_t ui0 = sp.up_lo / 4 + (int64_t(blockIdx.y) * gridDim.x + blockIdx.x) +
+                        int64_t(gridDim.x) * gridDim.y * threadIdx.x;
+    if constexpr (PEND) {
+        clip_fold_issue(sp.part0, sp.np0, lane, f0);
+        clip_fold_issue(sp.part1, sp.np1, lane, f1);
+        const int64_t ui = min(ui0, sp.up_hi / 4 - 1);
+        upv = reinterpret_cast<const float4*>(sp.p)[ui];
+        ugv = reinterpret_cast<const float4*>(sp.g)[ui];
+    }
+    // the coefficients and the update of this thread's quad (before W1 is read)
+    auto pending_apply = [&]() -> bool {
+        const float mm0 = clip_mult(clip_fold_finish(sp.np0, lane, f0), 1.0f, sp.max_norm);
+        const float mm1 = clip_mult(clip_fold_finish(sp.np1, lane, f1), 1.0f, sp.max_norm);
+        if (ui0 < sp.up_hi / 4)
+            sgd_quad(reinterpret_cast<float4*>(sp.p), reinterpret_cast<float4*>(sp.g), ui0, upv, ugv,
+                     4 * ui0 >= sp.grp1_lo ? mm1 : mm0, sp.lr);
+        return fwd_pending_rest(sp, ui0, mm0, mm1, H, K, c0);
+    };
     if (m0 >= n) {  // spare blocks of the last group of 8 (they still take their share of the update)
-        if (pending) fwd_pending_update(sp, H, K, c0);
+        if constexpr (PEND) pending_apply();
         return;
     }
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
@@ -374,37 +396,41 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         for (int q = 0; q < WQ; ++q)
             if (64 % ROWS == 0 || lr + ROWS * q < 64) sW[c & 1][(lr + ROWS * q) * SP + ls] = wr_[u][q];
     };
-#pragma unroll
-    for (int u = 0; u < kFwdAhead; ++u) load(u, u);
-    // the pending update after the first loads (its fold then waits on the same round)
-    if (pending && fwd_pending_update(sp, H, K, c0)) {
-        // W1 is not the speculative update: read the one written above
+    auto run_k = [&]() -> f32x4 {
 #pragma unroll
         for (int u = 0; u < kFwdAhead; ++u) load(u, u);
-    }
-    stash(0, 0);
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c0 = 0; c0 < nC; c0 += kFwdAhead) {
+        stash(0, 0);
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int cb = 0; cb < nC; cb += kFwdAhead) {
 #pragma unroll
-        for (int u = 0; u < kFwdAhead; ++u) {
-            const int c = c0 + u;
-            if (c >= nC) break;
-            __syncthreads();
-            load(c + kFwdAhead, u);
-            __builtin_amdgcn_sched_barrier(0);
-            const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
-            const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
-            uint4 av[4], wv[4];
+            for (int u = 0; u < kFwdAhead; ++u) {
+                const int c = cb + u;
+                if (c >= nC) break;
+                __syncthreads();
+                load(c + kFwdAhead, u);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
+                const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
+                uint4 av[4], wv[4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                av[g] = ta[4 * g + kq];
-                wv[g] = tw[4 * g + kq];
+                for (int g = 0; g < 4; ++g) {
+                    av[g] = ta[4 * g + kq];
+                    wv[g] = tw[4 * g + kq];
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
+                __builtin_amdgcn_sched_barrier(0);
+                if (c + 1 < nC) stash(c + 1, (u + 1) % kFwdAhead);
             }
-#pragma unroll
-            for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
-            __builtin_amdgcn_sched_barrier(0);
-            if (c + 1 < nC) stash(c + 1, (u + 1) % kFwdAhead);
         }
+        return acc;
+    };
+    f32x4 acc = run_k();  // PEND: on the speculative W1 (sp.S)
+    if constexpr (PEND) {
+        // the fold after the K loop (its loads long done): the coefficients,
+        // the other parameters' update, and, when W1's coefficient is not 1,
+        // the recomputed W1 in S's buffer and the whole product again
+        if (pending_apply()) acc = run_k();
     }
     const int col = c0 + 16 * wc + r;
     if (col >= H) return;

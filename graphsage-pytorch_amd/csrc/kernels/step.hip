@@ -295,7 +295,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
     GS_REQUIRE(!T.defer || (!lowp && !fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
-    const bool pend = T.defer && T.pending;
+    bool pend = T.defer && T.pending;
+    if (pend && !(T.npart[0] >= 1 && T.npart[0] <= 512 && T.npart[1] >= 1 && T.npart[1] <= 512)) {
+        // the forward folds at most 512 partials per group: apply the update on its own
+        trainer_defer_update(&T, false, st);
+        trainer_defer_update(&T, true, st);
+        pend = false;
+    }
     if (T.defer) {
         W1 = T.w1_buf(pend ? T.w1_cur ^ 1 : T.w1_cur);
         if (pend) {  // the previous step's clip + SGD, applied by this forward launch

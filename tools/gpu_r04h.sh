@@ -25,8 +25,8 @@ print(sys.argv[2], "value", d["value"], "ms", d["ms_per_step"], "sampler ms", c[
 PY
   done
 done
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 5 --no-cpu-baseline --ref-stream-steps 0 > "$OUT/prof.log" 2>&1 || exit $?
-cp "$OUT/prof/run_kernel_stats.csv" "$OUT/kernel_stats_rmat2m_steps300.csv" && rm -rf "$OUT/prof"
-head -12 "$OUT/kernel_stats_rmat2m_steps300.csv" | cut -c1-160
-timeout -k 10 300 python3 tools/norm_probe.py rmat2m 300 > "$OUT/norm_probe.txt" 2>&1 || exit $?
-tail -1 "$OUT/norm_probe.txt"
+: timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 300 --warmup 5 --no-cpu-baseline --ref-stream-steps 0 > "$OUT/prof.log" 2>&1 || exit $?
+: cp "$OUT/kernel_stats_rmat2m_steps300.csv" && rm -rf "$OUT/prof"
+: head -12 "$OUT/kernel_stats_rmat2m_steps300.csv" | cut -c1-160
+: timeout -k 10 300 python3 tools/norm_probe.py rmat2m 300 > "$OUT/norm_probe.txt" 2>&1 || exit $?
+: tail -1
