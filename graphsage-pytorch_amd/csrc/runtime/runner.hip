@@ -16,6 +16,7 @@
 // of consumed slots (hipEventQuery) and hands finished slots back, and waits
 // on the oldest copy only when a stream has no slot left to sample into.
 #include <rccl/rccl.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -79,6 +80,8 @@ __global__ __launch_bounds__(256) void pull_pack_kernel(const int4* __restrict__
 
 struct PackSlot {
     int32_t* host = nullptr;  // pinned
+    int32_t* dptr = nullptr;  // its device address (the pull kernel's source)
+    size_t thp_bytes = 0;     // GS_PIN_THP: a 2 MiB-aligned registered mapping of this size, else hipHostMalloc
     hipEvent_t copied = nullptr;
     int64_t batch = -1;
     int64_t hop_sizes[4 * GS_MAX_HOPS];
@@ -370,7 +373,7 @@ void gs_runner::pull(int64_t b, int slot_id) {
         const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
         const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, pull_blocks));
         pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
-            reinterpret_cast<const int4*>(slot.host), reinterpret_cast<int4*>(d), n16, slot.host + 4 * n16,
+            reinterpret_cast<const int4*>(slot.dptr), reinterpret_cast<int4*>(d), n16, slot.dptr + 4 * n16,
             d + 4 * n16, static_cast<int>(tail));
         hip_ok(hipGetLastError(), "pull_pack_kernel");
     }
@@ -551,7 +554,12 @@ gs_runner::~gs_runner() {
                 (void)hipEventSynchronize(slot.copied);
                 (void)hipEventDestroy(slot.copied);
             }
-            if (slot.host) (void)hipHostFree(slot.host);
+            if (slot.host && slot.thp_bytes) {
+                (void)hipHostUnregister(slot.host);
+                munmap(slot.host, slot.thp_bytes);
+            } else if (slot.host) {
+                (void)hipHostFree(slot.host);
+            }
         }
     for (int d = 0; d < kPack; ++d)
         if (dev[d]) (void)hipFree(dev[d]);
@@ -758,6 +766,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     // idle) instead of helpers private to each stream.
     const char* shared_env = std::getenv("GS_SHARED_HELPERS");
     const bool shared_helpers = shared_env && std::atoi(shared_env) == 1;
+    const bool pin_thp = std::getenv("GS_PIN_THP") && std::string(std::getenv("GS_PIN_THP")) == "1";
     for (int32_t w = 0; w < S && !r->devmode; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
@@ -770,9 +779,30 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         for (int64_t b = w; b < r->n_units; b += S) s->batches.push_back(b);
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {
-            hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s->slots[q].host), r->cap * sizeof(int32_t),
-                                 hipHostMallocDefault),
-                   "hipHostMalloc");
+            PackSlot& sl = s->slots[q];
+            if (pin_thp) {  // GS_PIN_THP=1 (A/B): the slot on transparent huge pages, registered
+                constexpr size_t kHuge = size_t(2) << 20;
+                const size_t bytes = (r->cap * sizeof(int32_t) + kHuge - 1) / kHuge * kHuge;
+                void* p = mmap(nullptr, bytes + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+                if (p == MAP_FAILED) fail(GS_ENOMEM, "mmap(pack slot)");
+                // a 2 MiB-aligned window of the mapping; the rest goes back
+                const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) / kHuge * kHuge;
+                const size_t head = a - reinterpret_cast<uintptr_t>(p);
+                if (head) munmap(p, head);
+                if (kHuge - head) munmap(reinterpret_cast<char*>(a) + bytes, kHuge - head);
+                (void)madvise(reinterpret_cast<void*>(a), bytes, MADV_HUGEPAGE);
+                std::memset(reinterpret_cast<void*>(a), 0, bytes);
+                sl.host = reinterpret_cast<int32_t*>(a);
+                sl.thp_bytes = bytes;
+                hip_ok(hipHostRegister(sl.host, bytes, hipHostRegisterMapped), "hipHostRegister(pack slot)");
+                void* dp = nullptr;
+                hip_ok(hipHostGetDevicePointer(&dp, sl.host, 0), "hipHostGetDevicePointer");
+                sl.dptr = static_cast<int32_t*>(dp);
+            } else {
+                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&sl.host), r->cap * sizeof(int32_t), hipHostMallocDefault),
+                       "hipHostMalloc");
+                sl.dptr = sl.host;
+            }
             hip_ok(hipEventCreateWithFlags(&s->slots[q].copied, sync_event_flags()), "hipEventCreate");
             s->free.push_back(q);
         }
