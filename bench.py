@@ -21,6 +21,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -284,24 +285,37 @@ def rocprof_stats_file(config_name, batch):
     return None
 
 
+def kernel_key(name):
+    """A kernel's name without its parameter list, and without the
+    deferred-update flag of the layer-1 forward (linear_fwd_wide_kernel's fifth
+    template argument: the instance with the previous step's update pending and
+    the one without, at a run's first step, are one kernel here)."""
+    key = name.split("(")[0].strip()
+    m = re.match(r"^(.*linear_fwd_wide_kernel<[^,<>]+, \d+, (?:true|false), (?:true|false)), (?:true|false)>$", key)
+    return m.group(1) + ">" if m else key
+
+
 def load_rocprof_avg(config_name, batch, kernel):
     rel = rocprof_stats_file(config_name, batch)
     if not rel:
         return None
-    key = kernel.split("(")[0].strip()
+    key = kernel_key(kernel)
+    best = None
     with open(os.path.join(ROOT, rel)) as f:
-        for row in csv.DictReader(f):
-            if row.get("Name", "").split("(")[0].strip() == key:
-                return {"avg_us": round(float(row["AverageNs"]) / 1e3, 2), "min_us": round(float(row["MinNs"]) / 1e3, 2),
-                        "source": rel}
-    return None
+        for row in csv.DictReader(f):  # the matching instance with the most calls
+            if kernel_key(row.get("Name", "")) == key and (best is None or int(row["Calls"]) > int(best["Calls"])):
+                best = row
+    if best is None:
+        return None
+    return {"avg_us": round(float(best["AverageNs"]) / 1e3, 2), "min_us": round(float(best["MinNs"]) / 1e3, 2),
+            "source": rel}
 
 
 def load_traffic(config_name, batch, kernel):
     """Per-launch HBM bytes of `kernel` (its launched name) from the newest
     committed rocprofv3 --pmc summary (profiles/*pmc*.json, tools/pmc_summary.py)
     recorded for this config and this batch size, else None."""
-    key = kernel.split("(")[0].strip()
+    key = kernel_key(kernel)
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -310,7 +324,7 @@ def load_traffic(config_name, batch, kernel):
             continue
         if d.get("config") != config_name or int(d.get("batch", -1)) != int(batch):
             continue
-        k = d.get("kernels", {}).get(key)
+        k = next((v for n, v in d.get("kernels", {}).items() if kernel_key(n) == key), None)
         if k and "hbm_bytes" in k:
             best = {"hbm_bytes": k["hbm_bytes"], "source": os.path.relpath(p, ROOT)}
     return best

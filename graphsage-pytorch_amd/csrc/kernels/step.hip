@@ -162,7 +162,9 @@ static std::string demangle(const char* sym) {
 static inline void timed_done(gs_trainer& T, int site, bool armed) {
     if (!armed) return;
     GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
-    if (T.timer[site].kernel.empty()) T.timer[site].kernel = demangle(g_launch_name);
+    // the kernel of the latest timed launch (the layer-1 forward has two instances:
+    // with the deferred update pending, and without, at a run's first step)
+    if (g_launch_name) T.timer[site].kernel = demangle(g_launch_name);
     ++T.timer[site].n;
 }
 

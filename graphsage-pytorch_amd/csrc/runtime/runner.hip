@@ -766,7 +766,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     // idle) instead of helpers private to each stream.
     const char* shared_env = std::getenv("GS_SHARED_HELPERS");
     const bool shared_helpers = shared_env && std::atoi(shared_env) == 1;
-    const bool pin_thp = std::getenv("GS_PIN_THP") && std::string(std::getenv("GS_PIN_THP")) == "1";
+    // pack slots on transparent huge pages (GS_PIN_THP=0: hipHostMalloc): the pull kernel's
+    // host reads then need one translation per 2 MiB instead of per 4 KiB page
+    const bool pin_thp = !(std::getenv("GS_PIN_THP") && std::string(std::getenv("GS_PIN_THP")) == "0");
     for (int32_t w = 0; w < S && !r->devmode; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
@@ -780,7 +782,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {
             PackSlot& sl = s->slots[q];
-            if (pin_thp) {  // GS_PIN_THP=1 (A/B): the slot on transparent huge pages, registered
+            if (pin_thp) {  // the slot on transparent huge pages (madvise), registered
                 constexpr size_t kHuge = size_t(2) << 20;
                 const size_t bytes = (r->cap * sizeof(int32_t) + kHuge - 1) / kHuge * kHuge;
                 void* p = mmap(nullptr, bytes + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
