@@ -73,7 +73,7 @@ bool sum_slabs_pair_ok(int64_t len1);
 // spec_S: also W1's speculative update spec_S = spec_P - lr·(layer-1 sum) (the
 // trainer's deferred update), and the launch takes the done flag (g_done_flag).
 int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P = nullptr,
-                          float* spec_S = nullptr, float lr = 0.f);
+                          float* spec_S = nullptr, float lr = 0.f, uint16_t* spec_S_lp = nullptr);
 // The pending update's tail at the end of a deferred-update run: the flat
 // parameters and gradients become what the separate clip + SGD launch would
 // have left (W1 from sp.S or recomputed into w1_out, the others updated).

@@ -151,6 +151,8 @@ struct FwdSpec {
     const float* S = nullptr;    // W1 - lr·G1 (clip coefficient 1)
     const float* P = nullptr;    // W1 before the update
     float* Wn = nullptr;         // S's buffer: the updated W1 when the coefficient is not 1
+    const uint16_t* S_lp = nullptr;  // bf16 features: S in bf16 (the forward's W1), and its buffer
+    uint16_t* Wn_lp = nullptr;       //   for the recomputed W1 (nullptr: fp32 features)
     const float* G1 = nullptr;   // W1's gradient
     const float* part0 = nullptr;  // norm partials, group 0 (the sage weights) and 1 (the classifier)
     const float* part1 = nullptr;

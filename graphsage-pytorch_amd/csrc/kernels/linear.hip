@@ -28,6 +28,7 @@ struct SlabSpec {
     const float* P = nullptr;
     float* S = nullptr;
     float lr = 0.f;
+    uint16_t* S_lp = nullptr;  // bf16 features: S in bf16 too (sgd4's shadow conversion)
 };
 __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __restrict__ slabs, int S, int64_t len,
                                                      float* __restrict__ out, float* __restrict__ part,
@@ -77,6 +78,12 @@ __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __rest
             pn.z = sgd_elem(pv.z, s.z, 1.0f, spec.lr, gi.z);
             pn.w = sgd_elem(pv.w, s.w, 1.0f, spec.lr, gi.w);
             reinterpret_cast<float4*>(spec.S)[i] = pn;
+            if (spec.S_lp) {
+                uint2 b;
+                b.x = static_cast<uint32_t>(f2bf(pn.x)) | (static_cast<uint32_t>(f2bf(pn.y)) << 16);
+                b.y = static_cast<uint32_t>(f2bf(pn.z)) | (static_cast<uint32_t>(f2bf(pn.w)) << 16);
+                reinterpret_cast<uint2*>(spec.S_lp)[i] = b;
+            }
         }
     }
     if (part) block_sum_to(sq, part + bx);
@@ -333,8 +340,9 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     // a pending clip + SGD (the trainer's deferred update): the fp32 wide kernel applies it
     const FwdSpec sp = g_fwd_spec;
     g_fwd_spec = {};
-    GS_REQUIRE(!sp.on || (dt == GS_F32 && Wd == sp.S && K % 4 == 0 && self && relu && sp.np0 >= 1 &&
-                          sp.np0 <= 512 && sp.np1 >= 1 && sp.np1 <= 512 && sp.up_hi > sp.up_lo),
+    GS_REQUIRE(!sp.on || ((dt == GS_F32 ? (Wd == sp.S && !sp.Wn_lp) : (Wd == sp.S_lp && sp.Wn_lp != nullptr)) &&
+                          K % 4 == 0 && self && relu && sp.np0 >= 1 && sp.np0 <= 512 && sp.np1 >= 1 &&
+                          sp.np1 <= 512 && sp.up_hi > sp.up_lo),
                GS_EINVAL, "pending update: bad forward");
     // read per call (tests switch it between launches): wres | wide32 | wide | sk | chunked
     const std::string fwd_mode = std::getenv("GS_LIN_FWD") ? std::getenv("GS_LIN_FWD") : "";
@@ -435,14 +443,20 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
 #define GS_LFWDW_R(TT, RR) \
         do { if (self) { if (relu) GS_LFWDW(TT, RR, true, true); else GS_LFWDW(TT, RR, true, false); } \
              else { if (relu) GS_LFWDW(TT, RR, false, true); else GS_LFWDW(TT, RR, false, false); } } while (0)
-        if (dt == GS_F32 && sp.on) {  // self rows and relu (checked above): the pending-update instances
-#define GS_LFWDP(RR)                                                                                          \
-            launch_k(linear_fwd_wide_kernel<float, RR, true, true, true>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K, \
-                     static_cast<const float*>(Xs), ldxs, sidx, static_cast<const float*>(A), lda,            \
-                     static_cast<const float*>(Wd), out, ldo, sp)
-            if (R == 32) GS_LFWDP(32);
-            else if (R == 48) GS_LFWDP(48);
-            else GS_LFWDP(64);
+        if (sp.on) {  // self rows and relu (checked above): the pending-update instances
+#define GS_LFWDP(TT, RR)                                                                                    \
+            launch_k(linear_fwd_wide_kernel<TT, RR, true, true, true>, gw, dim3(RR * 16), 0, st, nn, ff, hh, K, \
+                     static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,                 \
+                     static_cast<const TT*>(Wd), out, ldo, sp)
+            if (dt == GS_F32) {
+                if (R == 32) GS_LFWDP(float, 32);
+                else if (R == 48) GS_LFWDP(float, 48);
+                else GS_LFWDP(float, 64);
+            } else {
+                if (R == 32) GS_LFWDP(bf16_t, 32);
+                else if (R == 48) GS_LFWDP(bf16_t, 48);
+                else GS_LFWDP(bf16_t, 64);
+            }
 #undef GS_LFWDP
         } else if (dt == GS_F32) {
             if (R == 32) GS_LFWDW_R(float, 32);
@@ -594,7 +608,7 @@ int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* 
 bool sum_slabs_pair_ok(int64_t len1) { return slab_split_on(len1); }
 
 int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P, float* spec_S,
-                          float lr) {
+                          float lr, uint16_t* spec_S_lp) {
     GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1, GS_EINVAL, "slab pair: layer-1 sum not split");
     const int nb1 = static_cast<int>(slab_split_blocks(s1.len));
     const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
@@ -602,7 +616,8 @@ int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, 
     DoneFlag done;
     if (spec_S) {  // the step's last launch: it carries the done flag
         GS_REQUIRE(spec_P && aligned16(spec_P) && aligned16(spec_S), GS_EINVAL, "slab pair: bad update buffers");
-        spec = SlabSpec{spec_P, spec_S, lr};
+        GS_REQUIRE(!spec_S_lp || reinterpret_cast<uintptr_t>(spec_S_lp) % 8 == 0, GS_EINVAL, "slab pair: bad bf16 buffer");
+        spec = SlabSpec{spec_P, spec_S, lr, spec_S_lp};
         done = g_done_flag;
         g_done_flag = {};
     }

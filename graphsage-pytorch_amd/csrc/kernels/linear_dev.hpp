@@ -301,6 +301,7 @@ __device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, 
     const float4* P4 = reinterpret_cast<const float4*>(sp.P) + int64_t(c0) * k4;
     const float4* G4 = reinterpret_cast<const float4*>(sp.G1) + int64_t(c0) * k4;
     float4* N4 = reinterpret_cast<float4*>(sp.Wn) + int64_t(c0) * k4;
+    uint2* L4 = sp.Wn_lp ? reinterpret_cast<uint2*>(sp.Wn_lp) + int64_t(c0) * k4 : nullptr;
     for (int i = threadIdx.x; i < rows * k4; i += blockDim.x) {
         const float4 pv = P4[i], gv = G4[i];
         float4 gi, pn;
@@ -309,6 +310,12 @@ __device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, 
         pn.z = sgd_elem(pv.z, gv.z, m0, sp.lr, gi.z);
         pn.w = sgd_elem(pv.w, gv.w, m0, sp.lr, gi.w);
         N4[i] = pn;
+        if (L4) {  // the bf16 W1 the forward reads (sgd4's shadow conversion)
+            uint2 b;
+            b.x = static_cast<uint32_t>(f2bf(pn.x)) | (static_cast<uint32_t>(f2bf(pn.y)) << 16);
+            b.y = static_cast<uint32_t>(f2bf(pn.z)) | (static_cast<uint32_t>(f2bf(pn.w)) << 16);
+            L4[i] = b;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
@@ -321,7 +328,6 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo,
     FwdSpec sp) {
-    static_assert(!PEND || std::is_same<T, float>::value, "the pending update is fp32");
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks

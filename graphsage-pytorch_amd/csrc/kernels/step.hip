@@ -90,8 +90,13 @@ struct gs_trainer {
     float* w1_alt = nullptr;
     int w1_cur = 0;
     float* w1_buf(int i) { return i == 0 ? cfg.params + w_off[0] : w1_alt; }
+    // bf16 features: the forward's bf16 W1 beside each buffer (lp_buf(w1_cur)
+    // is current while deferring: the slab sum and the recompute write both)
+    uint16_t* w1_lp_alt = nullptr;
+    uint16_t* lp_buf(int i) { return i == 0 ? w1_lp : w1_lp_alt; }
     ~gs_trainer() {
         if (w1_alt) (void)hipFree(w1_alt);
+        if (w1_lp_alt) (void)hipFree(w1_lp_alt);
         if (norm_part) (void)hipFree(norm_part);
         if (dw_cnt) (void)hipFree(dw_cnt);
         if (w1_lp) (void)hipFree(w1_lp);
@@ -289,14 +294,19 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     float* P = c.params;
     float* G = c.grads;
     // ---- forward (models.py:255-267)
-    if (lowp && !(T.lp_keep && T.lp_valid)) {
+    if (lowp && T.defer) {  // deferring: lp_buf(w1_cur) is cast once, then kept by the updates
+        if (!T.lp_valid && !T.pending) {
+            ok(gs_cast_f32_bf16(T.w1_buf(T.w1_cur), T.lp_buf(T.w1_cur), T.w_rows[0] * T.w_cols[0], st));
+            T.lp_valid = true;
+        }
+    } else if (lowp && !(T.lp_keep && T.lp_valid)) {
         ok(gs_cast_f32_bf16(P + T.w_off[0], T.w1_lp, T.w_rows[0] * T.w_cols[0], st));
         T.lp_valid = T.lp_keep;
     }
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
     const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
-    GS_REQUIRE(!T.defer || (!lowp && !fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
+    GS_REQUIRE(!T.defer || (!fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
     bool pend = T.defer && T.pending;
     if (pend && !(T.npart[0] >= 1 && T.npart[0] <= 512 && T.npart[1] >= 1 && T.npart[1] <= 512)) {
         // the forward folds at most 512 partials per group: apply the update on its own
@@ -305,13 +315,18 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         pend = false;
     }
     if (T.defer) {
-        W1 = T.w1_buf(pend ? T.w1_cur ^ 1 : T.w1_cur);
+        const int wb = pend ? T.w1_cur ^ 1 : T.w1_cur;
+        W1 = lowp ? static_cast<const void*>(T.lp_buf(wb)) : static_cast<const void*>(T.w1_buf(wb));
         if (pend) {  // the previous step's clip + SGD, applied by this forward launch
             FwdSpec sp;
             sp.on = 1;
             sp.S = T.w1_buf(T.w1_cur ^ 1);
             sp.P = T.w1_buf(T.w1_cur);
             sp.Wn = T.w1_buf(T.w1_cur ^ 1);
+            if (lowp) {
+                sp.S_lp = T.lp_buf(T.w1_cur ^ 1);
+                sp.Wn_lp = T.lp_buf(T.w1_cur ^ 1);
+            }
             sp.G1 = G + T.w_off[0];
             sp.part0 = T.norm_part;
             sp.part1 = T.norm_part + T.pstride;
@@ -520,7 +535,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                                   n_cls <= T.pstride;
                 np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st,
                                             spec ? T.w1_buf(T.w1_cur) : nullptr,
-                                            spec ? T.w1_buf(T.w1_cur ^ 1) : nullptr, c.lr);
+                                            spec ? T.w1_buf(T.w1_cur ^ 1) : nullptr, c.lr,
+                                            spec && lowp ? T.lp_buf(T.w1_cur ^ 1) : nullptr);
                 T.pending = spec;
             } else if (defer) {
                 if (d2.S > 1) sum_slabs_launch(d2.slabs, d2.S, d2.len, d2.out, nullptr, st);
@@ -656,16 +672,21 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
         w1_home(t, st);
         t->defer = false;
         t->norm_ready = false;
+        t->lp_valid = false;  // the next bf16 forward casts the flat W1 again
         return false;
     }
     const gs_trainer_config& c = t->cfg;
     const int64_t n1 = t->w_rows[0] * t->w_cols[0];
-    const bool ok = c.feat_dtype == GS_F32 && !t->fused1 && t->fuse_bwd && t->use_top && c.n_layers == 2 && !c.gcn &&
+    const bool ok = (c.feat_dtype == GS_F32 || (c.feat_dtype == GS_BF16 && t->w1_lp)) && !t->fused1 && t->fuse_bwd &&
+                    t->use_top && c.n_layers == 2 && !c.gcn &&
                     !t->fuse_update && !t->upper_hook && !t->w1_chunk_hook && n1 % 4 == 0 &&
                     t->cls_w_off % 4 == 0 && t->total % 4 == 0 && aligned16(c.params) && aligned16(c.grads);
     if (!ok) return false;
     if (!t->w1_alt)
         GS_REQUIRE(hipMalloc(&t->w1_alt, n1 * sizeof(float)) == hipSuccess, GS_ENOMEM, "hipMalloc(W1 buffer)");
+    if (c.feat_dtype == GS_BF16 && !t->w1_lp_alt)
+        GS_REQUIRE(hipMalloc(&t->w1_lp_alt, n1 * sizeof(uint16_t)) == hipSuccess, GS_ENOMEM, "hipMalloc(bf16 W1)");
+    t->lp_valid = false;  // the first forward casts W1 into lp_buf(0)
     t->defer = true;
     t->pending = false;
     t->w1_cur = 0;

@@ -308,8 +308,8 @@ def test_native_runner_matches_python_loop(gs, S, agg, gcn):
 
 
 @pytest.mark.parametrize("max_norm", [5.0, 1e-3, 0.05])
-@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
-def test_runner_deferred_update_matches_python_loop(gs, agg, max_norm):
+@pytest.mark.parametrize("agg,dtype", [("MEAN", "f32"), ("MAX", "f32"), ("MAX", "bf16"), ("MEAN", "bf16")])
+def test_runner_deferred_update_matches_python_loop(gs, agg, dtype, max_norm):
     """The runner's deferred update (each step's clip + SGD applied by the next
     step's launches: W1's update for clip coefficient 1 written by the slab
     sum and read by the next forward, recomputed there when the gradients
@@ -318,9 +318,12 @@ def test_runner_deferred_update_matches_python_loop(gs, agg, max_norm):
     clipped gradients of the Python loop's separate update launches, bit for
     bit: the reference's max_norm (5.0: the first steps clip, the later ones
     do not), clipping at every step (1e-3), and a mix (0.05), over runs of
-    1, 2 and 4 steps."""
+    1, 2 and 4 steps.  bf16 features: the forward's bf16 W1 comes from the
+    slab sum / the recompute instead of a cast of the updated W1."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    if dtype == "bf16":
+        X = X.to(torch.bfloat16)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:7]
     a = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=max_norm, seed=824)
