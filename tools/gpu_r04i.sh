@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 pass I: the defaults after the deferred update and the huge-page
-# pack slots: the whole GPU suite, smoke(), two default bench lines.
+# pack slots (fp32 and bf16): the whole GPU suite, smoke(), bench lines
+# alternating rmat2m / rmat2m-max-bf16.
 set -o pipefail
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
@@ -11,8 +12,10 @@ timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thre
 tail -1 "$OUT/gpu_tests.log"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
 tail -1 "$OUT/smoke.log"
-for i in 1 2; do
-  timeout -k 10 400 python3 bench.py > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.err" || exit $?
+for i in 1 2 3 4; do
+  C=rmat2m; [ $((i % 2)) -eq 0 ] && C=rmat2m-max-bf16
+  timeout -k 10 400 python3 bench.py --config $C > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.err" || exit $?
+  echo -n "$C "
   python3 - "$OUT/bench_$i.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
