@@ -33,3 +33,7 @@ c = d["config"]
 print(sys.argv[1].split("/")[-1], "value", d["value"], "ms", d["ms_per_step"], "sampler ms", c["sampler"]["ms_per_batch"], "sustained", d["sustained"]["value"], d["sustained"]["ms_per_step"], "ref", (d.get("reference_stream") or {}).get("value"))
 PY
 done
+# kernel trace of a short default bench: the step's timeline (main / side overlap)
+timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --sustain 0 --ref-stream-steps 0 > "$OUT/trace.log" 2>&1 || exit $?
+cp "$OUT/trace/run_kernel_trace.csv" "$OUT/kernel_trace.csv" && rm -rf "$OUT/trace"
+python3 tools/timeline.py "$OUT/kernel_trace.csv" > "$OUT/timeline.txt" 2>&1; cat "$OUT/timeline.txt"
