@@ -117,6 +117,20 @@ inline thread_local LaunchEvents g_launch_events;
 // a timer site reports which kernel variant it actually timed.
 inline thread_local const char* g_launch_name = nullptr;
 
+// In-kernel span of a timed launch (the bench's roofline timers, step.hip):
+// when set, the next launch of a kernel that supports it (the layer-1 wide
+// forward, the top launch) stores the 100 MHz s_memrealtime clock of its
+// first wave's start (atomicMin into *start) and of every wave's end
+// (atomicMax into *end): the first-wave-to-last-wave span rocprofv3's kernel
+// trace reports.  The launcher takes it (and drops g_launch_events: an event
+// pair's start marker is processed before the dispatch, so its span also
+// covers the wait for the previous launch of a full queue).
+struct KStamp {
+    unsigned long long* start = nullptr;
+    unsigned long long* end = nullptr;
+};
+inline thread_local KStamp g_kernel_stamp;
+
 // Host-visible step-completion flag (runtime/runner.hip): when set, the next
 // SGD launch of this thread stores `value` into `ptr` (fine-grained pinned
 // memory, system scope) from its first thread at kernel start -- by stream
@@ -161,12 +175,40 @@ struct FwdSpec {
     float* p = nullptr;          // flat params / grads
     float* g = nullptr;
     int64_t up_lo = 0, up_hi = 0, grp1_lo = 0;  // the other parameters; group 1 from grp1_lo
+    KStamp stamp;                // a timed launch's span (g_kernel_stamp), independent of `on`
 };
 inline thread_local FwdSpec g_fwd_spec;
+
+#ifdef __HIPCC__
+__device__ __forceinline__ void kstamp_begin(const KStamp& k) {
+    if (k.start && threadIdx.x == 0) atomicMin(k.start, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+}
+__device__ __forceinline__ void kstamp_end(const KStamp& k) {  // by each wave, as it leaves
+    if (k.end && (threadIdx.x & 63) == 0)
+        atomicMax(k.end, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+}
+#endif
+
+// A launcher whose kernel stores its span: take the armed stamp, if any (the
+// next launch_k then records the kernel's name, as an event-bound one does).
+inline thread_local bool g_name_next = false;
+inline KStamp take_kernel_stamp() {
+    const KStamp k = g_kernel_stamp;
+    g_kernel_stamp = {};
+    if (k.start) {
+        g_launch_events = {};
+        g_name_next = true;
+    }
+    return k;
+}
 
 template <typename... KArgs, typename... Args>
 inline void launch_k(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t st, Args... args) {
     LaunchEvents ev = g_launch_events;
+    if (g_name_next) {
+        g_name_next = false;
+        g_launch_name = hipKernelNameRefByPtr(reinterpret_cast<const void*>(kernel), st);
+    }
     if (ev.start) {
         g_launch_events = {};
         g_launch_name = hipKernelNameRefByPtr(reinterpret_cast<const void*>(kernel), st);

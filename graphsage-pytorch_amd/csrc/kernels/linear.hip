@@ -338,7 +338,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     hipStream_t st = as_stream(stream);
     const int nn = static_cast<int>(n), ff = static_cast<int>(F), hh = static_cast<int>(H);
     // a pending clip + SGD (the trainer's deferred update): the fp32 wide kernel applies it
-    const FwdSpec sp = g_fwd_spec;
+    FwdSpec sp = g_fwd_spec;
     g_fwd_spec = {};
     GS_REQUIRE(!sp.on || ((dt == GS_F32 ? (Wd == sp.S && !sp.Wn_lp) : (Wd == sp.S_lp && sp.Wn_lp != nullptr)) &&
                           K % 4 == 0 && self && relu && sp.np0 >= 1 && sp.np0 <= 512 && sp.np1 >= 1 &&
@@ -410,6 +410,7 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
     static const bool bf16_chunked = std::getenv("GS_LIN_FWD_BF16") &&
                                      std::string(std::getenv("GS_LIN_FWD_BF16")) == "chunked";
     if ((wide_on || wide32_on) && vload && (dt == GS_F32 || !bf16_chunked)) {
+        sp.stamp = take_kernel_stamp();  // a timed launch: the kernel stores its own span
         // Rows per tile: 32, or 48 when 32-row tiles would need more than one
         // workgroup per CU (a second round on some CUs: layer 1 at rmat2m
         // measured 10.5 us at 256 workgroups against 15.0 us at 264-300) and

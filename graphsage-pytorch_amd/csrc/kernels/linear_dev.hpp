@@ -328,6 +328,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo,
     FwdSpec sp) {
+    kstamp_begin(sp.stamp);
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
     constexpr int SP = kSlots + 1;  // row pitch in 16-byte slots: 16 rows of one slot column hit distinct banks
@@ -377,6 +378,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     };
     if (m0 >= n) {  // spare blocks of the last group of 8 (they still take their share of the update)
         if constexpr (PEND) pending_apply();
+        kstamp_end(sp.stamp);
         return;
     }
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
@@ -439,15 +441,17 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         if (pending_apply()) acc = run_k();
     }
     const int col = c0 + 16 * wc + r;
-    if (col >= H) return;
+    if (col < H) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = m0 + 16 * wr + 4 * kq + j;
-        if (row < n) {
-            const float v = acc[j];
-            out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;
+        for (int j = 0; j < 4; ++j) {
+            const int row = m0 + 16 * wr + 4 * kq + j;
+            if (row < n) {
+                const float v = acc[j];
+                out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;
+            }
         }
     }
+    kstamp_end(sp.stamp);
 }
 
 // Forward, fp32, split-K inside the block ("sk").  Block = 16 rows x 32

@@ -29,6 +29,11 @@ struct gs_trainer {
         int64_t n = 0;
         int64_t every = 1, calls = 0;  // time one launch of every `every`, the last of each run
         std::string kernel;  // demangled name of the kernel the site last timed
+        // sites 1 and 3: the kernel's own span (KStamp, kcommon.hpp) per entry,
+        // when the launch took it (else the entry's events timed it)
+        unsigned long long* st0 = nullptr;  // device: first-wave start per entry (100 MHz ticks)
+        unsigned long long* st1 = nullptr;  // device: last-wave end per entry
+        std::vector<char> stamped;
     } timer[kSites];
     std::vector<hipEvent_t>& ev0 = timer[0].ev0;
     std::vector<hipEvent_t>& ev1 = timer[0].ev1;
@@ -111,6 +116,8 @@ struct gs_trainer {
             if (p) (void)hipFree(p);
         for (int32_t* p : top_slot)
             if (p) (void)hipFree(p);
+        for (auto& tm : timer)
+            if (tm.st0) (void)hipFree(tm.st0);
     }
 };
 
@@ -144,6 +151,8 @@ static inline bool timed_arm(gs_trainer& T, int site) {
     if (tm.n >= static_cast<int64_t>(tm.ev0.size())) return false;
     if (++tm.calls % tm.every) return false;
     g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
+    if (tm.st0) g_kernel_stamp = {tm.st0 + tm.n, tm.st1 + tm.n};
+    g_launch_name = nullptr;  // set by the timed launch
     return true;
 }
 // Timer events only measure: no system-scope release when they complete (a
@@ -166,6 +175,9 @@ static std::string demangle(const char* sym) {
 
 static inline void timed_done(gs_trainer& T, int site, bool armed) {
     if (!armed) return;
+    auto& tm = T.timer[site];
+    if (tm.st0) tm.stamped[tm.n] = g_kernel_stamp.start == nullptr;  // the launch took the stamp
+    g_kernel_stamp = {};
     GS_REQUIRE(!g_launch_events.start, GS_EINVAL, "timed launch did not consume its events");
     // the kernel of the latest timed launch (the layer-1 forward has two instances:
     // with the deferred update pending, and without, at a run's first step)
@@ -881,6 +893,17 @@ int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capa
         const int64_t cap = (site_mask >> s) & 1 ? capacity : 0;
         tm.ev0.assign(cap, nullptr);
         tm.ev1.assign(cap, nullptr);
+        if (tm.st0) (void)hipFree(tm.st0);
+        tm.st0 = tm.st1 = nullptr;
+        tm.stamped.assign(cap, 0);
+        if ((s == 1 || s == 3) && cap > 0 && std::getenv("GS_TIMER_EVENTS") == nullptr) {  // span stamps
+            GS_REQUIRE(hipMalloc(&tm.st0, 2 * cap * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
+                       "hipMalloc(timer stamps)");
+            tm.st1 = tm.st0 + cap;
+            GS_REQUIRE(hipMemset(tm.st0, 0xFF, cap * sizeof(unsigned long long)) == hipSuccess &&
+                           hipMemset(tm.st1, 0, cap * sizeof(unsigned long long)) == hipSuccess,
+                       GS_EHIP, "hipMemset(timer stamps)");
+        }
         for (int64_t i = 0; i < cap; ++i)
             GS_REQUIRE(hipEventCreateWithFlags(&tm.ev0[i], gs::timer_event_flags()) == hipSuccess &&
                            hipEventCreateWithFlags(&tm.ev1[i], gs::timer_event_flags()) == hipSuccess,
@@ -899,7 +922,21 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
     if (!t || !ms || site < 0 || site >= gs_trainer::kSites) return -1;
     auto& tm = t->timer[site];
     const int64_t n = std::min(cap, tm.n);
+    std::vector<unsigned long long> a, b;
+    if (tm.st0 && n > 0) {
+        if (hipDeviceSynchronize() != hipSuccess) return -1;
+        a.resize(n);
+        b.resize(n);
+        if (hipMemcpy(a.data(), tm.st0, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(b.data(), tm.st1, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+    }
     for (int64_t i = 0; i < n; ++i) {
+        if (tm.st0 && tm.stamped[i]) {  // the kernel's own span, 100 MHz ticks
+            if (b[i] < a[i]) return -1;
+            ms[i] = static_cast<float>(static_cast<double>(b[i] - a[i]) * 1e-5);
+            continue;
+        }
         if (hipEventSynchronize(tm.ev1[i]) != hipSuccess || hipEventElapsedTime(&ms[i], tm.ev0[i], tm.ev1[i]) != hipSuccess)
             return -1;
     }

@@ -66,6 +66,7 @@ struct TopArgs {
     float* slab;         // classifier partials, one [C][H+1] + 1 slab per block
     const int* tids;     // optional: per root [self | list padded to tk with -1] (resolve_top_launch)
     int tk;
+    KStamp stamp;        // a timed launch's span (g_kernel_stamp)
 };
 
 // k offset of step i (0..15) inside a 16-wide block: the MFMA kernels' order.
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     const int nr = min(kTopRows, a.B - r0);
 
     GS_TOP_STAMP(0);
+    kstamp_begin(a.stamp);
     // ---- W2 -> LDS by DMA (no registers), issued before anything else so its
     // latency hides under the gather.  Row c is one wave instruction of 64
     // 16-byte quads; quad q of the row lands in slot q ^ (c & 15), which keeps
@@ -438,6 +440,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             if (j < nr) a.dIn[static_cast<int64_t>(r0 + j) * K + kc] = acc[j];
     }
     GS_TOP_STAMP(6);
+    kstamp_end(a.stamp);
 }
 
 static size_t top_smem_bytes(int64_t C) {
@@ -476,7 +479,7 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
                    aligned16(dIn) && (agg == GS_AGG_MEAN || (argmax && aligned16(argmax))),
                GS_EINVAL, "top: unaligned operand");
     TopArgs a{static_cast<int>(B), static_cast<int>(C), Hprev, ptr, nbr, self, W, Wc, bc, labels, roots,
-              aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0};
+              aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
     if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);
