@@ -119,14 +119,16 @@ inline thread_local const char* g_launch_name = nullptr;
 
 // In-kernel span of a timed launch (the bench's roofline timers, step.hip):
 // when set, the next launch of a kernel that supports it (the layer-1 wide
-// forward, the top launch) stores the 100 MHz s_memrealtime clock of its
-// first wave's start (atomicMin into *start) and of every wave's end
-// (atomicMax into *end): the first-wave-to-last-wave span rocprofv3's kernel
-// trace reports.  The launcher takes it (and drops g_launch_events: an event
-// pair's start marker is processed before the dispatch, so its span also
-// covers the wait for the previous launch of a full queue).
+// forward, the top launch) stores the 100 MHz s_memrealtime clock at each
+// workgroup's start and end (plain stores, one slot per workgroup: no
+// atomics on a shared word, which serialise across the chip), and the host
+// takes min(start) .. max(end): the first-wave-to-last-wave span rocprofv3's
+// kernel trace reports.  The launcher takes it (and drops g_launch_events: an
+// event pair's start marker is processed before the dispatch, so its span
+// also covers the wait for the previous launch of a full queue).
+constexpr int kStampBlocks = 1024;  // workgroups per timed launch with a slot (more: not timed)
 struct KStamp {
-    unsigned long long* start = nullptr;
+    unsigned long long* start = nullptr;  // [kStampBlocks], zeroed
     unsigned long long* end = nullptr;
 };
 inline thread_local KStamp g_kernel_stamp;
@@ -179,15 +181,17 @@ struct FwdSpec {
 };
 inline thread_local FwdSpec g_fwd_spec;
 
-#ifdef __HIPCC__
+__device__ __forceinline__ int kstamp_block() { return blockIdx.x + blockIdx.y * gridDim.x; }
 __device__ __forceinline__ void kstamp_begin(const KStamp& k) {
-    if (k.start && threadIdx.x == 0) atomicMin(k.start, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+    if (k.start && threadIdx.x == 0 && kstamp_block() < kStampBlocks)
+        k.start[kstamp_block()] = __builtin_amdgcn_s_memrealtime();
 }
-__device__ __forceinline__ void kstamp_end(const KStamp& k) {  // by each wave, as it leaves
-    if (k.end && (threadIdx.x & 63) == 0)
-        atomicMax(k.end, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+// At the workgroup's end; every thread of the workgroup calls it (a barrier).
+__device__ __forceinline__ void kstamp_end(const KStamp& k) {
+    if (!k.end) return;
+    __syncthreads();
+    if (threadIdx.x == 0 && kstamp_block() < kStampBlocks) k.end[kstamp_block()] = __builtin_amdgcn_s_memrealtime();
 }
-#endif
 
 // A launcher whose kernel stores its span: take the armed stamp, if any (the
 // next launch_k then records the kernel's name, as an event-bound one does).

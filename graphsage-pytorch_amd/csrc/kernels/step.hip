@@ -31,8 +31,8 @@ struct gs_trainer {
         std::string kernel;  // demangled name of the kernel the site last timed
         // sites 1 and 3: the kernel's own span (KStamp, kcommon.hpp) per entry,
         // when the launch took it (else the entry's events timed it)
-        unsigned long long* st0 = nullptr;  // device: first-wave start per entry (100 MHz ticks)
-        unsigned long long* st1 = nullptr;  // device: last-wave end per entry
+        unsigned long long* st0 = nullptr;  // device: per entry, kStampBlocks workgroup starts (100 MHz ticks)
+        unsigned long long* st1 = nullptr;  // device: per entry, the workgroup ends
         std::vector<char> stamped;
     } timer[kSites];
     std::vector<hipEvent_t>& ev0 = timer[0].ev0;
@@ -151,7 +151,7 @@ static inline bool timed_arm(gs_trainer& T, int site) {
     if (tm.n >= static_cast<int64_t>(tm.ev0.size())) return false;
     if (++tm.calls % tm.every) return false;
     g_launch_events = {tm.ev0[tm.n], tm.ev1[tm.n]};
-    if (tm.st0) g_kernel_stamp = {tm.st0 + tm.n, tm.st1 + tm.n};
+    if (tm.st0) g_kernel_stamp = {tm.st0 + tm.n * kStampBlocks, tm.st1 + tm.n * kStampBlocks};
     g_launch_name = nullptr;  // set by the timed launch
     return true;
 }
@@ -897,12 +897,12 @@ int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capa
         tm.st0 = tm.st1 = nullptr;
         tm.stamped.assign(cap, 0);
         if ((s == 1 || s == 3) && cap > 0 && std::getenv("GS_TIMER_EVENTS") == nullptr) {  // span stamps
-            GS_REQUIRE(hipMalloc(&tm.st0, 2 * cap * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
+            const int64_t words = cap * gs::kStampBlocks;
+            GS_REQUIRE(hipMalloc(&tm.st0, 2 * words * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
                        "hipMalloc(timer stamps)");
-            tm.st1 = tm.st0 + cap;
-            GS_REQUIRE(hipMemset(tm.st0, 0xFF, cap * sizeof(unsigned long long)) == hipSuccess &&
-                           hipMemset(tm.st1, 0, cap * sizeof(unsigned long long)) == hipSuccess,
-                       GS_EHIP, "hipMemset(timer stamps)");
+            tm.st1 = tm.st0 + words;
+            GS_REQUIRE(hipMemset(tm.st0, 0, 2 * words * sizeof(unsigned long long)) == hipSuccess, GS_EHIP,
+                       "hipMemset(timer stamps)");
         }
         for (int64_t i = 0; i < cap; ++i)
             GS_REQUIRE(hipEventCreateWithFlags(&tm.ev0[i], gs::timer_event_flags()) == hipSuccess &&
@@ -923,18 +923,24 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
     auto& tm = t->timer[site];
     const int64_t n = std::min(cap, tm.n);
     std::vector<unsigned long long> a, b;
+    const int64_t W = gs::kStampBlocks;
     if (tm.st0 && n > 0) {
         if (hipDeviceSynchronize() != hipSuccess) return -1;
-        a.resize(n);
-        b.resize(n);
-        if (hipMemcpy(a.data(), tm.st0, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
-            hipMemcpy(b.data(), tm.st1, n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        a.resize(n * W);
+        b.resize(n * W);
+        if (hipMemcpy(a.data(), tm.st0, n * W * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(b.data(), tm.st1, n * W * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
             return -1;
     }
     for (int64_t i = 0; i < n; ++i) {
-        if (tm.st0 && tm.stamped[i]) {  // the kernel's own span, 100 MHz ticks
-            if (b[i] < a[i]) return -1;
-            ms[i] = static_cast<float>(static_cast<double>(b[i] - a[i]) * 1e-5);
+        if (tm.st0 && tm.stamped[i]) {  // the kernel's own span: min start .. max end, 100 MHz ticks
+            unsigned long long lo = ~0ull, hi = 0;
+            for (int64_t w = 0; w < W; ++w) {
+                if (a[i * W + w]) lo = std::min(lo, a[i * W + w]);
+                hi = std::max(hi, b[i * W + w]);
+            }
+            if (hi == 0 || lo == ~0ull || hi < lo) return -1;
+            ms[i] = static_cast<float>(static_cast<double>(hi - lo) * 1e-5);
             continue;
         }
         if (hipEventSynchronize(tm.ev1[i]) != hipSuccess || hipEventElapsedTime(&ms[i], tm.ev0[i], tm.ev1[i]) != hipSuccess)

@@ -23,3 +23,17 @@ for k, v in d.get("roofline_kernels", {}).items():
     print("   ", k, v.get("avg_launch_us"), v.get("achieved"), v.get("frac"), (v.get("rocprof") or {}).get("avg_us"))
 PY
 done
+# the pack pull on the copy engine (GS_PULL_COPY=1) against the pull kernel, with the deferred step
+for i in 1 2; do
+  for P in 0 1; do
+    if [ $P -eq 1 ]; then export GS_PULL_COPY=1; else unset GS_PULL_COPY; fi
+    timeout -k 10 400 python3 bench.py --no-cpu-baseline --ref-stream-steps 0 > "$OUT/bench_pc${P}_$i.json" 2> "$OUT/bench_pc${P}_$i.err" || exit $?
+    echo -n "pull_copy $P "
+    python3 - "$OUT/bench_pc${P}_$i.json" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print("value", d["value"], "ms", d["ms_per_step"], "sustained", d["sustained"]["value"], d["sustained"]["ms_per_step"])
+PY
+  done
+done
+unset GS_PULL_COPY
