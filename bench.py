@@ -11,10 +11,13 @@ Throughput = roots processed by all ranks / max-over-ranks wall time of the
 timed steps (weak scaling: B roots per GPU per step).
 
 Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel (the
-layer-1 gather-aggregate, K-agg) from its algorithmic bytes and its HIP-event
-duration inside the timed region; `cpu_baseline` times the oracle (the CPU
-restatement of the reference's algorithm) on a bounded sample of the same
-workload on this host.
+largest average in the committed rocprofv3 summary of the config: the layer-1
+forward GEMM at fp32, the top launch at bf16) from its algorithmic flops or
+bytes and its launch duration inside the timed region: the kernel's own span
+(per-workgroup s_memrealtime stamps, min start .. max end) for the forward
+and top launches, kernel-bound HIP events for the gather and dW;
+`cpu_baseline` times the oracle (the CPU restatement of the reference's
+algorithm) on a bounded sample of the same workload on this host.
 """
 import argparse
 import csv
@@ -866,6 +869,9 @@ def main():
                 rocprof=prof_avg[site],
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
+                timer=("kernel span (per-workgroup s_memrealtime stamps, min start .. max end)"
+                       if site in (1, 3) and not os.environ.get("GS_TIMER_EVENTS")
+                       else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
                 timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
                 **work)
