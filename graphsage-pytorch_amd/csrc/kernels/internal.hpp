@@ -36,7 +36,7 @@ void trainer_fuse_update(gs_trainer* t, bool fuse);
 // pending).  Returns whether deferral is on; off (at the end of the loop)
 // applies the last pending update, so the flat parameters and gradients are
 // those of the separate update launch.
-bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st);
+bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st, bool comm = false);
 // A fused SGD launch's grid barrier gave up waiting (never expected).
 bool trainer_barrier_failed(gs_trainer* t);
 int64_t trainer_w1_floats(const gs_trainer* t);
@@ -121,6 +121,12 @@ int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float
                     hipStream_t st);
 void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart, int pstride, float* params,
                     float* grads, const float* part, float grad_scale, float max_norm, float lr, hipStream_t st);
+// The deferred update after an all-reduce: gs_clip_sgd's norm partials (into
+// part, kNormBlocks per group; returns that count) and W1's speculative update
+// S = P - lr·(scale·g) (+ S_lp in bf16) for the elements [0, n1); takes the
+// done flag.
+int sumsq_spec_launch(int32_t n_groups, const int64_t* goff_host, const float* grads, float* part, const float* P,
+                      float* S, uint16_t* S_lp, int64_t n1, float lr, float scale, hipStream_t st);
 
 // bwd.hip: the backward of one layer l >= 2 (fp32 activations, relu already
 // folded into dZ) in two launches, each running independent kernels side by

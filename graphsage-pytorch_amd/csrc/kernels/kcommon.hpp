@@ -174,6 +174,7 @@ struct FwdSpec {
     const float* part1 = nullptr;
     int np0 = 0, np1 = 0;
     float lr = 0.f, max_norm = 0.f;
+    float scale = 1.f;           // gradient scale (1 / world after an all-reduce): S used m = scale
     float* p = nullptr;          // flat params / grads
     float* g = nullptr;
     int64_t up_lo = 0, up_hi = 0, grp1_lo = 0;  // the other parameters; group 1 from grp1_lo

@@ -635,8 +635,8 @@ int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, 
 __global__ __launch_bounds__(kThreads) void spec_finalize_kernel(FwdSpec sp, float* __restrict__ w1_out,
                                                                  int64_t w1_floats) {
     const int lane = threadIdx.x & 63;
-    const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), 1.0f, sp.max_norm);
-    const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), 1.0f, sp.max_norm);
+    const float m0 = clip_mult(clip_fold(sp.part0, sp.np0, lane), sp.scale, sp.max_norm);
+    const float m1 = clip_mult(clip_fold(sp.part1, sp.np1, lane), sp.scale, sp.max_norm);
     const int64_t stride = int64_t(gridDim.x) * blockDim.x, t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     float4* G1 = reinterpret_cast<float4*>(const_cast<float*>(sp.G1));
     const float4* S4 = reinterpret_cast<const float4*>(sp.S);
@@ -644,14 +644,15 @@ __global__ __launch_bounds__(kThreads) void spec_finalize_kernel(FwdSpec sp, flo
     float4* O4 = reinterpret_cast<float4*>(w1_out);
     for (int64_t i = t; i < w1_floats / 4; i += stride) {
         const float4 gv = G1[i];
-        const float4 pv = m0 == 1.0f ? S4[i] : P4[i];
+        const bool spec = m0 == sp.scale;  // clip coefficient 1: S is the update
+        const float4 pv = spec ? S4[i] : P4[i];
         float4 gi, pn;
         pn.x = sgd_elem(pv.x, gv.x, m0, sp.lr, gi.x);
         pn.y = sgd_elem(pv.y, gv.y, m0, sp.lr, gi.y);
         pn.z = sgd_elem(pv.z, gv.z, m0, sp.lr, gi.z);
         pn.w = sgd_elem(pv.w, gv.w, m0, sp.lr, gi.w);
         G1[i] = gi;
-        O4[i] = m0 == 1.0f ? pv : pn;
+        O4[i] = spec ? pv : pn;
     }
     float4* p4 = reinterpret_cast<float4*>(sp.p);
     float4* g4 = reinterpret_cast<float4*>(sp.g);

@@ -296,7 +296,7 @@ __device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, 
     float4* g4 = reinterpret_cast<float4*>(sp.g);
     for (int64_t i = i0 + stride; i < sp.up_hi / 4; i += stride)
         sgd_quad(p4, g4, i, p4[i], g4[i], 4 * i >= sp.grp1_lo ? m1 : m0, sp.lr);
-    if (m0 == 1.0f) return false;
+    if (m0 == sp.scale) return false;  // clip coefficient 1: S is the update
     const int k4 = K / 4, rows = min(64, H - c0);
     const float4* P4 = reinterpret_cast<const float4*>(sp.P) + int64_t(c0) * k4;
     const float4* G4 = reinterpret_cast<const float4*>(sp.G1) + int64_t(c0) * k4;
@@ -369,8 +369,8 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     }
     // the coefficients and the update of this thread's quad (before W1 is read)
     auto pending_apply = [&]() -> bool {
-        const float mm0 = clip_mult(clip_fold_finish(sp.np0, lane, f0), 1.0f, sp.max_norm);
-        const float mm1 = clip_mult(clip_fold_finish(sp.np1, lane, f1), 1.0f, sp.max_norm);
+        const float mm0 = clip_mult(clip_fold_finish(sp.np0, lane, f0), sp.scale, sp.max_norm);
+        const float mm1 = clip_mult(clip_fold_finish(sp.np1, lane, f1), sp.scale, sp.max_norm);
         if (ui0 < sp.up_hi / 4)
             sgd_quad(reinterpret_cast<float4*>(sp.p), reinterpret_cast<float4*>(sp.g), ui0, upv, ugv,
                      4 * ui0 >= sp.grp1_lo ? mm1 : mm0, sp.lr);

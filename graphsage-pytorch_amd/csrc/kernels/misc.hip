@@ -250,6 +250,64 @@ __global__ __launch_bounds__(kTb) void group_sumsq_kernel(Groups G, const float*
     }
 }
 
+// group_sumsq_kernel with the deferred update's speculative W1 (after an
+// all-reduce, gs_trainer_update in deferred mode): the elements [0, n1) of
+// group 0 also get S = P - lr·(scale·g) (sgd_elem with m = scale: the update
+// when the clip coefficient is 1; + its bf16 copy), and the launch stores
+// the step's done flag (it is the step's last).
+struct SumsqSpec {
+    const float* P;
+    float* S;
+    uint16_t* S_lp;
+    int64_t n1;
+    float lr, scale;
+    int64_t* done;
+    int64_t done_value;
+};
+__global__ __launch_bounds__(kTb) void group_sumsq_spec_kernel(Groups G, const float* __restrict__ g,
+                                                               float* __restrict__ part, SumsqSpec sp) {
+    signal_done(sp.done, sp.done_value);
+    __shared__ float red[kTb / 64];
+    const int grp = blockIdx.y;
+    const int64_t lo = G.off[grp], hi = G.off[grp + 1];
+    float s = 0.f;
+#pragma unroll 8
+    for (int64_t i = lo + blockIdx.x * int64_t(kTb) + threadIdx.x; i < hi; i += int64_t(kNormBlocks) * kTb) {
+        const float v = g[i];
+        s = fmaf(v, v, s);
+        if (i < sp.n1) {
+            float gi;
+            const float pn = sgd_elem(sp.P[i], v, sp.scale, sp.lr, gi);
+            sp.S[i] = pn;
+            if (sp.S_lp) sp.S_lp[i] = f2bf(pn);
+        }
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < kTb / 64; ++w) t += red[w];
+        part[grp * G.pstride + blockIdx.x] = t;
+    }
+}
+
+int sumsq_spec_launch(int32_t n_groups, const int64_t* goff_host, const float* grads, float* part, const float* P,
+                      float* S, uint16_t* S_lp, int64_t n1, float lr, float scale, hipStream_t st) {
+    GS_REQUIRE(n_groups >= 1 && n_groups <= 8 && goff_host && grads && part && P && S, GS_EINVAL, "sumsq_spec: bad args");
+    GS_REQUIRE(goff_host[0] == 0 && n1 <= goff_host[1], GS_EINVAL, "sumsq_spec: W1 not at the front of group 0");
+    Groups G;
+    G.n = n_groups;
+    G.pstride = kNormBlocks;
+    for (int i = 0; i < n_groups; ++i) G.npart[i] = kNormBlocks;
+    for (int i = 0; i <= n_groups; ++i) G.off[i] = goff_host[i];
+    const SumsqSpec sp{P, S, S_lp, n1, lr, scale, g_done_flag.ptr, g_done_flag.value};
+    g_done_flag = {};
+    group_sumsq_spec_kernel<<<dim3(kNormBlocks, n_groups), kTb, 0, st>>>(G, grads, part, sp);
+    check_launch("sumsq_spec");
+    return kNormBlocks;
+}
+
 // Each block first folds the per-group partial sums (same fixed order in
 // every block) into clip_coef = max_norm / (||scale·g|| + 1e-6) clamped to 1,
 // then p -= lr · (scale · coef) · g and g is left scaled like torch's in-place

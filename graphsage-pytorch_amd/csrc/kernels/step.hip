@@ -92,6 +92,13 @@ struct gs_trainer {
     // flat params, buffer 1 w1_alt; trainer_defer_update(false) puts the
     // result of the last pending update back into the flat params.
     bool defer = false, pending = false;
+    bool defer_comm = false;  // the all-reduce path: gs_trainer_update leaves the update pending
+    // the pending update's norm partials (the step's own, or gs_trainer_update's
+    // after the all-reduce), per-group counts and stride, gradient scale
+    const float* pend_part = nullptr;
+    int pend_pstride = 0;
+    int pend_np[2] = {0, 0};
+    float pend_scale = 1.f;
     float* w1_alt = nullptr;
     int w1_cur = 0;
     float* w1_buf(int i) { return i == 0 ? cfg.params + w_off[0] : w1_alt; }
@@ -320,7 +327,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const bool fused1 = T.fused1 && a1_slot < 0;
     GS_REQUIRE(!T.defer || (!fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
     bool pend = T.defer && T.pending;
-    if (pend && !(T.npart[0] >= 1 && T.npart[0] <= 512 && T.npart[1] >= 1 && T.npart[1] <= 512)) {
+    if (pend && !(T.pend_np[0] >= 1 && T.pend_np[0] <= 512 && T.pend_np[1] >= 1 && T.pend_np[1] <= 512)) {
         // the forward folds at most 512 partials per group: apply the update on its own
         trainer_defer_update(&T, false, st);
         trainer_defer_update(&T, true, st);
@@ -340,12 +347,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 sp.Wn_lp = T.lp_buf(T.w1_cur ^ 1);
             }
             sp.G1 = G + T.w_off[0];
-            sp.part0 = T.norm_part;
-            sp.part1 = T.norm_part + T.pstride;
-            sp.np0 = T.npart[0];
-            sp.np1 = T.npart[1];
+            sp.part0 = T.pend_part;
+            sp.part1 = T.pend_part + T.pend_pstride;
+            sp.np0 = T.pend_np[0];
+            sp.np1 = T.pend_np[1];
             sp.lr = c.lr;
             sp.max_norm = c.max_norm;
+            sp.scale = T.pend_scale;
             sp.p = P;
             sp.g = G;
             sp.up_lo = T.w_off[0] + T.w_rows[0] * T.w_cols[0];
@@ -543,13 +551,20 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 // deferred update: this launch also writes W1's update for clip
                 // coefficient 1 (and carries the done flag); the clip + SGD
                 // itself is left to the next forward
-                const bool spec = T.defer && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
+                const bool spec = T.defer && !T.defer_comm && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
                                   n_cls <= T.pstride;
                 np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st,
                                             spec ? T.w1_buf(T.w1_cur) : nullptr,
                                             spec ? T.w1_buf(T.w1_cur ^ 1) : nullptr, c.lr,
                                             spec && lowp ? T.lp_buf(T.w1_cur ^ 1) : nullptr);
                 T.pending = spec;
+                if (spec) {
+                    T.pend_part = T.norm_part;
+                    T.pend_pstride = T.pstride;
+                    T.pend_np[0] = np;
+                    T.pend_np[1] = n_cls;
+                    T.pend_scale = 1.f;
+                }
             } else if (defer) {
                 if (d2.S > 1) sum_slabs_launch(d2.slabs, d2.S, d2.len, d2.out, nullptr, st);
                 parts = false;
@@ -658,7 +673,7 @@ static void w1_home(gs_trainer* t, hipStream_t st) {
     t->w1_cur = 0;
 }
 
-bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
+bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st, bool comm) {
     if (!on) {
         if (t->pending) {  // the last step's clip + SGD: the flat params become what sgd4 would leave
             FwdSpec sp;
@@ -666,12 +681,13 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
             sp.S = t->w1_buf(t->w1_cur ^ 1);
             sp.P = t->w1_buf(t->w1_cur);
             sp.G1 = t->cfg.grads + t->w_off[0];
-            sp.part0 = t->norm_part;
-            sp.part1 = t->norm_part + t->pstride;
-            sp.np0 = t->npart[0];
-            sp.np1 = t->npart[1];
+            sp.part0 = t->pend_part;
+            sp.part1 = t->pend_part + t->pend_pstride;
+            sp.np0 = t->pend_np[0];
+            sp.np1 = t->pend_np[1];
             sp.lr = t->cfg.lr;
             sp.max_norm = t->cfg.max_norm;
+            sp.scale = t->pend_scale;
             sp.p = t->cfg.params;
             sp.g = t->cfg.grads;
             sp.up_lo = t->w_off[0] + t->w_rows[0] * t->w_cols[0];
@@ -683,6 +699,7 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
         }
         w1_home(t, st);
         t->defer = false;
+        t->defer_comm = false;
         t->norm_ready = false;
         t->lp_valid = false;  // the next bf16 forward casts the flat W1 again
         return false;
@@ -690,8 +707,8 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
     const gs_trainer_config& c = t->cfg;
     const int64_t n1 = t->w_rows[0] * t->w_cols[0];
     const bool ok = (c.feat_dtype == GS_F32 || (c.feat_dtype == GS_BF16 && t->w1_lp)) && !t->fused1 && t->fuse_bwd &&
-                    t->use_top && c.n_layers == 2 && !c.gcn &&
-                    !t->fuse_update && !t->upper_hook && !t->w1_chunk_hook && n1 % 4 == 0 &&
+                    t->use_top && c.n_layers == 2 && !c.gcn && !t->fuse_update &&
+                    (comm || (!t->upper_hook && !t->w1_chunk_hook)) && n1 % 4 == 0 &&
                     t->cls_w_off % 4 == 0 && t->total % 4 == 0 && aligned16(c.params) && aligned16(c.grads);
     if (!ok) return false;
     if (!t->w1_alt)
@@ -700,6 +717,7 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st) {
         GS_REQUIRE(hipMalloc(&t->w1_lp_alt, n1 * sizeof(uint16_t)) == hipSuccess, GS_ENOMEM, "hipMalloc(bf16 W1)");
     t->lp_valid = false;  // the first forward casts W1 into lp_buf(0)
     t->defer = true;
+    t->defer_comm = comm;
     t->pending = false;
     t->w1_cur = 0;
     return true;
@@ -989,7 +1007,25 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
     t->norm_ready = false;
     GS_REQUIRE(!t->update_done, GS_EINVAL, "the step's fused launch already applied the SGD");
-    GS_REQUIRE(!t->pending, GS_EINVAL, "a deferred update is pending (all-reduce paths do not defer)");
+    GS_REQUIRE(!t->pending, GS_EINVAL, "gs_trainer_update with an update already pending");
+    if (t->defer && t->defer_comm) {
+        // deferred after the all-reduce: the norm partials of the summed gradient
+        // and W1's speculative update in one launch; the next forward (or
+        // trainer_defer_update(false)) applies the clip + SGD
+        const int64_t goff[3] = {0, t->cls_w_off, t->total};
+        const int64_t n1 = t->w_rows[0] * t->w_cols[0];
+        const bool lowp = t->cfg.feat_dtype == GS_BF16;
+        const int np = gs::sumsq_spec_launch(2, goff, t->cfg.grads, ws, t->w1_buf(t->w1_cur), t->w1_buf(t->w1_cur ^ 1),
+                                             lowp ? t->lp_buf(t->w1_cur ^ 1) : nullptr, n1, t->cfg.lr, grad_scale,
+                                             gs::as_stream(stream));
+        t->pending = true;
+        t->pend_part = ws;
+        t->pend_pstride = np;
+        t->pend_np[0] = np;
+        t->pend_np[1] = np;
+        t->pend_scale = grad_scale;
+        return GS_OK;
+    }
     gs::w1_home(t, gs::as_stream(stream));
     const int64_t goff[3] = {0, t->cls_w_off, t->total};
     ShadowArm arm(t);

@@ -923,16 +923,17 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
     } fuse_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && std::getenv("GS_FUSED_SGD")
                       ? r->cfg.trainer
                       : nullptr};
-    // No all-reduce: each step's clip + SGD is deferred into the next step's
-    // launches (the last slab sum writes W1's update for clip coefficient 1,
-    // the next layer-1 forward applies the update) instead of a launch between
-    // the steps; the loop's end applies the last one (GS_DEFER_SGD=0: off).
+    // Each step's clip + SGD is deferred into the next step's launches (W1's
+    // update for clip coefficient 1 written by the last slab sum, or with a
+    // communicator by the norm launch after the all-reduce; the next layer-1
+    // forward applies the update) instead of a launch between the steps; the
+    // loop's end applies the last one (GS_DEFER_SGD=0: off).
     struct DeferUpdate {
         gs_trainer* t;
         hipStream_t st;
         bool on = false;
-        DeferUpdate(gs_trainer* t_, hipStream_t s) : t(t_), st(s) {
-            if (t) on = gs::trainer_defer_update(t, true, st);
+        DeferUpdate(gs_trainer* t_, hipStream_t s, bool comm) : t(t_), st(s) {
+            if (t) on = gs::trainer_defer_update(t, true, st, comm);
         }
         ~DeferUpdate() {
             if (!on) return;
@@ -942,11 +943,11 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 std::fprintf(stderr, "graphsage_amd: runner: applying the last deferred update failed: %s\n", e.what());
             }
         }
-    } defer_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && !fuse_update.t &&
+    } defer_update{r->cfg.trainer && !r->cfg.embed_out && !fuse_update.t &&
                            !(std::getenv("GS_DEFER_SGD") && std::string(std::getenv("GS_DEFER_SGD")) == "0")
                        ? r->cfg.trainer
                        : nullptr,
-                   st};
+                   st, r->cfg.comm != nullptr};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();

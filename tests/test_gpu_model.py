@@ -525,6 +525,39 @@ def test_runner_distributed_path_single_rank(gs, agg):
     comm.close()
 
 
+@pytest.mark.parametrize("max_norm,dtype", [(5.0, "f32"), (1e-3, "f32"), (5.0, "bf16"), (1e-3, "bf16")])
+def test_runner_deferred_update_with_allreduce(gs, monkeypatch, max_norm, dtype):
+    """With a communicator the deferred update starts after the all-reduce:
+    one launch computes the norm partials of the summed gradient and W1's
+    speculative update, the next forward applies the clip + SGD.  Parameters
+    and clipped gradients bitwise those of GS_DEFER_SGD=0 (the all-reduce
+    path's separate norm + SGD launches), one rank, bucketed all-reduce."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    if dtype == "bf16":
+        X = X.to(torch.bfloat16)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:6]
+    comm = train.Communicator(0, 1, DEV)
+    out = []
+    for env in ("0", None):
+        if env is None:
+            monkeypatch.delenv("GS_DEFER_SGD", raising=False)
+        else:
+            monkeypatch.setenv("GS_DEFER_SGD", env)
+        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), max_norm=max_norm, seed=824)
+        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10], depth=2,
+                         comm=comm, ar_buckets=2)
+        r.run(2)
+        r.run(len(batches) - 2)
+        torch.cuda.synchronize()
+        out.append((t.p.params.clone(), t.p.grads.clone()))
+        r.close()
+    comm.close()
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("every", [1, 3])
 def test_kernel_timer_sites_strided(gs, every):
     """The bench's kernel-bound timers (gs_trainer_time_kernels_every): with
