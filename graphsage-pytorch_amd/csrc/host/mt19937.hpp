@@ -357,15 +357,14 @@ inline bool select_fast16(MT19937& rng, int64_t n, int64_t k, OutT* out) {
     return true;
 }
 
-// Pool branch, split in two: the draws (r[i] = randbelow(n - i), i < k — all
-// the stream words sample() consumes) and the pool swaps that turn them into
-// positions (result[i] = pool[r[i]]; pool[r[i]] = pool[n-i-1]).  The swaps
-// never feed back into the draws, so the sampler's last hop can leave them to
-// a helper (pool_apply).  pool_word_draws: one loop over words whose only
-// unpredictable decision is a counter increment; requires k <= 32 and the
-// draws to fit in the current block (otherwise false, nothing consumed).
-template <class RT>
-inline bool pool_word_draws(MT19937& rng, int64_t n, int64_t k, RT* out) {
+// Pool branch: the draws' word consumption first (each randbelow(n - i)
+// takes words until one is below n - i; a rejected word just advances the
+// stream), as one loop over words whose only unpredictable decision is a
+// counter increment, then the pool swaps (result[i] = pool[j];
+// pool[j] = pool[n-i-1]).  Requires k <= 32 and the draws to fit in the
+// current block (checked: otherwise false, nothing consumed).
+template <class OutT>
+inline bool pool_fast(MT19937& rng, int64_t n, int64_t k, OutT* out, int32_t* pool) {
     constexpr int kMaxWords = 96;  // enough for k <= 32 at rejection rates < 1/2, else fall back
     int idx = rng.index;
     const int end = std::min(MT19937::N, idx + kMaxWords);
@@ -390,43 +389,45 @@ inline bool pool_word_draws(MT19937& rng, int64_t n, int64_t k, RT* out) {
     }
     if (i < k) return false;
     rng.index = idx;
-    for (int64_t q = 0; q < k; ++q) out[q] = static_cast<RT>(r[q]);
+    for (int64_t t = 0; t < n; ++t) pool[t] = static_cast<int32_t>(t);
+    for (int64_t q = 0; q < k; ++q) {
+        const uint32_t j = r[q];
+        out[q] = static_cast<OutT>(pool[j]);
+        pool[j] = pool[n - q - 1];
+    }
     return true;
 }
 
-// Pool draws for k <= 16 from a 32-word window: the accepted word of draw i
+// Pool branch for k <= 16 from a 32-word window: the accepted word of draw i
 // is the first word at or after the previous draw's whose top bits,
 // (w >> clz(n - i)), fall below n - i.  Each draw's accept mask over the 32
 // words is a few vector shifts and compares, independent of the other draws,
-// so the only serial chain left is one tzcnt per draw (the per-word loop
-// carries i -> bound -> shift -> compare through every word).  Returns false,
-// having consumed nothing, when the 32 words run out.
-template <class RT>
-inline bool pool_window_draws(MT19937& rng, int64_t n, int64_t k, RT* out) {
+// so the only serial chain left is one tzcnt per draw (the per-word loop of
+// pool_fast carries i -> bound -> shift -> compare through every word).
+// Returns false, having consumed nothing, when the 32 words run out.
+template <class OutT>
+inline bool pool_fast_window(MT19937& rng, int64_t n, int64_t k, OutT* out, int32_t* pool) {
     static_assert(MT19937::kExt >= 32, "the window reads 32 words");
     if (k > 16) return false;
     if (rng.index >= MT19937::N) rng.twist();
     if (rng.index + 32 > MT19937::N && !rng.ext) rng.extend();
     const uint32_t nn = static_cast<uint32_t>(n);
     const uint32_t* wp = rng.out + rng.index;
-    // (w >> sh) < m  <=>  w < (m << sh) for sh = clz(m): one unsigned compare
-    // per word against the normalised bound, done as a signed compare of both
-    // sides with the top bit flipped (no shift of the words per draw)
-    const __m256i flip = _mm256_set1_epi32(static_cast<int32_t>(0x80000000u));
     __m256i w[4];
 #pragma GCC unroll 4
-    for (int q = 0; q < 4; ++q)
-        w[q] = _mm256_xor_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(wp) + q), flip);
+    for (int q = 0; q < 4; ++q) w[q] = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(wp) + q);
     uint32_t r[16];
     uint64_t p = 0;  // words consumed so far
     for (int i = 0; i < k; ++i) {
         const uint32_t m = nn - static_cast<uint32_t>(i);
         const int sh = __builtin_clz(m);
-        const __m256i tv = _mm256_set1_epi32(static_cast<int32_t>((m << sh) ^ 0x80000000u));
+        const __m128i shv = _mm_cvtsi32_si128(sh);
+        const __m256i mv = _mm256_set1_epi32(static_cast<int32_t>(m));
         uint32_t acc = 0;
 #pragma GCC unroll 4
-        for (int q = 0; q < 4; ++q)
-            acc |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(tv, w[q]))))
+        for (int q = 0; q < 4; ++q)  // w >> sh < m, as signed: both below 2^31 (sh >= 1)
+            acc |= static_cast<uint32_t>(_mm256_movemask_ps(_mm256_castsi256_ps(
+                       _mm256_cmpgt_epi32(mv, _mm256_srl_epi32(w[q], shv)))))
                    << (8 * q);
         const uint64_t live = static_cast<uint64_t>(acc) & (~uint64_t(0) << p);
         if (!live) return false;
@@ -434,31 +435,15 @@ inline bool pool_window_draws(MT19937& rng, int64_t n, int64_t k, RT* out) {
         r[i] = wp[j] >> sh;
         p = static_cast<uint64_t>(j) + 1;
     }
-    for (int q = 0; q < k; ++q) out[q] = static_cast<RT>(r[q]);
-    rng.index += static_cast<int>(p);
-    rng.settle();
-    return true;
-}
-
-// The pool branch's draws for k <= 32 (the fast paths, else randbelow word by
-// word: the same words either way).
-template <class RT>
-inline void pool_draws(MT19937& rng, int64_t n, int64_t k, RT* r) {
-    if (GS_SELECT_SMALL && k <= 16 && n < (int64_t(1) << 31) && pool_window_draws(rng, n, k, r)) return;
-    if (GS_SELECT_SMALL && pool_word_draws(rng, n, k, r)) return;
-    for (int64_t i = 0; i < k; ++i) r[i] = static_cast<RT>(rng.randbelow(static_cast<uint64_t>(n - i)));
-}
-
-// The pool swaps of the draws r[0..k): out[i] = pool[r[i]].  out may be r
-// itself (each r[i] is read before out[i] is written).  `pool` holds n.
-template <class OutT, class RT>
-inline void pool_apply(int64_t n, int64_t k, const RT* r, OutT* out, int32_t* pool) {
     for (int64_t t = 0; t < n; ++t) pool[t] = static_cast<int32_t>(t);
     for (int64_t q = 0; q < k; ++q) {
-        const int64_t j = static_cast<int64_t>(r[q]);
+        const uint32_t j = r[q];
         out[q] = static_cast<OutT>(pool[j]);
         pool[j] = pool[n - q - 1];
     }
+    rng.index += static_cast<int>(p);
+    rng.settle();
+    return true;
 }
 
 // random.sample(population, k) expressed on positions 0..n-1 of the
@@ -468,12 +453,8 @@ template <class OutT>
 inline void sample_positions(MT19937& rng, int64_t n, int64_t k, int64_t setsize, OutT* out,
                              int32_t* pool) {
     if (n <= setsize) {
-        if (k <= 32) {
-            uint32_t r[32];
-            pool_draws(rng, n, k, r);
-            pool_apply(n, k, r, out, pool);
-            return;
-        }
+        if (GS_SELECT_SMALL && k <= 16 && n < (int64_t(1) << 31) && pool_fast_window(rng, n, k, out, pool)) return;
+        if (GS_SELECT_SMALL && k <= 32 && pool_fast(rng, n, k, out, pool)) return;
         // pool branch: pool = list(population); j = randbelow(n-i);
         // result[i] = pool[j]; pool[j] = pool[n-i-1]   (positions stand in
         // for the population items).

@@ -26,7 +26,6 @@
 
 #ifndef GS_PHASE  // phase marks of the sampler thread for tools/sampler_bench.cpp; no-ops in the library
 #define GS_PHASE(i)  // 1 draws (hops before the last), 2 sets + union, 3 frontier list, 4 last-hop draws, 5 join
-                     // (two-pass last hop: 6 degrees and offsets, 7 the draws, 4 the tail)
 #endif
 
 namespace gs {
@@ -75,104 +74,8 @@ struct Sample {
 // and dst_ids go straight into the pack, h.pos / h.ent stay empty, and the
 // destinations left empty by the self rule are counted on the way when asked
 // (only a lone entry can be self: one col read — a cache miss — for those).
-// The last hop of a pack run with helpers, in two passes.  The stream's
-// thread walks the destinations in order and only draws: the pool branch
-// leaves its randbelow values (pool_draws), the selected branch its
-// positions, in the destination's own entry slots.  Chunks of destinations it
-// has passed are finished by the helpers — the pool swaps (pool_apply), the
-// row offsets, dst_ids, the empty count — and, once its draws are done, by the
-// thread itself.  The same words drawn in the same order, the same entries.
-struct DrawTail {
-    static constexpr int64_t kChunk = 128;
-    std::atomic<int64_t> drawn{0};  // destinations drawn (released once per chunk)
-    std::atomic<int64_t> next{0};   // next chunk to finish
-    std::atomic<int64_t> empties{0};
-    std::atomic<bool> cancel{false};
-};
-
-static int64_t draw_two_pass(const Graph& g, MT19937& rng, const Hop& h, const int64_t* deg, const int32_t* pptr,
-                             int32_t* ent, int32_t* dst_out, int64_t setsize, bool gcn, bool count_empties,
-                             Team* team) {
-    GS_PHASE(6);
-    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    const int64_t k = h.k;
-    const int64_t* rp = g.row_ptr.data();
-    DrawTail tail;
-    const int64_t n_chunks = (n + DrawTail::kChunk - 1) / DrawTail::kChunk;
-    auto finish = [&](int64_t c) {
-        thread_local std::vector<int32_t> pool;
-        pool.resize(std::max<int64_t>(setsize, 1));
-        const int64_t a = c * DrawTail::kChunk, b = std::min(n, a + DrawTail::kChunk);
-        int64_t empty = 0;
-        for (int64_t r = a; r < b; ++r) {
-            const int64_t v = h.dst_ids[r];
-            const int64_t d = deg[r];
-            const int32_t rs = static_cast<int32_t>(rp[v]);
-            int32_t* ep = ent + pptr[r];
-            const int64_t cnt = pptr[r + 1] - pptr[r];
-            if (d >= k) {
-                if (d <= setsize) pool_apply(d, k, ep, ep, pool.data());
-                for (int64_t t = 0; t < k; ++t) ep[t] += rs;
-            } else {
-                for (int64_t t = 0; t < d; ++t) ep[t] = rs + static_cast<int32_t>(t);
-            }
-            dst_out[r] = static_cast<int32_t>(v);
-            if (count_empties && !gcn) empty += cnt == 0 || (cnt == 1 && g.col[ep[0]] == v);
-        }
-        tail.empties.fetch_add(empty, std::memory_order_relaxed);
-    };
-    // claim chunks until none is left; a claimed chunk waits for the draws to pass it
-    auto help = [&] {
-        for (;;) {
-            const int64_t c = tail.next.fetch_add(1, std::memory_order_relaxed);
-            if (c >= n_chunks) return;
-            const int64_t need = std::min(n, (c + 1) * DrawTail::kChunk);
-            while (tail.drawn.load(std::memory_order_acquire) < need) {
-                if (tail.cancel.load(std::memory_order_relaxed)) return;
-                _mm_pause();
-            }
-            finish(c);
-        }
-    };
-    // helpers that would find no chunk are not asked (with a pool shared by
-    // the streams they would only spin here while another stream's sets wait)
-    const int n_aux = static_cast<int>(std::min<int64_t>(team->helpers(), n_chunks - 1));
-    struct Guard {  // never leave helpers spinning on draws that will not come
-        Team* t;
-        DrawTail& tl;
-        bool posted = false, done = false;
-        ~Guard() {
-            if (posted && !done) {
-                tl.cancel.store(true);
-                try {
-                    t->wait_aux();
-                } catch (...) {
-                }
-            }
-        }
-    } guard{team, tail};
-    if (n_aux > 0) {
-        team->start_aux(n_aux, [&](int) { help(); });
-        guard.posted = true;
-    }
-    for (int64_t r = 0; r < n; ++r) {
-        const int64_t d = deg[r];
-        if (d >= k) {
-            int32_t* ep = ent + pptr[r];
-            if (d <= setsize) pool_draws(rng, d, k, ep);
-            else sample_positions(rng, d, k, setsize, ep, nullptr);  // selected branch: no pool
-        }
-        if (((r + 1) & (DrawTail::kChunk - 1)) == 0 || r + 1 == n) tail.drawn.store(r + 1, std::memory_order_release);
-    }
-    GS_PHASE(7);
-    help();
-    guard.done = true;
-    if (guard.posted) team->wait_aux();
-    return tail.empties.load();
-}
-
 static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = nullptr, int32_t hop = 0,
-                           bool gcn = false, bool count_empties = false, Team* team = nullptr) {
+                           bool gcn = false, bool count_empties = false) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
     int32_t* pptr;
     if (po) {
@@ -203,8 +106,7 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = n
     if (po) {
         ent = po->buf + po->put(hop, GS_PK_POS, total);
         int32_t* d = po->buf + po->put(hop, GS_PK_DST_IDS, n);
-        if (!team)  // else with the draws' second pass
-            for (int64_t r = 0; r < n; ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
+        for (int64_t r = 0; r < n; ++r) d[r] = static_cast<int32_t>(h.dst_ids[r]);
         h.pos.clear();
         h.ent.clear();
     } else {
@@ -216,11 +118,6 @@ static void draw_positions(const Graph& g, MT19937& rng, Hop& h, PackOut* po = n
     const int64_t setsize = sample_setsize(h.k);
     thread_local std::vector<int32_t> pool, tmp;
     pool.resize(std::max<int64_t>(setsize, 1));
-    if (po && team && h.k > 0 && h.k <= 32) {
-        h.n_empty = draw_two_pass(g, rng, h, deg.data(), pptr, ent, po->buf + po->off[hop][GS_PK_DST_IDS], setsize,
-                                  gcn, count_empties, team);
-        return;
-    }
     int64_t empty = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t d = deg[r];
@@ -364,7 +261,6 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
         });
     PySet& u = sc.u;
     u.reset();
-    const int64_t* rp = g.row_ptr.data();
     int64_t n_items = 0;
     for (int64_t c = 0; c < nch; ++c) {
         while (!sc.chunk_done[c].load(std::memory_order_acquire)) {
@@ -385,10 +281,6 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
         } else {
             u.merge_runs(items.data(), ptr, b - a);
         }
-        // the union's keys are the next hop's frontier, whose draws start by
-        // reading each one's row_ptr (random DRAM lines): fetch them under the
-        // remaining merges, which work in the cache-resident table
-        for (const int64_t key : items) __builtin_prefetch(rp + key);
     }
     if (helped) team->wait();  // every helper is out of the chunk loop
     sc.n_items = n_items;
@@ -545,7 +437,7 @@ static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const in
         h.dst_ids.swap(frontier);
         const bool last = (j == n_hops - 1);
         if (last && po) {
-            draw_positions(g, rng, h, po, j, gcn, count_empties, team);  // pos_ptr, entries, dst_ids into the pack
+            draw_positions(g, rng, h, po, j, gcn, count_empties);  // pos_ptr, entries, dst_ids into the pack
             GS_PHASE(4);
             continue;
         }

@@ -191,28 +191,14 @@ class Team {
     // that never returns): it is reported on stderr and the process aborts,
     // rather than hanging silently or unwinding while helpers still run.
     static constexpr int kStallSeconds = 120;
-    void wait() { wait_job(job_); }
-
-    // A second job beside start()'s (the last hop's draw tail runs under the
-    // previous hop's lists job): the same rules, its own wait.
-    void start_aux(int n, std::function<void(int)> fn) { pool_->post(&aux_, n, std::move(fn)); }
-    void wait_aux() { wait_job(aux_); }
-
-    // start() + wait(): the caller is one more worker.
-    void parallel_for(int n, std::function<void(int)> fn) {
-        start(n, std::move(fn));
-        wait();
-    }
-
-  private:
-    void wait_job(Pool::Job& job) {
-        pool_->run_own(&job);
-        const int n = job.n;  // set by this thread's start()
-        int seen = job.done.load(std::memory_order_acquire);
+    void wait() {
+        pool_->run_own(&job_);
+        const int n = job_.n;  // set by this thread's start()
+        int seen = job_.done.load(std::memory_order_acquire);
         auto t_seen = std::chrono::steady_clock::now();
         for (uint64_t spin = 0; seen < n; ++spin) {
             _mm_pause();
-            const int now = job.done.load(std::memory_order_acquire);
+            const int now = job_.done.load(std::memory_order_acquire);
             if (now != seen) {
                 seen = now;
                 t_seen = std::chrono::steady_clock::now();
@@ -223,11 +209,18 @@ class Team {
                 std::abort();
             }
         }
-        if (std::exception_ptr e = pool_->retire(&job)) std::rethrow_exception(e);
+        if (std::exception_ptr e = pool_->retire(&job_)) std::rethrow_exception(e);
     }
 
+    // start() + wait(): the caller is one more worker.
+    void parallel_for(int n, std::function<void(int)> fn) {
+        start(n, std::move(fn));
+        wait();
+    }
+
+  private:
     std::shared_ptr<Pool> pool_;
-    Pool::Job job_, aux_;
+    Pool::Job job_;
 };
 
 }  // namespace gs

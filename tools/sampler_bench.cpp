@@ -111,9 +111,8 @@ int main(int argc, char** argv) {
     double mean = 0;
     for (double p : per) mean += p / streams;
     std::printf("stream 0 phases (us per batch): draws hop 1 %.1f, sets + union %.1f, frontier %.1f, last-hop draws %.1f, "
-                "join %.1f (two-pass last hop: offsets %.1f, draws %.1f, tail %.1f)\n", g_phase[1] / batches,
-                g_phase[2] / batches, g_phase[3] / batches, (g_phase[4] + g_phase[6] + g_phase[7]) / batches,
-                g_phase[5] / batches, g_phase[6] / batches, g_phase[7] / batches, g_phase[4] / batches);
+                "join %.1f\n", g_phase[1] / batches, g_phase[2] / batches, g_phase[3] / batches, g_phase[4] / batches,
+                g_phase[5] / batches);
     gs_team_destroy(pool);
     std::printf("helpers %d streams %d%s: %.1f us per batch per stream, %.0f batches/s total; pack hash %016llx\n",
                 helpers, streams, shared ? " shared" : "", mean, streams * batches / wall, static_cast<unsigned long long>(check[0]));
