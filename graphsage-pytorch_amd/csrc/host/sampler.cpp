@@ -11,6 +11,7 @@
 // device expands the sampled positions through the CSR itself.
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -786,7 +787,12 @@ int64_t gs_sample_pack_bound_multi(const gs_graph* gp, int64_t n_roots, int64_t 
 int gs_team_create(int32_t helpers, gs_team** out) {
     GS_API_BEGIN
     GS_REQUIRE(out && helpers >= 0 && helpers <= 64, GS_EINVAL, "helpers out of [0, 64]");
-    *out = reinterpret_cast<gs_team*>(new gs::Team(helpers));
+    // GS_HELPER_SPIN_US: how long an idle helper polls before sleeping (A/B knob; default 500)
+    static const int spin_us = [] {
+        const char* e = std::getenv("GS_HELPER_SPIN_US");
+        return e ? std::max(0, std::atoi(e)) : 500;
+    }();
+    *out = reinterpret_cast<gs_team*>(new gs::Team(helpers, spin_us));
     GS_API_END
 }
 

@@ -39,3 +39,17 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python3 bench.py --steps 60 --warmup 5 --no-cpu-baseline --sustain 0 --ref-stream-steps 0 > "$OUT/trace.log" 2>&1 || exit $?
 cp "$OUT/trace/run_kernel_trace.csv" "$OUT/kernel_trace.csv" && rm -rf "$OUT/trace"
 python3 tools/timeline.py "$OUT/kernel_trace.csv" > "$OUT/timeline.txt" 2>&1; cat "$OUT/timeline.txt"
+# helper spin A/B (GS_HELPER_SPIN_US: how long an idle helper polls before sleeping)
+for i in 1 2; do
+  for SP in 500 100 20; do
+    GS_HELPER_SPIN_US=$SP timeout -k 10 300 python3 bench.py --no-cpu-baseline > "$OUT/bench_spin${SP}_$i.json" 2> "$OUT/bench_spin${SP}_$i.err" || exit $?
+    python3 - "$OUT/bench_spin${SP}_$i.json" "spin $SP" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+c = d["config"]
+print(sys.argv[2], "value", d["value"], "ms", d["ms_per_step"], "sampler ms", c["sampler"]["ms_per_batch"],
+      "sustained", d["sustained"]["value"], d["sustained"]["ms_per_step"], "misses", d["sustained"]["lookahead_misses"],
+      "ref", d["reference_stream"]["value"], d["reference_stream"]["sampler"]["ms_per_batch"])
+PY
+  done
+done
