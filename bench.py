@@ -337,6 +337,28 @@ def load_traffic(config_name, batch, kernel):
     return best
 
 
+def load_mfma_busy(config_name, kernel):
+    """MFMA utilisation of `kernel` (SQ_VALU_MFMA_BUSY_CYCLES over the SIMDs'
+    cycles, per dispatch) from the newest committed rocprofv3 --pmc summary of
+    this config (profiles/*pmc_mfma_<config>.json, tools/pmc_mfma_summary.py),
+    else None."""
+    def bare(n):  # the PMC summaries name kernels with or without the return type
+        k = kernel_key(n)
+        return k[5:] if k.startswith("void ") else k
+    key = bare(kernel)
+    best = None
+    pat = os.path.join(ROOT, "profiles", f"*pmc_mfma_{config_name.replace('-', '_')}.json")
+    for p in sorted(glob.glob(pat)):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        k = next((v for n, v in d.get("kernels", {}).items() if bare(n) == key), None)
+        if k and "mfma_util" in k:
+            best = {"mfma_util": k["mfma_util"], "source": os.path.relpath(p, ROOT)}
+    return best
+
+
 def pubmed_workload(cfg, device, seed=824):
     """A citation graph from the reference's cites file (cfg["graph"]: pubmed or cora)."""
     g = np.load(os.path.join(ROOT, "tests", "golden", "graphs.npz"))
@@ -864,6 +886,8 @@ def main():
                 peak = MFMA_PEAK_TFS[cfg["dtype"]]
                 achieved, unit, bound = gemm_flops / (us * 1e-6) / 1e12, "TFLOP/s", "mfma"
                 work = {"algo_flops_per_launch": int(gemm_flops)}
+                mb = load_mfma_busy(args.config, names[site])
+                work.update(mfma_busy=(mb["mfma_util"] if mb else None), mfma_busy_source=(mb["source"] if mb else None))
             tr = load_traffic(args.config, cfg["batch"], names[site])
             rooflines[SITE_NAMES[site]] = dict(
                 bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
