@@ -97,14 +97,19 @@ struct RawVec<bf16_t, 8> {
 // Same lane groups, chunking and accumulation order as agg_fwd_kernel's
 // expand mode (empty slots add +0 / never win a max), so the output is
 // bitwise that kernel's; the only index load is the destination's k ids.
-template <int OP, typename T, int VEC, int G>
+// SELF: also copy each destination's own feature row X[dst_ids[r]] to
+// self_out[r] (its load in the same memory round as the neighbours'), so the
+// layer-1 GEMMs read [self | agg] as one dense block instead of gathering the
+// self rows through their index (GS_SELF_ROWS).
+template <int OP, typename T, int VEC, int G, bool SELF>
 __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X, int64_t ldx, int F, int n_dst, int k,
                                                          const int* __restrict__ ids, const int* __restrict__ dst_ids,
-                                                         int gcn, T* __restrict__ out, int64_t ldo) {
+                                                         int gcn, T* __restrict__ out, int64_t ldo,
+                                                         T* __restrict__ self_out, int64_t ldso) {
     const int gl = threadIdx.x % G;
     // grid-stride over destinations (the launch caps the grid: agg_ids_block_cap)
     for (int r = blockIdx.x * (kBlock / G) + threadIdx.x / G; r < n_dst; r += gridDim.x * (kBlock / G)) {
-    const int node = gcn ? dst_ids[r] : 0;
+    const int node = (gcn || SELF) ? dst_ids[r] : 0;
     const int* rid = ids + static_cast<int64_t>(r) * k;
     // 16 rows in flight for 16-byte fp32 and bf16 vectors alike, so a fanout
     // <= 16 neighbourhood is one memory round (8 for bf16 split a 10-slot
@@ -115,6 +120,9 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
         const int f0 = fi * G * VEC + gl * VEC;
         const bool act = f0 < F;
         const int f0c = act ? f0 : 0;
+        using Raw = typename RawVec<T, VEC>::type;
+        Raw xself{};
+        if (SELF) xself = *reinterpret_cast<const Raw*>(X + static_cast<int64_t>(node) * ldx + f0c);
         float acc[VEC];
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
@@ -135,7 +143,6 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
                     ok[u] = (j + u < m) && rows[u] >= 0;
                 }
                 const int fallback = rows[0] >= 0 ? rows[0] : node;
-                using Raw = typename RawVec<T, VEC>::type;
                 Raw x[NR];
 #pragma unroll
                 for (int u = 0; u < NR; ++u)
@@ -168,6 +175,7 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
             }
         }
         if (!act) continue;
+        if (SELF) *reinterpret_cast<Raw*>(self_out + static_cast<int64_t>(r) * ldso + f0) = xself;
         if (OP == GS_AGG_MEAN) {
             const float inv = 1.0f / static_cast<float>(cnt);
 #pragma unroll
@@ -213,18 +221,27 @@ static int agg_ids_block_cap() {
 }
 
 void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
-                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st) {
+                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st,
+                    void* self_out, int64_t ldso) {
     GS_REQUIRE(op == GS_AGG_MEAN || op == GS_AGG_MAX, GS_EINVAL, "agg_func must be MEAN or MAX");
     GS_REQUIRE(F >= 1 && n_dst >= 0 && k >= 1 && ldx >= F && ldo >= F, GS_EINVAL, "bad sizes");
+    GS_REQUIRE(!self_out || (dst_ids && ldso >= F), GS_EINVAL, "self rows need dst_ids and ldso >= F");
     if (n_dst == 0) return;
     const int V = dt == GS_F32 ? 4 : 8;
-    const bool vec = F % V == 0 && ldx % V == 0 && ldo % V == 0 && aligned16(X) && aligned16(out);
+    const bool vec = F % V == 0 && ldx % V == 0 && ldo % V == 0 && aligned16(X) && aligned16(out) &&
+                     (!self_out || (ldso % V == 0 && aligned16(self_out)));
     const int f = static_cast<int>(F), n = static_cast<int>(n_dst);
     static const int cap = agg_ids_block_cap();
 #define GS_IDS(OPV, TT, VV, GG)                                                                                  \
-    launch_k(agg_ids_kernel<OPV, TT, VV, GG>, dim3(std::min((n + (kBlock / GG) - 1) / (kBlock / GG), cap)),      \
-             dim3(kBlock), 0, st,                                                                                \
-             static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo)
+    do {                                                                                                         \
+        const dim3 grid_(std::min((n + (kBlock / GG) - 1) / (kBlock / GG), cap));                                \
+        if (self_out)                                                                                            \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, true>, grid_, dim3(kBlock), 0, st, static_cast<const TT*>(X), \
+                     ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo, static_cast<TT*>(self_out), ldso); \
+        else                                                                                                     \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, false>, grid_, dim3(kBlock), 0, st, static_cast<const TT*>(X), \
+                     ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo, static_cast<TT*>(nullptr), ldso); \
+    } while (0)
 #define GS_IDS_T(OPV, TT)                                                     \
     do {                                                                      \
         constexpr int VV = sizeof(TT) == 4 ? 4 : 8;                           \

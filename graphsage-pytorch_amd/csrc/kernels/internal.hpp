@@ -112,8 +112,10 @@ void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
 // Padded hop-1 records for the fused top launch, one buffer per gather slot
 // (2-layer training steps; B roots, fanout tk <= 31).
 void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk);
+// self_out (optional): each destination's own row X[dst_ids[r]] copied to self_out[r]
 void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
-                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st);
+                    const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st,
+                    void* self_out = nullptr, int64_t ldso = 0);
 
 // misc.hip
 int cls_rows_launch(int64_t B, int64_t D, int64_t C, const float* E, const float* Wc, const float* bc,

@@ -43,6 +43,12 @@ struct gs_trainer {
     static constexpr int kSlots = 3;
     void* a1_slot[kSlots] = {};
     int64_t a1_rows = 0;
+    // GS_SELF_ROWS (default on, "0" off; read at gs_trainer_gather_reserve): each gather slot is
+    // [self | agg] rows of 2F; the side-stream gather also copies the layer-1
+    // rows' own features, so the layer-1 forward and dW read one dense block
+    // (no self-index round).  self_in_slot: the slot's self half was written.
+    bool self_rows = false;
+    bool self_in_slot[kSlots] = {};
     // per slot, the layer-1 neighbour ids resolved ahead of the gather
     // (k_ids slots per destination), when reserved with a fanout
     int32_t* ids_slot[kSlots] = {};
@@ -195,7 +201,7 @@ static inline void timed_done(gs_trainer& T, int site, bool armed) {
 // The layer-1 gather-aggregate of one packed sample (models.py:291-330 at
 // layer 1) into `out`, bracketed by the timing events when armed.
 static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
-                    void* out, hipStream_t st) {
+                    void* out, hipStream_t st, int64_t ldo = 0) {
     const gs_trainer_config& c = T.cfg;
     const int L = c.n_layers;
     const int64_t F = c.feat_dim;
@@ -207,7 +213,7 @@ static void gather1(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes
     const bool timed = timed_arm(T, 0);
     ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F,
                   hop_sizes[4 * (L - 1)], fld(GS_PK_POS_PTR), fld(GS_PK_POS), nullptr, c.col, fld(GS_PK_DST_IDS),
-                  c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), F, nullptr, st));
+                  c.gcn, out, static_cast<gs_dtype>(c.feat_dtype), ldo > 0 ? ldo : F, nullptr, st));
     timed_done(T, 0, timed);
 }
 
@@ -241,8 +247,17 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                            st);
     }
     const bool timed = timed_arm(T, 0);
-    agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim, n_dst,
-                   T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, T.a1_slot[slot], c.feat_dim, st);
+    if (T.self_rows) {  // [self | agg] rows
+        char* base = static_cast<char*>(T.a1_slot[slot]);
+        const int64_t xsz = c.feat_dtype == GS_BF16 ? 2 : 4;
+        agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim,
+                       n_dst, T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, base + c.feat_dim * xsz, 2 * c.feat_dim, st,
+                       base, 2 * c.feat_dim);
+        T.self_in_slot[slot] = true;
+    } else {
+        agg_ids_launch(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, c.feat_dim,
+                       n_dst, T.k_ids, ids, fld(GS_PK_DST_IDS), c.gcn, T.a1_slot[slot], c.feat_dim, st);
+    }
     timed_done(T, 0, timed);
 }
 
@@ -323,6 +338,22 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         T.lp_valid = T.lp_keep;
     }
     const int32_t* dst_L = fld(L, GS_PK_DST_IDS);
+    // the layer-1 GEMMs' operands: X[dst_L] | agg, or the gather slot's dense
+    // [self | agg] rows (GS_SELF_ROWS)
+    const void* x1 = c.gcn ? nullptr : c.X;
+    int64_t ldx1 = c.feat_ld, lda1 = F;
+    const int32_t* sidx1 = dst_L;
+    const void* a1 = agg[0];
+    if (a1_slot >= 0 && T.self_rows) {
+        const int64_t xsz1 = c.feat_dtype == GS_BF16 ? 2 : 4;
+        a1 = static_cast<const char*>(agg[0]) + F * xsz1;
+        lda1 = 2 * F;
+        if (T.self_in_slot[a1_slot] && !c.gcn) {
+            x1 = agg[0];
+            ldx1 = 2 * F;
+            sidx1 = nullptr;
+        }
+    }
     const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
     const bool fused1 = T.fused1 && a1_slot < 0;
     GS_REQUIRE(!T.defer || (!fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
@@ -373,8 +404,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     }
     if (!fused1) {
         const bool armed = timed_arm(T, 1);
-        ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X, c.feat_ld,
-                              dst_L, agg[0], F, W1, h[0], H, 1, st));
+        ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1, lda1, W1, h[0],
+                              H, 1, st));
         g_launch_events = {};  // an alternative kernel that does not time leaves it armed
         timed_done(T, 1, armed);
         if (pend) {  // the launch took the pending update: W1 is now the other buffer
@@ -493,10 +524,9 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 for (int q = 0; q < T.w1_chunks; ++q) {
                     const int64_t h0 = q * Hc;
                     float* dWq = G + T.w_off[0] + h0 * K1;
-                    const int Sq = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, Hc,
-                                                   c.gcn ? nullptr : c.X, c.feat_ld, dst_L, agg[0], F,
-                                                   lb.back().dH + h0, h[0] + h0, H, 0, dWq, dw_ws, dw_need, st,
-                                                   nullptr, H);
+                    const int Sq = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, Hc, x1, ldx1,
+                                                   sidx1, a1, lda1, lb.back().dH + h0, h[0] + h0, H, 0, dWq, dw_ws,
+                                                   dw_need, st, nullptr, H);
                     if (Sq > 1) sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), Sq, Hc * K1, dWq, nullptr, st);
                     T.w1_chunk_hook(st, T.w_off[0] + h0 * K1, Hc * K1);
                 }
@@ -510,16 +540,15 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             DwGroups grp{T.dw_cnt, T.dw_n_cnt, dw_gpart};
             int S1 = -1;
             if (dw_plus) {
-                S1 = dw1_plus_launch(rows[0], F, H, static_cast<const float*>(c.X), c.feat_ld, dst_L,
-                                     static_cast<const float*>(agg[0]), F, lb.back().dH, H, G + T.w_off[0], dw_ws,
+                S1 = dw1_plus_launch(rows[0], F, H, static_cast<const float*>(x1), ldx1, sidx1,
+                                     static_cast<const float*>(a1), lda1, lb.back().dH, H, G + T.w_off[0], dw_ws,
                                      dw_need, moved, st);
                 GS_REQUIRE(S1 > 1, GS_EINVAL, "GS_DW_PLUS: the layer-1 dW launch could not take the moved roles");
                 grp.slabs = reinterpret_cast<const float*>(dw_ws);
                 grp.S = S1;
             } else {
-                S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, c.gcn ? nullptr : c.X,
-                                     c.feat_ld, dst_L, agg[0], F, lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws,
-                                     dw_need, st, &grp);
+                S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1, lda1,
+                                     lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws, dw_need, st, &grp);
             }
             g_launch_events = {};
             timed_done(T, 2, armed);
@@ -590,12 +619,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     for (int l = L; l >= 1; --l) {
         const int j = L - l + 1;
         const bool first = l == 1;
-        const void* x_in = first ? c.X : h[l - 2];
-        const int32_t* sidx = first ? dst_L : fld(j, GS_PK_SELF);
-        const int64_t fin = in_dim[l - 1], ldx = first ? c.feat_ld : H;
+        const void* x_in = first ? x1 : (c.gcn ? nullptr : h[l - 2]);
+        const int32_t* sidx = first ? sidx1 : fld(j, GS_PK_SELF);
+        const int64_t fin = in_dim[l - 1], ldx = first ? ldx1 : H;
         if (first && L >= 2 && T.upper_hook) T.upper_hook(st);
-        ok(gs_sage_linear_bwd_weight(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H,
-                                     c.gcn ? nullptr : x_in, ldx, sidx, agg[l - 1], fin, dH, h[l - 1], H, relu,
+        ok(gs_sage_linear_bwd_weight(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H, x_in,
+                                     ldx, sidx, first ? a1 : agg[l - 1], first ? lda1 : fin, dH, h[l - 1], H, relu,
                                      G + T.w_off[l - 1], dw_ws, dw_need, st));
         if (first) break;
         const int64_t ldd = c.gcn ? H : 2 * H;
@@ -826,9 +855,13 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_
 int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout) {
     GS_API_BEGIN
     GS_REQUIRE(t && max_rows >= 0 && max_fanout >= 0, GS_EINVAL, "bad arguments");
-    if (max_rows <= t->a1_rows && max_fanout <= t->k_ids) return GS_OK;
+    const char* sr = std::getenv("GS_SELF_ROWS");  // default on; "0": the GEMMs gather the self rows
+    const bool self_rows = !(sr && std::string(sr) == "0") && !t->cfg.gcn && t->cfg.n_layers >= 1;
+    if (max_rows <= t->a1_rows && max_fanout <= t->k_ids && self_rows == t->self_rows) return GS_OK;
     max_rows = std::max(max_rows, t->a1_rows);
-    const int64_t bytes = max_rows * t->cfg.feat_dim * (t->cfg.feat_dtype == GS_BF16 ? 2 : 4);
+    t->self_rows = self_rows;
+    for (bool& b : t->self_in_slot) b = false;
+    const int64_t bytes = max_rows * t->cfg.feat_dim * (self_rows ? 2 : 1) * (t->cfg.feat_dtype == GS_BF16 ? 2 : 4);
     for (void*& p : t->a1_slot) {
         if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
         p = nullptr;
@@ -859,10 +892,16 @@ int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_siz
     GS_REQUIRE(hop_sizes[4 * (L - 1)] <= t->a1_rows && t->a1_slot[slot], GS_EINVAL,
                "gather slot too small (gs_trainer_gather_reserve)");
     const int64_t n_dst = hop_sizes[4 * (L - 1)], n_pos = hop_sizes[4 * (L - 1) + 1];
-    if (t->k_ids > 0 && n_pos <= n_dst * t->k_ids)  // every neighbourhood fits k_ids slots
+    if (t->k_ids > 0 && n_pos <= n_dst * t->k_ids) {  // every neighbourhood fits k_ids slots
         gs::gather1_ids(*t, pack, hop_sizes, offsets, slot, gs::as_stream(stream));
-    else
+    } else if (t->self_rows) {  // the agg half only: the GEMMs gather the self rows themselves
+        const int64_t F = t->cfg.feat_dim, xsz = t->cfg.feat_dtype == GS_BF16 ? 2 : 4;
+        gs::gather1(*t, pack, hop_sizes, offsets, static_cast<char*>(t->a1_slot[slot]) + F * xsz,
+                    gs::as_stream(stream), 2 * F);
+        t->self_in_slot[slot] = false;
+    } else {
         gs::gather1(*t, pack, hop_sizes, offsets, t->a1_slot[slot], gs::as_stream(stream));
+    }
     GS_API_END
 }
 

@@ -400,6 +400,38 @@ def test_dw_plus_matches_default(gs, monkeypatch, agg):
     assert out[0][2] == out[1][2]
 
 
+@pytest.mark.parametrize("agg,bf16,gcn", [("MEAN", False, False), ("MAX", False, False), ("MEAN", True, False),
+                                          ("MAX", True, False), ("MEAN", False, True)])
+def test_self_rows_matches_default(gs, monkeypatch, agg, bf16, gcn):
+    """GS_SELF_ROWS (default on: the side-stream gather also copies the
+    layer-1 rows' own features into the slot, [self | agg] rows of 2F, and the
+    layer-1 forward and dW read that block without the self-index round) feeds
+    the GEMMs the same values in the same order as GS_SELF_ROWS=0 (the GEMMs
+    gather X[dst] themselves): loss, gradients and parameters bitwise equal
+    (gcn: the slot keeps the agg half only)."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    if bf16:
+        X = X.to(torch.bfloat16)
+    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 9))[:5]
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("GS_SELF_ROWS", env)
+        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, gcn=gcn, max_norm=0.05,
+                                seed=824)
+        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
+                         fail_empty=agg == "MAX", gcn=gcn, depth=2)
+        r.run(len(batches))
+        torch.cuda.synchronize()
+        out.append((t.p.params.clone(), t.p.grads.clone(), float(t.loss)))
+        r.close()
+    monkeypatch.delenv("GS_SELF_ROWS", raising=False)
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
+
+
 @pytest.mark.parametrize("agg,gcn,layers,name,B", [
     ("MEAN", False, 2, "rmat", 96), ("MAX", False, 2, "rmat", 96), ("MEAN", True, 2, "rmat", 96),
     ("MEAN", False, 3, "rmat", 96),
