@@ -411,13 +411,16 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                                      std::string(std::getenv("GS_LIN_FWD_BF16")) == "chunked";
     if ((wide_on || wide32_on) && vload && (dt == GS_F32 || !bf16_chunked)) {
         sp.stamp = take_kernel_stamp();  // a timed launch: the kernel stores its own span
-        // Rows per tile: 32, or 48 when 32-row tiles would need more than one
-        // workgroup per CU (a second round on some CUs: layer 1 at rmat2m
-        // measured 10.5 us at 256 workgroups against 15.0 us at 264-300) and
-        // 48-row tiles fit one (GS_FWD_ROWS=32 keeps 32: A/B).  Every row tile
-        // runs the same MFMA chain, so the output is bitwise the same.
+        // Rows per tile: 32.  GS_FWD_ROWS=48 takes 48-row tiles when 32-row
+        // tiles would need more than one workgroup per CU and 48-row ones fit
+        // one: the round-3 default (with the self rows gathered through their
+        // index, 32-row tiles measured 15.0 us at 264-300 workgroups against
+        // 10.5 us at 256); with the dense [self | agg] slot the 32-row tiles
+        // are faster in situ (sustained 9.10-9.12 against 8.67-9.00 M roots/s,
+        // profiles/r04d_fwd_rows_ab.txt).  Every row tile runs the same MFMA
+        // chain, so the output is bitwise the same.
         const char* rows_env = std::getenv("GS_FWD_ROWS");  // read per call (tests switch it)
-        const bool rows32 = rows_env && std::string(rows_env) == "32";
+        const bool rows32 = !(rows_env && std::string(rows_env) == "48");
         int R = wide32_on ? 32 : kWideRows;
         {
             static const int ncu = [] {

@@ -274,12 +274,12 @@ def test_fullsize_grouped_dw_matches_slab_sum(wl, native, monkeypatch):
 
 
 def test_fullsize_fwd_rows48_matches_rows32(wl, native, monkeypatch):
-    """The layer-1 forward on 48-row tiles (taken when 32-row tiles would need
-    a second workgroup round on some CUs, i.e. most rmat2m batches) gives the
-    32-row kernel's losses and parameters bit for bit (GS_FWD_ROWS=32): every
-    row tile runs the same MFMA chain."""
+    """The layer-1 forward on 48-row tiles (GS_FWD_ROWS=48: taken when 32-row
+    tiles would need a second workgroup round on some CUs, i.e. most rmat2m
+    batches) gives the default 32-row kernel's losses and parameters bit for
+    bit: every row tile runs the same MFMA chain."""
     tr, losses, sizes = native
-    monkeypatch.setenv("GS_FWD_ROWS", "32")
+    monkeypatch.setenv("GS_FWD_ROWS", "48")
     tr2, losses2, sizes2 = _run(wl)
     assert losses == losses2
     assert torch.equal(tr.p.params, tr2.p.params)
