@@ -39,9 +39,7 @@ __global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, c
                                                              int* __restrict__ ids, int n_top, int tk,
                                                              const int* __restrict__ tptr,
                                                              const int* __restrict__ tnbr,
-                                                             const int* __restrict__ tself, int* __restrict__ tout,
-                                                             int n_src1, const int* __restrict__ ttp,
-                                                             const int* __restrict__ tti, int* __restrict__ trec) {
+                                                             const int* __restrict__ tself, int* __restrict__ tout) {
     const int64_t t = blockIdx.x * int64_t(kBlock) + threadIdx.x;
     const int64_t n1 = static_cast<int64_t>(n_dst) * k;
     if (t < n1) {
@@ -54,20 +52,7 @@ __global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, c
         return;
     }
     const int64_t u = t - n1;
-    if (u >= static_cast<int64_t>(n_top) * (tk + 1)) {
-        // third role: source c's transposed top-layer list as one record
-        // {n, entries} (n = -1 past 7 entries: the backward reads tptr / tidx)
-        const int64_t c = u - static_cast<int64_t>(n_top) * (tk + 1);
-        if (c >= n_src1) return;
-        const int beg = ttp[c], n = ttp[c + 1] - beg;
-        int v[7];
-#pragma unroll
-        for (int q = 0; q < 7; ++q) v[q] = q < n ? tti[beg + q] : 0;
-        int4* o = reinterpret_cast<int4*>(trec) + 2 * c;
-        o[0] = make_int4(n <= 7 ? n : -1, v[0], v[1], v[2]);
-        o[1] = make_int4(v[3], v[4], v[5], v[6]);
-        return;
-    }
+    if (u >= static_cast<int64_t>(n_top) * (tk + 1)) return;
     const int r = static_cast<int>(u / (tk + 1)), j = static_cast<int>(u - static_cast<int64_t>(r) * (tk + 1));
     int v;
     if (j == 0) {
@@ -213,18 +198,15 @@ void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
 
 void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
-                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st, int64_t n_src1,
-                        const int32_t* ttp, const int32_t* tti, int32_t* trec) {
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st) {
     GS_REQUIRE(n_dst >= 0 && k >= 1 && n_dst * k < (int64_t(1) << 31) && n_top >= 0 && tk >= 1 &&
                    n_top * (tk + 1) < (int64_t(1) << 30),
                GS_EINVAL, "bad sizes");
-    GS_REQUIRE(n_src1 >= 0 && n_src1 < (int64_t(1) << 30) && (n_src1 == 0 || (ttp && tti && trec)), GS_EINVAL,
-               "bad transposed-record arguments");
-    const int64_t total = n_dst * k + n_top * (tk + 1) + n_src1;
+    const int64_t total = n_dst * k + n_top * (tk + 1);
     if (total == 0) return;
     resolve_top_kernel<<<dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
         static_cast<int>(n_dst), k, ptr, ent, col, dst_ids, gcn, ids, static_cast<int>(n_top), tk, tptr, tnbr, tself,
-        tout, static_cast<int>(n_src1), ttp, tti, trec);
+        tout);
     check_launch("resolve_top");
 }
 

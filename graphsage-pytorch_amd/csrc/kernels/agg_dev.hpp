@@ -144,28 +144,11 @@ __device__ __forceinline__ void agg_bwd_body(
     int bx, int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,
     const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
     int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
-    float* __restrict__ dH, const int* __restrict__ trec = nullptr) {
+    float* __restrict__ dH) {
     const int gl = threadIdx.x % G;
     const int c = bx * (kBlock / G) + threadIdx.x / G;
     if (c >= n_src) return;
-    int beg = tptr[c], end = tptr[c + 1];
-#if GS_AGG_BWD_BATCH
-    // trec (optional, written a step ahead by resolve_top_kernel): the
-    // source's transposed list as one 32-byte record {n, up to 7 entries},
-    // n = -1 past 7 -- loaded in the same round as tptr, so the rows follow
-    // in the second round instead of the third (tptr -> tidx -> rows)
-    int rn = -1, rent[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (trec) {
-        const int4 r0 = reinterpret_cast<const int4*>(trec)[2 * static_cast<int64_t>(c)];
-        const int4 r1 = reinterpret_cast<const int4*>(trec)[2 * static_cast<int64_t>(c) + 1];
-        rn = r0.x;
-        rent[0] = r0.y; rent[1] = r0.z; rent[2] = r0.w; rent[3] = r1.x; rent[4] = r1.y; rent[5] = r1.z; rent[6] = r1.w;
-    }
-    if (rn >= 0) {
-        beg = 0;
-        end = rn;
-    }
-#endif
+    const int beg = tptr[c], end = tptr[c + 1];
     for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
         const bool act = f0 < F;
         float g[VEC];
@@ -177,17 +160,10 @@ __device__ __forceinline__ void agg_bwd_body(
         // one more, then the adds in entry order (the same sums as one entry
         // at a time).  Addresses are clamped, values selected at use.
         const int f0c = act ? f0 : 0;
-        float hm[VEC];  // the relu-mask row, loaded with the first round
-        if (Hprev) RowIO<float, VEC>::load(Hprev + static_cast<int64_t>(c) * ldh + f0c, hm);
         for (int t0 = beg; t0 < end; t0 += 8) {
             int e[8];
-            if (rn >= 0) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) e[u] = (u < 7 && u < end) ? rent[u < 7 ? u : 0] : rent[0];
-            } else {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) e[u] = tidx[min(t0 + u, end - 1)];
-            }
+            for (int u = 0; u < 8; ++u) e[u] = tidx[min(t0 + u, end - 1)];
             float x[8][VEC], w[8];
             int am[8][VEC];
 #pragma unroll
@@ -249,12 +225,8 @@ __device__ __forceinline__ void agg_bwd_body(
 #endif
         if (!act) continue;
         if (Hprev) {
-#if GS_AGG_BWD_BATCH
-            const float* h = hm;
-#else
             float h[VEC];
             RowIO<float, VEC>::load(Hprev + static_cast<int64_t>(c) * ldh + f0, h);
-#endif
 #pragma unroll
             for (int v = 0; v < VEC; ++v) g[v] = h[v] > 0.f ? g[v] : 0.f;
         }

@@ -59,7 +59,6 @@ struct BwdB {
     const int* argmax;
     const float* Hprev;
     float* dH;
-    const int* trec;  // optional per-source transposed records (resolve_top_kernel)
 };
 
 template <int OP, int G>
@@ -70,7 +69,7 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_b_kernel(BwdB b) {
         return;
     }
     agg_bwd_body<OP, 4, G>(bx - b.sum_nb, b.n_src, b.F, b.tptr, b.tidx, b.ptr, b.dA, b.dSelf, b.ldd, b.argmax,
-                           b.Hprev, b.F, b.dH, b.trec);
+                           b.Hprev, b.F, b.dH);
 }
 
 struct BwdT {
@@ -97,7 +96,7 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
     }
     b -= t.cls_nb;
     agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd, t.b.argmax,
-                           t.b.Hprev, t.b.F, t.b.dH, t.b.trec);
+                           t.b.Hprev, t.b.F, t.b.dH);
 }
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
@@ -256,7 +255,6 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     Bq.F = static_cast<int>(a.H);
     Bq.tptr = a.tptr;
     Bq.tidx = a.tidx;
-    Bq.trec = a.trec;
     Bq.ptr = a.ptr;
     Bq.dA = A.dA;
     Bq.dSelf = A.dSelf;
@@ -317,7 +315,6 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     Bq.F = static_cast<int>(a.H);
     Bq.tptr = a.tptr;
     Bq.tidx = a.tidx;
-    Bq.trec = a.trec;
     Bq.ptr = a.ptr;
     Bq.dSelf = a.dIn;
     Bq.dA = a.dIn + a.fin;

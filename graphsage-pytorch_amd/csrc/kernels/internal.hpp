@@ -108,9 +108,7 @@ void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
 // (tout[r][0] = self, [1..tk] = the list, -1 past it; n_top roots).
 void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
-                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st,
-                        int64_t n_src1 = 0, const int32_t* ttp = nullptr, const int32_t* tti = nullptr,
-                        int32_t* trec = nullptr);
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st);
 // Padded hop-1 records for the fused top launch, one buffer per gather slot
 // (2-layer training steps; B roots, fanout tk <= 31).
 void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk);
@@ -154,7 +152,6 @@ struct LayerBwd {
     int64_t n_src;                        // rows of the previous layer
     const int32_t* tptr;                  // transposed neighbourhoods (GS_PK_TPTR / TIDX)
     const int32_t* tidx;
-    const int32_t* trec = nullptr;        // optional: the same lists as 8-int records (resolve_top_kernel)
     const int32_t* ptr;                   // forward neighbourhood offsets (mean weights)
     const int32_t* argmax;                // MAX routing, [n][H]
     const float* Hprev;                   // previous layer's output (relu mask), [n_src][H]

@@ -49,10 +49,6 @@ struct gs_trainer {
     // (no self-index round).  self_in_slot: the slot's self half was written.
     bool self_rows = false;
     bool self_in_slot[kSlots] = {};
-    // the top layer's transposed lists as 8-int records per layer-1 row, written
-    // by the side stream's resolve_top beside the top records (GS_TREC=0: off)
-    int32_t* trec_slot[kSlots] = {};
-    bool trec_ready[kSlots] = {};
     // per slot, the layer-1 neighbour ids resolved ahead of the gather
     // (k_ids slots per destination), when reserved with a fanout
     int32_t* ids_slot[kSlots] = {};
@@ -132,8 +128,6 @@ struct gs_trainer {
         for (int32_t* p : ids_slot)
             if (p) (void)hipFree(p);
         for (int32_t* p : top_slot)
-            if (p) (void)hipFree(p);
-        for (int32_t* p : trec_slot)
             if (p) (void)hipFree(p);
         for (auto& tm : timer)
             if (tm.st0) (void)hipFree(tm.st0);
@@ -240,23 +234,14 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const int64_t n_top = hop_sizes[0];
     T.top_ready[slot] = T.top_k > 0 && L == 2 && !c.gcn && n_top <= T.top_rows && T.top_slot[slot] &&
                         hop_sizes[3] <= n_top * T.top_k;  // every root's list fits tk slots
-    T.trec_ready[slot] = false;
     if (T.top_ready[slot]) {
         auto f1 = [&](int f) -> const int32_t* {
             const int64_t o = offsets[f];  // hop 1
             GS_REQUIRE(o >= 0, GS_EINVAL, "pack field missing");
             return pack + o;
         };
-        const int64_t n_src1 = hop_sizes[2];  // hop 1's sources: the layer-1 rows
-        const char* trec_env = std::getenv("GS_TREC");  // read per gather (tests switch it)
-        const bool trec_off = trec_env && std::string(trec_env) == "0";
-        const bool trec = !trec_off && T.trec_slot[slot] && n_src1 <= T.a1_rows && offsets[GS_PK_TPTR] >= 0 &&
-                          offsets[GS_PK_TIDX] >= 0;
         resolve_top_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
-                           n_top, T.top_k, f1(GS_PK_NBR_PTR), f1(GS_PK_NBR), f1(GS_PK_SELF), T.top_slot[slot], st,
-                           trec ? n_src1 : 0, trec ? f1(GS_PK_TPTR) : nullptr, trec ? f1(GS_PK_TIDX) : nullptr,
-                           trec ? T.trec_slot[slot] : nullptr);
-        T.trec_ready[slot] = trec;
+                           n_top, T.top_k, f1(GS_PK_NBR_PTR), f1(GS_PK_NBR), f1(GS_PK_SELF), T.top_slot[slot], st);
     } else {
         resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
                            st);
@@ -475,8 +460,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             a.n_src = rows[l - 2];
             a.tptr = fld(j, GS_PK_TPTR);
             a.tidx = fld(j, GS_PK_TIDX);
-            if (j == 1 && a1_slot >= 0 && T.trec_ready[a1_slot] && a.n_src == hs[0].n_src)
-                a.trec = T.trec_slot[a1_slot];
             a.ptr = fld(j, GS_PK_NBR_PTR);
             a.argmax = am[l - 1];
             a.Hprev = h[l - 2];
@@ -887,14 +870,6 @@ int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanou
     for (int32_t*& p : t->ids_slot) {
         if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
         p = nullptr;
-    }
-    for (int q = 0; q < gs_trainer::kSlots; ++q) {
-        int32_t*& p = t->trec_slot[q];
-        if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
-        p = nullptr;
-        t->trec_ready[q] = false;
-        GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(max_rows * 8 * 4, 256)) == hipSuccess, GS_ENOMEM,
-                   "hipMalloc(transposed records)");
     }
     t->k_ids = 0;
     if (max_fanout > 0) {

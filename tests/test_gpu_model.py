@@ -432,34 +432,6 @@ def test_self_rows_matches_default(gs, monkeypatch, agg, bf16, gcn):
     assert out[0][2] == out[1][2]
 
 
-@pytest.mark.parametrize("agg,bf16", [("MEAN", False), ("MAX", False), ("MAX", True)])
-def test_transposed_records_match_lists(gs, monkeypatch, agg, bf16):
-    """The layer-2 backward's transposed gather from the 8-int per-source
-    records that the side stream's resolve_top writes (default) adds the same
-    entries in the same order as from tptr / tidx (GS_TREC=0): loss,
-    gradients and parameters bitwise equal."""
-    graph, g, n = _graph(gs, "rmat")
-    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
-    if bf16:
-        X = X.to(torch.bfloat16)
-    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
-    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 9))[:5]
-    out = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("GS_TREC", env)
-        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=0.05, seed=824)
-        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
-                         fail_empty=agg == "MAX", depth=2)
-        r.run(len(batches))
-        torch.cuda.synchronize()
-        out.append((t.p.params.clone(), t.p.grads.clone(), float(t.loss)))
-        r.close()
-    monkeypatch.delenv("GS_TREC", raising=False)
-    assert torch.equal(out[0][0], out[1][0])
-    assert torch.equal(out[0][1], out[1][1])
-    assert out[0][2] == out[1][2]
-
-
 @pytest.mark.parametrize("agg,gcn,layers,name,B", [
     ("MEAN", False, 2, "rmat", 96), ("MAX", False, 2, "rmat", 96), ("MEAN", True, 2, "rmat", 96),
     ("MEAN", False, 3, "rmat", 96),
