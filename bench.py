@@ -185,11 +185,15 @@ def top_bytes(B, n_nbr, H, C):
     return (n_nbr + B) * H * 4 + n_nbr * 4 + H * 2 * H * 4 + C * (H + 1) * 4 + B * 5 * H * 4
 
 
-def agg1_ids_bytes(n_dst, n_pos, F, elem, k):
+def agg1_ids_bytes(n_dst, n_pos, F, elem, k, self_rows=None):
     """Algorithmic HBM bytes of one launch of the runner's layer-1 gather over
     resolved ids (agg_ids_kernel): one feature row per sampled edge, the
-    destination's k padded neighbour ids (4 B each), one output row."""
-    return n_pos * F * elem + n_dst * (k * 4 + F * elem)
+    destination's k padded neighbour ids (4 B each), one output row; with the
+    self rows in the slot (GS_SELF_ROWS, default on) also the destination's
+    own row read and written beside it."""
+    if self_rows is None:
+        self_rows = os.environ.get("GS_SELF_ROWS", "1") != "0"
+    return n_pos * F * elem + n_dst * (k * 4 + F * elem) + (2 * n_dst * F * elem if self_rows else 0)
 
 
 def replay_frontiers(graph, batches, n_streams, fanouts, seed, rank, upto):
@@ -266,7 +270,8 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 # and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
 # the kernel beside the live event-timed one
 # (newest round first: the first file present is used)
-ROCPROF_STATS = {("rmat2m", 512): ["profiles/r04d_kernel_stats_rmat2m_steps300.csv",
+ROCPROF_STATS = {("rmat2m", 512): ["profiles/r04e_kernel_stats_rmat2m_steps300.csv",
+                                   "profiles/r04d_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04c_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04b_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04_kernel_stats_rmat2m_steps300.csv",
@@ -274,7 +279,8 @@ ROCPROF_STATS = {("rmat2m", 512): ["profiles/r04d_kernel_stats_rmat2m_steps300.c
                                    "profiles/r03b_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r03_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r02_kernel_stats_rmat2m_steps300.csv"],
-                 ("rmat2m-max-bf16", 512): ["profiles/r04d_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                 ("rmat2m-max-bf16", 512): ["profiles/r04e_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                                            "profiles/r04d_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04c_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04b_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04_kernel_stats_rmat2m_max_bf16_steps300.csv",
