@@ -509,7 +509,10 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
  * > 0 (the last hop's fanout, which bounds every sampled neighbourhood)
  * gs_trainer_gather runs as two launches: the positions resolved into
  * padded neighbour ids, then the row gather through them (bitwise the same
- * aggregate, without the index chain in the gather). */
+ * aggregate, without the index chain in the gather); that gather also copies
+ * each destination's own feature row beside its aggregate (slot rows
+ * [self | agg] of 2F, so the layer-1 GEMMs read no self index; GS_SELF_ROWS=0
+ * at reserve time keeps F-wide slots). */
 int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout);
 int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
                       const int64_t* offsets, int32_t slot, void* stream);
