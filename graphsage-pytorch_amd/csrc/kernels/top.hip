@@ -42,7 +42,17 @@
 namespace gs {
 
 constexpr int kTopRows = 4;
-constexpr int kTopThreads = 256;
+// Threads per block: 512 (8 waves) by default.  The extra waves issue the W2
+// DMA (six waves instead of two) and take one 16-column E tile each (two
+// waves per SIMD interleave the dependent MFMA chains instead of two
+// accumulators per wave); the gather, head, slab and dIn stages keep waves
+// 0-3.  Lab, per launch: 15.3 -> 14.0 us, outputs bitwise equal
+// (profiles/r04e_top_lab_e8_ab.txt).  GS_TOP_E8=0 (runtime) or -DGS_TOP_E8=0
+// (the lab) restores 4 waves.
+#ifndef GS_TOP_E8
+#define GS_TOP_E8 1
+#endif
+constexpr int kTopThreads = GS_TOP_E8 ? 512 : 256;
 constexpr int kTopH = 128;
 constexpr int kTopK = 2 * kTopH;
 constexpr int kTopMaxC = 32;
@@ -72,8 +82,8 @@ struct TopArgs {
 // k offset of step i (0..15) inside a 16-wide block: the MFMA kernels' order.
 __device__ __forceinline__ constexpr int mfma_k(int i) { return 4 * (i & 3) + (i >> 2); }
 
-template <int OP>
-__global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
+template <int OP, int NT>
+__global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
     constexpr int H = kTopH, K = kTopK, D = kTopH;
     // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, Wc, dlogits, loss
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -101,7 +111,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // dependent load rounds would otherwise queue behind the DMA (vmcnt
     // retires in order).
     if (w >= 2)
-        for (int c = w - 2; c < H; c += 2)
+        for (int c = w - 2; c < H; c += NT / 64 - 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
                                              0, 0);
 
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     const float b_lane = a.bc[min(cl, C - 1)];
     {
         const int nW4 = C * D / 4;
-        for (int q = tid; q < nW4; q += kTopThreads) {
+        for (int q = tid; q < nW4; q += NT) {
             const float4 v = reinterpret_cast<const float4*>(a.Wc)[q];
             const int t = 4 * q;
             float* d = sW + t + t / D;  // row pitch D + 1 (D % 4 == 0: a quad stays in one row)
@@ -213,6 +223,47 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     __syncthreads();
     GS_TOP_STAMP(2);
 
+    if constexpr (NT == 512)
+    // ---- stage 2 (8 waves): E = relu([self | agg] · W2ᵀ), wave w owns the
+    // 16 columns 16w .. 16w+15 (one tile, the same MFMA chain per tile)
+    {
+        const int r = lane & 15, kq = lane >> 4;
+        const bool rowok = r < nr;
+        const uint4* xr = reinterpret_cast<const uint4*>(sX[min(r, nr - 1)]);
+        const uint4* wq = reinterpret_cast<const uint4*>(sW2);
+        const int c0 = 16 * w + r;
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto ld = [&](int k0, uint4& av, uint4& b0) {
+            const int q = (k0 >> 2) + kq;
+            av = xr[q];
+            b0 = wq[c0 * (K / 4) + (q ^ (c0 & 15))];
+        };
+        uint4 an, bn0;
+        ld(0, an, bn0);
+#pragma unroll 2
+        for (int k0 = 0; k0 < K; k0 += 16) {
+            uint4 av = an;
+            const uint4 b0 = bn0;
+            ld(min(k0 + 16, K - 16), an, bn0);
+            if (!rowok) av = make_uint4(0, 0, 0, 0);
+            const float a4[4] = {__uint_as_float(av.x), __uint_as_float(av.y), __uint_as_float(av.z),
+                                 __uint_as_float(av.w)};
+            const float w0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
+                                 __uint_as_float(b0.w)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w0[j], acc0, 0, 0, 0);
+        }
+        if (kq == 0) {
+#pragma unroll
+            for (int j = 0; j < kTopRows; ++j) {
+                if (j >= nr) break;
+                const float v0 = (!(acc0[j] > 0.f) && acc0[j] == acc0[j]) ? 0.f : acc0[j];  // relu (NaN kept)
+                sE[j][c0] = v0;
+                a.E[static_cast<int64_t>(r0 + j) * H + c0] = v0;
+            }
+        }
+    }
+    else
     // ---- stage 2: E = relu([self | agg] · W2ᵀ) on the matrix cores, as the
     // linear kernel's tiles: wave w owns columns 32w .. 32w+31 (two 16x16
     // tiles); the 4 rows ride in a 16-row A tile (rows >= nr are zero).
@@ -331,7 +382,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // 15.4-15.6 us against 16.3 for one thread per flat slab element, the
     // fallback above 16 classes; same sums).
 #ifndef GS_TOP_SLAB_FLAT
-    if (C * 16 <= kTopThreads) {
+    if (C * 16 <= NT) {
         const int per = C * (D + 1);
         float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
         const int c = tid >> 4;
@@ -366,11 +417,11 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                 }
             }
         }
-        if (tid >= kTopThreads - 64) {
+        if (tid >= NT - 64) {
             float s = 0.f;
-            for (int ii = tid - (kTopThreads - 64); ii < nr; ii += 64) s += sloss[ii];
+            for (int ii = tid - (NT - 64); ii < nr; ii += 64) s += sloss[ii];
             s = wave_sum(s);
-            if (tid == kTopThreads - 64) out[per] = s;
+            if (tid == NT - 64) out[per] = s;
         }
     } else
 #endif
@@ -378,9 +429,9 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     {
         const int per = C * (D + 1);
         float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
-        int c = tid / (D + 1), d = tid - c * (D + 1);  // advanced by kTopThreads per step, no divides
-        constexpr int dc = kTopThreads / (D + 1), dd = kTopThreads % (D + 1);
-        for (int t = tid; t < per; t += kTopThreads) {
+        int c = tid / (D + 1), d = tid - c * (D + 1);  // advanced by NT per step, no divides
+        constexpr int dc = NT / (D + 1), dd = NT % (D + 1);
+        for (int t = tid; t < per; t += NT) {
             float s = 0.f;
 #pragma unroll
             for (int ii = 0; ii < kTopRows; ++ii)
@@ -407,7 +458,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // columns of one instruction (lane l: column 64w + l), one h per
     // instruction in linear_dx_body's order (0,4,8,12, 1,5,9,13, ... per
     // 16-wide h block): the same fmaf chains, bit for bit.
-    {
+    if (w < 4) {  // (waves >= 4 under GS_TOP_E8: no dIn role)
         const int arow = lane & 3, kc = 64 * w + lane;
         const bool rowok = arow < nr;
         const float4* zr = reinterpret_cast<const float4*>(sZ[min(arow, nr - 1)]);
@@ -455,12 +506,16 @@ static bool top_lds_ready(int64_t C) {
     const size_t need = top_smem_bytes(C);
     if (ok_bytes < 0) {
         const size_t want = top_smem_bytes(kTopMaxC);
-        const bool a = hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) == hipSuccess;
-        const bool b = hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) == hipSuccess;
+        auto raise = [&](const void* f) {
+            return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) ==
+                   hipSuccess;
+        };
+        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, 512>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, 512>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, 256>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, 256>));
         (void)hipGetLastError();
-        ok_bytes = (a && b) ? static_cast<int>(want) : 0;
+        ok_bytes = a ? static_cast<int>(want) : 0;
     }
     return need <= static_cast<size_t>(ok_bytes);
 }
@@ -482,8 +537,15 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
               aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
-    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);
-    else launch_k(sage_top_kernel<GS_AGG_MAX>, grid, dim3(kTopThreads), smem, st, a);
+    const char* e8 = std::getenv("GS_TOP_E8");  // read per launch (tests switch it)
+    const bool w8 = e8 ? std::string(e8) != "0" : kTopThreads == 512;
+    if (w8) {
+        if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, 512>, grid, dim3(512), smem, st, a);
+        else launch_k(sage_top_kernel<GS_AGG_MAX, 512>, grid, dim3(512), smem, st, a);
+    } else {
+        if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, 256>, grid, dim3(256), smem, st, a);
+        else launch_k(sage_top_kernel<GS_AGG_MAX, 256>, grid, dim3(256), smem, st, a);
+    }
     check_launch("sage_top");
     return static_cast<int>(grid.x);
 }

@@ -476,15 +476,18 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name,
     assert done >= 1
 
 
+@pytest.mark.parametrize("e8", ["1", "0"])
 @pytest.mark.parametrize("agg,name,B", [("MEAN", "pubmed", 512), ("MAX", "pubmed", 512), ("MEAN", "rmat", 97),
                                          ("MAX", "pubmed", 1536)])
-def test_top_launch_matches_separate_launches(gs, monkeypatch, agg, name, B):
+def test_top_launch_matches_separate_launches(gs, monkeypatch, agg, name, B, e8):
     """The one-launch top layer + loss head (kernels/top.hip: layer-2
     aggregate, linear, relu, NLL head, dZ and dIn on the matrix cores) against the
     separate launches it replaces (agg_fwd, the MFMA linear, cls_rows, the
     MFMA dIn role): it repeats their product chains in the f32 MFMA order, so
     loss, every gradient and the updated parameters are bitwise equal,
-    including a batch that leaves its last 4-row block partial."""
+    including a batch that leaves its last 4-row block partial; on 8 waves
+    (the default) and on 4 (GS_TOP_E8=0)."""
+    monkeypatch.setenv("GS_TOP_E8", e8)
     graph, g, n = _graph(gs, name)
     X = torch.from_numpy(uniform_features(7, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
