@@ -47,7 +47,8 @@ constexpr int kTopRows = 4;
 // waves per SIMD interleave the dependent MFMA chains instead of two
 // accumulators per wave); the gather, head, slab and dIn stages keep waves
 // 0-3.  Lab, per launch: 15.3 -> 14.0 us, outputs bitwise equal
-// (profiles/r04e_top_lab_e8_ab.txt).  GS_TOP_E8=0 (runtime) or -DGS_TOP_E8=0
+// (profiles/r04e_top_lab_e8_ab.txt; 16 waves, fourteen of them DMA: 14.6 us,
+// profiles/r04f_top_lab_e16_ab.txt).  GS_TOP_E8=0 (runtime) or -DGS_TOP_E8=0
 // (the lab) restores 4 waves.
 #ifndef GS_TOP_E8
 #define GS_TOP_E8 1
@@ -223,10 +224,10 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
     __syncthreads();
     GS_TOP_STAMP(2);
 
-    if constexpr (NT == 512)
+    if constexpr (NT >= 512) {
     // ---- stage 2 (8 waves): E = relu([self | agg] · W2ᵀ), wave w owns the
     // 16 columns 16w .. 16w+15 (one tile, the same MFMA chain per tile)
-    {
+    if (w < 8) {
         const int r = lane & 15, kq = lane >> 4;
         const bool rowok = r < nr;
         const uint4* xr = reinterpret_cast<const uint4*>(sX[min(r, nr - 1)]);
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
             }
         }
     }
-    else
+    } else
     // ---- stage 2: E = relu([self | agg] · W2ᵀ) on the matrix cores, as the
     // linear kernel's tiles: wave w owns columns 32w .. 32w+31 (two 16x16
     // tiles); the 4 rows ride in a 16-row A tile (rows >= nr are zero).
