@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <sched.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -163,6 +164,7 @@ struct gs_runner {
     // the last step of each gs_runner_run call (teardown) and as the
     // GS_RUNNER_EVENTS=1 A/B path.
     bool use_flag = false;
+    bool yield_polls = false;  // GS_RUNNER_YIELD
     int64_t* done_host = nullptr;          // hipHostMalloc, coherent
     int64_t* done_dev = nullptr;
     int64_t flag_step[kDev] = {-1, -1, -1};  // batch whose SGD signals entry k free (-1: none pending)
@@ -172,6 +174,11 @@ struct gs_runner {
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t spin = 0; __atomic_load_n(done_host, __ATOMIC_ACQUIRE) < want; ++spin) {
                 __builtin_ia32_pause();
+                // GS_RUNNER_YIELD (default on, "0" off): offer the core to
+                // runnable sampler threads every 64 polls while the step runs
+                // (the runner is two steps ahead, so a few microseconds of
+                // reaction cost nothing; profiles/r04f_runner_yield_ab.txt)
+                if (yield_polls && (spin & 63) == 63) sched_yield();
                 if ((spin & 0xfffff) == 0xfffff &&
                     std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
                     // no progress for 5 s: let the runtime report a device error, then give up
@@ -676,6 +683,10 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
     r->use_flag = std::getenv("GS_RUNNER_EVENTS") == nullptr && !cfg->embed_out;
+    {
+        const char* y = std::getenv("GS_RUNNER_YIELD");  // default on; "0": pure spin
+        r->yield_polls = !(y && std::string(y) == "0");
+    }
     if (r->use_flag) {
         void* hp = nullptr;
         hip_ok(hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc(done flag)");
