@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 pass AI: the final build once more — the whole GPU suite, smoke(),
+# Round-4 pass AI (and AL, after the runner yield): the final build once more — the whole GPU suite, smoke(),
 # and the driver's default bench command.
 set -o pipefail
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$PWD}
-OUT=$ROOT/gpurun_out/r04ai
+OUT=$ROOT/gpurun_out/r04al
 mkdir -p "$OUT"; cd "$ROOT"
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests \
     > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
