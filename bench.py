@@ -160,16 +160,6 @@ def cgroup_throttle():
     return None
 
 
-def layer1_fused_bytes(n_dst, n_pos, F, H, elem, gcn=False):
-    """Algorithmic HBM bytes of one fused layer-1 launch (gs_sage1_fwd,
-    DESIGN.md §4): per sampled edge the neighbour row + entry + col id; per
-    destination the self row (not in gcn), the aggregate row written back, the
-    fp32 output row and its pos_ptr / dst id; W once."""
-    K = F if gcn else 2 * F
-    per_dst = (0 if gcn else F * elem) + F * elem + H * 4 + 8
-    return n_pos * (F * elem + 8) + n_dst * per_dst + H * K * elem
-
-
 def agg1_bytes(n_dst, n_pos, F, elem):
     """Algorithmic HBM bytes of one layer-1 K-agg launch:
     neighbour feature rows once per sampled edge + sampled positions and CSR
@@ -185,14 +175,12 @@ def top_bytes(B, n_nbr, H, C):
     return (n_nbr + B) * H * 4 + n_nbr * 4 + H * 2 * H * 4 + C * (H + 1) * 4 + B * 5 * H * 4
 
 
-def agg1_ids_bytes(n_dst, n_pos, F, elem, k, self_rows=None):
+def agg1_ids_bytes(n_dst, n_pos, F, elem, k, self_rows=True):
     """Algorithmic HBM bytes of one launch of the runner's layer-1 gather over
     resolved ids (agg_ids_kernel): one feature row per sampled edge, the
     destination's k padded neighbour ids (4 B each), one output row; with the
-    self rows in the slot (GS_SELF_ROWS, default on) also the destination's
-    own row read and written beside it."""
-    if self_rows is None:
-        self_rows = os.environ.get("GS_SELF_ROWS", "1") != "0"
+    self rows in the slot (the trainer's default) also the destination's own
+    row read and written beside it."""
     return n_pos * F * elem + n_dst * (k * 4 + F * elem) + (2 * n_dst * F * elem if self_rows else 0)
 
 
@@ -341,10 +329,19 @@ def load_traffic(config_name, batch, kernel):
             continue
         if d.get("config") != config_name or int(d.get("batch", -1)) != int(batch):
             continue
-        k = next((v for n, v in d.get("kernels", {}).items() if kernel_key(n) == key), None)
+        k = _most_dispatched(d, lambda n: kernel_key(n) == key)
         if k and "hbm_bytes" in k:
-            best = {"hbm_bytes": k["hbm_bytes"], "source": os.path.relpath(p, ROOT)}
+            best = {"hbm_bytes": k["hbm_bytes"], "dispatches": k.get("dispatches"),
+                    "source": os.path.relpath(p, ROOT)}
     return best
+
+
+def _most_dispatched(summary, match):
+    """The matching kernel instance of a PMC summary with the most dispatches
+    (the in-step one: e.g. the layer-1 forward's pending-update instance runs
+    every step but a run's first)."""
+    cands = [v for n, v in summary.get("kernels", {}).items() if match(n)]
+    return max(cands, key=lambda v: v.get("dispatches", 0)) if cands else None
 
 
 def load_mfma_busy(config_name, kernel):
@@ -363,9 +360,10 @@ def load_mfma_busy(config_name, kernel):
             d = json.load(open(p))
         except Exception:
             continue
-        k = next((v for n, v in d.get("kernels", {}).items() if bare(n) == key), None)
+        k = _most_dispatched(d, lambda n: bare(n) == key)
         if k and "mfma_util" in k:
-            best = {"mfma_util": k["mfma_util"], "source": os.path.relpath(p, ROOT)}
+            best = {"mfma_util": k["mfma_util"], "dispatches": k.get("dispatches"),
+                    "source": os.path.relpath(p, ROOT)}
     return best
 
 
@@ -854,12 +852,9 @@ def main():
         runner = None
         ref_stream = reference_stream_window(trainer, wl, cfg, args, batches)
     n_edges = float(sizes[:L, 1].sum()) * args.steps
-    fused1 = bool(lib.gs_trainer_layer1_fused(trainer._h))
     n1, e1 = float(sizes[L - 1, 0]), float(sizes[L - 1, 1])
-    if fused1:
-        agg_bytes = layer1_fused_bytes(n1, e1, cfg["feat"], 128, elem)
-    else:  # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
-        agg_bytes = agg1_ids_bytes(n1, e1, cfg["feat"], elem, cfg["fanouts"][-1])
+    # the runner reserves id slots for the last hop's fanout: resolve, then agg_ids_kernel (timed)
+    agg_bytes = agg1_ids_bytes(n1, e1, cfg["feat"], elem, cfg["fanouts"][-1])
     gemm_flops = 2.0 * n1 * (2 * cfg["feat"]) * 128  # 2·|L1|·2F·H per layer-1 GEMM
 
     # the BASELINE metric literally: sampled nodes (B + |L1| + |L0|, the
@@ -890,24 +885,32 @@ def main():
             us = float(np.mean(tt)) * 1e3
             if site in (0, 3):
                 nb = agg_bytes if site == 0 else top_bytes(cfg["batch"], float(sizes[0, 3]), 128, cfg["classes"])
-                achieved, peak, unit, bound = float(nb) / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s", "hbm"
+                peak, unit, bound, scale = HBM_PEAK_GBS, "GB/s", "hbm", float(nb) / 1e9
                 work = {"algo_bytes_per_launch": int(nb)}
             else:
-                peak = MFMA_PEAK_TFS[cfg["dtype"]]
-                achieved, unit, bound = gemm_flops / (us * 1e-6) / 1e12, "TFLOP/s", "mfma"
+                peak, unit, bound, scale = MFMA_PEAK_TFS[cfg["dtype"]], "TFLOP/s", "mfma", gemm_flops / 1e12
                 work = {"algo_flops_per_launch": int(gemm_flops)}
                 mb = load_mfma_busy(args.config, names[site])
-                work.update(mfma_busy=(mb["mfma_util"] if mb else None), mfma_busy_source=(mb["source"] if mb else None))
+                work.update(mfma_busy=(mb["mfma_util"] if mb else None), mfma_busy_source=(mb["source"] if mb else None),
+                            mfma_busy_dispatches=(mb["dispatches"] if mb else None))
+            achieved_live = scale / (us * 1e-6)
+            # `achieved` / `frac` on the committed rocprofv3 average of this kernel
+            # (the same command under --kernel-trace --stats, profiles/), so the
+            # line reproduces from profiles/; the live in-step timing beside it
+            rp = prof_avg[site]
+            achieved = scale / (rp["avg_us"] * 1e-6) if rp else achieved_live
             tr = load_traffic(args.config, cfg["batch"], names[site])
             rooflines[SITE_NAMES[site]] = dict(
                 bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
                 traffic=(tr["hbm_bytes"] if tr else None), traffic_source=(tr["source"] if tr else None),
-                rocprof=prof_avg[site],
+                traffic_dispatches=(tr["dispatches"] if tr else None),
+                achieved_from=("rocprofv3 average launch (rocprof.avg_us)" if rp else "live in-step timing"),
+                rocprof=rp,
+                achieved_live=round(achieved_live, 2), frac_live=round(achieved_live / peak, 4),
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
                 timer=("kernel span (per-workgroup s_memrealtime stamps, min start .. max end)"
-                       if site in (1, 3) and not os.environ.get("GS_TIMER_EVENTS")
-                       else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
+                       if site in (1, 3) else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
                 timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
                 **work)

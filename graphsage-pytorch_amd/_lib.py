@@ -27,6 +27,7 @@ GS_AGG_MEAN, GS_AGG_MAX = 0, 1
 GS_SAMPLE_GCN, GS_SAMPLE_FULL = 1, 2
 GS_DSAMPLER_NO_AUX = 8  # gs_dsampler_create: every kernel on the caller's stream
 GS_MAX_HOPS = 8
+GS_TOPT_FUSED_BWD, GS_TOPT_TOP_LAUNCH, GS_TOPT_SELF_ROWS, GS_TOPT_DEFER_UPDATE = range(4)
 (GS_PK_POS_PTR, GS_PK_POS, GS_PK_DST_IDS, GS_PK_NBR_PTR, GS_PK_NBR, GS_PK_SELF,
  GS_PK_TPTR, GS_PK_TIDX, GS_PK_NFIELDS) = range(9)
 
@@ -140,7 +141,9 @@ _SIGS = {
     "gs_trainer_time_kernels_every": (_i32, [_vp, _i32, _i64, _i64]),
     "gs_trainer_kernel_name": (ctypes.c_char_p, [_vp, _i32]),
     "gs_trainer_grads": (_vp, [_vp]),
-    "gs_trainer_layer1_fused": (_i32, [_vp]),
+    "gs_trainer_set_option": (_i32, [_vp, _i32, _i32]),
+    "gs_trainer_capture": (_i32, [_vp, _vp, _i64, _vp, _i64]),
+    "gs_trainer_captured": (_i64, [_vp]),
     "gs_comm_unique_id": (_i32, [_vp]),
     "gs_comm_create": (_i32, [_vp, _i32, _i32, _p(_vp)]),
     "gs_comm_destroy": (None, [_vp]),

@@ -10,6 +10,8 @@
 // only orders the rows of a gather, so by default it is skipped and the
 // device expands the sampled positions through the CSR itself.
 #include <algorithm>
+#include <exception>
+#include <mutex>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -248,12 +250,27 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     for (int64_t c = 0; c < nch; ++c) sc.chunk_done[c].store(0, std::memory_order_relaxed);
     sc.next_chunk.store(0, std::memory_order_relaxed);
     int32_t* counts = h.set_ptr.data() + 1;
+    // A chunk build that throws (bad_alloc in a set or an items vector) marks
+    // its chunk failed (2) instead of done (1), so the merge loop stops
+    // instead of spinning on it; the first exception is rethrown here once
+    // every helper has left the chunk loop (their job refers to this frame).
+    std::exception_ptr err;
+    std::mutex err_mu;
+    auto keep_error = [&] {
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (!err) err = std::current_exception();
+    };
     auto build = [&](int64_t c) {
-        const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
-        auto& items = sc.part_items[c];
-        items.clear();
-        sets_range(g, h, a, b, items, counts, c == 0 ? &sc.first : nullptr);
-        sc.chunk_done[c].store(1, std::memory_order_release);
+        try {
+            const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
+            auto& items = sc.part_items[c];
+            items.clear();
+            sets_range(g, h, a, b, items, counts, c == 0 ? &sc.first : nullptr);
+            sc.chunk_done[c].store(1, std::memory_order_release);
+        } catch (...) {
+            keep_error();
+            sc.chunk_done[c].store(2, std::memory_order_release);
+        }
     };
     const bool helped = team && nch > 1;
     if (helped)
@@ -261,29 +278,37 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
             for (int64_t c; (c = sc.next_chunk.fetch_add(1, std::memory_order_relaxed)) < nch;) build(c);
         });
     PySet& u = sc.u;
-    u.reset();
     int64_t n_items = 0;
-    for (int64_t c = 0; c < nch; ++c) {
-        while (!sc.chunk_done[c].load(std::memory_order_acquire)) {
-            const int64_t m = sc.next_chunk.fetch_add(1, std::memory_order_relaxed);
-            if (m < nch) build(m);  // m >= c: everything before c was claimed already
-            else _mm_pause();
+    try {
+        u.reset();
+        for (int64_t c = 0; c < nch; ++c) {
+            int st;
+            while ((st = sc.chunk_done[c].load(std::memory_order_acquire)) == 0) {
+                const int64_t m = sc.next_chunk.fetch_add(1, std::memory_order_relaxed);
+                if (m < nch) build(m);  // m >= c: everything before c was claimed already
+                else _mm_pause();
+            }
+            if (st != 1) break;  // that chunk's build failed: err holds why
+            const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
+            const auto& items = sc.part_items[c];
+            n_items += static_cast<int64_t>(items.size());
+            // this chunk's runs: set_ptr-style offsets into `items`
+            int32_t ptr[kChunk + 1];
+            ptr[0] = 0;
+            for (int64_t r = a; r < b; ++r) ptr[r - a + 1] = ptr[r - a] + counts[r];
+            if (c == 0) {
+                copy_into(u, sc.first);  // non-empty: merge_runs never sees fill == 0
+                u.merge_runs(items.data(), ptr + 1, b - a - 1);
+            } else {
+                u.merge_runs(items.data(), ptr, b - a);
+            }
         }
-        const int64_t a = c * kChunk, b = std::min(n, a + kChunk);
-        const auto& items = sc.part_items[c];
-        n_items += static_cast<int64_t>(items.size());
-        // this chunk's runs: set_ptr-style offsets into `items`
-        int32_t ptr[kChunk + 1];
-        ptr[0] = 0;
-        for (int64_t r = a; r < b; ++r) ptr[r - a + 1] = ptr[r - a] + counts[r];
-        if (c == 0) {
-            copy_into(u, sc.first);  // non-empty: merge_runs never sees fill == 0
-            u.merge_runs(items.data(), ptr + 1, b - a - 1);
-        } else {
-            u.merge_runs(items.data(), ptr, b - a);
-        }
+    } catch (...) {
+        keep_error();
     }
+    if (err) sc.next_chunk.store(nch, std::memory_order_relaxed);  // no helper claims another chunk
     if (helped) team->wait();  // every helper is out of the chunk loop
+    if (err) std::rethrow_exception(err);
     sc.n_items = n_items;
     GS_PHASE(2);
 }
@@ -787,11 +812,7 @@ int64_t gs_sample_pack_bound_multi(const gs_graph* gp, int64_t n_roots, int64_t 
 int gs_team_create(int32_t helpers, gs_team** out) {
     GS_API_BEGIN
     GS_REQUIRE(out && helpers >= 0 && helpers <= 64, GS_EINVAL, "helpers out of [0, 64]");
-    // GS_HELPER_SPIN_US: how long an idle helper polls before sleeping (A/B knob; default 500)
-    static const int spin_us = [] {
-        const char* e = std::getenv("GS_HELPER_SPIN_US");
-        return e ? std::max(0, std::atoi(e)) : 500;
-    }();
+    constexpr int spin_us = 500;  // how long an idle helper polls before sleeping
     *out = reinterpret_cast<gs_team*>(new gs::Team(helpers, spin_us));
     GS_API_END
 }

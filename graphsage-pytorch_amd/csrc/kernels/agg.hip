@@ -210,15 +210,9 @@ void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
     check_launch("resolve_top");
 }
 
-// GS_AGG_BLOCKS=n caps the grid (grid-stride over the destinations; unset or
-// 0: one pass, a block per 256/G destinations).  One block per CU (256) made
-// the side-stream gather 10 -> 17 us without moving the step: medians over six
-// alternating rounds 64.95 against 65.05 us.
-static int agg_ids_block_cap() {
-    const char* e = std::getenv("GS_AGG_BLOCKS");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : (1 << 30);
-}
+// One pass, a block per 256/G destinations (a grid capped at one block per
+// CU made the side-stream gather 10 -> 17 us without moving the step).
+static int agg_ids_block_cap() { return 1 << 30; }
 
 void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t F, int64_t n_dst, int k,
                     const int32_t* ids, const int32_t* dst_ids, int gcn, void* out, int64_t ldo, hipStream_t st,

@@ -101,87 +101,6 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
 
-// The layer-1 weight gradient (linear_dw_xcd_kernel's workgroups, first, so
-// their XCD map is unchanged) with the top path's dW_2 slabs and classifier
-// reduce appended (GS_DW_PLUS=1): those two roles of layer_bwd_top_kernel do
-// not feed the layer-1 gradient, so they can leave the launch that the
-// layer-1 dW waits for and run beside the dW instead.  Same bodies, same
-// sums.
-struct Dw1 {
-    int n, F, H, K, rps, gx, tiles, S, nb;
-    const float* Xs;
-    int64_t ldxs;
-    const int* sidx;
-    const float* A;
-    int64_t lda;
-    const float* dout;
-    int64_t ldo;
-    float* target;
-    int64_t split_stride;
-};
-
-__global__ __launch_bounds__(kThreads) void dw1_plus_kernel(Dw1 d, BwdA a, int cls_nb) {
-    int b = blockIdx.x;
-    if (b < d.nb) {
-        const int j = b / kXcds;
-        const int z = b % kXcds + kXcds * (j / d.tiles);
-        if (z >= d.S) return;
-        const int t = j % d.tiles;
-        linear_dw_body<float, true, false, true, true>(t % d.gx, t / d.gx, z, d.n, d.F, d.H, d.K, d.rps, d.Xs, d.ldxs,
-                                                       d.sidx, d.A, d.lda, d.dout, nullptr, d.ldo, d.target,
-                                                       d.split_stride);
-        return;
-    }
-    b -= d.nb;
-    if (b < a.dw_nb) {
-        const int g2 = a.dw_gx * a.dw_gy;
-        linear_dw_body<float, true, false, true, true>(b % a.dw_gx, (b % g2) / a.dw_gx, b / g2, a.n, a.F, a.H, a.K,
-                                                       a.rps, a.Xs, a.ldxs, a.sidx, a.A, a.F, a.dZ, nullptr, a.H,
-                                                       a.target, static_cast<int64_t>(a.H) * a.K);
-        return;
-    }
-    b -= a.dw_nb;
-    if (b < cls_nb) cls_reduce_body(b, a.B, a.D, a.C, a.cls_rows, a.cls_slab, a.dWc, a.dbc, a.loss, a.cls_part);
-}
-
-int dw1_plus_launch(int64_t n, int64_t F, int64_t H, const float* Xs, int64_t ldxs, const int32_t* sidx,
-                    const float* A, int64_t lda, const float* dout, int64_t ldo, float* dW, void* ws,
-                    int64_t ws_bytes, const BwdMoved& mv, hipStream_t st) {
-    const int64_t K = 2 * F;
-    const bool ok = n >= 1 && n < (int64_t(1) << 31) && Xs && A && dout && F % 4 == 0 && lda % 4 == 0 &&
-                    ldxs % 4 == 0 && aligned16(A) && aligned16(Xs) && H % 4 == 0 && ldo % 4 == 0 &&
-                    aligned16(dout) && aligned16(ws);
-    if (!ok) return -1;
-    const int S = dw_splits(n, K, H);
-    if (S < 2) return -1;
-    GS_REQUIRE(ws_bytes >= static_cast<int64_t>(S) * K * H * 4, GS_EINVAL, "workspace too small");
-    Dw1 d{};
-    d.n = static_cast<int>(n);
-    d.F = static_cast<int>(F);
-    d.H = static_cast<int>(H);
-    d.K = static_cast<int>(K);
-    d.rps = dw_rows_per_split(n, K, H);
-    d.gx = static_cast<int>((K + 63) / 64);
-    d.tiles = d.gx * static_cast<int>((H + 63) / 64);
-    d.S = S;
-    d.nb = kXcds * d.tiles * ((S + kXcds - 1) / kXcds);
-    d.Xs = Xs;
-    d.ldxs = ldxs;
-    d.sidx = sidx;
-    d.A = A;
-    d.lda = lda;
-    d.dout = dout;
-    d.ldo = ldo;
-    d.target = static_cast<float*>(ws);
-    d.split_stride = H * K;
-    (void)dW;
-    launch_k(dw1_plus_kernel, dim3(static_cast<unsigned>(d.nb + mv.a.dw_nb + mv.cls_nb)), dim3(kThreads), 0, st, d,
-             mv.a, mv.cls_nb);
-    check_launch("dw1_plus");
-    return S;
-}
-
-
 bool layer_bwd_fusable(const LayerBwd& a) {
     const int64_t K = a.Xs ? 2 * a.fin : a.fin;
     const bool al = aligned16(a.A) && aligned16(a.dZ) && aligned16(a.W) && aligned16(a.dW) && aligned16(a.slabs) &&
@@ -278,7 +197,7 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     return Bq.sum_nb;
 }
 
-int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st, BwdMoved* moved) {
+int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st) {
     GS_REQUIRE(layer_bwd_fusable(a) && a.din_ready && a.Xs, GS_EINVAL, "top backward: not the fused top path");
     const int64_t K = 2 * a.fin;
     const int S = dw_splits(a.n, K, a.H);
@@ -324,12 +243,6 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     Bq.dH = a.dH;
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
-    if (moved) {  // dW_2 slabs and the classifier reduce go to the layer-1 dW launch (dw1_plus_launch)
-        moved->a = A;
-        moved->cls_nb = t.cls_nb;
-        A.dw_nb = 0;
-        t.cls_nb = 0;
-    }
     const dim3 grid(static_cast<unsigned>(A.dw_nb + t.cls_nb + agg_nb));
 #define GS_BWDT(OP)                                                                     \
     do {                                                                                \

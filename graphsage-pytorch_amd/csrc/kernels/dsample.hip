@@ -932,6 +932,11 @@ __global__ void begin_kernel(Ctl* c, const int32_t* __restrict__ roots, int32_t*
         c->total = 0;
         c->used = 0;
         c->pos_batch = c->pos_cur;
+        // every run starts on a fresh mark epoch: a union reads epoch + 1 and
+        // only finish_union advances it, so a run that failed before its
+        // finish_union (kStTable / kStSize / kStSpin, then GS_DS_BAIL) left
+        // marks at epoch + 1 that would outrank this run's own at that epoch
+        c->epoch += 1;
     }
 }
 

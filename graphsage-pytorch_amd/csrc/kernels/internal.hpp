@@ -24,40 +24,25 @@ void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook
 // use the whole gradient's row slabs: the same sums bit for bit.
 void trainer_set_w1_chunk_hook(gs_trainer* t, int chunks,
                                std::function<void(hipStream_t, int64_t, int64_t)> hook);
-// Called on the step's stream right after the layer-1 forward launch of a training step.
-void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook);
 // Inside a runner loop: the SGD keeps the bf16 W1 current (no per-step cast).
 void trainer_keep_lowp(gs_trainer* t, bool keep);
-// Inside a runner loop without an all-reduce: the step's last launch runs the
-// clip + SGD too (gs_trainer_update_local is then a no-op for that step).
-void trainer_fuse_update(gs_trainer* t, bool fuse);
 // Inside a runner loop without an all-reduce (fp32 2-layer steps): defer each
 // step's clip + SGD into the next step's launches (gs_trainer fields defer /
 // pending).  Returns whether deferral is on; off (at the end of the loop)
 // applies the last pending update, so the flat parameters and gradients are
 // those of the separate update launch.
 bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st, bool comm = false);
-// A fused SGD launch's grid barrier gave up waiting (never expected).
-bool trainer_barrier_failed(gs_trainer* t);
 int64_t trainer_w1_floats(const gs_trainer* t);
 
 // linear.hip
-// In-launch grouping of the weight-gradient slabs (linear_dw_grp_kernel):
-// cnt holds n_cnt zeroed ints (8 per 64x64 tile at least), gpart room for 8
-// slabs of H*K floats.  On return, slabs / S name what the slab sum must add
-// (the group partials and their count, or ws and the slab count unchanged).
-struct DwGroups {
-    int* cnt;
-    int64_t n_cnt;
-    float* gpart;
-    const float* slabs = nullptr;
-    int S = 0;
-};
-inline constexpr int kDwGroupParts = 8;
+// Whether gs_sage_linear_fwd takes the wide (16-B load) kernel for these
+// operands: the only forward that applies a pending deferred update.
+bool linear_fwd_wide_ok(gs_dtype dt, int64_t F, const void* Xs, int64_t ldxs, const void* A, int64_t lda,
+                        const void* W);
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
-                    DwGroups* grp = nullptr, int64_t H_split = -1);
+                    int64_t H_split = -1);
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 // One slab sum: out = Σ_s slabs[s] (S slabs of len floats), norm partials to part.
 struct SlabSum {
@@ -78,27 +63,6 @@ int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, 
 // parameters and gradients become what the separate clip + SGD launch would
 // have left (W1 from sp.S or recomputed into w1_out, the others updated).
 void spec_finalize_launch(const FwdSpec& sp, float* w1_out, int64_t w1_floats, hipStream_t st);
-// The clip + SGD that follows a step's last slab sum (no all-reduce between):
-// flat params / grads, group offsets and norm partials as sgd_with_parts
-// takes them, the bf16 W1 shadow (g_lowp_shadow) and the done flag
-// (g_done_flag) of the launching thread.
-struct FusedSgd {
-    int32_t n_groups;
-    const int64_t* goff_host;
-    const int* npart;
-    int pstride;
-    float* params;
-    float* grads;
-    const float* part;
-    float max_norm, lr;
-    unsigned long long* bar;     // grid-barrier counter (device, never reset)
-    unsigned long long* bar_gen; // host copy: arrivals so far
-    int* bar_err;                // set when a barrier wait gave up (device)
-};
-// sum_slabs_pair_launch, a grid barrier, then the clip + SGD in the same
-// launch (one dependent kernel boundary and the SGD's own launch fewer).
-int sum_slabs_pair_sgd_launch(const SlabSum& s1, const SlabSum& s2, int np_before, const FusedSgd& u,
-                              hipStream_t st);
 int sum_slabs_grid(int64_t len);
 
 // agg.hip: the runner's layer-1 gather in two launches (resolve, then rows)
@@ -194,19 +158,7 @@ struct BwdA {
     float* loss;
     float* cls_part;
 };
-struct BwdMoved {
-    BwdA a;
-    int cls_nb = 0;
-};
-int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st,
-                  BwdMoved* moved = nullptr);
-// With `moved` (GS_DW_PLUS=1) layer_bwd_top launches only the agg backward and
-// leaves its dW_2 slab and classifier-reduce roles here, for the layer-1 dW
-// launch (dw1_plus_launch: fp32, self rows, 16-B aligned; -1 = not taken,
-// else the slab count; the slabs go to ws).
-int dw1_plus_launch(int64_t n, int64_t F, int64_t H, const float* Xs, int64_t ldxs, const int32_t* sidx,
-                    const float* A, int64_t lda, const float* dout, int64_t ldo, float* dW, void* ws,
-                    int64_t ws_bytes, const BwdMoved& mv, hipStream_t st);
+int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hipStream_t st);
 
 bool layer_bwd_fusable(const LayerBwd& a);
 int cls_reduce_grid(int64_t C, int64_t D);

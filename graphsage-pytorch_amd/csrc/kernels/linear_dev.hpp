@@ -323,10 +323,12 @@ __device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, 
     return true;
 }
 
+// W is not __restrict__: with PEND a recomputed W1 is written into W's buffer
+// (sp.Wn) and read back through W by the second K loop.
 template <typename T, int ROWS, bool HAS_SELF, bool RELU, bool PEND = false>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
-    const T* __restrict__ A, int64_t lda, const T* __restrict__ W, float* __restrict__ out, int64_t ldo,
+    const T* __restrict__ A, int64_t lda, const T* W, float* __restrict__ out, int64_t ldo,
     FwdSpec sp) {
     kstamp_begin(sp.stamp);
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
@@ -452,183 +454,6 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         }
     }
     kstamp_end(sp.stamp);
-}
-
-// Forward, fp32, split-K inside the block ("sk").  Block = 16 rows x 32
-// output columns, 4 waves; wave w owns K quarter w for both 16-column tiles
-// and issues all of that quarter's A and W slots (up to kSkChunks chunks of 64)
-// before its first MFMA, so a wave waits through one load round, not one per
-// chunk.  The four partial tiles are added in LDS in wave order (fixed, no
-// atomics) and wave 0 applies relu and stores.  Many small blocks (n/16 ·
-// H/32) keep ~4 waves per SIMD to overlap those rounds.
-constexpr int kSkChunks = 2;  // chunks of 64 per wave issued at once (K <= 512 in one round)
-// W-resident forward (fp32, K a multiple of 256 up to 512: a row of the slice
-// is whole 64-quad DMA instructions): each block keeps one 32-column slice of W
-// ([32][K] fp32, <= 64 KiB) in LDS for its whole life, filled by
-// LDS-DMA (global_load_lds_dwordx4) with quad-swizzled rows (quad q of row c
-// in slot q ^ (c & 15): the per-MFMA b128 reads of 16 rows hit 16 distinct
-// slots), and each of its 4 waves runs one 16-row tile against both 16-column
-// halves of the slice (two interleaved accumulators), streaming its A rows
-// [X[sidx] | A] from global memory kWresAhead 64-k chunks ahead in registers.
-// No workgroup barrier after the fill: the K loop reads only its own
-// registers and the (read-only) W slice.  MFMA operands and order are the
-// chunked / wide kernels' (mfma_slot over slots 4g + kq, chunks ascending), so
-// the output is bitwise theirs.  Grid: (ceil(tiles / 4), H / 32); two blocks
-// fit a CU.  Blocks y (slices) of one x share an XCD (x-major dispatch of a
-// 2-D grid keeps them 1 apart in linear order; see the launcher's remap).
-constexpr int kWresAhead = 4;
-constexpr int kWresCols = 32;
-
-template <bool HAS_SELF, bool RELU>
-__global__ __launch_bounds__(kThreads) void linear_fwd_wres_kernel(
-    int n, int F, int H, int K, int n_tiles_x, const float* __restrict__ Xs, int64_t ldxs,
-    const int* __restrict__ sidx, const float* __restrict__ A, int64_t lda, const float* __restrict__ W,
-    float* __restrict__ out, int64_t ldo) {
-    extern __shared__ uint4 sWq[];  // [kWresCols][K / 4] quads, swizzled
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // linear block id -> (row-tile group, slice): the H/32 slices of one
-    // group are 8 apart in dispatch order, i.e. on one XCD (round-robin)
-    const int nsl = H / kWresCols;
-    const int b = blockIdx.x;
-    const int sl = (b >> 3) % nsl;
-    const int tg = (b & 7) + 8 * (b / (8 * nsl));
-    const int KQ = K >> 2;
-    const int r = lane & 15, kq = lane >> 4;
-    const int tile = tg * 4 + wave;
-    if (tg >= n_tiles_x) return;  // padding block of the remap (block-uniform: no barrier skipped)
-    const int row = min(tile * 16 + r, n - 1);
-    const int srow_i = HAS_SELF ? (sidx ? sidx[row] : row) : 0;
-    // fill the slice: row c is KQ / 64 wave instructions of 64 quads
-    const int per_row = KQ >> 6;
-    for (int i = wave; i < kWresCols * per_row; i += kThreads / 64) {
-        const int c = i / per_row, part = i - c * per_row;
-        const int qsrc = (part * 64 + lane) ^ (c & 15);
-        const int gc = min(sl * kWresCols + c, H - 1);
-        __builtin_amdgcn_global_load_lds(W + static_cast<int64_t>(gc) * K + 4 * qsrc, sWq + c * KQ + part * 64, 16,
-                                         0, 0);
-    }
-    const float* arow = A + static_cast<int64_t>(row) * lda;
-    const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(srow_i) * ldxs : nullptr;
-    const int nC = K >> 6;
-    uint4 ar[kWresAhead][4];
-    auto load = [&](int c, uint4 (&dst)[4]) {
-        const int kn = min(c, nC - 1) * 64;  // past the end: re-read the last chunk (unused)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, kn + 4 * (4 * g + kq));
-    };
-#pragma unroll
-    for (int u = 0; u < kWresAhead; ++u) load(u, ar[u]);
-    __builtin_amdgcn_s_waitcnt(0);  // the fill (and the first chunks) landed for this wave
-    __syncthreads();                // ... and for every wave
-    if (tile * 16 >= n) return;
-    const int c0 = r, c1 = 16 + r;  // this lane's W rows (output columns) within the slice
-    const uint4* w0 = sWq + c0 * KQ;
-    const uint4* w1 = sWq + c1 * KQ;
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    for (int c = 0; c < nC; c += kWresAhead) {
-#pragma unroll
-        for (int u = 0; u < kWresAhead; ++u) {
-            const int cc = c + u;
-            if (cc >= nC) break;
-            uint4 av[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) av[g] = ar[u][g];
-            load(cc + kWresAhead, ar[u]);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int q = cc * 16 + 4 * g + kq;
-                const uint4 b0 = w0[q ^ (c0 & 15)];
-                const uint4 b1 = w1[q ^ (c1 & 15)];
-                const float a4[4] = {__uint_as_float(av[g].x), __uint_as_float(av[g].y), __uint_as_float(av[g].z),
-                                     __uint_as_float(av[g].w)};
-                const float x0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
-                                     __uint_as_float(b0.w)};
-                const float x1[4] = {__uint_as_float(b1.x), __uint_as_float(b1.y), __uint_as_float(b1.z),
-                                     __uint_as_float(b1.w)};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {  // = mfma_slot's order on each accumulator
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], x0[j], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], x1[j], acc1, 0, 0, 0);
-                }
-            }
-        }
-    }
-    const int col0 = sl * kWresCols + r, col1 = col0 + 16;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int orow = tile * 16 + 4 * kq + j;
-        if (orow >= n) continue;
-        const float v0 = acc0[j], v1 = acc1[j];
-        if (col0 < H) out[static_cast<int64_t>(orow) * ldo + col0] = (RELU && !(v0 > 0.f) && v0 == v0) ? 0.f : v0;
-        if (col1 < H) out[static_cast<int64_t>(orow) * ldo + col1] = (RELU && !(v1 > 0.f) && v1 == v1) ? 0.f : v1;
-    }
-}
-
-template <bool HAS_SELF, bool RELU>
-__global__ __launch_bounds__(kThreads) void linear_fwd_sk_kernel(
-    int n, int F, int H, int K, const float* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
-    const float* __restrict__ A, int64_t lda, const float* __restrict__ W, float* __restrict__ out, int64_t ldo) {
-    __shared__ f32x4 red[3][2][64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 15, kq = lane >> 4;
-    const int m0 = blockIdx.x * 16, c0 = blockIdx.y * 32;
-    const int row_i = min(m0 + r, n - 1);
-    const float* arow = A + static_cast<int64_t>(row_i) * lda;
-    const float* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[row_i] : row_i) * ldxs : nullptr;
-    const float* w0 = W + static_cast<int64_t>(min(c0 + r, H - 1)) * K;
-    const float* w1 = W + static_cast<int64_t>(min(c0 + 16 + r, H - 1)) * K;
-    const int nC = (K + 63) / 64;
-    const int cq = (nC + 3) / 4;  // chunks per quarter
-    const int cb = wave * cq, ce = min(nC, cb + cq);
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    for (int c = cb; c < ce; c += kSkChunks) {
-        uint4 a[kSkChunks][4], b0[kSkChunks][4], b1[kSkChunks][4];
-#pragma unroll
-        for (int u = 0; u < kSkChunks; ++u) {
-            const int k0 = min(c + u, ce - 1) * 64;  // a chunk past the quarter re-reads the last one (masked below)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int k = k0 + (4 * g + kq) * 4;
-                a[u][g] = concat_slot<float, HAS_SELF, true>(srow, arow, F, K, k);
-                b0[u][g] = concat_slot<float, false, true>(nullptr, w0, K, K, k);
-                b1[u][g] = concat_slot<float, false, true>(nullptr, w1, K, K, k);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kSkChunks; ++u) {
-            if (c + u >= ce) break;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                acc0 = mfma_slot<float>(a[u][g], b0[u][g], acc0);
-                acc1 = mfma_slot<float>(a[u][g], b1[u][g], acc1);
-            }
-        }
-    }
-    if (wave > 0) {
-        red[wave - 1][0][lane] = acc0;
-        red[wave - 1][1][lane] = acc1;
-    }
-    __syncthreads();
-    if (wave > 0) return;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        acc0 += red[q][0][lane];
-        acc1 += red[q][1][lane];
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int col = c0 + 16 * t + r;
-        if (col >= H) continue;
-        const f32x4 v4 = t ? acc1 : acc0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int row = m0 + 4 * kq + j;
-            if (row < n) {
-                const float v = v4[j];
-                out[static_cast<int64_t>(row) * ldo + col] = (RELU && !(v > 0.f) && v == v) ? 0.f : v;
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------------ weight grad
@@ -789,94 +614,6 @@ __global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
                                                    lda, dout, out, ldo, dst, split_stride);
 }
 
-// The XCD-grouped row slabs.  The slab sum adds the S slabs in kSlabParts
-// groups of P = ceil(S / kSlabParts) consecutive slabs, each from zero in slab
-// order, then the group sums in group order (sum_slabs_body below).  Here the
-// groups are formed inside the launch: group q's slabs [qP, qP + P) are given
-// to workgroups w with w % 8 == q (one XCD under round-robin placement, so a
-// group's slabs are written and re-read in one L2), and of the P workgroups
-// of one tile the last to finish (an arrival counter per (group, tile),
-// agent-scope release by every writer, acquire by the last one) adds the
-// group's P slab tiles from zero in slab order into gpart[q].  The slab sum
-// then reads NG = ceil(S / P) <= 8 group partials instead of S slabs: with
-// one "slab" per group its order is exactly the two-level order above, so the
-// gradients are bitwise those of the ungrouped launch.  A different placement
-// changes only speed, never the result.  Counters start at zero (the trainer
-// zeroes them once) and the reducer resets its own.  Needs K % 4 == 0.
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
-__global__ __launch_bounds__(kThreads) void linear_dw_grp_kernel(
-    int n, int F, int H, int K, int rows_per_split, int gx, int tiles, int S, int P, const T* __restrict__ Xs,
-    int64_t ldxs, const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda,
-    const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo, float* __restrict__ dst,
-    int64_t split_stride, float* __restrict__ gpart, int* __restrict__ cnt) {
-    __shared__ int s_last;
-    const int w = blockIdx.x;
-    const int q = w % kXcds, j = w / kXcds;
-    const int m = j / tiles, t = j % tiles;
-    const int g0 = q * P;
-    const int z = g0 + m;
-    if (m >= P || z >= S) return;
-    linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx, A,
-                                                   lda, dout, out, ldo, dst, split_stride);
-    // publish this slab tile (guide recipe: drain, barrier, one release, ticket)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int gs = min(P, S - g0);
-    if (threadIdx.x == 0) {
-        int* c = cnt + q * tiles + t;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == gs - 1;
-        if (last) {
-            __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // the group's tile: 64 rows x 16 float4 columns, 4 per thread; every
-    // slab's loads of a round issued before any add (clamped addresses, the
-    // selects after the loads)
-    const int k0 = (t % gx) * 64, h0 = (t / gx) * 64;
-    constexpr int kE = 64 * 16 / kThreads;
-    int64_t off[kE];
-    bool ok[kE];
-#pragma unroll
-    for (int i = 0; i < kE; ++i) {
-        const int e = threadIdx.x + i * kThreads;
-        const int h = h0 + (e >> 4), k = k0 + (e & 15) * 4;
-        ok[i] = h < H && k < K;
-        off[i] = ok[i] ? static_cast<int64_t>(h) * K + k : 0;
-    }
-    float4 s[kE];
-#pragma unroll
-    for (int i = 0; i < kE; ++i) s[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    constexpr int kU = 4;
-    for (int u0 = 0; u0 < gs; u0 += kU) {
-        float4 v[kU][kE];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const float* sl = dst + static_cast<int64_t>(g0 + min(u0 + u, gs - 1)) * split_stride;
-#pragma unroll
-            for (int i = 0; i < kE; ++i) v[u][i] = *reinterpret_cast<const float4*>(sl + off[i]);
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (u0 + u >= gs) break;
-#pragma unroll
-            for (int i = 0; i < kE; ++i) {
-                s[i].x += v[u][i].x; s[i].y += v[u][i].y; s[i].z += v[u][i].z; s[i].w += v[u][i].w;
-            }
-        }
-    }
-    float* gp = gpart + static_cast<int64_t>(q) * split_stride;
-#pragma unroll
-    for (int i = 0; i < kE; ++i)
-        if (ok[i]) *reinterpret_cast<float4*>(gp + off[i]) = s[i];
-}
 
 // out[i] = Σ_s slabs[s][i] in one fixed order shared by every slab-sum
 // kernel: the S slabs fall into kSlabParts consecutive groups of
@@ -1025,11 +762,7 @@ __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
 // fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
 constexpr int kDwTargetBlocks = 512;  // two blocks per CU (measured best of 256 / 512 / 1024 in the step)
 
-inline int dw_target_blocks() {  // GS_DW_BLOCKS: measurement override
-    static const int v = std::getenv("GS_DW_BLOCKS") ? std::max(1, std::atoi(std::getenv("GS_DW_BLOCKS")))
-                                                       : kDwTargetBlocks;
-    return v;
-}
+inline int dw_target_blocks() { return kDwTargetBlocks; }
 
 inline int dw_rows_per_split(int64_t n, int64_t K, int64_t H) {
     const int64_t tiles = ((K + 63) / 64) * ((H + 63) / 64);

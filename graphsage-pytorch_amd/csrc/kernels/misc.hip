@@ -436,7 +436,7 @@ void sgd_with_parts(int32_t n_groups, const int64_t* goff_host, const int* npart
     G.sh = sh.p;
     G.sh_lo = sh.lo;
     G.sh_hi = sh.hi;
-    bool vec = aligned16(params) && aligned16(grads) && std::getenv("GS_SGD_SCALAR") == nullptr;
+    bool vec = aligned16(params) && aligned16(grads);
     for (int i = 0; i <= n_groups; ++i) vec = vec && G.off[i] % 4 == 0;
     vec = vec && (!sh.p || (sh.lo % 4 == 0 && sh.hi % 4 == 0 && reinterpret_cast<uintptr_t>(sh.p) % 8 == 0));
     if (vec) {  // 4.9 us -> see DESIGN §4 (rmat2m, ~100k parameters)

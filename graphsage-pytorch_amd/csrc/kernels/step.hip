@@ -18,8 +18,6 @@ struct gs_trainer {
     std::vector<int64_t> w_off;  // element offset of each parameter in the flat buffer
     std::vector<int64_t> w_rows, w_cols;
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
-    bool fused1 = false;  // layer 1 through gs_sage1_fwd (gather + linear in one launch)
-    bool fused2 = false;  // layers >= 2 likewise (explicit lists; MEAN)
     // optional kernel-bound HIP-event timing (bench roofline): site 0 the
     // layer-1 gather-aggregate, 1 the layer-1 linear forward, 2 its weight
     // gradient (the MFMA kernels), 3 the fused top layer + loss head (top.hip)
@@ -43,10 +41,11 @@ struct gs_trainer {
     static constexpr int kSlots = 3;
     void* a1_slot[kSlots] = {};
     int64_t a1_rows = 0;
-    // GS_SELF_ROWS (default on, "0" off; read at gs_trainer_gather_reserve): each gather slot is
-    // [self | agg] rows of 2F; the side-stream gather also copies the layer-1
-    // rows' own features, so the layer-1 forward and dW read one dense block
-    // (no self-index round).  self_in_slot: the slot's self half was written.
+    // Each gather slot is [self | agg] rows of 2F (option GS_TOPT_SELF_ROWS,
+    // default on; applied at gs_trainer_gather_reserve): the side-stream gather
+    // also copies the layer-1 rows' own features, so the layer-1 forward and dW
+    // read one dense block (no self-index round).  self_in_slot: the slot's self
+    // half was written.
     bool self_rows = false;
     bool self_in_slot[kSlots] = {};
     // per slot, the layer-1 neighbour ids resolved ahead of the gather
@@ -61,8 +60,11 @@ struct gs_trainer {
     // clip-norm partials produced by the fused backward's reduce launches
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
-    bool fuse_bwd = true;
-    bool use_top = true;  // GS_NO_TOP=1: layer 2 + loss head as separate launches (A/B)
+    // gs_trainer_set_option switches (bitwise-equal alternatives the tests compare)
+    bool fuse_bwd = true;    // GS_TOPT_FUSED_BWD: layers >= 2 backward in fused launches
+    bool use_top = true;     // GS_TOPT_TOP_LAUNCH: layer 2 + loss head + dIn2 in one launch
+    bool want_self_rows = true;  // GS_TOPT_SELF_ROWS
+    bool opt_defer = true;   // GS_TOPT_DEFER_UPDATE: runner loops defer each clip + SGD
     float* norm_part = nullptr;
     int pstride = 0;
     int npart[2] = {0, 0};
@@ -70,24 +72,12 @@ struct gs_trainer {
     std::function<void(hipStream_t)> upper_hook;  // internal.hpp trainer_set_upper_hook
     std::function<void(hipStream_t, int64_t, int64_t)> w1_chunk_hook;  // trainer_set_w1_chunk_hook
     int w1_chunks = 1;
-    std::function<void(hipStream_t)> fwd1_hook;   // after the layer-1 forward launch (trainer_set_fwd1_hook)
     // bf16 features: W1 in bf16 for the layer-1 forward.  Cast from the fp32
     // W1 before a forward, except inside a runner loop (lp_keep), where the
     // SGD launch writes it beside W1 (g_lowp_shadow) and it stays valid from
     // one step to the next: nothing else writes the parameters there.
     uint16_t* w1_lp = nullptr;
     bool lp_keep = false, lp_valid = false;
-    // Inside a runner loop without an all-reduce (fuse_update): the step's
-    // last slab sum also runs the clip + SGD (sum_slabs_pair_sgd_launch) and
-    // gs_trainer_update_local then has nothing left to do (update_done).
-    bool fuse_update = false, update_done = false;
-    unsigned long long* bar = nullptr;  // its grid-barrier counter (device) and arrivals so far
-    unsigned long long bar_gen = 0;
-    int* bar_err = nullptr;
-    // arrival counters of the grouped layer-1 weight-gradient launch (zeroed once;
-    // each group's reducer resets its own), kDwGroupParts per 64x64 tile of W1
-    int* dw_cnt = nullptr;
-    int64_t dw_n_cnt = 0;
     // Deferred update (trainer_defer_update, runner loops without an
     // all-reduce): a step's clip + SGD is not a launch of its own.  The step's
     // last slab sum writes W1's update for clip coefficient 1 into the other
@@ -112,13 +102,22 @@ struct gs_trainer {
     // is current while deferring: the slab sum and the recompute write both)
     uint16_t* w1_lp_alt = nullptr;
     uint16_t* lp_buf(int i) { return i == 0 ? w1_lp : w1_lp_alt; }
+    // Parity capture (gs_trainer_capture; tests only): after each training
+    // step's launches, the step's root embeddings (the top layer's output) and
+    // the flat gradient as the step left it (before its clip + SGD) are copied
+    // on the step's stream into caller buffers.
+    struct Capture {
+        float* emb = nullptr;
+        int64_t emb_stride = 0;
+        float* grads = nullptr;
+        int64_t max_steps = 0, n = 0;
+    } cap;
+    const float* last_emb = nullptr;  // the last run_step's [B, H] top-layer output
     ~gs_trainer() {
         if (w1_alt) (void)hipFree(w1_alt);
         if (w1_lp_alt) (void)hipFree(w1_lp_alt);
         if (norm_part) (void)hipFree(norm_part);
-        if (dw_cnt) (void)hipFree(dw_cnt);
         if (w1_lp) (void)hipFree(w1_lp);
-        if (bar) (void)hipFree(bar);
         for (auto& tm : timer) {
             for (auto e : tm.ev0) (void)hipEventDestroy(e);
             for (auto e : tm.ev1) (void)hipEventDestroy(e);
@@ -170,12 +169,8 @@ static inline bool timed_arm(gs_trainer& T, int site) {
 }
 // Timer events only measure: no system-scope release when they complete (a
 // system-scope release writes back and invalidates the caches under the work
-// that follows, which is what made event-bound launches cost the step
-// time).  GS_TIMER_SYSFENCE=1 restores the default events for A/B runs.
-static unsigned timer_event_flags() {
-    static const bool sysfence = std::getenv("GS_TIMER_SYSFENCE") != nullptr;
-    return sysfence ? hipEventDefault : hipEventDisableSystemFence;
-}
+// that follows, which is what made event-bound launches cost the step time).
+static unsigned timer_event_flags() { return hipEventDisableSystemFence; }
 
 static std::string demangle(const char* sym) {
     if (!sym) return "?";
@@ -302,6 +297,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         }
         else agg[l - 1] = cv.take<float>(rows[l - 1] * H);
         h[l - 1] = (embed_out && l == L) ? embed_out : cv.take<float>(rows[l - 1] * H);
+        if (l == L) T.last_emb = h[l - 1];
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
     }
     float* demb = cv.take<float>(B * H);
@@ -315,8 +311,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         }
     }
     char* dw_ws = cv.take<char>(dw_need);
-    // the layer-1 weight gradient's group partials (linear_dw_grp_kernel)
-    float* dw_gpart = cv.take<float>(kDwGroupParts * H * T.w_cols[0]);
     // the fused top path's dW_2 slabs outlive the layer-1 dW (their sum runs with layer 1's)
     const int64_t dw2_need = L == 2 ? gs_sage_linear_bwd_weight_ws(rows[1], T.w_cols[1], H) : 0;
     char* dw2_ws = dw2_need > 0 ? cv.take<char>(dw2_need) : nullptr;
@@ -355,11 +349,14 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         }
     }
     const void* W1 = lowp ? static_cast<const void*>(T.w1_lp) : static_cast<const void*>(P + T.w_off[0]);
-    const bool fused1 = T.fused1 && a1_slot < 0;
-    GS_REQUIRE(!T.defer || (!fused1 && !embed_out), GS_EINVAL, "deferred update: unsupported step");
+    GS_REQUIRE(!T.defer || !embed_out, GS_EINVAL, "deferred update: unsupported step");
     bool pend = T.defer && T.pending;
-    if (pend && !(T.pend_np[0] >= 1 && T.pend_np[0] <= 512 && T.pend_np[1] >= 1 && T.pend_np[1] <= 512)) {
-        // the forward folds at most 512 partials per group: apply the update on its own
+    if (pend && !(T.pend_np[0] >= 1 && T.pend_np[0] <= 512 && T.pend_np[1] >= 1 && T.pend_np[1] <= 512 &&
+                  linear_fwd_wide_ok(static_cast<gs_dtype>(c.feat_dtype), F, x1, ldx1, a1, lda1,
+                                     lowp ? static_cast<const void*>(T.lp_buf(T.w1_cur ^ 1))
+                                          : static_cast<const void*>(T.w1_buf(T.w1_cur ^ 1))))) {
+        // the forward folds at most 512 partials per group, and only the wide
+        // (16-B load) forward applies a pending update: apply it on its own
         trainer_defer_update(&T, false, st);
         trainer_defer_update(&T, true, st);
         pend = false;
@@ -393,16 +390,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             g_fwd_spec = sp;
         }
     }
-    if (fused1) {  // gather + concat-linear in one launch (kernels/sage1.hip)
-        const bool timed = timed_arm(T, 0);
-        ok(gs_sage1_fwd(static_cast<gs_agg>(c.agg), static_cast<gs_dtype>(c.feat_dtype), c.X, c.feat_ld, F, H,
-                        rows[0], fld(L, GS_PK_POS_PTR), fld(L, GS_PK_POS), c.col, dst_L, c.gcn, W1, agg[0], F, h[0],
-                        H, 1, st));
-        timed_done(T, 0, timed);
-    } else if (a1_slot < 0) {
-        gather1(T, pack, hop_sizes, offsets, agg[0], st);
-    }
-    if (!fused1) {
+    if (a1_slot < 0) gather1(T, pack, hop_sizes, offsets, agg[0], st);
+    {
         const bool armed = timed_arm(T, 1);
         ok(gs_sage_linear_fwd(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1, lda1, W1, h[0],
                               H, 1, st));
@@ -413,7 +402,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             T.w1_cur ^= 1;
             T.pending = false;
         }
-        if (T.fwd1_hook && !embed_out) T.fwd1_hook(st);
     }
     // a 2-layer training step runs layer 2, the loss head and layer 2's dIn in
     // one launch (top.hip) inside the fused backward below
@@ -421,12 +409,6 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                      top_supported(H, c.n_classes, c.gcn != 0);
     for (int l = 2; l <= L && !top; ++l) {
         const int j = L - l + 1;
-        if (T.fused2 && c.agg == GS_AGG_MEAN) {  // MAX needs the argmax the fused kernel does not keep
-            ok(gs_sage1_fwd(GS_AGG_MEAN, GS_F32, h[l - 2], H, H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
-                            fld(j, GS_PK_NBR), nullptr, fld(j, GS_PK_SELF), c.gcn, P + T.w_off[l - 1], agg[l - 1], H,
-                            h[l - 1], H, 1, st));
-            continue;
-        }
         ok(gs_agg_fwd(static_cast<gs_agg>(c.agg), GS_F32, h[l - 2], H, H, rows[l - 1], fld(j, GS_PK_NBR_PTR),
                       fld(j, GS_PK_NBR), nullptr, nullptr, nullptr, 0, agg[l - 1], GS_F32, H, am[l - 1], st));
         ok(gs_sage_linear_fwd(GS_F32, rows[l - 1], H, H, c.gcn ? nullptr : h[l - 2], H, fld(j, GS_PK_SELF),
@@ -473,8 +455,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             int cls_rows;
             if (top) {
                 const bool armed = timed_arm(T, 3);
-                static const bool no_tids = std::getenv("GS_TOP_NO_TIDS") != nullptr;  // A/B: the pack's lists
-                const bool tids = !no_tids && a1_slot >= 0 && T.top_ready[a1_slot];
+                const bool tids = a1_slot >= 0 && T.top_ready[a1_slot];
                 cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
                                        fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
                                        roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st,
@@ -490,22 +471,14 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             const int64_t K1 = T.w_cols[0];
             // top path, 2 layers, no bucketed all-reduce hook: one backward launch for
             // layer 2 and its slab sum beside layer 1's (same sums, partials, order)
-            static const bool split_b = std::getenv("GS_BWD_SPLIT_B") != nullptr;  // A/B: launches A + B
-            const bool defer = top && lb.size() == 1 && !T.upper_hook && !split_b && dw2_ws &&
-                               sum_slabs_pair_ok(H * K1);
+            const bool defer = top && lb.size() == 1 && !T.upper_hook && dw2_ws && sum_slabs_pair_ok(H * K1);
             int np = 0;
             bool parts = true;
             SlabSum d2{};
-            // GS_DW_PLUS=1 (A/B): the dW_2 slabs and the classifier reduce move from
-            // the layer-2 backward launch into the layer-1 dW launch (dw1_plus_launch)
-            const char* dw_plus_s = std::getenv("GS_DW_PLUS");  // read per step (tests switch it)
-            const bool dw_plus_env = dw_plus_s && std::string(dw_plus_s) == "1";
-            const bool dw_plus = defer && dw_plus_env && !lowp && !c.gcn && !T.w1_chunk_hook;
-            BwdMoved moved{};
             if (defer) {
                 lb[0].slabs = reinterpret_cast<float*>(dw2_ws);
                 lb[0].slab_bytes = dw2_need;
-                np = layer_bwd_top(lb[0], cr, &d2, st, dw_plus ? &moved : nullptr);
+                np = layer_bwd_top(lb[0], cr, &d2, st);
                 parts = np > 0;
             } else {
                 for (size_t i = 0; i < lb.size(); ++i) {
@@ -526,7 +499,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                     float* dWq = G + T.w_off[0] + h0 * K1;
                     const int Sq = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, Hc, x1, ldx1,
                                                    sidx1, a1, lda1, lb.back().dH + h0, h[0] + h0, H, 0, dWq, dw_ws,
-                                                   dw_need, st, nullptr, H);
+                                                   dw_need, st, H);
                     if (Sq > 1) sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), Sq, Hc * K1, dWq, nullptr, st);
                     T.w1_chunk_hook(st, T.w_off[0] + h0 * K1, Hc * K1);
                 }
@@ -537,44 +510,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 return cv.at;
             }
             const bool armed = timed_arm(T, 2);
-            DwGroups grp{T.dw_cnt, T.dw_n_cnt, dw_gpart};
-            int S1 = -1;
-            if (dw_plus) {
-                S1 = dw1_plus_launch(rows[0], F, H, static_cast<const float*>(x1), ldx1, sidx1,
-                                     static_cast<const float*>(a1), lda1, lb.back().dH, H, G + T.w_off[0], dw_ws,
-                                     dw_need, moved, st);
-                GS_REQUIRE(S1 > 1, GS_EINVAL, "GS_DW_PLUS: the layer-1 dW launch could not take the moved roles");
-                grp.slabs = reinterpret_cast<const float*>(dw_ws);
-                grp.S = S1;
-            } else {
-                S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1, lda1,
-                                     lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws, dw_need, st, &grp);
-            }
+            const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1,
+                                           lda1, lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws, dw_need, st);
             g_launch_events = {};
             timed_done(T, 2, armed);
-            // what the slab sum adds: the group partials (bitwise the same sums) or the slabs
-            const float* s1_src = S1 > 1 ? grp.slabs : nullptr;
-            const int s1_n = S1 > 1 ? grp.S : S1;
+            const float* s1_src = S1 > 1 ? reinterpret_cast<const float*>(dw_ws) : nullptr;
+            const int s1_n = S1;
             const int n_cls = cls_reduce_grid(c.n_classes, H);
-            if (defer && S1 > 1 && T.fuse_update && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
-                n_cls <= T.pstride) {
-                // the clip + SGD in the same launch (gs_trainer_update_local's work)
-                d2.part = T.norm_part;
-                const int64_t goff[3] = {0, T.cls_w_off, T.total};
-                const int npart[2] = {0, n_cls};
-                const FusedSgd u{2, goff, npart, T.pstride, P, G, T.norm_part, c.max_norm, c.lr, T.bar, &T.bar_gen,
-                                 T.bar_err};
-                T.lp_valid = false;
-                if (T.lp_keep && T.w1_lp)
-                    g_lowp_shadow = {T.w1_lp, T.w_off[0], T.w_off[0] + T.w_rows[0] * T.w_cols[0]};
-                sum_slabs_pair_sgd_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np},
-                                          d2, np, u, st);
-                g_lowp_shadow = {};
-                T.lp_valid = T.lp_keep && T.w1_lp;
-                T.update_done = true;
-                T.norm_ready = false;
-                return cv.at;
-            }
             if (defer && S1 > 1) {
                 d2.part = T.norm_part;
                 // deferred update: this launch also writes W1's update for clip
@@ -641,6 +583,23 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     return cv.at;
 }
 
+// The parity capture of one finished training step (gs_trainer_capture).
+static void capture_step(gs_trainer& T, int64_t B, hipStream_t st) {
+    auto& c = T.cap;
+    if (c.n >= c.max_steps || (!c.emb && !c.grads)) return;
+    if (c.emb) {
+        GS_REQUIRE(B * T.cfg.hidden <= c.emb_stride, GS_EINVAL, "capture: batch larger than the embedding stride");
+        GS_REQUIRE(hipMemcpyAsync(c.emb + c.n * c.emb_stride, T.last_emb, B * T.cfg.hidden * sizeof(float),
+                                  hipMemcpyDeviceToDevice, st) == hipSuccess,
+                   GS_EHIP, "hipMemcpyAsync(capture)");
+    }
+    if (c.grads)
+        GS_REQUIRE(hipMemcpyAsync(c.grads + c.n * T.total, T.cfg.grads, T.total * sizeof(float),
+                                  hipMemcpyDeviceToDevice, st) == hipSuccess,
+                   GS_EHIP, "hipMemcpyAsync(capture)");
+    ++c.n;
+}
+
 void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->upper_hook = std::move(hook); }
 void trainer_set_w1_chunk_hook(gs_trainer* t, int chunks, std::function<void(hipStream_t, int64_t, int64_t)> hook) {
     t->w1_chunks = hook ? std::max(1, chunks) : 1;
@@ -660,7 +619,6 @@ void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk) {
     t->top_rows = B;
     t->top_k = tk;
 }
-void trainer_set_fwd1_hook(gs_trainer* t, std::function<void(hipStream_t)> hook) { t->fwd1_hook = std::move(hook); }
 
 int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols[0]; }
 
@@ -686,10 +644,6 @@ void trainer_keep_lowp(gs_trainer* t, bool keep) {
     t->lp_valid = false;
 }
 
-void trainer_fuse_update(gs_trainer* t, bool fuse) {
-    t->fuse_update = fuse;
-    t->update_done = false;
-}
 
 // W1 back in the flat params (a pending update stays pending: its S and P
 // buffers are then the flat W1 and w1_alt, or it is finalised by the caller).
@@ -735,9 +689,14 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st, bool comm) {
     }
     const gs_trainer_config& c = t->cfg;
     const int64_t n1 = t->w_rows[0] * t->w_cols[0];
-    const bool ok = (c.feat_dtype == GS_F32 || (c.feat_dtype == GS_BF16 && t->w1_lp)) && !t->fused1 && t->fuse_bwd &&
-                    t->use_top && c.n_layers == 2 && !c.gcn && !t->fuse_update &&
+    // the pending update is applied by the wide (16-B load) layer-1 forward:
+    // its feature rows must take 16-B loads (run_step re-checks each step's
+    // operands and applies the update on its own where they do not)
+    const int64_t epv = c.feat_dtype == GS_F32 ? 4 : 8;
+    const bool ok = t->opt_defer && (c.feat_dtype == GS_F32 || (c.feat_dtype == GS_BF16 && t->w1_lp)) &&
+                    t->fuse_bwd && t->use_top && c.n_layers == 2 && !c.gcn &&
                     (comm || (!t->upper_hook && !t->w1_chunk_hook)) && n1 % 4 == 0 &&
+                    c.feat_dim % epv == 0 && c.feat_ld % epv == 0 && aligned16(c.X) &&
                     t->cls_w_off % 4 == 0 && t->total % 4 == 0 && aligned16(c.params) && aligned16(c.grads);
     if (!ok) return false;
     if (!t->w1_alt)
@@ -752,12 +711,6 @@ bool trainer_defer_update(gs_trainer* t, bool on, hipStream_t st, bool comm) {
     return true;
 }
 
-bool trainer_barrier_failed(gs_trainer* t) {
-    int e = 0;
-    if (hipMemcpy(&e, t->bar_err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-        fail(GS_EHIP, "hipMemcpy(barrier flag)");
-    return e != 0;
-}
 }  // namespace gs
 
 extern "C" {
@@ -799,26 +752,7 @@ int gs_trainer_create(const gs_trainer_config* cfg, gs_trainer** out) {
             delete T;
             gs::fail(GS_ENOMEM, "hipMalloc(bf16 W1)");
         }
-        if (hipMalloc(&T->bar, 16) != hipSuccess || hipMemset(T->bar, 0, 16) != hipSuccess) {
-            delete T;
-            gs::fail(GS_ENOMEM, "hipMalloc(barrier)");
-        }
-        T->bar_err = reinterpret_cast<int*>(T->bar + 1);
-        T->dw_n_cnt = gs::kDwGroupParts * ((T->w_cols[0] + 63) / 64) * ((cfg->hidden + 63) / 64);
-        if (hipMalloc(&T->dw_cnt, T->dw_n_cnt * sizeof(int)) != hipSuccess ||
-            hipMemset(T->dw_cnt, 0, T->dw_n_cnt * sizeof(int)) != hipSuccess) {
-            delete T;
-            gs::fail(GS_ENOMEM, "hipMalloc(dW group counters)");
-        }
     }
-    T->fuse_bwd = std::getenv("GS_NO_FUSED_BWD") == nullptr;
-    T->use_top = std::getenv("GS_NO_TOP") == nullptr;
-    T->fused1 = gs_sage1_fwd_supported(static_cast<gs_dtype>(cfg->feat_dtype), cfg->feat_dim, cfg->hidden,
-                                       cfg->gcn) != 0 &&
-                cfg->feat_ld % (cfg->feat_dtype == GS_F32 ? 4 : 8) == 0 && gs::aligned16(cfg->X) &&
-                std::getenv("GS_FUSED1") != nullptr;  // opt-in: measured slower than agg + linear
-    T->fused2 = gs_sage1_fwd_supported(GS_F32, cfg->hidden, cfg->hidden, cfg->gcn) != 0 &&
-                std::getenv("GS_FUSED2") != nullptr;  // opt-in: measured slower than agg + linear
     *out = T;
     GS_API_END
 }
@@ -829,7 +763,20 @@ int64_t gs_trainer_n_params(const gs_trainer* t) { return t ? t->total : -1; }
 
 float* gs_trainer_grads(const gs_trainer* t) { return t ? t->cfg.grads : nullptr; }
 
-int32_t gs_trainer_layer1_fused(const gs_trainer* t) { return t && t->fused1 ? 1 : 0; }
+int gs_trainer_set_option(gs_trainer* t, int32_t opt, int32_t value) {
+    GS_API_BEGIN
+    GS_REQUIRE(t, GS_EINVAL, "NULL argument");
+    GS_REQUIRE(!t->defer && !t->pending, GS_EINVAL, "options cannot change inside a runner loop");
+    const bool on = value != 0;
+    switch (opt) {
+        case GS_TOPT_FUSED_BWD: t->fuse_bwd = on; break;
+        case GS_TOPT_TOP_LAUNCH: t->use_top = on; break;
+        case GS_TOPT_SELF_ROWS: t->want_self_rows = on; break;
+        case GS_TOPT_DEFER_UPDATE: t->opt_defer = on; break;
+        default: GS_REQUIRE(false, GS_EINVAL, "unknown trainer option");
+    }
+    GS_API_END
+}
 
 int64_t gs_trainer_ws_bytes(gs_trainer* t, const int64_t* hop_sizes) {
     try {
@@ -849,14 +796,27 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack, const int64_
     GS_REQUIRE(t && pack && hop_sizes && offsets && roots && ws && loss, GS_EINVAL, "NULL argument");
     gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
                  gs::as_stream(stream));
+    gs::capture_step(*t, n_roots, gs::as_stream(stream));
     GS_API_END
 }
+
+int gs_trainer_capture(gs_trainer* t, float* emb, int64_t emb_stride, float* grads, int64_t max_steps) {
+    GS_API_BEGIN
+    GS_REQUIRE(t && max_steps >= 0 && (!emb || emb_stride >= t->cfg.hidden), GS_EINVAL, "bad arguments");
+    t->cap = {};
+    t->cap.emb = emb;
+    t->cap.emb_stride = emb_stride;
+    t->cap.grads = grads;
+    t->cap.max_steps = max_steps;
+    GS_API_END
+}
+
+int64_t gs_trainer_captured(const gs_trainer* t) { return t ? t->cap.n : -1; }
 
 int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout) {
     GS_API_BEGIN
     GS_REQUIRE(t && max_rows >= 0 && max_fanout >= 0, GS_EINVAL, "bad arguments");
-    const char* sr = std::getenv("GS_SELF_ROWS");  // default on; "0": the GEMMs gather the self rows
-    const bool self_rows = !(sr && std::string(sr) == "0") && !t->cfg.gcn && t->cfg.n_layers >= 1;
+    const bool self_rows = t->want_self_rows && !t->cfg.gcn && t->cfg.n_layers >= 1;
     if (max_rows <= t->a1_rows && max_fanout <= t->k_ids && self_rows == t->self_rows) return GS_OK;
     max_rows = std::max(max_rows, t->a1_rows);
     t->self_rows = self_rows;
@@ -913,6 +873,7 @@ int gs_trainer_forward_backward_gathered(gs_trainer* t, const int32_t* pack, con
                GS_EINVAL, "bad arguments");
     gs::run_step(*t, pack, hop_sizes, offsets, roots, n_roots, static_cast<char*>(ws), ws_bytes, loss,
                  gs::as_stream(stream), slot);
+    gs::capture_step(*t, n_roots, gs::as_stream(stream));
     GS_API_END
 }
 
@@ -953,7 +914,7 @@ int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capa
         if (tm.st0) (void)hipFree(tm.st0);
         tm.st0 = tm.st1 = nullptr;
         tm.stamped.assign(cap, 0);
-        if ((s == 1 || s == 3) && cap > 0 && std::getenv("GS_TIMER_EVENTS") == nullptr) {  // span stamps
+        if ((s == 1 || s == 3) && cap > 0) {  // span stamps
             const int64_t words = cap * gs::kStampBlocks;
             GS_REQUIRE(hipMalloc(&tm.st0, 2 * words * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
                        "hipMalloc(timer stamps)");
@@ -1016,11 +977,6 @@ const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site) {
 int gs_trainer_update_local(gs_trainer* t, void* stream) {
     GS_API_BEGIN
     GS_REQUIRE(t, GS_EINVAL, "NULL argument");
-    if (t->update_done) {  // the step's last launch already ran the clip + SGD
-        t->update_done = false;
-        t->norm_ready = false;
-        return GS_OK;
-    }
     if (t->pending) {  // deferred update: the next forward (or trainer_defer_update(false)) applies it
         t->norm_ready = false;
         return GS_OK;
@@ -1045,7 +1001,6 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     GS_API_BEGIN
     GS_REQUIRE(t && ws, GS_EINVAL, "NULL argument");
     t->norm_ready = false;
-    GS_REQUIRE(!t->update_done, GS_EINVAL, "the step's fused launch already applied the SGD");
     GS_REQUIRE(!t->pending, GS_EINVAL, "gs_trainer_update with an update already pending");
     if (t->defer && t->defer_comm) {
         // deferred after the all-reduce: the norm partials of the summed gradient

@@ -48,8 +48,8 @@ constexpr int kTopRows = 4;
 // accumulators per wave); the gather, head, slab and dIn stages keep waves
 // 0-3.  Lab, per launch: 15.3 -> 14.0 us, outputs bitwise equal
 // (profiles/r04e_top_lab_e8_ab.txt; 16 waves, fourteen of them DMA: 14.6 us,
-// profiles/r04f_top_lab_e16_ab.txt).  GS_TOP_E8=0 (runtime) or -DGS_TOP_E8=0
-// (the lab) restores 4 waves.
+// profiles/r04f_top_lab_e16_ab.txt).  -DGS_TOP_E8=0 (tools/lab/top_lab.hip)
+// builds the 4-wave kernel.
 #ifndef GS_TOP_E8
 #define GS_TOP_E8 1
 #endif
@@ -511,10 +511,8 @@ static bool top_lds_ready(int64_t C) {
             return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) ==
                    hipSuccess;
         };
-        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, 512>)) &&
-                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, 512>)) &&
-                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, 256>)) &&
-                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, 256>));
+        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, kTopThreads>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, kTopThreads>));
         (void)hipGetLastError();
         ok_bytes = a ? static_cast<int>(want) : 0;
     }
@@ -538,15 +536,8 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
               aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
-    const char* e8 = std::getenv("GS_TOP_E8");  // read per launch (tests switch it)
-    const bool w8 = e8 ? std::string(e8) != "0" : kTopThreads == 512;
-    if (w8) {
-        if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, 512>, grid, dim3(512), smem, st, a);
-        else launch_k(sage_top_kernel<GS_AGG_MAX, 512>, grid, dim3(512), smem, st, a);
-    } else {
-        if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, 256>, grid, dim3(256), smem, st, a);
-        else launch_k(sage_top_kernel<GS_AGG_MAX, 256>, grid, dim3(256), smem, st, a);
-    }
+    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, kTopThreads>, grid, dim3(kTopThreads), smem, st, a);
+    else launch_k(sage_top_kernel<GS_AGG_MAX, kTopThreads>, grid, dim3(kTopThreads), smem, st, a);
     check_launch("sage_top");
     return static_cast<int>(grid.x);
 }

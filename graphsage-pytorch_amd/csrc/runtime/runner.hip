@@ -52,10 +52,9 @@ static void hip_ok(hipError_t e, const char* what) {
 // read, or a device buffer whose readers have finished), and cross-stream
 // consumers are ordered by them on one device.  So they skip the system-scope
 // release that a default event performs (a cache writeback + invalidate at
-// every step boundary).  GS_RUNNER_SYSFENCE=1 restores default events (A/B).
+// every step boundary).
 static unsigned sync_event_flags() {
-    static const bool sysfence = std::getenv("GS_RUNNER_SYSFENCE") != nullptr;
-    return hipEventDisableTiming | (sysfence ? 0u : static_cast<unsigned>(hipEventDisableSystemFence));
+    return hipEventDisableTiming | static_cast<unsigned>(hipEventDisableSystemFence);
 }
 
 // Device-side pull of a pinned host pack (hipHostMalloc memory is mapped into
@@ -82,7 +81,7 @@ __global__ __launch_bounds__(256) void pull_pack_kernel(const int4* __restrict__
 struct PackSlot {
     int32_t* host = nullptr;  // pinned
     int32_t* dptr = nullptr;  // its device address (the pull kernel's source)
-    size_t thp_bytes = 0;     // GS_PIN_THP: a 2 MiB-aligned registered mapping of this size, else hipHostMalloc
+    size_t thp_bytes = 0;     // a 2 MiB-aligned registered mapping of this size
     hipEvent_t copied = nullptr;
     int64_t batch = -1;
     int64_t hop_sizes[4 * GS_MAX_HOPS];
@@ -146,25 +145,19 @@ struct gs_runner {
     // three batches back released the ring entry, and that the gather of the
     // batch it is about to issue has completed.
     static constexpr int kDev = 3;
-    // Device pack buffers: a ring of 4 (b % kPack), one more than the gather
-    // ring, so batch b+1's pack can be pulled while batch b is gathered: the
-    // entry's previous user, step b-3, is the one wait_entry(b % kDev) has just
-    // waited for (GS_PULL_AHEAD).
-    static constexpr int kPack = 4;
+    // Device pack buffers: one per gather-ring entry (b % kDev); entry k's
+    // previous user, step b-3, is the one wait_entry(k) waits for.
+    static constexpr int kPack = kDev;
     int32_t* dev[kPack] = {};
     gs::Inflight pulled_slot[kPack];       // sampler stream + slot of the pack in entry p
-    int64_t pulled = 0;                    // batches whose pack pull is issued
-    bool pull_ahead = false;
     hipEvent_t dev_done[kDev] = {};        // main: step of the batch in entry k finished
     bool dev_busy[kDev] = {};
     // Step completion without an event between steps: the step's SGD launch
     // (with a deferred update: its last slab sum) stores its batch index into done_host (fine-grained pinned memory) when
     // it starts, i.e. once every launch that reads the step's ring entry has
     // completed (stream order); the host polls it.  dev_done events remain for
-    // the last step of each gs_runner_run call (teardown) and as the
-    // GS_RUNNER_EVENTS=1 A/B path.
+    // the last step of each gs_runner_run call (teardown) and for inference.
     bool use_flag = false;
-    bool yield_polls = false;  // GS_RUNNER_YIELD
     int64_t* done_host = nullptr;          // hipHostMalloc, coherent
     int64_t* done_dev = nullptr;
     int64_t flag_step[kDev] = {-1, -1, -1};  // batch whose SGD signals entry k free (-1: none pending)
@@ -174,11 +167,10 @@ struct gs_runner {
             const auto t0 = std::chrono::steady_clock::now();
             for (uint64_t spin = 0; __atomic_load_n(done_host, __ATOMIC_ACQUIRE) < want; ++spin) {
                 __builtin_ia32_pause();
-                // GS_RUNNER_YIELD (default on, "0" off): offer the core to
-                // runnable sampler threads every 64 polls while the step runs
-                // (the runner is two steps ahead, so a few microseconds of
-                // reaction cost nothing; profiles/r04f_runner_yield_ab.txt)
-                if (yield_polls && (spin & 63) == 63) sched_yield();
+                // offer the core to runnable sampler threads every 64 polls
+                // while the step runs (the runner is two steps ahead, so a few
+                // microseconds of reaction cost nothing; profiles/r04f_runner_yield_ab.txt)
+                if ((spin & 63) == 63) sched_yield();
                 if ((spin & 0xfffff) == 0xfffff &&
                     std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
                     // no progress for 5 s: let the runtime report a device error, then give up
@@ -192,23 +184,6 @@ struct gs_runner {
         if (dev_busy[k]) gs::hip_ok(hipEventSynchronize(dev_done[k]), "hipEventSynchronize");
     }
     hipEvent_t gathered[kDev] = {};        // side: pull + gather of the batch in entry k
-    // GS_RUNNER_GATE_FWD: the lookahead pull + gather of batch b waits (on the
-    // host) for the layer-1 forward of step b-2 instead of only for step b-3,
-    // so the side stream's work lands under that step's latency-bound launches
-    // rather than under its forward (A/B switch)
-    bool gate_fwd = false;
-    // GS_SIDE_GATE_STEP: the lookahead's side-stream work waits on the GPU for
-    // the previous step's last launch (an event recorded on the step stream
-    // just before this step's launches), so it starts under this step's
-    // forward and its gather lands under the top launch (A/B switch)
-    bool gate_step = false;
-    hipEvent_t gate_ev = nullptr;
-    hipEvent_t side_gate = nullptr;        // set around the lookahead issue
-    int64_t pull_blocks = 1 << 30;  // GS_PULL_BLOCKS: cap on the pull kernel's grid (grid-stride)
-    bool pull_copy = false;  // GS_PULL_COPY=1: the pack pull as a runtime copy (copy engine) instead of a kernel
-    hipEvent_t fwd_done[kDev] = {};
-    bool fwd_busy[kDev] = {};
-    int cur_k = -1;                        // ring entry of the step being issued (fwd1 hook)
     hipStream_t side = nullptr;
     gs::Inflight inflight[kDev];
     int64_t issued = 0;                    // batches whose pull + gather are issued
@@ -367,26 +342,20 @@ int gs_runner::take_slot(int64_t b, bool block) {
 }
 
 // Batch b's pack: pinned slot -> device pack entry b % kPack on the side
-// stream (a kernel reading the mapped slot, or the copy engine).  The entry's
-// previous user, step b - kPack, must have completed.
+// stream (a kernel reading the mapped slot; the copy engine measured no
+// faster).  The entry's previous user, step b - kPack, must have completed.
 void gs_runner::pull(int64_t b, int slot_id) {
     using namespace gs;
     PackSlot& slot = streams[b % cfg.n_streams]->slots[slot_id];
     int32_t* d = dev[b % kPack];
-    if (pull_copy) {
-        hip_ok(hipMemcpyAsync(d, slot.host, slot.used * sizeof(int32_t), hipMemcpyHostToDevice, side),
-               "hipMemcpyAsync");
-    } else {
-        const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
-        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, pull_blocks));
-        pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
-            reinterpret_cast<const int4*>(slot.dptr), reinterpret_cast<int4*>(d), n16, slot.dptr + 4 * n16,
-            d + 4 * n16, static_cast<int>(tail));
-        hip_ok(hipGetLastError(), "pull_pack_kernel");
-    }
+    const int64_t n16 = slot.used / 4, tail = slot.used - 4 * n16;
+    const int64_t blocks = std::max<int64_t>(1, (n16 + 255) / 256);
+    pull_pack_kernel<<<dim3(static_cast<unsigned>(blocks)), 256, 0, side>>>(
+        reinterpret_cast<const int4*>(slot.dptr), reinterpret_cast<int4*>(d), n16, slot.dptr + 4 * n16, d + 4 * n16,
+        static_cast<int>(tail));
+    hip_ok(hipGetLastError(), "pull_pack_kernel");
     hip_ok(hipEventRecord(slot.copied, side), "hipEventRecord");
     pulled_slot[b % kPack] = {static_cast<int>(b % cfg.n_streams), slot_id};
-    pulled = b + 1;
 }
 
 // Device sampler: enqueue stream w's next batches, up to dev_depth queued.
@@ -471,27 +440,21 @@ void gs_runner::dev_sync_rngs() {
     }
 }
 
-// Pull batch b's pack to the device (unless pulled ahead) and gather its
-// layer 1, both on the side stream; with pull_ahead, then pull batch b+1's
-// pack if it is sampled.  block == false: return false if b is not sampled yet.
+// Pull batch b's pack to the device and gather its layer 1, both on the side
+// stream.  block == false: return false if b is not sampled yet.
 bool gs_runner::issue(int64_t b, bool block) {
     using namespace gs;
     int slot_id = -1;
     if (devmode) {
         if (!dev_take(b, block)) return false;
-    } else if (pulled <= b) {
+    } else {
         slot_id = take_slot(b, block);
         if (slot_id < 0) return false;
     }
     const auto tr = Clock::now();
     const int k = static_cast<int>(b % kDev);
     wait_entry(k);  // batch b-3 done
-    if (gate_fwd && !block && b >= 2) {
-        const int kp = static_cast<int>((b - 2) % kDev);
-        if (fwd_busy[kp]) hip_ok(hipEventSynchronize(fwd_done[kp]), "hipEventSynchronize");  // step b-2's forward
-    }
     stats.wait_ring_s += secs(tr, Clock::now());
-    if (side_gate) hip_ok(hipStreamWaitEvent(side, side_gate, 0), "hipStreamWaitEvent");
     if (devmode) {
         const DevResult& R = dres[b % n_dpack];
         const int rc = gs_trainer_gather(cfg.trainer, dpack[b % n_dpack], R.hop_sizes, R.offsets, k, side);
@@ -504,7 +467,7 @@ bool gs_runner::issue(int64_t b, bool block) {
         dev_enqueue(static_cast<int>(b % cfg.n_streams));
         return true;
     }
-    if (pulled <= b) pull(b, slot_id);
+    pull(b, slot_id);
     const Inflight f = pulled_slot[b % kPack];
     PackSlot& slot = streams[f.stream]->slots[f.slot];
     const int rc = gs_trainer_gather(cfg.trainer, dev[b % kPack], slot.hop_sizes, slot.offsets, k, side);
@@ -512,11 +475,6 @@ bool gs_runner::issue(int64_t b, bool block) {
     hip_ok(hipEventRecord(gathered[k], side), "hipEventRecord");
     inflight[k] = f;
     issued = b + 1;
-    // entry (b+1) % kPack last held batch b-3, whose step wait_entry(k) saw complete
-    if (pull_ahead && b + 1 < n_units && pulled == b + 1) {
-        const int s1 = take_slot(b + 1, false);
-        if (s1 >= 0) pull(b + 1, s1);
-    }
     return true;
 }
 
@@ -551,7 +509,6 @@ gs_runner::~gs_runner() {
     // of it before any buffer is freed.
     if (side) (void)hipStreamSynchronize(side);
     if (comm_stream) (void)hipStreamSynchronize(comm_stream);
-    if (cfg.trainer && gate_fwd) gs::trainer_set_fwd1_hook(cfg.trainer, {});
     for (int d = 0; d < kDev; ++d)
         if (dev_busy[d]) (void)hipEventSynchronize(dev_done[d]);
     if (done_host) (void)hipHostFree(done_host);
@@ -575,10 +532,6 @@ gs_runner::~gs_runner() {
     if (roots_dev) (void)hipFree(roots_dev);
     for (int d = 0; d < kDev; ++d) {
         if (dev_done[d]) (void)hipEventDestroy(dev_done[d]);
-        if (fwd_done[d]) {
-            (void)hipEventSynchronize(fwd_done[d]);
-            (void)hipEventDestroy(fwd_done[d]);
-        }
         if (gathered[d]) (void)hipEventDestroy(gathered[d]);
     }
     if (cfg.trainer && comm_stream) {
@@ -586,15 +539,6 @@ gs_runner::~gs_runner() {
         gs::trainer_set_w1_chunk_hook(cfg.trainer, 1, {});
     }
     if (w1_ready) (void)hipEventDestroy(w1_ready);
-    if (cfg.trainer && !cfg.comm && !cfg.embed_out) {  // drained above; never expected
-        try {
-            if (gs::trainer_barrier_failed(cfg.trainer))
-                std::fprintf(stderr, "graphsage_amd: a fused SGD launch's grid barrier timed out; "
-                                     "the parameters of that step are not trustworthy\n");
-        } catch (...) {
-        }
-    }
-    if (gate_ev) (void)hipEventDestroy(gate_ev);
     if (upper_ready) (void)hipEventDestroy(upper_ready);
     if (upper_reduced) (void)hipEventDestroy(upper_reduced);
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
@@ -682,11 +626,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     for (int d = 0; d < gs_runner::kPack; ++d)
         hip_ok(hipMalloc(&r->dev[d], r->cap * sizeof(int32_t)), "hipMalloc(pack)");
     hip_ok(hipMalloc(&r->clip_ws, 64 * 8 * sizeof(float)), "hipMalloc(clip ws)");
-    r->use_flag = std::getenv("GS_RUNNER_EVENTS") == nullptr && !cfg->embed_out;
-    {
-        const char* y = std::getenv("GS_RUNNER_YIELD");  // default on; "0": pure spin
-        r->yield_polls = !(y && std::string(y) == "0");
-    }
+    r->use_flag = !cfg->embed_out;
     if (r->use_flag) {
         void* hp = nullptr;
         hip_ok(hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc(done flag)");
@@ -765,8 +705,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
             d.next = w;
         }
         r->dcap = std::max<int64_t>(r->cap, gs_dsampler_pack_bound(r->dstreams[0].ds, cfg->batch));
-        const char* depth_env = std::getenv("GS_DS_DEPTH");  // runs queued per device stream (1 or 2)
-        r->dev_depth = depth_env && std::atoi(depth_env) == 1 ? 1 : gs_runner::kDevDepthMax;
+        r->dev_depth = gs_runner::kDevDepthMax;
         r->n_dpack = r->dev_depth * S + 3;
         r->dpack.assign(r->n_dpack, nullptr);
         for (auto& p : r->dpack) hip_ok(hipMalloc(&p, r->dcap * sizeof(int32_t)), "hipMalloc(pack)");
@@ -777,9 +716,9 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
     // idle) instead of helpers private to each stream.
     const char* shared_env = std::getenv("GS_SHARED_HELPERS");
     const bool shared_helpers = shared_env && std::atoi(shared_env) == 1;
-    // pack slots on transparent huge pages (GS_PIN_THP=0: hipHostMalloc): the pull kernel's
-    // host reads then need one translation per 2 MiB instead of per 4 KiB page
-    const bool pin_thp = !(std::getenv("GS_PIN_THP") && std::string(std::getenv("GS_PIN_THP")) == "0");
+    // pack slots on transparent huge pages: the pull kernel's host reads then
+    // need one translation per 2 MiB instead of per 4 KiB page (pull kernel
+    // 13.26 -> 12.63 us)
     for (int32_t w = 0; w < S && !r->devmode; ++w) {
         auto s = std::make_unique<SamplerStream>();
         s->rng = cfg->rngs[w];
@@ -793,7 +732,7 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
         s->slots.resize(cfg->depth);
         for (int32_t q = 0; q < cfg->depth; ++q) {
             PackSlot& sl = s->slots[q];
-            if (pin_thp) {  // the slot on transparent huge pages (madvise), registered
+            {  // the slot on transparent huge pages (madvise), registered
                 constexpr size_t kHuge = size_t(2) << 20;
                 const size_t bytes = (r->cap * sizeof(int32_t) + kHuge - 1) / kHuge * kHuge;
                 void* p = mmap(nullptr, bytes + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
@@ -811,10 +750,6 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
                 void* dp = nullptr;
                 hip_ok(hipHostGetDevicePointer(&dp, sl.host, 0), "hipHostGetDevicePointer");
                 sl.dptr = static_cast<int32_t*>(dp);
-            } else {
-                hip_ok(hipHostMalloc(reinterpret_cast<void**>(&sl.host), r->cap * sizeof(int32_t), hipHostMallocDefault),
-                       "hipHostMalloc");
-                sl.dptr = sl.host;
             }
             hip_ok(hipEventCreateWithFlags(&s->slots[q].copied, sync_event_flags()), "hipEventCreate");
             s->free.push_back(q);
@@ -852,22 +787,6 @@ int gs_runner_create(const gs_runner_config* cfg, gs_runner** out) {
                 ++rp->w1_issued;
             });
         }
-    }
-    r->gate_fwd = std::getenv("GS_RUNNER_GATE_FWD") != nullptr && !cfg->embed_out;
-    r->gate_step = std::getenv("GS_SIDE_GATE_STEP") != nullptr && !cfg->embed_out;
-    if (r->gate_step) hip_ok(hipEventCreateWithFlags(&r->gate_ev, hipEventDisableTiming), "hipEventCreate");
-    r->pull_copy = std::getenv("GS_PULL_COPY") != nullptr;
-    r->pull_ahead = std::getenv("GS_PULL_AHEAD") != nullptr;
-    if (const char* e = std::getenv("GS_PULL_BLOCKS")) r->pull_blocks = std::max(1, std::atoi(e));
-    if (r->gate_fwd) {
-        for (int d = 0; d < gs_runner::kDev; ++d)
-            hip_ok(hipEventCreateWithFlags(&r->fwd_done[d], sync_event_flags()), "hipEventCreate");
-        gs_runner* rp = r.get();
-        trainer_set_fwd1_hook(cfg->trainer, [rp](hipStream_t st) {
-            if (rp->cur_k < 0) return;
-            hip_ok(hipEventRecord(rp->fwd_done[rp->cur_k], st), "hipEventRecord");
-            rp->fwd_busy[rp->cur_k] = true;
-        });
     }
     for (auto& s : r->streams) {
         SamplerStream* sp = s.get();
@@ -919,26 +838,11 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             if (t) gs::trainer_keep_lowp(t, false);
         }
     } keep_lowp{r->cfg.trainer};
-    // GS_FUSED_SGD=1, no all-reduce: the step's last launch runs the clip + SGD
-    // behind a grid barrier.  Off: the barrier waits out the side stream's
-    // gather (blocks not yet resident), 88 us against 8.3 + 4.2 us for the
-    // two launches (rocprof, rmat2m).
-    struct FuseUpdate {
-        gs_trainer* t;
-        explicit FuseUpdate(gs_trainer* t_) : t(t_) {
-            if (t) gs::trainer_fuse_update(t, true);
-        }
-        ~FuseUpdate() {
-            if (t) gs::trainer_fuse_update(t, false);
-        }
-    } fuse_update{r->cfg.trainer && !r->cfg.comm && !r->cfg.embed_out && std::getenv("GS_FUSED_SGD")
-                      ? r->cfg.trainer
-                      : nullptr};
     // Each step's clip + SGD is deferred into the next step's launches (W1's
     // update for clip coefficient 1 written by the last slab sum, or with a
     // communicator by the norm launch after the all-reduce; the next layer-1
     // forward applies the update) instead of a launch between the steps; the
-    // loop's end applies the last one (GS_DEFER_SGD=0: off).
+    // loop's end applies the last one (trainer option GS_TOPT_DEFER_UPDATE = 0: off).
     struct DeferUpdate {
         gs_trainer* t;
         hipStream_t st;
@@ -954,11 +858,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
                 std::fprintf(stderr, "graphsage_amd: runner: applying the last deferred update failed: %s\n", e.what());
             }
         }
-    } defer_update{r->cfg.trainer && !r->cfg.embed_out && !fuse_update.t &&
-                           !(std::getenv("GS_DEFER_SGD") && std::string(std::getenv("GS_DEFER_SGD")) == "0")
-                       ? r->cfg.trainer
-                       : nullptr,
-                   st, r->cfg.comm != nullptr};
+    } defer_update{r->cfg.trainer && !r->cfg.embed_out ? r->cfg.trainer : nullptr, st, r->cfg.comm != nullptr};
     for (int64_t step = 0; step < n_steps; ++step) {
         const int64_t b = r->next_batch;
         const auto t0 = Clock::now();
@@ -969,14 +869,7 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         }
         // look ahead: batch b+1's pull + gather run on the side stream under
         // this step (never block here: with a slow sampler that would idle the GPU)
-        if (b + 1 < r->n_units && r->issued == b + 1) {
-            if (r->gate_step) {
-                hip_ok(hipEventRecord(r->gate_ev, st), "hipEventRecord");
-                r->side_gate = r->gate_ev;
-            }
-            r->issue(b + 1, false);
-            r->side_gate = nullptr;
-        }
+        if (b + 1 < r->n_units && r->issued == b + 1) r->issue(b + 1, false);
         const int k = static_cast<int>(b % gs_runner::kDev);
         const auto tg = Clock::now();
         hip_ok(hipEventSynchronize(r->gathered[k]), "hipEventSynchronize");  // normally long done
@@ -1022,7 +915,6 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             if (rc != GS_OK) fail(rc, gs_last_error());
             t3 = Clock::now();
         } else {
-            r->cur_k = k;
             // the done flag goes to the step's SGD launch: the fused slab sum
             // inside the step, or gs_trainer_update* below
             if (r->use_flag) g_done_flag = {r->done_dev, b};
@@ -1030,7 +922,6 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
             int rc = gs_trainer_forward_backward_gathered(r->cfg.trainer, pk, hop_sizes, offsets,
                                                           pk + pack_total, r->cfg.batch, k, r->ws, r->ws_bytes, loss,
                                                           st);
-            r->cur_k = -1;
             if (rc != GS_OK) fail(rc, gs_last_error());
             t3 = Clock::now();
             // with a communicator (any world size, so one rank exercises the same
@@ -1085,15 +976,6 @@ int gs_runner_run(gs_runner* r, int64_t n_steps, float* loss, void* stream) {
         gs::trainer_defer_update(defer_update.t, false, st);
     }
     unwind.armed = false;
-    // GS_FUSED_SGD: a grid barrier that gave up ran its SGD on partial sums;
-    // the run fails here (after its steps drained) instead of training on
-    // with corrupted parameters
-    if (fuse_update.t && n_steps > 0) {
-        hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-        if (trainer_barrier_failed(r->cfg.trainer))
-            fail(GS_EHIP, "runner: a fused clip+SGD launch's grid barrier timed out (GS_FUSED_SGD); the parameters "
-                          "of that step are not trustworthy");
-    }
     GS_API_END
 }
 

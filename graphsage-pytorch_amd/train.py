@@ -128,6 +128,29 @@ class NativeTrainer:
                                        _lib.stream_ptr(self.device)))
         return out
 
+    _OPTIONS = {"fused_bwd": _lib.GS_TOPT_FUSED_BWD, "top_launch": _lib.GS_TOPT_TOP_LAUNCH,
+                "self_rows": _lib.GS_TOPT_SELF_ROWS, "defer_update": _lib.GS_TOPT_DEFER_UPDATE}
+
+    def set_option(self, name, value):
+        """gs_trainer_set_option: switch a bitwise-equal alternative of the
+        step (fused_bwd, top_launch, self_rows, defer_update; default all on)."""
+        check(lib().gs_trainer_set_option(self._h, self._OPTIONS[name], int(bool(value))))
+        return self
+
+    def capture(self, n_steps, batch):
+        """Parity capture (tests): the next n_steps training steps' root
+        embeddings [n_steps, batch, hidden] and flat gradients before their
+        clip + SGD [n_steps, n_params] (gs_trainer_capture); returns both
+        tensors, filled in stream order as the steps run."""
+        emb = torch.zeros(n_steps, batch, self.H, dtype=torch.float32, device=self.device)
+        grads = torch.zeros(n_steps, self.p.params.numel(), dtype=torch.float32, device=self.device)
+        self._cap = (emb, grads)  # kept alive while the trainer may write them
+        check(lib().gs_trainer_capture(self._h, emb.data_ptr(), batch * self.H, grads.data_ptr(), n_steps))
+        return emb, grads
+
+    def captured(self):
+        return int(lib().gs_trainer_captured(self._h))
+
     def update(self, grad_scale=1.0):
         """gs_trainer_update: grads *= grad_scale, clip per model, SGD — what
         every rank runs after the gradient all-reduce (grad_scale = 1/world)."""

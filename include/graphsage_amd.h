@@ -511,8 +511,8 @@ int gs_trainer_forward_backward(gs_trainer* t, const int32_t* pack,
  * padded neighbour ids, then the row gather through them (bitwise the same
  * aggregate, without the index chain in the gather); that gather also copies
  * each destination's own feature row beside its aggregate (slot rows
- * [self | agg] of 2F, so the layer-1 GEMMs read no self index; GS_SELF_ROWS=0
- * at reserve time keeps F-wide slots). */
+ * [self | agg] of 2F, so the layer-1 GEMMs read no self index;
+ * GS_TOPT_SELF_ROWS = 0 at reserve time keeps F-wide slots). */
 int gs_trainer_gather_reserve(gs_trainer* t, int64_t max_rows, int32_t max_fanout);
 int gs_trainer_gather(gs_trainer* t, const int32_t* pack, const int64_t* hop_sizes,
                       const int64_t* offsets, int32_t slot, void* stream);
@@ -540,7 +540,7 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream);
 int gs_trainer_update_local(gs_trainer* t, void* stream);
 /* Measurement only: record HIP events on the launch stream around the next
  * `capacity` layer-1 launches — the fused gather + linear kernel when
- * gs_trainer_layer1_fused(t), else the gather-aggregate; gs_trainer_agg_times
+ * the gather-aggregate; gs_trainer_agg_times
  * synchronises and returns their durations (ms). */
 int gs_trainer_time_agg(gs_trainer* t, int64_t capacity);
 int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
@@ -565,8 +565,24 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
 const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site);
 /* The flat gradient buffer (cfg.grads), gs_trainer_n_params floats. */
 float* gs_trainer_grads(const gs_trainer* t);
-/* 1 when layer 1 runs through gs_sage1_fwd (opt-in: GS_FUSED1 set at create). */
-int32_t gs_trainer_layer1_fused(const gs_trainer* t);
+/* Parity capture (tests): after each of the next max_steps training steps
+ * (gs_trainer_forward_backward[_gathered], inside gs_runner_run too), copy on
+ * the step's stream the step's [n_roots, hidden] root embeddings (the top
+ * SageLayer's output, models.py:241-269) to emb + i * emb_stride and the flat
+ * gradient as the step's backward left it — before its clip_grad_norm_ and
+ * SGD (utils.py:184-187) — to grads + i * gs_trainer_n_params.  Either buffer
+ * may be NULL; max_steps 0 disarms.  gs_trainer_captured: steps copied. */
+int gs_trainer_capture(gs_trainer* t, float* emb, int64_t emb_stride, float* grads, int64_t max_steps);
+int64_t gs_trainer_captured(const gs_trainer* t);
+/* Trainer options (gs_trainer_set_option, value 0 / 1; not inside a runner
+ * loop).  Each alternative computes bitwise the default's results and exists
+ * for the tests that prove it:
+ *   GS_TOPT_FUSED_BWD     1: layers >= 2 backward in fused launches
+ *   GS_TOPT_TOP_LAUNCH    1: a 2-layer step's layer 2 + loss head + dIn2 in one launch
+ *   GS_TOPT_SELF_ROWS     1: gather slots hold [self | agg] rows (next gs_trainer_gather_reserve)
+ *   GS_TOPT_DEFER_UPDATE  1: runner loops defer each step's clip + SGD into the next step */
+enum { GS_TOPT_FUSED_BWD = 0, GS_TOPT_TOP_LAUNCH = 1, GS_TOPT_SELF_ROWS = 2, GS_TOPT_DEFER_UPDATE = 3 };
+int gs_trainer_set_option(gs_trainer* t, int32_t opt, int32_t value);
 
 /* ------------------------------------------------------- RCCL communicator
  * One communicator per data-parallel rank for the gradient all-reduce of the

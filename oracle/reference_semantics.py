@@ -148,13 +148,19 @@ def nll_loss(logp, labels):
 
 
 def train_step_dense(adj, roots, fanouts, X, weights, cls_w, cls_b, labels, agg="MEAN", gcn=False,
-                     lr=0.7, max_norm=5.0, rng=random, bf16_layer1=False):
-    """One supervised step of utils.py:144-191 (without extend_nodes)."""
+                     lr=0.7, max_norm=5.0, rng=random, bf16_layer1=False, capture=None):
+    """One supervised step of utils.py:144-191 (without extend_nodes).
+    capture (a dict, optional): receives the step's root embeddings ("emb")
+    and its flat gradient [W1 | ... | WL | cls_w | cls_b] before the clip
+    ("grads"), the layout of the native trainer's flat buffer."""
     hops = sample_layers(adj, roots, fanouts, rng)
     emb = forward_dense(hops, X, weights, agg, gcn, bf16_layer1)
     logp = torch.log_softmax(emb.mm(cls_w.t()) + cls_b, 1)
     loss = nll_loss(logp, labels)
     loss.backward()
+    if capture is not None:
+        capture["emb"] = emb.detach().clone()
+        capture["grads"] = torch.cat([p.grad.detach().reshape(-1) for p in list(weights) + [cls_w, cls_b]])
     with torch.no_grad():
         for group in (list(weights), [cls_w, cls_b]):
             torch.nn.utils.clip_grad_norm_(group, max_norm)

@@ -126,3 +126,56 @@ def check_embeddings_vs_oracle(gs_models, graph, X, X_rows, hops, roots, fanouts
     assert emb.shape == ref.shape
     torch.testing.assert_close(emb, ref, atol=tol, rtol=tol)
     return emb
+
+
+def check_timed_steps_vs_oracle(train, wl, adj, X_dev, X_rows, fanouts, classes, agg="MEAN", bf16=False,
+                                tols=(1e-5, 1e-5), n_steps=2, streams=2, seed=824, hidden=128):
+    """The bench's own training step against the oracle, step by step.
+
+    The native path is exactly what bench.py times: NativeTrainer + Runner
+    (`streams` sampler streams held until release, the resolved-id gather into
+    the [self | agg] slot on the side stream, the layer-1 forward, the fused
+    top launch, the layer-2 backward, the layer-1 dW and its slab sum), all
+    n_steps in ONE gs_runner_run call — so every step after the first runs the
+    layer-1 forward instance that applies the previous step's deferred clip +
+    SGD (linear_fwd_wide_kernel<..., true>) and reads the speculative W1 the
+    previous slab sum wrote.  gs_trainer_capture copies each step's root
+    embeddings and its flat gradient [dW1 | dW2 | dWc | dbc] before the clip +
+    SGD; oracle.train_step_dense (autograd over the dense-mask restatement,
+    models.py:241-330, utils.py:157-187) runs the same batches on the same
+    `random` streams and its weights carry over step to step.  tols[i]: the
+    tolerance (atol = rtol) of step i's embeddings and gradients."""
+    import time
+    import torch
+    B = len(wl["batches"][0])
+    batches = wl["batches"][:n_steps]
+    tr = train.NativeTrainer(wl["graph"], X_dev, wl["labels"], classes, fanouts=fanouts, agg_func=agg, seed=seed)
+    emb, grads = tr.capture(n_steps, B)
+    r = train.Runner(tr, wl["graph"], batches, [train.make_rng(seed, 0, w) for w in range(streams)], fanouts,
+                     fail_empty=agg == "MAX", depth=2, hold=True)
+    time.sleep(0.1)
+    r.release(len(batches))
+    r.run(n_steps)  # one call: the deferred update is pending between the steps
+    torch.cuda.synchronize()
+    r.close()
+    assert tr.captured() == n_steps
+    emb, grads = emb.cpu(), grads.cpu()
+    labels = wl["labels"].cpu().long()
+    feat = X_dev.shape[1]
+    sage_w, cw, cb = train.reference_init(2, feat, hidden, classes, False, seed)
+    W = [w.clone().requires_grad_(True) for w in sage_w]
+    cw, cb = cw.clone().requires_grad_(True), cb.clone().requires_grad_(True)
+    rngs = [random.Random(train.rank_seed(seed, 0, w)) for w in range(streams)]
+    worst = []
+    for i, roots in enumerate(batches):
+        cap = {}
+        oracle.train_step_dense(adj, roots.tolist(), fanouts, X_rows, W, cw, cb, labels[torch.from_numpy(roots)],
+                                agg=agg, rng=rngs[i % streams], bf16_layer1=bf16, capture=cap)
+        tol = tols[min(i, len(tols) - 1)]
+        e_ref, g_ref = cap["emb"], cap["grads"]
+        assert g_ref.numel() == grads.shape[1]
+        torch.testing.assert_close(emb[i, :len(roots)], e_ref, atol=tol, rtol=tol, msg=lambda m: f"step {i} emb: {m}")
+        torch.testing.assert_close(grads[i], g_ref, atol=tol, rtol=tol, msg=lambda m: f"step {i} grads: {m}")
+        worst.append((float((emb[i, :len(roots)] - e_ref).abs().max()), float((grads[i] - g_ref).abs().max()),
+                      float(g_ref.abs().max())))
+    return worst

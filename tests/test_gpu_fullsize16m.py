@@ -28,7 +28,7 @@ import pytest
 import torch
 
 import oracle
-from tests.fullsize_parity import check_embeddings_vs_oracle, check_pack_vs_oracle
+from tests.fullsize_parity import check_embeddings_vs_oracle, check_pack_vs_oracle, check_timed_steps_vs_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -109,6 +109,14 @@ def test_rmat16m_first_batch_indices_and_embeddings_vs_oracle(wl, adj):
     hops = check_pack_vs_oracle(wl["graph"], adj, roots, FAN, seed)
     W = [w.to(DEV) for w in train.reference_init(2, F, H, C, False, SEED)[0]]
     check_embeddings_vs_oracle(models, wl["graph"], wl["X"], _Rows(wl["X"]), hops, roots, FAN, W, seed, DEV)
+
+
+def test_rmat16m_timed_step_embeddings_and_grads_vs_oracle(wl, adj):
+    """configs[4]'s per-GPU step as the bench times it (F = 128): root
+    embeddings and every gradient before clip + SGD over steps 1 and 2 of one
+    runner call, against oracle autograd at 1e-5 (tests/fullsize_parity.py)."""
+    worst = check_timed_steps_vs_oracle(train, wl, adj, wl["X"], _Rows(wl["X"]), FAN, C)
+    print("max |emb diff|, max |grad diff|, max |grad| per step:", worst)
 
 
 def test_rmat16m_runner_vs_oracle_train_steps(wl, native, adj):

@@ -133,29 +133,28 @@ def test_sage_linear_fwd_bwd(n, F, H, gcn, dtype):
                                    (513, 128, 64), (100, 64, 32), (2048, 256, 256), (6200, 256, 128),
                                    (17, 256, 128)])
 @pytest.mark.parametrize("gcn", [False, True])
-def test_wres_forward_bitwise_equals_tiled_kernels(monkeypatch, n, F, H, gcn):
-    """The W-resident fp32 forward (linear_fwd_wres_kernel: a 32-column W
-    slice per block in LDS by LDS-DMA) feeds the same MFMA operands in the
-    same order as the 32-row and 16-row tiled kernels: outputs bitwise
-    equal, partial last tiles and the self-row gather included."""
+def test_wide_forward_bitwise_equals_chunked_kernel(n, F, H, gcn):
+    """The 32-row W-in-LDS forward (linear_fwd_wide_kernel, taken for 16-B
+    aligned operands) feeds the same MFMA operands in the same order as the
+    16-row chunked kernel (linear_fwd_kernel, taken here by an aggregate whose
+    rows are not 16-B aligned): outputs bitwise equal, partial last tiles and
+    the self-row gather included."""
     torch.manual_seed(n + F + H)
     n_src = n + 29
     Xs = torch.randn(n_src, F, device=DEV)
     A = torch.randn(n, F, device=DEV)
+    A_odd = torch.empty(n, F + 1, device=DEV)[:, 1:]  # lda = F + 1, row 0 at +4 B: the chunked kernel
+    A_odd.copy_(A)
     sidx = torch.randint(0, n_src, (n,), dtype=torch.int32, device=DEV)
     K = F if gcn else 2 * F
     W = torch.randn(H, K, device=DEV) * 0.05
-    outs = {}
-    for mode in ("wres", "wide32", "chunked", "wstat"):
-        monkeypatch.setenv("GS_LIN_FWD", mode)
+    outs = []
+    for a in (A, A_odd):
         out = torch.full((n, H), float("nan"), device=DEV)
-        ops.sage_linear_fwd(A, W, out, Xs=None if gcn else Xs, sidx=None if gcn else sidx)
+        ops.sage_linear_fwd(a, W, out, Xs=None if gcn else Xs, sidx=None if gcn else sidx)
         torch.cuda.synchronize()
-        outs[mode] = out
-    assert torch.equal(outs["wres"], outs["wide32"])
-    assert torch.equal(outs["wres"], outs["chunked"])
-    # the W-stationary kernel (layer-1 shape: K = 512, H = 128, self rows; other shapes fall back)
-    assert torch.equal(outs["wstat"], outs["chunked"])
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("agg", ["MEAN", "MAX"])

@@ -351,20 +351,17 @@ def test_runner_deferred_update_matches_python_loop(gs, agg, dtype, max_norm):
         assert all(x > max_norm for x in norms), norms
 
 
-def test_runner_deferred_update_switch(gs, monkeypatch):
-    """GS_DEFER_SGD=0 (a separate update launch per step) and the default
+def test_runner_deferred_update_switch(gs):
+    """defer_update off (a separate update launch per step) and the default
     deferred update leave the same parameters bit for bit."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:6]
     out = []
-    for env in ("0", None):
-        if env is None:
-            monkeypatch.delenv("GS_DEFER_SGD", raising=False)
-        else:
-            monkeypatch.setenv("GS_DEFER_SGD", env)
+    for defer in (False, True):
         t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), max_norm=0.05, seed=824)
+        t.set_option("defer_update", defer)
         r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10], depth=2)
         r.run(len(batches))
         torch.cuda.synchronize()
@@ -373,42 +370,15 @@ def test_runner_deferred_update_switch(gs, monkeypatch):
     assert torch.equal(out[0], out[1])
 
 
-@pytest.mark.parametrize("agg", ["MEAN", "MAX"])
-def test_dw_plus_matches_default(gs, monkeypatch, agg):
-    """GS_DW_PLUS=1 (the top path's dW_2 slabs and classifier reduce launched
-    beside the layer-1 dW instead of in the layer-2 backward launch) runs the
-    same bodies: loss, gradients and parameters bitwise the default's."""
-    graph, g, n = _graph(gs, "rmat")
-    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
-    labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
-    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 9))[:5]
-    out = []
-    for env in (None, "1"):
-        if env is None:
-            monkeypatch.delenv("GS_DW_PLUS", raising=False)
-        else:
-            monkeypatch.setenv("GS_DW_PLUS", env)
-        t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, max_norm=0.05, seed=824)
-        r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
-                         fail_empty=agg == "MAX", depth=2)
-        r.run(len(batches))
-        torch.cuda.synchronize()
-        out.append((t.p.params.clone(), t.p.grads.clone(), float(t.loss)))
-        r.close()
-    assert torch.equal(out[0][0], out[1][0])
-    assert torch.equal(out[0][1], out[1][1])
-    assert out[0][2] == out[1][2]
-
-
 @pytest.mark.parametrize("agg,bf16,gcn", [("MEAN", False, False), ("MAX", False, False), ("MEAN", True, False),
                                           ("MAX", True, False), ("MEAN", False, True)])
-def test_self_rows_matches_default(gs, monkeypatch, agg, bf16, gcn):
-    """GS_SELF_ROWS (default on: the side-stream gather also copies the
-    layer-1 rows' own features into the slot, [self | agg] rows of 2F, and the
-    layer-1 forward and dW read that block without the self-index round) feeds
-    the GEMMs the same values in the same order as GS_SELF_ROWS=0 (the GEMMs
-    gather X[dst] themselves): loss, gradients and parameters bitwise equal
-    (gcn: the slot keeps the agg half only)."""
+def test_self_rows_matches_default(gs, agg, bf16, gcn):
+    """self_rows (default on: the side-stream gather also copies the layer-1
+    rows' own features into the slot, [self | agg] rows of 2F, and the layer-1
+    forward and dW read that block without the self-index round) feeds the
+    GEMMs the same values in the same order as self_rows off (the GEMMs gather
+    X[dst] themselves): loss, gradients and parameters bitwise equal (gcn: the
+    slot keeps the agg half only)."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
     if bf16:
@@ -416,17 +386,16 @@ def test_self_rows_matches_default(gs, monkeypatch, agg, bf16, gcn):
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 96, 0, 1, 9))[:5]
     out = []
-    for env in ("0", "1"):
-        monkeypatch.setenv("GS_SELF_ROWS", env)
+    for self_rows in (False, True):
         t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), agg_func=agg, gcn=gcn, max_norm=0.05,
                                 seed=824)
+        t.set_option("self_rows", self_rows)
         r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10],
                          fail_empty=agg == "MAX", gcn=gcn, depth=2)
         r.run(len(batches))
         torch.cuda.synchronize()
         out.append((t.p.params.clone(), t.p.grads.clone(), float(t.loss)))
         r.close()
-    monkeypatch.delenv("GS_SELF_ROWS", raising=False)
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
     assert out[0][2] == out[1][2]
@@ -438,7 +407,7 @@ def test_self_rows_matches_default(gs, monkeypatch, agg, bf16, gcn):
     # B >= 1024: the layer-2 weight gradient spans more than 8 row slabs, so the
     # fused launch's slab sum and the standalone split kernel both group slabs
     ("MEAN", False, 2, "pubmed", 1536), ("MAX", False, 2, "pubmed", 1536)])
-def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name, B):
+def test_fused_backward_matches_unfused(gs, agg, gcn, layers, name, B):
     """The horizontally fused backward launches (kernels/bwd.hip) run the same
     per-role kernels and summation orders as the five-launch sequence (the
     slab sums in one shared grouped order, linear_dev.hpp sum_slabs_body):
@@ -450,9 +419,8 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name,
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     fan = [25, 10, 5][:layers]
     a = train.NativeTrainer(graph, X, labels, 16, num_layers=layers, fanouts=fan, agg_func=agg, gcn=gcn, seed=824)
-    monkeypatch.setenv("GS_NO_FUSED_BWD", "1")
     b = train.NativeTrainer(graph, X, labels, 16, num_layers=layers, fanouts=fan, agg_func=agg, gcn=gcn, seed=824)
-    monkeypatch.delenv("GS_NO_FUSED_BWD")
+    b.set_option("fused_bwd", False)
     rng = gs.RNG(21)
     done = 0
     for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 13):
@@ -476,26 +444,22 @@ def test_fused_backward_matches_unfused(gs, monkeypatch, agg, gcn, layers, name,
     assert done >= 1
 
 
-@pytest.mark.parametrize("e8", ["1", "0"])
 @pytest.mark.parametrize("agg,name,B", [("MEAN", "pubmed", 512), ("MAX", "pubmed", 512), ("MEAN", "rmat", 97),
                                          ("MAX", "pubmed", 1536)])
-def test_top_launch_matches_separate_launches(gs, monkeypatch, agg, name, B, e8):
+def test_top_launch_matches_separate_launches(gs, agg, name, B):
     """The one-launch top layer + loss head (kernels/top.hip: layer-2
     aggregate, linear, relu, NLL head, dZ and dIn on the matrix cores) against the
     separate launches it replaces (agg_fwd, the MFMA linear, cls_rows, the
     MFMA dIn role): it repeats their product chains in the f32 MFMA order, so
     loss, every gradient and the updated parameters are bitwise equal,
-    including a batch that leaves its last 4-row block partial; on 8 waves
-    (the default) and on 4 (GS_TOP_E8=0)."""
-    monkeypatch.setenv("GS_TOP_E8", e8)
+    including a batch that leaves its last 4-row block partial."""
     graph, g, n = _graph(gs, name)
     X = torch.from_numpy(uniform_features(7, n, 256)).to(DEV)
     labels = torch.from_numpy((np.arange(n) % 16).astype(np.int32)).to(DEV)
     fan = [25, 10]
     a = train.NativeTrainer(graph, X, labels, 16, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
-    monkeypatch.setenv("GS_NO_TOP", "1")
     b = train.NativeTrainer(graph, X, labels, 16, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
-    monkeypatch.delenv("GS_NO_TOP")
+    b.set_option("top_launch", False)
     rng = gs.RNG(5)
     done = 0
     for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 17):
@@ -561,11 +525,11 @@ def test_runner_distributed_path_single_rank(gs, agg):
 
 
 @pytest.mark.parametrize("max_norm,dtype", [(5.0, "f32"), (1e-3, "f32"), (5.0, "bf16"), (1e-3, "bf16")])
-def test_runner_deferred_update_with_allreduce(gs, monkeypatch, max_norm, dtype):
+def test_runner_deferred_update_with_allreduce(gs, max_norm, dtype):
     """With a communicator the deferred update starts after the all-reduce:
     one launch computes the norm partials of the summed gradient and W1's
     speculative update, the next forward applies the clip + SGD.  Parameters
-    and clipped gradients bitwise those of GS_DEFER_SGD=0 (the all-reduce
+    and clipped gradients bitwise those of defer_update off (the all-reduce
     path's separate norm + SGD launches), one rank, bucketed all-reduce."""
     graph, g, n = _graph(gs, "rmat")
     X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
@@ -575,12 +539,9 @@ def test_runner_deferred_update_with_allreduce(gs, monkeypatch, max_norm, dtype)
     batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:6]
     comm = train.Communicator(0, 1, DEV)
     out = []
-    for env in ("0", None):
-        if env is None:
-            monkeypatch.delenv("GS_DEFER_SGD", raising=False)
-        else:
-            monkeypatch.setenv("GS_DEFER_SGD", env)
+    for defer in (False, True):
         t = train.NativeTrainer(graph, X, labels, 16, fanouts=(25, 10), max_norm=max_norm, seed=824)
+        t.set_option("defer_update", defer)
         r = train.Runner(t, graph, batches, [train.make_rng(11, 0, w) for w in range(2)], [25, 10], depth=2,
                          comm=comm, ar_buckets=2)
         r.run(2)
