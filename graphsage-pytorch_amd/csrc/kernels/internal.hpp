@@ -42,7 +42,11 @@ bool linear_fwd_wide_ok(gs_dtype dt, int64_t F, const void* Xs, int64_t ldxs, co
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
-                    int64_t H_split = -1);
+                    int64_t H_split = -1, int phases = 1);
+// Row phases of the layer-1 weight gradient (linear_dw_body<PH>): 512-thread
+// workgroups, half the slabs.  Layers >= 2 keep one phase (the fused layer
+// backward's slabs, which the unfused path must match).
+inline constexpr int kDw1Phases = 2;
 int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* part, hipStream_t st);
 // One slab sum: out = Σ_s slabs[s] (S slabs of len floats), norm partials to part.
 struct SlabSum {

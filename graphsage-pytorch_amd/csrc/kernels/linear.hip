@@ -222,8 +222,9 @@ namespace gs {
 int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs, int64_t ldxs,
                     const int32_t* sidx, const void* A, int64_t lda, const float* dout, const float* out,
                     int64_t ldo, int32_t relu, float* dW, void* ws, int64_t ws_bytes, hipStream_t st,
-                    int64_t H_split) {
+                    int64_t H_split, int phases) {
     GS_REQUIRE(dt == GS_F32 || dt == GS_BF16, GS_EINVAL, "dtype must be f32 or bf16");
+    GS_REQUIRE(phases == 1 || phases == 2, GS_EINVAL, "dW: 1 or 2 row phases");
     GS_REQUIRE(n >= 0 && n < (int64_t(1) << 31) && F >= 1 && H >= 1 && H <= 4096, GS_EINVAL, "bad sizes");
     const bool self = Xs != nullptr;
     const int64_t K = self ? 2 * F : F;
@@ -235,8 +236,10 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
     // H_split: the row slabs of an H_split-row gradient (a chunk of its rows
     // then has the whole gradient's slabs, hence its sums bit for bit)
     const int64_t Hs = H_split > 0 ? H_split : H;
-    const int S = dw_splits(n, K, Hs);
-    const int rps = dw_rows_per_split(n, K, Hs);
+    // phases = 2: two row phases per 512-thread workgroup (linear_dw_body<PH = 2>),
+    // half the slabs of the 256-thread form at the same chunk loop per workgroup
+    const int S = dw_splits(n, K, Hs, phases);
+    const int rps = dw_rows_per_split(n, K, Hs, phases);
     const int64_t need = static_cast<int64_t>(S > 1 ? S : 0) * K * H * 4;
     GS_REQUIRE(ws_bytes >= need && (need == 0 || ws), GS_EINVAL, "workspace too small");
     float* target = (S > 1) ? static_cast<float*>(ws) : dW;
@@ -253,10 +256,12 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
     // workgroups mapped XCD by XCD: every tile of slab z on XCD z % 8 (PMC HBM
     // bytes 35.2 -> 19.4 MB per launch: dZ no longer fetched by all 8 XCDs)
     const dim3 grid_x(static_cast<unsigned>(kXcds * tiles * ((S + kXcds - 1) / kXcds)));
-#define GS_LDW1(TT, SELF, RELU, VL, ZV)                                                              \
-    launch_k(linear_dw_xcd_kernel<TT, SELF, RELU, VL, ZV>, grid_x, dim3(kThreads), 0, st, nn, ff, hh, kk, \
+#define GS_LDW2(TT, SELF, RELU, VL, ZV, PH)                                                                   \
+    launch_k(linear_dw_xcd_kernel<TT, SELF, RELU, VL, ZV, PH>, grid_x, dim3(kThreads * PH), 0, st, nn, ff, hh, kk, \
              rps, gx, tiles, S, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda, dout, \
              out, ldo, target, H * K)
+#define GS_LDW1(TT, SELF, RELU, VL, ZV) \
+    do { if (phases == 2) GS_LDW2(TT, SELF, RELU, VL, ZV, 2); else GS_LDW2(TT, SELF, RELU, VL, ZV, 1); } while (0)
 #define GS_LDW_Z(TT, SELF, RELU, VL) \
     do { if (zvec) GS_LDW1(TT, SELF, RELU, VL, true); else GS_LDW1(TT, SELF, RELU, VL, false); } while (0)
 #define GS_LDW_V(TT, SELF, RELU) \
@@ -272,6 +277,7 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
 #undef GS_LDW_V
 #undef GS_LDW_Z
 #undef GS_LDW1
+#undef GS_LDW2
     check_launch("gs_sage_linear_bwd_weight");
     return S;
 }

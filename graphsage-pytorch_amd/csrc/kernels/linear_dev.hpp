@@ -475,23 +475,34 @@ constexpr int kDwRpt = kDwCh / 16;  // rows each thread loads per chunk
 #endif
 constexpr int kDwAhead = GS_DW_AHEAD;  // row chunks whose global loads are in flight ahead of the MFMAs
 
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
+// PH row phases (blockDim = 256·PH): the waves of phase ph run the chunks
+// ph, ph + PH, ... of the slab on their own LDS ring (one barrier per
+// iteration for the whole block), each into its own accumulators; at the end
+// phase 1 hands its sums to phase 0 through LDS, which adds them (fixed order,
+// so deterministic) and stores the slab.  PH = 2 puts twice the rows in a slab
+// at the same chunk loop length: half the slabs (and half the split-K bytes
+// the slab sum re-reads) for the same per-workgroup latency.
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC, int PH = 1>
 __device__ __forceinline__ void linear_dw_body(
     int bx, int by, int bz, int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
     const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
     const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
-    __shared__ float sZ[2][kDwCh * kDwPitch];
-    __shared__ float sI[2][kDwCh * kDwPitch];
+    static_assert(PH == 1 || PH == 2, "one or two row phases");
+    __shared__ float sbuf[PH][2][2][kDwCh * kDwPitch];  // [phase][dZ | inputs][ring buffer]
     __shared__ int sIdx[HAS_SELF ? kDwMaxSlab : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ph = PH == 1 ? 0 : static_cast<int>(threadIdx.x >> 8);
+    const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63, wave = tid >> 6;
+    float (&sZ)[2][kDwCh * kDwPitch] = sbuf[ph][0];
+    float (&sI)[2][kDwCh * kDwPitch] = sbuf[ph][1];
     const int r = lane & 15, kq = lane >> 4;
     const int k0 = bx * 64, h0 = by * 64;
     const int i_beg = bz * rows_per_split;
     const int i_end = min(n, i_beg + rows_per_split);
     const int nC = (i_end - i_beg + kDwCh - 1) / kDwCh;
+    const int nI = (nC + PH - 1) / PH;  // iterations: this phase's chunks (the last may be past the slab: zeros)
     const int lr = tid >> 4, lq = (tid & 15) * 4;
     if (HAS_SELF)
-        for (int t = tid; t < i_end - i_beg; t += kThreads) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
+        for (int t = threadIdx.x; t < i_end - i_beg; t += kThreads * PH) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
     __syncthreads();
 
     // Rows past the slab read a valid row and are zeroed at the LDS store
@@ -500,7 +511,8 @@ __device__ __forceinline__ void linear_dw_body(
     struct Ld {
         float4 z[kDwRpt], o[kDwRpt], x[kDwRpt];
     };
-    auto load = [&](int c, Ld& L) {
+    auto load = [&](int it, Ld& L) {
+        const int c = PH * it + ph;
 #pragma unroll
         for (int q = 0; q < kDwRpt; ++q) {
             const int t = min(kDwCh * min(c, nC - 1) + lr + 16 * q, i_end - i_beg - 1);
@@ -512,7 +524,8 @@ __device__ __forceinline__ void linear_dw_body(
             L.x[q] = concat_quad_raw<T, HAS_SELF, VLOAD>(srow, arow, F, K, k0 + lq);
         }
     };
-    auto stash = [&](int c, const Ld& L) {
+    auto stash = [&](int it, const Ld& L) {
+        const int c = PH * it + ph;
 #pragma unroll
         for (int q = 0; q < kDwRpt; ++q) {
             float4 z = mask_quad(L.z[q], h0 + lq, H);
@@ -520,8 +533,8 @@ __device__ __forceinline__ void linear_dw_body(
             float4 x = mask_quad(L.x[q], k0 + lq, K);
             const int row = lr + 16 * q;
             if (kDwCh * c + row >= i_end - i_beg) z = x = make_float4(0.f, 0.f, 0.f, 0.f);
-            *reinterpret_cast<float4*>(&sZ[c & 1][row * kDwPitch + lq]) = z;
-            *reinterpret_cast<float4*>(&sI[c & 1][row * kDwPitch + lq]) = x;
+            *reinterpret_cast<float4*>(&sZ[it & 1][row * kDwPitch + lq]) = z;
+            *reinterpret_cast<float4*>(&sI[it & 1][row * kDwPitch + lq]) = x;
         }
     };
     f32x4 acc[4];
@@ -530,9 +543,9 @@ __device__ __forceinline__ void linear_dw_body(
     // One chunk: its LDS operands are all read before its first MFMA (one
     // wait instead of one per MFMA pair), then the MFMAs on 4 accumulators,
     // rows in ascending groups of 4 (the same sequence for any chunk size).
-    auto compute = [&](int c) {
-        const float* tz = sZ[c & 1];
-        const float* ti = sI[c & 1];
+    auto compute = [&](int it) {
+        const float* tz = sZ[it & 1];
+        const float* ti = sI[it & 1];
         constexpr int NS = kDwCh / 4;
         float a[NS], b[NS][4];
 #pragma unroll
@@ -548,26 +561,44 @@ __device__ __forceinline__ void linear_dw_body(
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
     };
-    // Global loads run kDwAhead chunks ahead of the MFMAs (a ring of register
-    // sets, loop unrolled by its length); LDS stays double-buffered.  Slot u
-    // holds chunk c (stashed one iteration earlier) when chunk c = u (mod
-    // kDwAhead) is computed, and is refilled with chunk c + kDwAhead then.
+    // Global loads run kDwAhead iterations ahead of the MFMAs (a ring of
+    // register sets, loop unrolled by its length); LDS stays double-buffered.
+    // Slot u holds iteration i (stashed one iteration earlier) when i = u (mod
+    // kDwAhead) is computed, and is refilled with iteration i + kDwAhead then.
     Ld ring[kDwAhead];
 #pragma unroll
     for (int u = 0; u < kDwAhead; ++u) load(u, ring[u]);
     stash(0, ring[0]);
-    for (int c0 = 0; c0 < nC; c0 += kDwAhead) {
+    for (int i0 = 0; i0 < nI; i0 += kDwAhead) {
 #pragma unroll
         for (int u = 0; u < kDwAhead; ++u) {
-            const int c = c0 + u;
-            if (c >= nC) break;
+            const int it = i0 + u;
+            if (it >= nI) break;
             __syncthreads();
-            load(c + kDwAhead, ring[u]);
+            load(it + kDwAhead, ring[u]);
             __builtin_amdgcn_sched_barrier(0);
-            compute(c);
+            compute(it);
             __builtin_amdgcn_sched_barrier(0);
             const int un = (u + 1) % kDwAhead;
-            if (c + 1 < nC) stash(c + 1, ring[un]);
+            if (it + 1 < nI) stash(it + 1, ring[un]);
+        }
+    }
+    if constexpr (PH == 2) {
+        // phase 1's sums to phase 0 through phase 1's ring (free: every
+        // phase-1 wave is past its last compute once all reach the barrier)
+        float* xch = &sbuf[1][0][0][0];
+        static_assert(4 * kDwCh * kDwPitch >= kThreads * 16, "exchange area");
+        __syncthreads();
+        if (ph == 1)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                *reinterpret_cast<f32x4*>(&xch[(t * kThreads + tid) * 4]) = acc[t];
+        __syncthreads();
+        if (ph == 1) return;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x4 o = *reinterpret_cast<const f32x4*>(&xch[(t * kThreads + tid) * 4]);
+            acc[t] = acc[t] + o;
         }
     }
     float* slab = dst + static_cast<int64_t>(bz) * split_stride;
@@ -599,8 +630,8 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
 // XCD fetched every dZ row).  Grid: 8 · tiles · ceil(S / 8); spare
 // workgroups exit.
 constexpr int kXcds = 8;
-template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
-__global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
+template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC, int PH = 1>
+__global__ __launch_bounds__(kThreads * PH) void linear_dw_xcd_kernel(
     int n, int F, int H, int K, int rows_per_split, int gx, int tiles, int S, const T* __restrict__ Xs,
     int64_t ldxs, const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda,
     const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo, float* __restrict__ dst,
@@ -610,8 +641,8 @@ __global__ __launch_bounds__(kThreads) void linear_dw_xcd_kernel(
     const int z = w % kXcds + kXcds * (j / tiles);
     if (z >= S) return;
     const int t = j % tiles;
-    linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx, A,
-                                                   lda, dout, out, ldo, dst, split_stride);
+    linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC, PH>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx,
+                                                       A, lda, dout, out, ldo, dst, split_stride);
 }
 
 
@@ -762,19 +793,20 @@ __global__ __launch_bounds__(kThreads) void linear_dx_kernel(
 // fill the chip, at least 64 rows per slab, slab heights a multiple of 16.
 constexpr int kDwTargetBlocks = 512;  // two blocks per CU (measured best of 256 / 512 / 1024 in the step)
 
-inline int dw_target_blocks() { return kDwTargetBlocks; }
+// phases = 2 (the layer-1 weight gradient): workgroups of 512 threads, half as many
+inline int dw_target_blocks(int phases = 1) { return kDwTargetBlocks / phases; }
 
-inline int dw_rows_per_split(int64_t n, int64_t K, int64_t H) {
+inline int dw_rows_per_split(int64_t n, int64_t K, int64_t H, int phases = 1) {
     const int64_t tiles = ((K + 63) / 64) * ((H + 63) / 64);
-    const int64_t want = std::max<int64_t>(1, (dw_target_blocks() + tiles - 1) / tiles);
+    const int64_t want = std::max<int64_t>(1, (dw_target_blocks(phases) + tiles - 1) / tiles);
     const int64_t cap = std::max<int64_t>(1, n / 64);
     const int64_t S = std::max(std::min(want, cap), (n + kDwMaxSlab - 1) / kDwMaxSlab);
     const int64_t rows = (n + S - 1) / S;
     return static_cast<int>(std::min<int64_t>(kDwMaxSlab, std::max<int64_t>(16, (rows + 15) / 16 * 16)));
 }
 
-inline int dw_splits(int64_t n, int64_t K, int64_t H) {
-    const int rps = dw_rows_per_split(n, K, H);
+inline int dw_splits(int64_t n, int64_t K, int64_t H, int phases = 1) {
+    const int rps = dw_rows_per_split(n, K, H, phases);
     return static_cast<int>(std::max<int64_t>(1, (n + rps - 1) / rps));
 }
 

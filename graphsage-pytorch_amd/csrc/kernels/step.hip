@@ -499,7 +499,7 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                     float* dWq = G + T.w_off[0] + h0 * K1;
                     const int Sq = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, Hc, x1, ldx1,
                                                    sidx1, a1, lda1, lb.back().dH + h0, h[0] + h0, H, 0, dWq, dw_ws,
-                                                   dw_need, st, H);
+                                                   dw_need, st, H, kDw1Phases);
                     if (Sq > 1) sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), Sq, Hc * K1, dWq, nullptr, st);
                     T.w1_chunk_hook(st, T.w_off[0] + h0 * K1, Hc * K1);
                 }
@@ -511,7 +511,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             }
             const bool armed = timed_arm(T, 2);
             const int S1 = linear_dw_slabs(static_cast<gs_dtype>(c.feat_dtype), rows[0], F, H, x1, ldx1, sidx1, a1,
-                                           lda1, lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws, dw_need, st);
+                                           lda1, lb.back().dH, h[0], H, 0, G + T.w_off[0], dw_ws, dw_need, st, -1,
+                                           kDw1Phases);
             g_launch_events = {};
             timed_done(T, 2, armed);
             const float* s1_src = S1 > 1 ? reinterpret_cast<const float*>(dw_ws) : nullptr;
@@ -565,9 +566,15 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
         const int32_t* sidx = first ? sidx1 : fld(j, GS_PK_SELF);
         const int64_t fin = in_dim[l - 1], ldx = first ? ldx1 : H;
         if (first && L >= 2 && T.upper_hook) T.upper_hook(st);
-        ok(gs_sage_linear_bwd_weight(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H, x_in,
-                                     ldx, sidx, first ? a1 : agg[l - 1], first ? lda1 : fin, dH, h[l - 1], H, relu,
-                                     G + T.w_off[l - 1], dw_ws, dw_need, st));
+        {  // the fused path's slabs: layer 1 in kDw1Phases row phases, layers >= 2 in one
+            const int64_t Kl = x_in ? 2 * fin : fin;
+            const int Sl = linear_dw_slabs(first ? static_cast<gs_dtype>(c.feat_dtype) : GS_F32, rows[l - 1], fin, H,
+                                           x_in, ldx, sidx, first ? a1 : agg[l - 1], first ? lda1 : fin, dH, h[l - 1],
+                                           H, relu, G + T.w_off[l - 1], dw_ws, dw_need, st, -1,
+                                           first ? kDw1Phases : 1);
+            if (Sl > 1) sum_slabs_launch(reinterpret_cast<const float*>(dw_ws), Sl, H * Kl, G + T.w_off[l - 1], nullptr,
+                                         st);
+        }
         if (first) break;
         const int64_t ldd = c.gcn ? H : 2 * H;
         float* dSelf = c.gcn ? nullptr : dIn;

@@ -7,30 +7,26 @@
 //   logits, log_softmax, NLL, dlogits = (softmax - onehot)/B  (models.py:8-27,
 //            utils.py:159-164), dZ_r = (dlogits · Wc) ⊙ (E_r > 0)
 //   dIn_r  = dZ_r · W2 = [dSelf_r | dA_r]                   (autograd of :219)
-// One block of 4 waves owns 4 rows (the loss head's row block, so its
+// One block of 8 waves owns 4 rows (the loss head's row block, so its
 // classifier partial slab is the one cls_rows_kernel writes) and runs the
-// four stages back to back with the rows in LDS: the three launches this
-// replaces (layer-2 aggregate, layer-2 linear, loss head) and the dIn role of
-// the layer backward each paid a kernel boundary and a global round trip of
-// their inputs.
+// stages back to back with the rows in LDS: the three launches this replaces
+// (layer-2 aggregate, layer-2 linear, loss head) and the dIn role of the layer
+// backward each paid a kernel boundary and a global round trip of their inputs.
 //
-// Numerics are those of the launches it replaces, bit for bit: the aggregate
-// adds neighbours in list order as agg_fwd_kernel does; every product chain
-// is the fmaf chain the f32 MFMA kernels form (within each 16-wide k block
-// the order 0,4,8,12, 1,5,9,13, ... of four v_mfma_f32_16x16x4_f32 over the
-// four k-lane groups; blocks ascending); the head is cls_rows_kernel's code.
-// The two GEMMs run on the matrix cores in the linear kernels' k order, from a
-// copy of W2 in LDS that an LDS-DMA fills under the gather: E on 16x16x4 tiles
-// (the 4 rows padded to 16; two accumulators alternate to hide the 40-cycle
-// dependent latency), dIn on 4x4x1 multi-block MFMAs (the 4 rows are one
-// block's rows, 16 blocks = 64 columns per instruction).  Measured (tools/lab/
-// top_lab.hip, per launch): dIn 4.09 -> 2.49 us on 4x4x1; E on 4x4x1 took
-// 5.0 us (4.15 with its operands one k block ahead) against 3.3 — one
-// accumulator per output chain (the k order is fixed) leaves its dependent
-// latency exposed at 32 columns per wave.  Measured alternatives: W2
-// streamed from L2 through registers took the kernel to 31 us (latency-bound
-// at ~25 GB/s per CU); VALU fmaf chains from LDS spent 3.4 + 3.7 us in the
-// two GEMMs, bound by the LDS broadcast reads of the rows.
+// The two GEMMs run on v_mfma_f32_4x4x1_16b_f32: one instruction is 16 blocks
+// of a 4-row x 4-column outer product, i.e. the block's 4 rows x 64 columns
+// for one k, with no padding of the 4 rows (a 16x16x4 tile would carry 12
+// zero rows: 4x the matrix-pipe cycles, which bound the round-4 kernel's E
+// stage at two waves per SIMD).  The K range is split over the waves (E: 4
+// quarters of 64 k for each half of the 128 columns; dIn: 2 halves of 64 h
+// for each of the 4 column groups of 64), each wave's chain runs on two
+// accumulators (even / odd k), and the partial sums are added in a fixed
+// order through LDS: deterministic, within fp32 rounding of the separate
+// launches' single k-ordered chains (tests/test_gpu_model.py compares them at
+// tolerance).  The loss head's logits are 8-way split dot products (16 d each,
+// an xor-butterfly sum), its softmax one wave, dZ one output per thread.
+// W2 arrives in LDS by DMA under the gather (quad-swizzled rows: conflict-free
+// for both the row reads of E and the column reads of dIn).
 #include "cls_dev.hpp"
 #include "internal.hpp"
 #include "linear_dev.hpp"
@@ -42,21 +38,12 @@
 namespace gs {
 
 constexpr int kTopRows = 4;
-// Threads per block: 512 (8 waves) by default.  The extra waves issue the W2
-// DMA (six waves instead of two) and take one 16-column E tile each (two
-// waves per SIMD interleave the dependent MFMA chains instead of two
-// accumulators per wave); the gather, head, slab and dIn stages keep waves
-// 0-3.  Lab, per launch: 15.3 -> 14.0 us, outputs bitwise equal
-// (profiles/r04e_top_lab_e8_ab.txt; 16 waves, fourteen of them DMA: 14.6 us,
-// profiles/r04f_top_lab_e16_ab.txt).  -DGS_TOP_E8=0 (tools/lab/top_lab.hip)
-// builds the 4-wave kernel.
-#ifndef GS_TOP_E8
-#define GS_TOP_E8 1
-#endif
-constexpr int kTopThreads = GS_TOP_E8 ? 512 : 256;
+constexpr int kTopThreads = 512;  // 8 waves
 constexpr int kTopH = 128;
 constexpr int kTopK = 2 * kTopH;
 constexpr int kTopMaxC = 32;
+constexpr int kTopPart = 4 * kTopRows * kTopH;  // floats of the partial-sum area (= 2 * kTopRows * kTopK)
+static_assert(kTopPart == 2 * kTopRows * kTopK, "E and dIn partials share one area");
 
 struct TopArgs {
     int B, C;
@@ -80,21 +67,27 @@ struct TopArgs {
     KStamp stamp;        // a timed launch's span (g_kernel_stamp)
 };
 
-// k offset of step i (0..15) inside a 16-wide block: the MFMA kernels' order.
-__device__ __forceinline__ constexpr int mfma_k(int i) { return 4 * (i & 3) + (i >> 2); }
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
 
-template <int OP, int NT>
-__global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
-    constexpr int H = kTopH, K = kTopK, D = kTopH;
-    // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, Wc, dlogits, loss
+template <int OP>
+__global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
+    constexpr int H = kTopH, K = kTopK, D = kTopH, NT = kTopThreads;
+    // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, the
+    // GEMMs' partial sums, Wc, logits / dlogits, loss
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sW2 = smem;                                        // [H][K]
     float (*sX)[K] = reinterpret_cast<float (*)[K]>(sW2 + H * K);
     float (*sE)[H] = reinterpret_cast<float (*)[H]>(sX[kTopRows]);
     float (*sZ)[H] = reinterpret_cast<float (*)[H]>(sE[kTopRows]);
-    float* sW = &sZ[kTopRows][0];                             // [C][D + 1]
+    // the GEMMs' partial sums: E [4 k quarters][rows][H], dIn [2 h halves][rows][K]
+    float* sP = &sZ[kTopRows][0];
+    float* sW = sP + kTopPart;                                // [C][D + 1]
     float* sdl = sW + a.C * (D + 1);                          // [rows][C]
     float* sloss = sdl + kTopRows * a.C;
+    float* sb = sloss + kTopRows;                             // [C] classifier bias
+    int* sy = reinterpret_cast<int*>(sb + a.C);               // [rows] labels
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int C = a.C;
     const int r0 = blockIdx.x * kTopRows;
@@ -102,25 +95,20 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
 
     GS_TOP_STAMP(0);
     kstamp_begin(a.stamp);
-    // ---- W2 -> LDS by DMA (no registers), issued before anything else so its
-    // latency hides under the gather.  Row c is one wave instruction of 64
-    // 16-byte quads; quad q of the row lands in slot q ^ (c & 15), which keeps
-    // both later access patterns free of bank conflicts: a column read by
-    // lanes = rows (ds_read_b128, 16 rows per quarter-wave on 16 distinct
-    // slots) and a row read by lanes = k.
-    // Waves 2 and 3 issue it: the gather below runs on waves 0 and 1, whose
-    // dependent load rounds would otherwise queue behind the DMA (vmcnt
-    // retires in order).
+    // ---- W2 -> LDS by DMA (no registers), issued first so its latency hides
+    // under the gather.  Row c is one wave instruction of 64 16-byte quads;
+    // quad q of the row lands in slot q ^ (c & 15).  Waves 2..7 issue it (the
+    // gather's dependent load rounds run on waves 0 and 1; vmcnt retires in
+    // order, so those would otherwise queue behind the DMA).
     if (w >= 2)
         for (int c = w - 2; c < H; c += NT / 64 - 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
                                              0, 0);
 
-    // ---- stage 0: loss-head operands (independent of the rest, issued first)
-    const int cl = lane & 15, dq = lane >> 4;
-    const int wr_ = min(w, nr - 1);
-    const int root = a.roots[r0 + wr_];
-    const float b_lane = a.bc[min(cl, C - 1)];
+    // ---- loss-head operands (independent of the rest, issued before the
+    // gather so their dependent loads, label[root[r]], are long done)
+    if (tid < kTopRows) sy[tid] = tid < nr ? a.labels[a.roots[r0 + tid]] : 0;
+    else if (tid >= 64 && tid < 64 + C) sb[tid - 64] = a.bc[tid - 64];
     {
         const int nW4 = C * D / 4;
         for (int q = tid; q < nW4; q += NT) {
@@ -133,12 +121,11 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
             d[3] = v.w;
         }
     }
-    const int y_w = a.labels[root];
 
-    // ---- stage 1: the aggregate (agg_fwd_kernel<OP, float, 4, 32, explicit>)
-    // and the self row, one 32-lane group per row.  With the padded records
-    // (a.tids) the root's self index and whole list arrive in one load round
-    // (lane gl holds list entry gl, as the pack path's lanes do).
+    // ---- stage 1: the aggregate (agg_fwd_kernel<OP, float, 4, 32, explicit>:
+    // neighbours added in list order) and the self row, one 32-lane group per
+    // row.  With the padded records (a.tids) the root's self index and whole
+    // list arrive in one load round (lane gl holds list entry gl).
     {
         constexpr int G = 32, NR = 32;
         const int g = tid / G, gl = tid % G;
@@ -217,6 +204,9 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
             if (OP == GS_AGG_MAX)
                 *reinterpret_cast<int4*>(a.argmax + static_cast<int64_t>(r) * H + f0) = make_int4(am[0], am[1], am[2],
                                                                                                    am[3]);
+        } else if (g < kTopRows) {  // a ragged last block: zero rows (never stored)
+            *reinterpret_cast<float4*>(&sX[g][gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(&sX[g][H + gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
     GS_TOP_STAMP(1);
@@ -224,280 +214,199 @@ __global__ __launch_bounds__(NT) void sage_top_kernel(TopArgs a) {
     __syncthreads();
     GS_TOP_STAMP(2);
 
-    if constexpr (NT >= 512) {
-    // ---- stage 2 (8 waves): E = relu([self | agg] · W2ᵀ), wave w owns the
-    // 16 columns 16w .. 16w+15 (one tile, the same MFMA chain per tile)
-    if (w < 8) {
-        const int r = lane & 15, kq = lane >> 4;
-        const bool rowok = r < nr;
-        const uint4* xr = reinterpret_cast<const uint4*>(sX[min(r, nr - 1)]);
-        const uint4* wq = reinterpret_cast<const uint4*>(sW2);
-        const int c0 = 16 * w + r;
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto ld = [&](int k0, uint4& av, uint4& b0) {
-            const int q = (k0 >> 2) + kq;
-            av = xr[q];
-            b0 = wq[c0 * (K / 4) + (q ^ (c0 & 15))];
-        };
-        uint4 an, bn0;
-        ld(0, an, bn0);
-#pragma unroll 2
-        for (int k0 = 0; k0 < K; k0 += 16) {
-            uint4 av = an;
-            const uint4 b0 = bn0;
-            ld(min(k0 + 16, K - 16), an, bn0);
-            if (!rowok) av = make_uint4(0, 0, 0, 0);
-            const float a4[4] = {__uint_as_float(av.x), __uint_as_float(av.y), __uint_as_float(av.z),
-                                 __uint_as_float(av.w)};
-            const float w0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
-                                 __uint_as_float(b0.w)};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w0[j], acc0, 0, 0, 0);
-        }
-        if (kq == 0) {
-#pragma unroll
-            for (int j = 0; j < kTopRows; ++j) {
-                if (j >= nr) break;
-                const float v0 = (!(acc0[j] > 0.f) && acc0[j] == acc0[j]) ? 0.f : acc0[j];  // relu (NaN kept)
-                sE[j][c0] = v0;
-                a.E[static_cast<int64_t>(r0 + j) * H + c0] = v0;
-            }
-        }
-    }
-    } else
-    // ---- stage 2: E = relu([self | agg] · W2ᵀ) on the matrix cores, as the
-    // linear kernel's tiles: wave w owns columns 32w .. 32w+31 (two 16x16
-    // tiles); the 4 rows ride in a 16-row A tile (rows >= nr are zero).
+    // ---- stage 2: E = relu([self | agg] · W2ᵀ), 4x4x1 multi-block MFMAs.
+    // Wave w: columns 64 (w & 1) + lane, k quarter w >> 1 (64 k).  Lane l
+    // supplies row l & 3 of A and column l of B; acc[j] = row j, column l.
     {
-        const int r = lane & 15, kq = lane >> 4;
-        const bool rowok = r < nr;
-        const uint4* xr = reinterpret_cast<const uint4*>(sX[min(r, nr - 1)]);
-        const uint4* wq = reinterpret_cast<const uint4*>(sW2);
-        const int c0 = 32 * w + r, c1 = c0 + 16;
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-        // operands one k block ahead; the two tiles' MFMAs alternate so each
-        // accumulator's dependent latency (40 cycles) hides under the other's issue
-        auto ld = [&](int k0, uint4& av, uint4& b0, uint4& b1) {
-            const int q = (k0 >> 2) + kq;  // this lane's 4-k slot
-            av = xr[q];
-            b0 = wq[c0 * (K / 4) + (q ^ (c0 & 15))];
-            b1 = wq[c1 * (K / 4) + (q ^ (c1 & 15))];
-        };
-        uint4 an, bn0, bn1;
-        ld(0, an, bn0, bn1);
-#pragma unroll 2
-        for (int k0 = 0; k0 < K; k0 += 16) {
-            uint4 av = an;
-            const uint4 b0 = bn0, b1 = bn1;
-            ld(min(k0 + 16, K - 16), an, bn0, bn1);
-            if (!rowok) av = make_uint4(0, 0, 0, 0);
-            const float a4[4] = {__uint_as_float(av.x), __uint_as_float(av.y), __uint_as_float(av.z),
-                                 __uint_as_float(av.w)};
-            const float w0[4] = {__uint_as_float(b0.x), __uint_as_float(b0.y), __uint_as_float(b0.z),
-                                 __uint_as_float(b0.w)};
-            const float w1[4] = {__uint_as_float(b1.x), __uint_as_float(b1.y), __uint_as_float(b1.z),
-                                 __uint_as_float(b1.w)};
+        const int col = 64 * (w & 1) + lane, kb = 64 * (w >> 1);
+        const float* xr = sX[lane & 3] + kb;
+        const float* wrow = sW2 + col * K;
+        float av[64], bv[64];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {  // = mfma_slot's order on each tile
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w0[j], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[j], w1[j], acc1, 0, 0, 0);
-            }
+        for (int m = 0; m < 16; ++m) {
+            const float4 x4 = *reinterpret_cast<const float4*>(xr + 4 * m);
+            const int q = (kb >> 2) + m;
+            const float4 w4 = *reinterpret_cast<const float4*>(wrow + 4 * (q ^ (col & 15)));
+            av[4 * m] = x4.x; av[4 * m + 1] = x4.y; av[4 * m + 2] = x4.z; av[4 * m + 3] = x4.w;
+            bv[4 * m] = w4.x; bv[4 * m + 1] = w4.y; bv[4 * m + 2] = w4.z; bv[4 * m + 3] = w4.w;
         }
-        if (kq == 0) {  // lanes 0..15 hold rows 0..3 of their column
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
-            for (int j = 0; j < kTopRows; ++j) {
-                if (j >= nr) break;
-                const float v0 = (!(acc0[j] > 0.f) && acc0[j] == acc0[j]) ? 0.f : acc0[j];  // relu (NaN kept)
-                const float v1 = (!(acc1[j] > 0.f) && acc1[j] == acc1[j]) ? 0.f : acc1[j];
-                sE[j][c0] = v0;
-                sE[j][c1] = v1;
-                a.E[static_cast<int64_t>(r0 + j) * H + c0] = v0;
-                a.E[static_cast<int64_t>(r0 + j) * H + c1] = v1;
-            }
+        for (int k = 0; k < 64; k += 2) {
+            c0 = mfma4(av[k], bv[k], c0);
+            c1 = mfma4(av[k + 1], bv[k + 1], c1);
         }
+        float* pp = sP + (w >> 1) * (kTopRows * H);  // partial of quarter w >> 1: [row][col]
+#pragma unroll
+        for (int j = 0; j < kTopRows; ++j) pp[j * H + col] = c0[j] + c1[j];
     }
     __syncthreads();
     GS_TOP_STAMP(3);
+    // the quarters added in order, relu (NaN kept), E to LDS and global
+    {
+        const int row = tid >> 7, col = tid & (H - 1);  // 512 threads = 4 rows x 128 columns
+        float e = sP[row * H + col];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) e += sP[q * (kTopRows * H) + row * H + col];
+        e = (!(e > 0.f) && e == e) ? 0.f : e;
+        sE[row][col] = e;
+        if (row < nr) a.E[static_cast<int64_t>(r0 + row) * H + col] = e;
+    }
+    __syncthreads();
 
-    // ---- stage 3: the loss head, one wave per row (cls_rows_kernel's code)
+    // ---- stage 3: the loss head (models.py:8-27, utils.py:159-164).
+    // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
+    // the eight parts are added by an xor butterfly.
     const float invB = 1.0f / static_cast<float>(a.B);
     const int wp = D + 1;
+    for (int base = 0; base < kTopRows * C; base += NT / 8) {
+        const int rc = base + (tid >> 3), part = tid & 7;
+        const int row = min(rc / C, kTopRows - 1), c = rc % C;
+        const float* e = sE[row] + 16 * part;
+        const float* wr = sW + static_cast<int64_t>(c) * wp + 16 * part;
+        float z = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) z = fmaf(e[t], wr[t], z);
+        z += __shfl_xor(z, 1, 64);
+        z += __shfl_xor(z, 2, 64);
+        z += __shfl_xor(z, 4, 64);
+        if (part == 0 && rc < kTopRows * C) sdl[row * C + c] = z + sb[c];
+    }
+    __syncthreads();
+    // softmax / NLL / dlogits: wave w < rows, lane = class (C <= 32 <= 64)
     if (w < nr) {
         const int ii = w;
-        const float* e = sE[ii];
-        const int y = y_w;
-        static_assert(D % 4 == 0, "whole D quarters");
-        constexpr int DQ = D / 4;  // whole quarters: a straight-line chain
-        const int d_lo = dq * DQ;
-        float mx = -INFINITY;
-        for (int c0 = 0; c0 < C; c0 += 16) {
-            const int c = c0 + cl;
-            const float* wr = sW + static_cast<int64_t>(min(c, C - 1)) * wp;
-            float pz = 0.f;
+        const int y = sy[ii];
+        const float z = lane < C ? sdl[ii * C + lane] : -INFINITY;
+        float mx = z;
 #pragma unroll
-            for (int t = 0; t < DQ; ++t) pz = fmaf(e[d_lo + t], wr[d_lo + t], pz);
-            pz += __shfl_xor(pz, 16, 64);
-            pz += __shfl_xor(pz, 32, 64);
-            const float z = pz + (c0 == 0 ? b_lane : a.bc[min(c, C - 1)]);
-            if (dq == 0 && c < C) sdl[ii * C + c] = z;
-            if (c < C) mx = fmaxf(mx, z);
+        for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        const float lse = logf(wave_sum(lane < C ? expf(z - mx) : 0.f));
+        if (lane < C) {
+            const float lp = z - mx - lse;
+            if (lane == y) sloss[ii] = -lp;
+            sdl[ii * C + lane] = (expf(lp) - (lane == y ? 1.f : 0.f)) * invB;
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        __builtin_amdgcn_wave_barrier();
-        float se = 0.f;
-        for (int c = lane; c < C; c += 64) se += expf(sdl[ii * C + c] - mx);
-        const float lse = logf(wave_sum(se));
-        for (int c = lane; c < C; c += 64) {
-            const float lp = sdl[ii * C + c] - mx - lse;
-            if (c == y) sloss[ii] = -lp;
-            sdl[ii * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
-        }
-        __builtin_amdgcn_wave_barrier();
-        for (int d = lane; d < D; d += 64) {
-            float s = 0.f;
-            int c = 0;
-            for (; c + 8 <= C; c += 8) {  // eight classes' operands read ahead of their chain
-                float g[8], v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    g[u] = sdl[ii * C + c + u];
-                    v[u] = sW[static_cast<int64_t>(c + u) * wp + d];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) s = fmaf(g[u], v[u], s);
-            }
-            for (; c < C; ++c) s = fmaf(sdl[ii * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
-            if (!(e[d] > 0.f)) s = 0.f;
-            sZ[ii][d] = s;
-            a.dZ[static_cast<int64_t>(r0 + ii) * D + d] = s;
-        }
+    } else if (w < kTopRows && lane < C) {
+        sdl[w * C + lane] = 0.f;  // ragged block: no gradient from the missing rows
     }
     __syncthreads();
     GS_TOP_STAMP(4);
-
-    // ---- stage 4: this block's classifier partial slab (cls_rows_kernel's
-    // sums): out[c][d] = Σ_rows dlogits[row][c] · [E[row] | 1][d].  Thread t
-    // owns class t / 16 (its 4 dlogits in registers) and columns t % 16 + 16 j;
-    // the E reads are LDS broadcasts across the class groups (per launch
-    // 15.4-15.6 us against 16.3 for one thread per flat slab element, the
-    // fallback above 16 classes; same sums).
-#ifndef GS_TOP_SLAB_FLAT
-    if (C * 16 <= NT) {
-        const int per = C * (D + 1);
-        float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
-        const int c = tid >> 4;
-        if (c < C) {
-            float dl[kTopRows];
+    // dZ = (dlogits · Wc) ⊙ (E > 0): thread t = (row, d), classes in order
+    // (eight classes' operands read ahead of their chain)
+    {
+        const int row = tid >> 7, d = tid & (D - 1);
+        float s = 0.f;
+        int c = 0;
+        for (; c + 8 <= C; c += 8) {
+            float g[8], v[8];
 #pragma unroll
-            for (int ii = 0; ii < kTopRows; ++ii) dl[ii] = ii < nr ? sdl[ii * C + c] : 0.f;
-            if (nr == kTopRows) {  // every block but a ragged last one: straight-line, same sums
-                float s[D / 16];
-#pragma unroll
-                for (int j = 0; j < D / 16; ++j) {
-                    const int d = (tid & 15) + 16 * j;
-                    s[j] = 0.f;
-#pragma unroll
-                    for (int ii = 0; ii < kTopRows; ++ii) s[j] = fmaf(dl[ii], sE[ii][d], s[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < D / 16; ++j) out[c * (D + 1) + (tid & 15) + 16 * j] = s[j];
-                if ((tid & 15) == 0) {
-                    float sb = 0.f;
-#pragma unroll
-                    for (int ii = 0; ii < kTopRows; ++ii) sb = fmaf(dl[ii], 1.f, sb);
-                    out[c * (D + 1) + D] = sb;
-                }
-            } else {
-                for (int d = tid & 15; d <= D; d += 16) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int ii = 0; ii < kTopRows; ++ii)
-                        if (ii < nr) s = fmaf(dl[ii], d < D ? sE[ii][d] : 1.f, s);
-                    out[c * (D + 1) + d] = s;
-                }
+            for (int u = 0; u < 8; ++u) {
+                g[u] = sdl[row * C + c + u];
+                v[u] = sW[static_cast<int64_t>(c + u) * wp + d];
             }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s = fmaf(g[u], v[u], s);
         }
-        if (tid >= NT - 64) {
-            float s = 0.f;
-            for (int ii = tid - (NT - 64); ii < nr; ii += 64) s += sloss[ii];
-            s = wave_sum(s);
-            if (tid == NT - 64) out[per] = s;
-        }
-    } else
-#endif
-    // ---- stage 4: this block's classifier partial slab (cls_rows_kernel's)
+        for (; c < C; ++c) s = fmaf(sdl[row * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
+        if (!(sE[row][d] > 0.f)) s = 0.f;
+        sZ[row][d] = s;
+        if (row < nr) a.dZ[static_cast<int64_t>(r0 + row) * D + d] = s;
+    }
+    // ---- this block's classifier partial slab (cls_rows_kernel's sums):
+    // out[c][d] = Σ_rows dlogits[row][c] · [E[row] | 1][d], rows in order.
+    // Thread t owns class t / 16 (its 4 dlogits in registers) and columns
+    // t % 16 + 16 j; the E reads are LDS broadcasts across the class groups.
     {
         const int per = C * (D + 1);
         float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
-        int c = tid / (D + 1), d = tid - c * (D + 1);  // advanced by NT per step, no divides
-        constexpr int dc = NT / (D + 1), dd = NT % (D + 1);
-        for (int t = tid; t < per; t += NT) {
-            float s = 0.f;
+        if (C * 16 <= NT) {
+            const int c = tid >> 4;
+            if (c < C) {
+                float dl[kTopRows];
 #pragma unroll
-            for (int ii = 0; ii < kTopRows; ++ii)
-                if (ii < nr) s = fmaf(sdl[ii * C + c], d < D ? sE[ii][d] : 1.f, s);
-            out[t] = s;
-            c += dc;
-            d += dd;
-            if (d > D) {
-                d -= D + 1;
-                ++c;
+                for (int ii = 0; ii < kTopRows; ++ii) dl[ii] = ii < nr ? sdl[ii * C + c] : 0.f;
+                float sv[D / 16];
+#pragma unroll
+                for (int j = 0; j < D / 16; ++j) {
+                    const int d = (tid & 15) + 16 * j;
+                    sv[j] = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < kTopRows; ++ii)
+                        if (ii < nr) sv[j] = fmaf(dl[ii], sE[ii][d], sv[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < D / 16; ++j) out[c * (D + 1) + (tid & 15) + 16 * j] = sv[j];
+                if ((tid & 15) == 0) {
+                    float sbias = 0.f;
+#pragma unroll
+                    for (int ii = 0; ii < kTopRows; ++ii)
+                        if (ii < nr) sbias = fmaf(dl[ii], 1.f, sbias);
+                    out[c * (D + 1) + D] = sbias;
+                }
+            }
+        } else {
+            for (int t = tid; t < per; t += NT) {
+                const int c = t / (D + 1), d = t - c * (D + 1);
+                float sv = 0.f;
+#pragma unroll
+                for (int ii = 0; ii < kTopRows; ++ii)
+                    if (ii < nr) sv = fmaf(sdl[ii * C + c], d < D ? sE[ii][d] : 1.f, sv);
+                out[t] = sv;
             }
         }
-        if (tid < 64) {
-            float s = 0.f;
-            for (int ii = tid; ii < nr; ii += 64) s += sloss[ii];
-            s = wave_sum(s);
-            if (tid == 0) out[per] = s;
+        if (tid >= NT - 64) {
+            float sl = 0.f;
+            for (int ii = tid - (NT - 64); ii < nr; ii += 64) sl += sloss[ii];
+            sl = wave_sum(sl);
+            if (tid == NT - 64) out[per] = sl;
         }
     }
-
+    __syncthreads();
     GS_TOP_STAMP(5);
-    // ---- stage 5: dIn = dZ · W2 on the matrix cores, 4x4x1 multi-block as
-    // stage 2: wave w owns input columns 64w .. 64w+63, the 16 blocks x 4
-    // columns of one instruction (lane l: column 64w + l), one h per
-    // instruction in linear_dx_body's order (0,4,8,12, 1,5,9,13, ... per
-    // 16-wide h block): the same fmaf chains, bit for bit.
-    if (w < 4) {  // (waves >= 4 under GS_TOP_E8: no dIn role)
-        const int arow = lane & 3, kc = 64 * w + lane;
-        const bool rowok = arow < nr;
-        const float4* zr = reinterpret_cast<const float4*>(sZ[min(arow, nr - 1)]);
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2
-        for (int g = 0; g < H / 16; ++g) {
-            float zv[16], wv[16];
+
+    // ---- stage 4: dIn = dZ · W2 (4x4x1 multi-block).  Wave w: input columns
+    // 64 (w & 3) + lane, h half w >> 2 (64 h); W2[h][kc] read down a column of
+    // the swizzled copy.
+    {
+        const int kc = 64 * (w & 3) + lane, hb = 64 * (w >> 2);
+        const float* zr = sZ[lane & 3] + hb;
+        float zv[64], wv[64];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float4 z = zr[4 * g + q];
-                if (!rowok) z = make_float4(0.f, 0.f, 0.f, 0.f);
-                zv[4 * q] = z.x;
-                zv[4 * q + 1] = z.y;
-                zv[4 * q + 2] = z.z;
-                zv[4 * q + 3] = z.w;
-            }
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int h = 16 * g + t;
-                wv[t] = sW2[h * K + 4 * ((kc >> 2) ^ (h & 15)) + (kc & 3)];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int kq = 0; kq < 4; ++kq)
-                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(zv[4 * kq + j], wv[4 * kq + j], acc, 0, 0, 0);
+        for (int m = 0; m < 16; ++m) {
+            const float4 z4 = *reinterpret_cast<const float4*>(zr + 4 * m);
+            zv[4 * m] = z4.x; zv[4 * m + 1] = z4.y; zv[4 * m + 2] = z4.z; zv[4 * m + 3] = z4.w;
         }
 #pragma unroll
-        for (int j = 0; j < kTopRows; ++j)
-            if (j < nr) a.dIn[static_cast<int64_t>(r0 + j) * K + kc] = acc[j];
+        for (int t = 0; t < 64; ++t) {
+            const int h = hb + t;
+            wv[t] = sW2[h * K + 4 * ((kc >> 2) ^ (h & 15)) + (kc & 3)];
+        }
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+        for (int t = 0; t < 64; t += 2) {
+            c0 = mfma4(zv[t], wv[t], c0);
+            c1 = mfma4(zv[t + 1], wv[t + 1], c1);
+        }
+        float* pp = sP + (w >> 2) * (kTopRows * K);
+#pragma unroll
+        for (int j = 0; j < kTopRows; ++j) pp[j * K + kc] = c0[j] + c1[j];
+    }
+    __syncthreads();
+    // the two halves added in order, dIn to global: thread t = (row, 2 columns)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int o = tid + u * NT, row = o >> 8, kc = o & (K - 1);
+        const float v = sP[row * K + kc] + sP[kTopRows * K + row * K + kc];
+        if (row < nr) a.dIn[static_cast<int64_t>(r0 + row) * K + kc] = v;
     }
     GS_TOP_STAMP(6);
     kstamp_end(a.stamp);
 }
 
 static size_t top_smem_bytes(int64_t C) {
-    return sizeof(float) * (static_cast<size_t>(kTopH) * kTopK + kTopRows * (kTopK + 2 * kTopH) + C * (kTopH + 1) +
-                            kTopRows * C + kTopRows);
+    return sizeof(float) * (static_cast<size_t>(kTopH) * kTopK + kTopRows * (kTopK + 2 * kTopH) + kTopPart +
+                            C * (kTopH + 1) + kTopRows * C + kTopRows + C + kTopRows);
 }
 
 // The kernel keeps W2 in LDS (~146 KiB at 16 classes): raise the launch limit
@@ -506,13 +415,15 @@ static bool top_lds_ready(int64_t C) {
     static int ok_bytes = -1;
     const size_t need = top_smem_bytes(C);
     if (ok_bytes < 0) {
-        const size_t want = top_smem_bytes(kTopMaxC);
+        // the whole 160 KiB of a CU: W2 alone is 128 KiB; classes beyond what
+        // fits (C > 20) keep the separate launches
+        const size_t want = std::min<size_t>(top_smem_bytes(kTopMaxC), 160 * 1024);
         auto raise = [&](const void* f) {
             return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) ==
                    hipSuccess;
         };
-        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, kTopThreads>)) &&
-                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, kTopThreads>));
+        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX>));
         (void)hipGetLastError();
         ok_bytes = a ? static_cast<int>(want) : 0;
     }
@@ -536,8 +447,8 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
               aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
-    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN, kTopThreads>, grid, dim3(kTopThreads), smem, st, a);
-    else launch_k(sage_top_kernel<GS_AGG_MAX, kTopThreads>, grid, dim3(kTopThreads), smem, st, a);
+    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);
+    else launch_k(sage_top_kernel<GS_AGG_MAX>, grid, dim3(kTopThreads), smem, st, a);
     check_launch("sage_top");
     return static_cast<int>(grid.x);
 }

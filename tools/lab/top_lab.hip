@@ -3,11 +3,17 @@
 // neighbours per root, H 128, 16 classes), event timing over repeated
 // launches, and per-stage s_memrealtime stamps (100 MHz) of every block.
 // Developer tool, not part of the library:
-//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include tools/lab/top_lab.hip -o tools/bin/top_lab
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include -I graphsage-pytorch_amd/csrc/kernels \
+//         tools/lab/top_lab.hip -o tools/bin/top_lab
 //   tools/bin/top_lab [tids]    (tids: the runner's padded list records, as in the step)
+// Runs the library kernel (kernels/top.hip) and the round-4 one (top_v1.hip)
+// on the same inputs: time per launch, error against a double-precision CPU
+// reference, and the library kernel's stage stamps.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <random>
 #include <string>
@@ -20,6 +26,7 @@ __device__ unsigned long long* g_stamps;
     } while (0)
 #include "../../graphsage-pytorch_amd/csrc/host/errors.cpp"
 #include "../../graphsage-pytorch_amd/csrc/kernels/top.hip"
+#include "top_v1.hip"  // the round-4 kernel (namespace gs::v1), for the A/B
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); return 2; } } while (0)
 
@@ -71,30 +78,91 @@ int main(int argc, char** argv) {
     if (!gs::top_supported(H, C, false)) { std::printf("top not supported (LDS)\n"); return 3; }
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    if (!gs::v1::top_supported(H, C, false)) { std::printf("v1 top not supported (LDS)\n"); return 3; }
     auto launch = [&] {
         gs::top_fwd_bwd(GS_AGG_MEAN, B, C, dh1, dptr, dnbr, dself, dW, dWc, dbc, dlab, droots, agg, nullptr, E, dZ,
                         dIn, slab, s, use_tids ? dtids : nullptr, use_tids ? tk : 0);
     };
-    for (int i = 0; i < 20; ++i) launch();
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    const int reps = 200;
-    CK(hipEventRecord(e0, s));
-    for (int i = 0; i < reps; ++i) launch();
-    CK(hipEventRecord(e1, s));
-    CK(hipEventSynchronize(e1));
-    float ms = 0;
-    CK(hipEventElapsedTime(&ms, e0, e1));
-    std::printf("top kernel: %.2f us per launch (back to back, %d launches)\n", ms * 1e3 / reps, reps);
-    {  // outputs' bit pattern (variants must agree bit for bit)
-        std::vector<uint32_t> hE(B * H), hI(B * K), hZ(B * H);
+    auto launch_v1 = [&] {
+        gs::v1::top_fwd_bwd(GS_AGG_MEAN, B, C, dh1, dptr, dnbr, dself, dW, dWc, dbc, dlab, droots, agg, nullptr, E,
+                            dZ, dIn, slab, s, use_tids ? dtids : nullptr, use_tids ? tk : 0);
+    };
+    // double-precision reference of the step's outputs (models.py:209-220, 8-27)
+    std::vector<double> rE(size_t(B) * H), rZ(size_t(B) * H), rI(size_t(B) * K), rS(size_t(nb) * (C * (H + 1) + 1), 0.0);
+    for (int r = 0; r < B; ++r) {
+        std::vector<double> x(K, 0.0);
+        for (int f = 0; f < H; ++f) x[f] = h1[size_t(self[r]) * H + f];
+        const int cnt = ptr[r + 1] - ptr[r];
+        for (int e = ptr[r]; e < ptr[r + 1]; ++e)
+            for (int f = 0; f < H; ++f) x[H + f] += h1[size_t(nbr[e]) * H + f] / cnt;
+        for (int c = 0; c < H; ++c) {
+            double z = 0;
+            for (int k = 0; k < K; ++k) z += x[k] * W[size_t(c) * K + k];
+            rE[size_t(r) * H + c] = z > 0 ? z : 0;
+        }
+        std::vector<double> lg(C);
+        double mx = -1e300;
+        for (int c = 0; c < C; ++c) {
+            double z = bc[c];
+            for (int d = 0; d < H; ++d) z += rE[size_t(r) * H + d] * Wc[size_t(c) * H + d];
+            lg[c] = z;
+            mx = std::max(mx, z);
+        }
+        double se = 0;
+        for (int c = 0; c < C; ++c) se += std::exp(lg[c] - mx);
+        std::vector<double> dl(C);
+        const int y = labels[roots[r]];
+        for (int c = 0; c < C; ++c) dl[c] = (std::exp(lg[c] - mx) / se - (c == y ? 1.0 : 0.0)) / B;
+        for (int d = 0; d < H; ++d) {
+            double z = 0;
+            for (int c = 0; c < C; ++c) z += dl[c] * Wc[size_t(c) * H + d];
+            rZ[size_t(r) * H + d] = rE[size_t(r) * H + d] > 0 ? z : 0;
+        }
+        for (int k = 0; k < K; ++k) {
+            double z = 0;
+            for (int h = 0; h < H; ++h) z += rZ[size_t(r) * H + h] * W[size_t(h) * K + k];
+            rI[size_t(r) * K + k] = z;
+        }
+        const int per = C * (H + 1);
+        for (int c = 0; c < C; ++c)
+            for (int d = 0; d <= H; ++d) rS[size_t(r / 4) * (per + 1) + c * (H + 1) + d] += dl[c] * (d < H ? rE[size_t(r) * H + d] : 1.0);
+        rS[size_t(r / 4) * (per + 1) + per] += -(lg[y] - mx - std::log(se));
+    }
+    auto check = [&](const char* tag) -> int {
+        std::vector<float> hE(B * H), hI(B * K), hZ(B * H), hS(rS.size());
         CK(hipMemcpy(hE.data(), E, B * H * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hI.data(), dIn, B * K * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hZ.data(), dZ, B * H * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hS.data(), slab, hS.size() * 4, hipMemcpyDeviceToHost));
+        auto err = [](const std::vector<float>& a, const std::vector<double>& b) {
+            double m = 0, s = 0;
+            for (size_t i = 0; i < a.size(); ++i) { m = std::max(m, std::fabs(a[i] - b[i])); s = std::max(s, std::fabs(b[i])); }
+            return std::make_pair(m, s);
+        };
+        auto e1 = err(hE, rE), e2 = err(hZ, rZ), e3 = err(hI, rI), e4 = err(hS, rS);
         unsigned long long hsh = 1469598103934665603ull;
         for (auto* v : {&hE, &hZ, &hI})
-            for (uint32_t x : *v) hsh = (hsh ^ x) * 1099511628211ull;
-        std::printf("  outputs hash %016llx\n", hsh);
+            for (float x : *v) { uint32_t u; std::memcpy(&u, &x, 4); hsh = (hsh ^ u) * 1099511628211ull; }
+        std::printf("  %s: max |err| (max |ref|): E %.2e (%.2e)  dZ %.2e (%.2e)  dIn %.2e (%.2e)  slab %.2e (%.2e)  hash %016llx\n",
+                    tag, e1.first, e1.second, e2.first, e2.second, e3.first, e3.second, e4.first, e4.second, hsh);
+        return 0;
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const int reps = 200;
+    for (int pass = 0; pass < 2; ++pass) {  // v1 / v2 / v1 / v2: alternating
+        for (int v = 0; v < 2; ++v) {
+            for (int i = 0; i < 20; ++i) v ? launch() : launch_v1();
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < reps; ++i) v ? launch() : launch_v1();
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            std::printf("%s top kernel: %.2f us per launch (back to back, %d launches)\n", v ? "v2" : "v1",
+                        ms * 1e3 / reps, reps);
+            if (pass == 0 && check(v ? "v2" : "v1")) return 2;
+        }
     }
     // stamps of one launch
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
@@ -112,8 +180,8 @@ int main(int argc, char** argv) {
         last_end = std::max(last_end, (h[b * 8 + 6] - t0) * 0.01);
         first_start = std::min(first_start, (h[b * 8] - t0) * 0.01);
     }
-    const char* names[] = {"", "dma issue + head loads + gather", "wait W2 DMA + barrier", "GEMM (E)", "loss head",
-                           "slab", "dIn GEMM"};
+    const char* names[] = {"", "dma issue + Wc + gather", "wait W2 DMA + barrier", "E (4x4x1 split-K)",
+                           "E combine + loss head", "dZ + slab", "dIn (4x4x1 split-K) + store"};
     for (int i = 1; i <= 6; ++i) std::printf("  stage %d %-32s mean %.2f us\n", i, names[i], acc[i] / nb);
     double spread = 0;
     for (int b = 0; b < nb; ++b) spread = std::max(spread, (h[b * 8] - t0) * 0.01);
