@@ -134,6 +134,24 @@ def build_workload(cfg, device, seed=824, world=1):
                 t_graph=t_graph, deg=deg, shm=shm, csr_shared=shm is not None)
 
 
+def block_stats_us(trainer, n, site):
+    """Per stamped launch of `site`: span, mean / max workgroup duration and
+    the spread of workgroup starts (us), medians over the launches; None for
+    an event-timed site."""
+    if not hasattr(gs._lib.lib(), "gs_trainer_kernel_block_stats"):  # an older library (A/B runs)
+        return None
+    out = np.zeros((max(n, 1), 4), np.float32)
+    got = int(gs._lib.lib().gs_trainer_kernel_block_stats(trainer._h, site, out.ctypes.data, n))
+    out = out[:max(got, 0)]
+    out = out[out[:, 0] >= 0]
+    if not len(out):
+        return None
+    med = np.median(out, axis=0)
+    return {"span": round(float(med[0]), 2), "workgroup_mean": round(float(med[1]), 2),
+            "workgroup_max": round(float(med[2]), 2), "start_spread": round(float(med[3]), 2),
+            "launches": int(len(out))}
+
+
 def kernel_times_ms(trainer, n, site=0):
     """Kernel-bound HIP-event durations recorded by the native step on its
     launch stream (gs_trainer_time_agg arms them): site 0 the layer-1
@@ -802,6 +820,7 @@ def main():
     thr1 = cgroup_throttle()
     st = runner.stats()
     times = {} if no_timer else {dominant: kernel_times_ms(trainer, 2 * args.steps // every, dominant)}
+    blocks = {} if no_timer else {dominant: block_stats_us(trainer, 2 * args.steps // every, dominant)}
     # calibration steps after the measured ones time the other sites (an
     # event-bound launch costs the stream a little: never inside the timed steps)
     runner.release(total_steps)
@@ -812,6 +831,7 @@ def main():
     for site in SITES:
         if site not in times:
             times[site] = kernel_times_ms(trainer, calib, site)
+            blocks[site] = block_stats_us(trainer, calib, site)
     loss = float(trainer.loss.item())
     # steady state: the remaining batches, with the sampler threads free to run
     # ahead (released since the calibration steps); reported beside `value`
@@ -913,7 +933,7 @@ def main():
                        if site in (1, 3) else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
                 timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
-                **work)
+                workgroup_us=blocks.get(site), **work)
         roof = dict(rooflines[SITE_NAMES[dominant]])
         roof["dominant_by"] = dominant_by
         cpu = None

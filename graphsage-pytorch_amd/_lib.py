@@ -137,6 +137,7 @@ _SIGS = {
     "gs_trainer_time_agg": (_i32, [_vp, _i64]),
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
+    "gs_trainer_kernel_block_stats": (_i64, [_vp, _i32, _vp, _i64]),
     "gs_trainer_time_kernels": (_i32, [_vp, _i32, _i64]),
     "gs_trainer_time_kernels_every": (_i32, [_vp, _i32, _i64, _i64]),
     "gs_trainer_kernel_name": (ctypes.c_char_p, [_vp, _i32]),
@@ -213,6 +214,11 @@ class DeviceLimit(RuntimeError):
     host path computes the same result."""
 
 
+# measurement-only entry points a bench run may do without (an A/B against a
+# library built before them); everything else must be exported
+_DIAGNOSTIC = {"gs_trainer_kernel_block_stats"}
+
+
 def lib():
     """Load (once) and return the configured ctypes library."""
     global _lib
@@ -223,7 +229,7 @@ def lib():
                 "`make -C graphsage-pytorch_amd/csrc` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)  # CDLL releases the GIL around every call
         for name, (res, args) in _SIGS.items():
-            if _ASAN_LIB and not hasattr(L, name):
+            if (_ASAN_LIB or name in _DIAGNOSTIC) and not hasattr(L, name):
                 continue  # device entry point: not in the host-only sanitizer build
             fn = getattr(L, name)
             fn.restype = res

@@ -31,7 +31,10 @@ __global__ __launch_bounds__(kBlock) void resolve_ids_kernel(int n_dst, int k, c
 // The same resolve, plus a second role for the fused top launch (top.hip):
 // the roots' hop-1 lists padded to `tk` slots behind their self row, one
 // record of 1 + tk ids per root (-1 past the list), so the top launch loads a
-// root's whole neighbourhood in one round instead of three (ptr, list, rows).
+// root's whole neighbourhood in one round instead of three (ptr, list, rows);
+// and a third for the layer-2 backward's gather (agg_bwd_rec_body): per
+// layer-1 row c, {n, beg, e0 .. e5} of its transposed hop-1 list (n_rec rows,
+// from the pack's GS_PK_TPTR / TIDX of hop 1; entries past n are 0).
 __global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, const int* __restrict__ ptr,
                                                              const int* __restrict__ ent,
                                                              const int* __restrict__ col,
@@ -39,7 +42,9 @@ __global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, c
                                                              int* __restrict__ ids, int n_top, int tk,
                                                              const int* __restrict__ tptr,
                                                              const int* __restrict__ tnbr,
-                                                             const int* __restrict__ tself, int* __restrict__ tout) {
+                                                             const int* __restrict__ tself, int* __restrict__ tout,
+                                                             int n_rec, const int* __restrict__ rptr,
+                                                             const int* __restrict__ ridx, int* __restrict__ rout) {
     const int64_t t = blockIdx.x * int64_t(kBlock) + threadIdx.x;
     const int64_t n1 = static_cast<int64_t>(n_dst) * k;
     if (t < n1) {
@@ -52,7 +57,15 @@ __global__ __launch_bounds__(kBlock) void resolve_top_kernel(int n_dst, int k, c
         return;
     }
     const int64_t u = t - n1;
-    if (u >= static_cast<int64_t>(n_top) * (tk + 1)) return;
+    const int64_t n2 = static_cast<int64_t>(n_top) * (tk + 1);
+    if (u >= n2) {  // third role: the backward's records, 8 ints per row
+        const int64_t q = u - n2;
+        if (q >= static_cast<int64_t>(n_rec) * 8) return;
+        const int c = static_cast<int>(q >> 3), j = static_cast<int>(q & 7);
+        const int b = rptr[c], n = rptr[c + 1] - b;
+        rout[q] = j == 0 ? n : j == 1 ? b : (j - 2 < n ? ridx[b + j - 2] : 0);
+        return;
+    }
     const int r = static_cast<int>(u / (tk + 1)), j = static_cast<int>(u - static_cast<int64_t>(r) * (tk + 1));
     int v;
     if (j == 0) {
@@ -198,15 +211,17 @@ void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t*
 
 void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
-                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st) {
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st, int64_t n_rec,
+                        const int32_t* rptr, const int32_t* ridx, int32_t* rout) {
     GS_REQUIRE(n_dst >= 0 && k >= 1 && n_dst * k < (int64_t(1) << 31) && n_top >= 0 && tk >= 1 &&
-                   n_top * (tk + 1) < (int64_t(1) << 30),
+                   n_top * (tk + 1) < (int64_t(1) << 30) && n_rec >= 0 && n_rec < (int64_t(1) << 27) &&
+                   (n_rec == 0 || (rptr && ridx && rout)),
                GS_EINVAL, "bad sizes");
-    const int64_t total = n_dst * k + n_top * (tk + 1);
+    const int64_t total = n_dst * k + n_top * (tk + 1) + n_rec * 8;
     if (total == 0) return;
     resolve_top_kernel<<<dim3(static_cast<unsigned>((total + kBlock - 1) / kBlock)), kBlock, 0, st>>>(
         static_cast<int>(n_dst), k, ptr, ent, col, dst_ids, gcn, ids, static_cast<int>(n_top), tk, tptr, tnbr, tself,
-        tout);
+        tout, static_cast<int>(n_rec), rptr, ridx, rout);
     check_launch("resolve_top");
 }
 

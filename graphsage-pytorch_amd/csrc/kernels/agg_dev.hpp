@@ -234,6 +234,96 @@ __device__ __forceinline__ void agg_bwd_body(
     }
 }
 
+// The same backward from per-row records written a step ahead by the side
+// stream (resolve_top_kernel's third role): int4 pair {n, beg, e0 .. e5} per
+// source row c = its transposed-list length, offset and first six entries.
+// The record and the row's relu-mask quad load in one round, the entries'
+// rows (+ MEAN counts / MAX argmax) in the next; entries past the sixth
+// (hub rows) follow one at a time from tidx.  Entries are added in list order
+// with agg_bwd_body's expressions: bitwise its result.
+constexpr int kTrec = 6;  // entries inline in a record
+template <int OP, int VEC, int G>
+__device__ __forceinline__ void agg_bwd_rec_body(
+    int bx, int n_src, int F, const int4* __restrict__ rec, const int* __restrict__ tidx,
+    const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
+    int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
+    float* __restrict__ dH) {
+    const int gl = threadIdx.x % G;
+    const int c = bx * (kBlock / G) + threadIdx.x / G;
+    if (c >= n_src) return;
+    const int4 ra = rec[2 * static_cast<int64_t>(c)], rb = rec[2 * static_cast<int64_t>(c) + 1];
+    const int n = ra.x, beg = ra.y;
+    const int e[kTrec] = {ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+    for (int f0 = gl * VEC; f0 < ((F + G * VEC - 1) / (G * VEC)) * G * VEC; f0 += G * VEC) {
+        const bool act = f0 < F;
+        const int f0c = act ? f0 : 0;
+        float h[VEC];
+        if (Hprev) RowIO<float, VEC>::load(Hprev + static_cast<int64_t>(c) * ldh + f0c, h);
+        float g[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) g[v] = 0.f;
+        float x[kTrec][VEC], w[kTrec];
+        int am[kTrec][VEC];
+#pragma unroll
+        for (int u = 0; u < kTrec; ++u) {
+            const int eu = e[u];
+            const bool self_e = eu < 0;
+            const int row = self_e ? -eu - 1 : eu;
+            const float* src = (self_e && dSelf) ? dSelf : dA;
+            RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
+            if (OP == GS_AGG_MEAN) {
+                const int re = self_e ? 0 : eu;
+                w[u] = 1.0f / static_cast<float>(ptr[re + 1] - ptr[re]);
+            } else {
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) am[u][v] = argmax[static_cast<int64_t>(self_e ? 0 : eu) * F + f0c + v];
+            }
+        }
+        if (!act) continue;
+#pragma unroll
+        for (int u = 0; u < kTrec; ++u) {
+            if (u >= n) break;
+            if (e[u] < 0) {
+                if (!dSelf) continue;  // gcn: self rows feed no linear input
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += x[u][v];
+            } else if (OP == GS_AGG_MEAN) {
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += x[u][v] * w[u];
+            } else {
+#pragma unroll
+                for (int v = 0; v < VEC; ++v)
+                    if (am[u][v] == c) g[v] += x[u][v];
+            }
+        }
+        for (int t = beg + kTrec; t < beg + n; ++t) {  // hub rows: the rest of the list
+            const int et = tidx[t];
+            float xt[VEC];
+            if (et < 0) {
+                if (!dSelf) continue;
+                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0, xt);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += xt[v];
+            } else if (OP == GS_AGG_MEAN) {
+                const float wt = 1.0f / static_cast<float>(ptr[et + 1] - ptr[et]);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) g[v] += xt[v] * wt;
+            } else {
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
+#pragma unroll
+                for (int v = 0; v < VEC; ++v)
+                    if (argmax[static_cast<int64_t>(et) * F + f0 + v] == c) g[v] += xt[v];
+            }
+        }
+        if (Hprev) {
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) g[v] = h[v] > 0.f ? g[v] : 0.f;
+        }
+        RowIO<float, VEC>::store(dH + static_cast<int64_t>(c) * ldh + f0, g);
+    }
+}
+
 template <int OP, int VEC, int G>
 __global__ __launch_bounds__(kBlock) void agg_bwd_kernel(
     int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,

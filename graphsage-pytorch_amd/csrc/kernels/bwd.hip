@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_a_kernel(BwdA a) {
     if (b < a.dw_nb) {
         const int g2 = a.dw_gx * a.dw_gy;
         linear_dw_body<float, HAS_SELF, false, true, ZVEC>(b % a.dw_gx, (b % g2) / a.dw_gx, b / g2, a.n, a.F, a.H,
-                                                           a.K, a.rps, a.Xs, a.ldxs, a.sidx, a.A, a.F, a.dZ,
+                                                           a.K, a.rps, a.Xs, a.ldxs, a.sidx, a.A, a.lda, a.dZ,
                                                            nullptr, a.H, a.target,
                                                            static_cast<int64_t>(a.H) * a.K);
         return;
@@ -59,6 +59,7 @@ struct BwdB {
     const int* argmax;
     const float* Hprev;
     float* dH;
+    const int4* rec = nullptr;  // agg_bwd_rec_body's records (layer_bwd_top only)
 };
 
 template <int OP, int G>
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
         const int g2 = t.a.dw_gx * t.a.dw_gy;
         linear_dw_body<float, true, false, true, true>(b % t.a.dw_gx, (b % g2) / t.a.dw_gx, b / g2, t.a.n, t.a.F,
                                                        t.a.H, t.a.K, t.a.rps, t.a.Xs, t.a.ldxs, t.a.sidx, t.a.A,
-                                                       t.a.F, t.a.dZ, nullptr, t.a.H, t.a.target,
+                                                       t.a.lda, t.a.dZ, nullptr, t.a.H, t.a.target,
                                                        static_cast<int64_t>(t.a.H) * t.a.K);
         return;
     }
@@ -95,15 +96,19 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
         return;
     }
     b -= t.cls_nb;
-    agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd, t.b.argmax,
-                           t.b.Hprev, t.b.F, t.b.dH);
+    if (t.b.rec)
+        agg_bwd_rec_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.rec, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
+                                   t.b.argmax, t.b.Hprev, t.b.F, t.b.dH);
+    else
+        agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
+                               t.b.argmax, t.b.Hprev, t.b.F, t.b.dH);
 }
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
 
 bool layer_bwd_fusable(const LayerBwd& a) {
     const int64_t K = a.Xs ? 2 * a.fin : a.fin;
-    const bool al = aligned16(a.A) && aligned16(a.dZ) && aligned16(a.W) && aligned16(a.dW) && aligned16(a.slabs) &&
+    const bool al = (a.lda == 0 || (a.lda >= a.fin && a.lda % 4 == 0)) && aligned16(a.A) && aligned16(a.dZ) && aligned16(a.W) && aligned16(a.dW) && aligned16(a.slabs) &&
                     aligned16(a.dIn) && aligned16(a.dH) && aligned16(a.Hprev) && (!a.Xs || aligned16(a.Xs));
     const int G = pick_group(static_cast<int>(a.H), 4);
     return al && a.fin == a.H && a.H % 16 == 0 && a.H <= 256 && K % 4 == 0 && a.ldxs % 4 == 0 && a.n >= 1 &&
@@ -128,6 +133,7 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     A.ldxs = a.ldxs;
     A.sidx = a.sidx;
     A.A = a.A;
+    A.lda = a.lda > 0 ? a.lda : a.fin;
     A.dZ = a.dZ;
     A.target = S > 1 ? a.slabs : a.dW;
     A.dw_gx = static_cast<int>((K + 63) / 64);
@@ -214,6 +220,7 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     A.ldxs = a.ldxs;
     A.sidx = a.sidx;
     A.A = a.A;
+    A.lda = a.lda > 0 ? a.lda : a.fin;
     A.dZ = a.dZ;
     A.target = S > 1 ? a.slabs : a.dW;
     A.dw_gx = static_cast<int>((K + 63) / 64);
@@ -241,6 +248,7 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     Bq.argmax = a.argmax;
     Bq.Hprev = a.Hprev;
     Bq.dH = a.dH;
+    Bq.rec = a.trec;
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
     const dim3 grid(static_cast<unsigned>(A.dw_nb + t.cls_nb + agg_nb));

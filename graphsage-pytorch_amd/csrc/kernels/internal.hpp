@@ -73,10 +73,13 @@ int sum_slabs_grid(int64_t len);
 void resolve_ids_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, hipStream_t st);
 // resolve_ids_launch plus the fused top launch's padded hop-1 records
-// (tout[r][0] = self, [1..tk] = the list, -1 past it; n_top roots).
+// (tout[r][0] = self, [1..tk] = the list, -1 past it; n_top roots) and, with
+// n_rec > 0, the layer-2 backward's per-row records of the transposed hop-1
+// lists (rout[c] = {n, beg, e0 .. e5}, agg_bwd_rec_body; n_rec = |L1|).
 void resolve_top_launch(int64_t n_dst, int k, const int32_t* ptr, const int32_t* ent, const int32_t* col,
                         const int32_t* dst_ids, int gcn, int32_t* ids, int64_t n_top, int tk, const int32_t* tptr,
-                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st);
+                        const int32_t* tnbr, const int32_t* tself, int32_t* tout, hipStream_t st, int64_t n_rec = 0,
+                        const int32_t* rptr = nullptr, const int32_t* ridx = nullptr, int32_t* rout = nullptr);
 // Padded hop-1 records for the fused top launch, one buffer per gather slot
 // (2-layer training steps; B roots, fanout tk <= 31).
 void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk);
@@ -109,7 +112,8 @@ struct LayerBwd {
     const float* Xs;                      // self rows source (nullptr: gcn), row stride ldxs
     int64_t ldxs;
     const int32_t* sidx;                  // self row of each output row
-    const float* A;                       // aggregate [n][fin]
+    const float* A;                       // aggregate [n][fin], row stride lda (0: fin)
+    int64_t lda = 0;
     const float* dZ;                      // [n][H], already masked by relu'
     const float* W;                       // [H][K]
     float* dW;                            // [H][K] gradient
@@ -122,6 +126,7 @@ struct LayerBwd {
     const int32_t* tidx;
     const int32_t* ptr;                   // forward neighbourhood offsets (mean weights)
     const int32_t* argmax;                // MAX routing, [n][H]
+    const int4* trec = nullptr;           // optional per-source records (agg_bwd_rec_body), n_src rows
     const float* Hprev;                   // previous layer's output (relu mask), [n_src][H]
     float* dH;                            // [n_src][H] gradient of the previous layer's output (masked)
     bool din_ready = false;               // dIn already written (top.hip): launch A skips its dIn role
@@ -147,6 +152,7 @@ struct BwdA {
     int64_t ldxs;
     const int* sidx;
     const float* A;
+    int64_t lda;    // A's row stride (F, or 2F for the top path's dense [self | agg] rows)
     const float* dZ;
     float* target;  // dW slabs (or dW itself when S == 1)
     int dw_gx, dw_gy, dw_nb;
@@ -172,6 +178,8 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
 
 // top.hip: a 2-layer model's layer 2 forward (aggregate + linear + relu), the
 // loss head and the layer's dIn in one launch (one block per 4 roots).
+// aggo receives each root's dense [self | agg] input row (2H floats: the
+// layer-2 weight gradient then reads no self index).
 // Returns the number of classifier partial slabs written (the loss head's).
 bool top_supported(int64_t H, int64_t C, bool gcn);
 // tids: optional padded hop-1 records (resolve_top_launch, 1 + tk ids per

@@ -56,6 +56,25 @@ __device__ __forceinline__ uint4 concat_slot(const T* srow, const T* arow, int F
     }
 }
 
+// concat_slot's load alone (VLOAD layout): the address clamped into the row,
+// no select on the value.  A select right after a load lets the compiler turn
+// it into an exec-masked load in its own basic block, and the wait-count pass
+// then drains every load in flight (vmcnt(0)) at the next use of any of them:
+// the K loop's prefetch ring would be gone.  Callers zero slots at and past K
+// when they stash them (slot_in_range).
+template <typename T, bool HAS_SELF>
+__device__ __forceinline__ uint4 concat_slot_raw(const T* srow, const T* arow, int F, int K, int k) {
+    const int kk = k < K ? k : 0;
+    const T* p = (HAS_SELF && kk < F) ? srow + kk : arow + (HAS_SELF ? kk - F : kk);
+    return *reinterpret_cast<const uint4*>(p);
+}
+
+__device__ __forceinline__ uint4 slot_in_range(uint4 v, int k, int K) {
+    const bool in = k < K;
+    v.x = in ? v.x : 0u; v.y = in ? v.y : 0u; v.z = in ? v.z : 0u; v.w = in ? v.w : 0u;
+    return v;
+}
+
 // 4 consecutive elements of the concat row as floats (dW operand).
 template <typename T, bool HAS_SELF, bool VLOAD>
 __device__ __forceinline__ float4 concat_quad(const T* srow, const T* arow, int F, int K, int k) {
@@ -396,41 +415,50 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     uint4 ar[kFwdAhead], wr_[kFwdAhead][WQ];
     auto load = [&](int c, int u) {
         const int kn = min(c, nC - 1) * BK;  // past the end: re-read the last chunk (never stored)
-        ar[u] = concat_slot<T, HAS_SELF, true>(srow, arow, F, K, kn + ls * EPV);
+        ar[u] = concat_slot_raw<T, HAS_SELF>(srow, arow, F, K, kn + ls * EPV);
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot<T, false, true>(nullptr, wrow[q], K, K, kn + ls * EPV);
+        for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot_raw<T, false>(nullptr, wrow[q], K, K, kn + ls * EPV);
     };
     auto stash = [&](int c, int u) {
-        sA[c & 1][lr * SP + ls] = ar[u];
+        const int k = c * BK + ls * EPV;  // slots at and past K are zeros (both operands)
+        sA[c & 1][lr * SP + ls] = slot_in_range(ar[u], k, K);
 #pragma unroll
         for (int q = 0; q < WQ; ++q)
-            if (64 % ROWS == 0 || lr + ROWS * q < 64) sW[c & 1][(lr + ROWS * q) * SP + ls] = wr_[u][q];
+            if (64 % ROWS == 0 || lr + ROWS * q < 64) sW[c & 1][(lr + ROWS * q) * SP + ls] = slot_in_range(wr_[u][q], k, K);
     };
     auto run_k = [&]() -> f32x4 {
 #pragma unroll
         for (int u = 0; u < kFwdAhead; ++u) load(u, u);
         stash(0, 0);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        // Every load and stash is unconditional (past the end: the last
+        // chunk's slots re-read, zeros stored into a buffer no wave reads
+        // again); only the MFMAs of a chunk past the end are skipped.  A
+        // guarded stash lets the compiler sink the slot's load into the
+        // guarded block, next to its use, and a loop exit between the ring's
+        // loads leaves paths with different loads in flight, which the
+        // wait-count pass merges into a full drain at the loop head.
         for (int cb = 0; cb < nC; cb += kFwdAhead) {
 #pragma unroll
             for (int u = 0; u < kFwdAhead; ++u) {
                 const int c = cb + u;
-                if (c >= nC) break;
                 __syncthreads();
                 load(c + kFwdAhead, u);
                 __builtin_amdgcn_sched_barrier(0);
-                const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
-                const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
-                uint4 av[4], wv[4];
+                if (kFwdAhead == 1 || c < nC) {
+                    const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
+                    const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
+                    uint4 av[4], wv[4];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    av[g] = ta[4 * g + kq];
-                    wv[g] = tw[4 * g + kq];
+                    for (int g = 0; g < 4; ++g) {
+                        av[g] = ta[4 * g + kq];
+                        wv[g] = tw[4 * g + kq];
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
                 }
-#pragma unroll
-                for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
                 __builtin_amdgcn_sched_barrier(0);
-                if (c + 1 < nC) stash(c + 1, (u + 1) % kFwdAhead);
+                stash(c + 1, (u + 1) % kFwdAhead);
             }
         }
         return acc;

@@ -57,6 +57,11 @@ struct gs_trainer {
     bool top_ready[kSlots] = {};
     int64_t top_rows = 0;
     int top_k = 0;
+    // per gather slot, the layer-2 backward's records of the transposed hop-1
+    // lists (8 ints per layer-1 row, rec_rows rows; written with the top records)
+    int32_t* rec_slot[kSlots] = {};
+    int64_t rec_rows = 0;
+    bool rec_ready[kSlots] = {};
     // clip-norm partials produced by the fused backward's reduce launches
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
@@ -127,6 +132,8 @@ struct gs_trainer {
         for (int32_t* p : ids_slot)
             if (p) (void)hipFree(p);
         for (int32_t* p : top_slot)
+            if (p) (void)hipFree(p);
+        for (int32_t* p : rec_slot)
             if (p) (void)hipFree(p);
         for (auto& tm : timer)
             if (tm.st0) (void)hipFree(tm.st0);
@@ -229,6 +236,8 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     const int64_t n_top = hop_sizes[0];
     T.top_ready[slot] = T.top_k > 0 && L == 2 && !c.gcn && n_top <= T.top_rows && T.top_slot[slot] &&
                         hop_sizes[3] <= n_top * T.top_k;  // every root's list fits tk slots
+    const int64_t n_rec = hop_sizes[2];  // |L1|: hop 1's sources
+    T.rec_ready[slot] = T.top_ready[slot] && T.rec_slot[slot] && n_rec <= T.rec_rows;
     if (T.top_ready[slot]) {
         auto f1 = [&](int f) -> const int32_t* {
             const int64_t o = offsets[f];  // hop 1
@@ -236,7 +245,8 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             return pack + o;
         };
         resolve_top_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
-                           n_top, T.top_k, f1(GS_PK_NBR_PTR), f1(GS_PK_NBR), f1(GS_PK_SELF), T.top_slot[slot], st);
+                           n_top, T.top_k, f1(GS_PK_NBR_PTR), f1(GS_PK_NBR), f1(GS_PK_SELF), T.top_slot[slot], st,
+                           T.rec_ready[slot] ? n_rec : 0, f1(GS_PK_TPTR), f1(GS_PK_TIDX), T.rec_slot[slot]);
     } else {
         resolve_ids_launch(n_dst, T.k_ids, fld(GS_PK_POS_PTR), fld(GS_PK_POS), c.col, fld(GS_PK_DST_IDS), c.gcn, ids,
                            st);
@@ -295,7 +305,9 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 agg[0] = cv.take<char>(rows[0] * F * static_cast<int64_t>(xsz));
             }
         }
-        else agg[l - 1] = cv.take<float>(rows[l - 1] * H);
+        // layer 2 of a 2-layer step: [self | agg] rows of 2H (the top launch writes
+        // them dense, so the layer-2 weight gradient reads no self index)
+        else agg[l - 1] = cv.take<float>(rows[l - 1] * (L == 2 ? 2 * H : H));
         h[l - 1] = (embed_out && l == L) ? embed_out : cv.take<float>(rows[l - 1] * H);
         if (l == L) T.last_emb = h[l - 1];
         if (l >= 2 && c.agg == GS_AGG_MAX) am[l - 1] = cv.take<int32_t>(rows[l - 1] * H);
@@ -432,6 +444,13 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             a.ldxs = H;
             a.sidx = fld(j, GS_PK_SELF);
             a.A = static_cast<const float*>(agg[l - 1]);
+            if (top && l == L) {  // the top launch's dense [self | agg] rows: no self index
+                a.Xs = static_cast<const float*>(agg[l - 1]);
+                a.ldxs = 2 * H;
+                a.sidx = nullptr;
+                a.A = static_cast<const float*>(agg[l - 1]) + H;
+                a.lda = 2 * H;
+            }
             a.dZ = l == L ? demb : dbuf[flip_f ^ 1];
             a.W = P + T.w_off[l - 1];
             a.dW = G + T.w_off[l - 1];
@@ -446,6 +465,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             a.argmax = am[l - 1];
             a.Hprev = h[l - 2];
             a.dH = dbuf[flip_f];
+            if (top && l == L && a1_slot >= 0 && T.rec_ready[a1_slot])  // the side stream's records of hop 1's lists
+                a.trec = reinterpret_cast<const int4*>(T.rec_slot[a1_slot]);
             flip_f ^= 1;
             fusable = fusable && layer_bwd_fusable(a);
             lb.push_back(a);
@@ -625,6 +646,15 @@ void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk) {
     for (bool& r : t->top_ready) r = false;
     t->top_rows = B;
     t->top_k = tk;
+    // the backward's records for up to a1_rows layer-1 rows (gs_trainer_gather_reserve first)
+    for (int32_t*& p : t->rec_slot) {
+        if (p) GS_REQUIRE(hipFree(p) == hipSuccess, GS_EHIP, "hipFree");
+        p = nullptr;
+        GS_REQUIRE(hipMalloc(&p, std::max<int64_t>(t->a1_rows * 8 * 4, 256)) == hipSuccess, GS_ENOMEM,
+                   "hipMalloc(backward records)");
+    }
+    for (bool& r : t->rec_ready) r = false;
+    t->rec_rows = t->a1_rows;
 }
 
 int64_t trainer_w1_floats(const gs_trainer* t) { return t->w_rows[0] * t->w_cols[0]; }
@@ -970,6 +1000,48 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
         }
         if (hipEventSynchronize(tm.ev1[i]) != hipSuccess || hipEventElapsedTime(&ms[i], tm.ev0[i], tm.ev1[i]) != hipSuccess)
             return -1;
+    }
+    return n;
+}
+
+int64_t gs_trainer_kernel_block_stats(gs_trainer* t, int32_t site, float* us4, int64_t cap) {
+    if (!t || !us4 || site < 0 || site >= gs_trainer::kSites) return -1;
+    auto& tm = t->timer[site];
+    const int64_t n = std::min(cap, tm.n);
+    const int64_t W = gs::kStampBlocks;
+    if (n <= 0) return 0;
+    if (!tm.st0) {  // an event-timed site
+        std::fill(us4, us4 + 4 * n, -1.f);
+        return n;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    std::vector<unsigned long long> a(n * W), b(n * W);
+    if (hipMemcpy(a.data(), tm.st0, n * W * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(b.data(), tm.st1, n * W * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    for (int64_t i = 0; i < n; ++i) {
+        float* o = us4 + 4 * i;
+        o[0] = o[1] = o[2] = o[3] = -1.f;
+        if (!tm.stamped[i]) continue;
+        unsigned long long lo = ~0ull, hi = 0, slo = ~0ull, shi = 0, dmax = 0;
+        double dsum = 0;
+        int64_t nb = 0;
+        for (int64_t w = 0; w < W; ++w) {
+            const unsigned long long s = a[i * W + w], e = b[i * W + w];
+            if (!s || e < s) continue;  // a workgroup past the stamp table, or none
+            lo = std::min(lo, s);
+            hi = std::max(hi, e);
+            slo = std::min(slo, s);
+            shi = std::max(shi, s);
+            dmax = std::max(dmax, e - s);
+            dsum += static_cast<double>(e - s);
+            ++nb;
+        }
+        if (!nb) continue;
+        o[0] = static_cast<float>((hi - lo) * 1e-2);  // 100 MHz ticks -> us
+        o[1] = static_cast<float>(dsum / nb * 1e-2);
+        o[2] = static_cast<float>(dmax * 1e-2);
+        o[3] = static_cast<float>((shi - slo) * 1e-2);
     }
     return n;
 }

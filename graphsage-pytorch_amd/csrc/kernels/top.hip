@@ -56,7 +56,7 @@ struct TopArgs {
     const float* bc;
     const int* labels;
     const int* roots;
-    float* agg;          // [B][H]
+    float* agg;          // [B][2H]: each root's [self | agg] row (layer 2's dense GEMM input)
     int* argmax;         // [B][H] (MAX)
     float* E;            // h2 [B][H]
     float* dZ;           // [B][H], masked by relu'(E)
@@ -200,7 +200,8 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             *reinterpret_cast<float4*>(&sX[g][f0]) = xs;
             const float4 av = make_float4(acc[0], acc[1], acc[2], acc[3]);
             *reinterpret_cast<float4*>(&sX[g][H + f0]) = av;
-            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * H + f0) = av;
+            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * K + f0) = xs;
+            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * K + H + f0) = av;
             if (OP == GS_AGG_MAX)
                 *reinterpret_cast<int4*>(a.argmax + static_cast<int64_t>(r) * H + f0) = make_int4(am[0], am[1], am[2],
                                                                                                    am[3]);

@@ -560,6 +560,11 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity);
 int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capacity, int64_t every);
 int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap);
+/* For a stamped site (the forward GEMM, the top launch): per timed launch,
+ * four floats in us — span (first workgroup start .. last end), mean and max
+ * workgroup duration, and the spread of workgroup starts; -1 for a launch
+ * timed by events.  Returns the launches written, -1 on error. */
+int64_t gs_trainer_kernel_block_stats(gs_trainer* t, int32_t site, float* us4, int64_t cap);
 /* Demangled name of the kernel timer site `site` timed since it was last
  * armed ("" before its first timed launch) — the variant actually launched. */
 const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site);

@@ -70,7 +70,8 @@ int main(int argc, char** argv) {
     }
     int* dtids;
     up(tids, &dtids);
-    CK(hipMalloc(&agg, B * H * 4)); CK(hipMalloc(&E, B * H * 4)); CK(hipMalloc(&dZ, B * H * 4));
+    CK(hipMalloc(&agg, B * K * 4));  // [self | agg] rows (v1 writes the agg half only)
+    CK(hipMalloc(&E, B * H * 4)); CK(hipMalloc(&dZ, B * H * 4));
     CK(hipMalloc(&dIn, B * K * 4)); CK(hipMalloc(&slab, (B / 4 + 1) * (C * (H + 1) + 1) * 4));
     unsigned long long* st;
     const int nb = (B + 3) / 4;
