@@ -930,7 +930,7 @@ def main():
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
                 timer=("kernel span (per-workgroup s_memrealtime stamps, min start .. max end)"
-                       if site in (1, 3) else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
+                       if site in (1, 2, 3) else "kernel-bound HIP events (hipExtLaunchKernelGGL)"),
                 timed_in=(f"{len(tt)} of the measured steps of both windows (one in {every})" if site == dominant else f"{calib} calibration steps after them"),
                 warmup_median_us=round(float(np.median(warm[site])) * 1e3, 2) if len(warm[site]) else None,
                 workgroup_us=blocks.get(site), **work)

@@ -97,6 +97,19 @@ __device__ __forceinline__ void block_sum_to(float v, float* dst) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Compute units of the current device (256 on MI355X), cached per thread.
+inline int device_cus() {
+    thread_local int dev = -1, cus = 256;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return cus;
+    if (d != dev) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && c > 0) cus = c;
+        dev = d;
+    }
+    return cus;
+}
+
 inline void check_launch(const char* what) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) fail(GS_EHIP, std::string(what) + ": " + hipGetErrorString(e));

@@ -159,27 +159,44 @@ int gs_sage_linear_fwd(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void*
                           sp.np1 <= 512 && sp.up_hi > sp.up_lo),
                GS_EINVAL, "pending update: bad forward");
     if (vload) {
-        // 32-row W-in-LDS tiles (bitwise the chunked kernel's sums: same MFMA
-        // operands in the same order; in-step at rmat2m the step ran
-        // 80.2-80.7 us against 82.3-82.4 us with the 16-row chunked kernel,
-        // which stays for operands the 16-B loads cannot take).
+        // W-in-LDS tiles (bitwise the chunked kernel's sums: same MFMA operands
+        // in the same order, whatever the row tiling), rows balanced over one
+        // workgroup per CU and column tile (FwdRows): each workgroup takes
+        // base or base + 1 row tiles of 16, at most 4
         sp.stamp = take_kernel_stamp();  // a timed launch: the kernel stores its own span
-        constexpr int R = 32;
+        const int64_t tiles = (n + 15) / 16, gy = (H + 63) / 64;
+        int64_t groups = std::max<int64_t>(1, device_cus() / gy);
+        int64_t per = (tiles + groups - 1) / groups;
+        if (per > 4) {  // more than 64 rows per CU: a whole number of workgroups per CU
+            groups *= (per + 3) / 4;
+            per = (tiles + groups - 1) / groups;
+        }
+        if (tiles <= groups) {
+            per = 1;
+            groups = tiles;
+        }
+        FwdRows rs;
+        rs.base = static_cast<int>(tiles / groups);
+        rs.extra = static_cast<int>(tiles % groups);
+        rs.groups = static_cast<int>(groups);
         // XCD map (a 1-D grid, the kernel derives its tile): the column tiles of
-        // a row tile share an XCD's L2 (PMC fabric reads 18.8 -> 10.9 MB per launch)
-        const int64_t gx = (n + R - 1) / R, gy = (H + 63) / 64;
-        const dim3 gw = gy == 1 ? dim3(static_cast<unsigned>(gx))
-                                : dim3(static_cast<unsigned>((gx + 7) / 8 * 8 * gy));
-#define GS_LFWDW(TT, SELF, RELU_, PEND)                                                                     \
+        // a row group share an XCD's L2 (PMC fabric reads 18.8 -> 10.9 MB per launch)
+        const dim3 gw = gy == 1 ? dim3(static_cast<unsigned>(groups))
+                                : dim3(static_cast<unsigned>((groups + 7) / 8 * 8 * gy));
+#define GS_LFWDW(TT, R, SELF, RELU_, PEND)                                                                  \
         launch_k(linear_fwd_wide_kernel<TT, R, SELF, RELU_, PEND>, gw, dim3(R * 16), 0, st, nn, ff, hh, K,   \
                  static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda,                       \
-                 static_cast<const TT*>(Wd), out, ldo, sp)
-#define GS_LFWDW_R(TT)                                                                                   \
-        do { if (sp.on) GS_LFWDW(TT, true, true, true);                                                  \
-             else if (self) { if (relu) GS_LFWDW(TT, true, true, false); else GS_LFWDW(TT, true, false, false); } \
-             else { if (relu) GS_LFWDW(TT, false, true, false); else GS_LFWDW(TT, false, false, false); } } while (0)
-        if (dt == GS_F32) GS_LFWDW_R(float);
-        else GS_LFWDW_R(bf16_t);
+                 static_cast<const TT*>(Wd), out, ldo, rs, sp)
+#define GS_LFWDW_R(TT, R)                                                                                \
+        do { if (sp.on) GS_LFWDW(TT, R, true, true, true);                                               \
+             else if (self) { if (relu) GS_LFWDW(TT, R, true, true, false); else GS_LFWDW(TT, R, true, false, false); } \
+             else { if (relu) GS_LFWDW(TT, R, false, true, false); else GS_LFWDW(TT, R, false, false, false); } } while (0)
+#define GS_LFWDW_T(TT)                                                                                   \
+        do { switch (per) { case 1: GS_LFWDW_R(TT, 16); break; case 2: GS_LFWDW_R(TT, 32); break;        \
+                            case 3: GS_LFWDW_R(TT, 48); break; default: GS_LFWDW_R(TT, 64); } } while (0)
+        if (dt == GS_F32) GS_LFWDW_T(float);
+        else GS_LFWDW_T(bf16_t);
+#undef GS_LFWDW_T
 #undef GS_LFWDW_R
 #undef GS_LFWDW
         check_launch("gs_sage_linear_fwd(wide)");
@@ -256,10 +273,11 @@ int linear_dw_slabs(gs_dtype dt, int64_t n, int64_t F, int64_t H, const void* Xs
     // workgroups mapped XCD by XCD: every tile of slab z on XCD z % 8 (PMC HBM
     // bytes 35.2 -> 19.4 MB per launch: dZ no longer fetched by all 8 XCDs)
     const dim3 grid_x(static_cast<unsigned>(kXcds * tiles * ((S + kXcds - 1) / kXcds)));
+    const KStamp ks = take_kernel_stamp();  // a timed launch: the kernel stores its own span
 #define GS_LDW2(TT, SELF, RELU, VL, ZV, PH)                                                                   \
     launch_k(linear_dw_xcd_kernel<TT, SELF, RELU, VL, ZV, PH>, grid_x, dim3(kThreads * PH), 0, st, nn, ff, hh, kk, \
              rps, gx, tiles, S, static_cast<const TT*>(Xs), ldxs, sidx, static_cast<const TT*>(A), lda, dout, \
-             out, ldo, target, H * K)
+             out, ldo, target, H * K, ks)
 #define GS_LDW1(TT, SELF, RELU, VL, ZV) \
     do { if (phases == 2) GS_LDW2(TT, SELF, RELU, VL, ZV, 2); else GS_LDW2(TT, SELF, RELU, VL, ZV, 1); } while (0)
 #define GS_LDW_Z(TT, SELF, RELU, VL) \

@@ -344,11 +344,20 @@ __device__ __forceinline__ bool fwd_pending_rest(const FwdSpec& sp, int64_t i0, 
 
 // W is not __restrict__: with PEND a recomputed W1 is written into W's buffer
 // (sp.Wn) and read back through W by the second K loop.
+// Row split of the wide forward: `groups` workgroups per column tile, the
+// first `extra` of them take base + 1 row tiles of 16, the rest base (the
+// launcher sizes groups to one workgroup per CU, so no CU runs two while
+// others idle: with fixed 32-row tiles 276 workgroups on 256 CUs left 20 CUs
+// with two, and the launch waited ~1.5x a workgroup's time for them).
+struct FwdRows {
+    int base = 0, extra = 0, groups = 0;
+};
+
 template <typename T, int ROWS, bool HAS_SELF, bool RELU, bool PEND = false>
 __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* W, float* __restrict__ out, int64_t ldo,
-    FwdSpec sp) {
+    FwdRows rs, FwdSpec sp) {
     kstamp_begin(sp.stamp);
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
@@ -371,7 +380,8 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         bx = (b / (8 * gy)) * 8 + (b & 7);
         by = (b >> 3) % gy;
     }
-    const int m0 = bx * ROWS, c0 = by * 64;
+    const int nt = rs.base + (bx < rs.extra ? 1 : 0);  // row tiles of this workgroup (<= RT)
+    const int m0 = 16 * (bx * rs.base + min(bx, rs.extra)), c0 = by * 64;
     // PEND: the pending update's loads before the first chunk's, branch-free
     // (the launcher guarantees 1 <= np0, np1 <= 512: clip_fold's one round),
     // so the fold's waits count past the K chunks' loads: the norm partials
@@ -397,13 +407,13 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
                      4 * ui0 >= sp.grp1_lo ? mm1 : mm0, sp.lr);
         return fwd_pending_rest(sp, ui0, mm0, mm1, H, K, c0);
     };
-    if (m0 >= n) {  // spare blocks of the last group of 8 (they still take their share of the update)
+    if (bx >= rs.groups || m0 >= n) {  // spare blocks of the last group of 8 (they still take their share of the update)
         if constexpr (PEND) pending_apply();
         kstamp_end(sp.stamp);
         return;
     }
     const int lr = tid >> 4, ls = tid & 15;  // this thread's load: row lr (+ ROWS·q of W), slot ls
-    const int arow_i = min(m0 + lr, n - 1);
+    const int arow_i = min(m0 + min(lr, 16 * nt - 1), n - 1);  // rows past this workgroup's: its last one
     const T* arow = A + static_cast<int64_t>(arow_i) * lda;
     const T* srow = HAS_SELF ? Xs + static_cast<int64_t>(sidx ? sidx[arow_i] : arow_i) * ldxs : nullptr;
     const T* wrow[WQ];
@@ -445,7 +455,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
                 __syncthreads();
                 load(c + kFwdAhead, u);
                 __builtin_amdgcn_sched_barrier(0);
-                if (kFwdAhead == 1 || c < nC) {
+                if ((kFwdAhead == 1 || c < nC) && wr < nt) {
                     const uint4* ta = sA[c & 1] + (16 * wr + r) * SP;
                     const uint4* tw = sW[c & 1] + (16 * wc + r) * SP;
                     uint4 av[4], wv[4];
@@ -471,7 +481,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         if (pending_apply()) acc = run_k();
     }
     const int col = c0 + 16 * wc + r;
-    if (col < H) {
+    if (col < H && wr < nt) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = m0 + 16 * wr + 4 * kq + j;
@@ -663,7 +673,8 @@ __global__ __launch_bounds__(kThreads * PH) void linear_dw_xcd_kernel(
     int n, int F, int H, int K, int rows_per_split, int gx, int tiles, int S, const T* __restrict__ Xs,
     int64_t ldxs, const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda,
     const float* __restrict__ dout, const float* __restrict__ out, int64_t ldo, float* __restrict__ dst,
-    int64_t split_stride) {
+    int64_t split_stride, KStamp ks) {
+    kstamp_begin(ks);
     const int w = blockIdx.x;
     const int j = w / kXcds;
     const int z = w % kXcds + kXcds * (j / tiles);
@@ -671,6 +682,7 @@ __global__ __launch_bounds__(kThreads * PH) void linear_dw_xcd_kernel(
     const int t = j % tiles;
     linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC, PH>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx,
                                                        A, lda, dout, out, ldo, dst, split_stride);
+    kstamp_end(ks);  // a timed launch's span (phase 1 of PH = 2 joins after handing its sums over)
 }
 
 

@@ -951,7 +951,7 @@ int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capa
         if (tm.st0) (void)hipFree(tm.st0);
         tm.st0 = tm.st1 = nullptr;
         tm.stamped.assign(cap, 0);
-        if ((s == 1 || s == 3) && cap > 0) {  // span stamps
+        if (s >= 1 && s <= 3 && cap > 0) {  // span stamps (forward, dW, top)
             const int64_t words = cap * gs::kStampBlocks;
             GS_REQUIRE(hipMalloc(&tm.st0, 2 * words * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
                        "hipMalloc(timer stamps)");
