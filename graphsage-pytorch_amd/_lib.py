@@ -138,6 +138,7 @@ _SIGS = {
     "gs_trainer_agg_times": (_i64, [_vp, _vp, _i64]),
     "gs_trainer_kernel_times": (_i64, [_vp, _i32, _vp, _i64]),
     "gs_trainer_kernel_block_stats": (_i64, [_vp, _i32, _vp, _i64]),
+    "gs_trainer_kernel_stamps": (_i64, [_vp, _i32, _i64, _vp, _vp]),
     "gs_trainer_time_kernels": (_i32, [_vp, _i32, _i64]),
     "gs_trainer_time_kernels_every": (_i32, [_vp, _i32, _i64, _i64]),
     "gs_trainer_kernel_name": (ctypes.c_char_p, [_vp, _i32]),
@@ -216,7 +217,7 @@ class DeviceLimit(RuntimeError):
 
 # measurement-only entry points a bench run may do without (an A/B against a
 # library built before them); everything else must be exported
-_DIAGNOSTIC = {"gs_trainer_kernel_block_stats"}
+_DIAGNOSTIC = {"gs_trainer_kernel_block_stats", "gs_trainer_kernel_stamps"}
 
 
 def lib():

@@ -25,11 +25,12 @@ template <bool HAS_SELF, bool ZVEC, bool CLS>
 __global__ __launch_bounds__(kThreads) void layer_bwd_a_kernel(BwdA a) {
     int b = blockIdx.x;
     if (b < a.dw_nb) {
+        __shared__ DwSmem<1> sm;
         const int g2 = a.dw_gx * a.dw_gy;
         linear_dw_body<float, HAS_SELF, false, true, ZVEC>(b % a.dw_gx, (b % g2) / a.dw_gx, b / g2, a.n, a.F, a.H,
                                                            a.K, a.rps, a.Xs, a.ldxs, a.sidx, a.A, a.lda, a.dZ,
                                                            nullptr, a.H, a.target,
-                                                           static_cast<int64_t>(a.H) * a.K);
+                                                           static_cast<int64_t>(a.H) * a.K, sm);
         return;
     }
     b -= a.dw_nb;
@@ -83,11 +84,12 @@ template <int OP, int G>
 __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
     int b = blockIdx.x;
     if (b < t.a.dw_nb) {
+        __shared__ DwSmem<1> sm;
         const int g2 = t.a.dw_gx * t.a.dw_gy;
         linear_dw_body<float, true, false, true, true>(b % t.a.dw_gx, (b % g2) / t.a.dw_gx, b / g2, t.a.n, t.a.F,
                                                        t.a.H, t.a.K, t.a.rps, t.a.Xs, t.a.ldxs, t.a.sidx, t.a.A,
                                                        t.a.lda, t.a.dZ, nullptr, t.a.H, t.a.target,
-                                                       static_cast<int64_t>(t.a.H) * t.a.K);
+                                                       static_cast<int64_t>(t.a.H) * t.a.K, sm);
         return;
     }
     b -= t.a.dw_nb;

@@ -81,13 +81,20 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// A workgroup barrier for a hand-off through LDS alone: the LDS ops done
+// (lgkmcnt), not the global stores in flight, which __syncthreads() waits for
+// (its fence drains vmcnt: a store round trip).  The memory clobber keeps the
+// compiler from moving memory accesses across it.  Not for a kernel with an
+// LDS-DMA in flight (the DMA is a vmcnt op writing LDS).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Sum of v over the (<= 1024-thread) block, written by thread 0 to *dst.
 // Every thread of the block must call it.
 __device__ __forceinline__ void block_sum_to(float v, float* dst) {
     __shared__ float red[16];
     v = wave_sum(v);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
+    lds_barrier();  // the caller's output stores need not land first
     if (threadIdx.x == 0) {
         float t = 0.f;
         for (int w = 0; w < static_cast<int>(blockDim.x + 63) / 64; ++w) t += red[w];

@@ -61,7 +61,7 @@ __device__ __forceinline__ void sum_slabs_split_body(int bx, const float* __rest
         }
     }
     if (q > 0) red[q - 1][c] = s;
-    __syncthreads();
+    lds_barrier();  // (the pair launch's done-flag store, a PCIe write, need not land first)
     float sq = 0.f;
     if (q == 0 && i < n4) {
 #pragma unroll
@@ -105,14 +105,15 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const 
 // runner's completion signal, otherwise stored by the SGD launch).
 __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum s1, int nb1, SlabSum s2, int nb2,
                                                                          SlabSpec spec, int64_t* done,
-                                                                         int64_t done_value) {
+                                                                         int64_t done_value, KStamp ks) {
+    kstamp_begin(ks);
     signal_done(done, done_value);
     const int bx = blockIdx.x;
-    if (bx < nb2) {  // the longer per-block chains first
+    if (bx < nb2)  // the longer per-block chains first
         sum_slabs_body(bx, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
-        return;
-    }
-    sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part, spec);
+    else
+        sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part, spec);
+    kstamp_end(ks);
 }
 
 static bool slab_split_on(int64_t len) { return len % 4 == 0; }
@@ -330,8 +331,9 @@ int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, 
         done = g_done_flag;
         g_done_flag = {};
     }
-    sum_slabs_pair_kernel<<<dim3(static_cast<unsigned>(nb1 + nb2)), kSlabParts * 64, 0, st>>>(s1, nb1, s2, nb2, spec,
-                                                                                              done.ptr, done.value);
+    const KStamp ks = take_kernel_stamp();  // a timed launch: the kernel stores its own span
+    launch_k(sum_slabs_pair_kernel, dim3(static_cast<unsigned>(nb1 + nb2)), dim3(kSlabParts * 64), 0, st, s1, nb1, s2,
+             nb2, spec, done.ptr, done.value, ks);
     check_launch("sum_slabs_pair");
     return nb1;
 }
@@ -401,7 +403,9 @@ int gs_sage_linear_bwd_weight(gs_dtype dt, int64_t n, int64_t F, int64_t H, cons
     GS_API_BEGIN
     using namespace gs;
     hipStream_t st = as_stream(stream);
-    const int S = linear_dw_slabs(dt, n, F, H, Xs, ldxs, sidx, A, lda, dout, out, ldo, relu, dW, ws, ws_bytes, st);
+    // two row phases per workgroup from 512 rows (the trainer's layer-1 form), one below
+    const int S = linear_dw_slabs(dt, n, F, H, Xs, ldxs, sidx, A, lda, dout, out, ldo, relu, dW, ws, ws_bytes, st,
+                                  -1, n >= 512 ? kDw1Phases : 1);
     if (S > 1) sum_slabs_launch(static_cast<const float*>(ws), S, H * (Xs ? 2 * F : F), dW, nullptr, st);
     GS_API_END
 }

@@ -272,6 +272,9 @@ __global__ __launch_bounds__(kThreads) void linear_fwd_kernel(
 // 32 (8 waves, ~270 blocks at the rmat2m layer-1 shape) is the fp32 default:
 // W traffic from L2 halves while the grid still covers the chip.
 constexpr int kWideRows = 64;
+#ifndef GS_FWD_STAMP  // stage stamps for tools/lab/fwd_lab.hip; no-ops in the library
+#define GS_FWD_STAMP(i)
+#endif
 #ifndef GS_FWD_AHEAD
 #define GS_FWD_AHEAD 2
 #endif
@@ -358,6 +361,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     int n, int F, int H, int K, const T* __restrict__ Xs, int64_t ldxs, const int* __restrict__ sidx,
     const T* __restrict__ A, int64_t lda, const T* W, float* __restrict__ out, int64_t ldo,
     FwdRows rs, FwdSpec sp) {
+    GS_FWD_STAMP(0);
     kstamp_begin(sp.stamp);
     constexpr int EPV = 16 / sizeof(T);  // elements per 16-byte slot
     constexpr int BK = kSlots * EPV;     // k per chunk
@@ -425,9 +429,15 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     uint4 ar[kFwdAhead], wr_[kFwdAhead][WQ];
     auto load = [&](int c, int u) {
         const int kn = min(c, nC - 1) * BK;  // past the end: re-read the last chunk (never stored)
+#ifdef GS_FWD_LAB_NO_GLOBAL  // tools/lab/fwd_lab.hip: the K loop without its global loads
+        ar[u] = make_uint4(kn, ls, lr, 0x3f800000u);
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) wr_[u][q] = make_uint4(kn, q, ls, 0x3f800000u);
+#else
         ar[u] = concat_slot_raw<T, HAS_SELF>(srow, arow, F, K, kn + ls * EPV);
 #pragma unroll
         for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot_raw<T, false>(nullptr, wrow[q], K, K, kn + ls * EPV);
+#endif
     };
     auto stash = [&](int c, int u) {
         const int k = c * BK + ls * EPV;  // slots at and past K are zeros (both operands)
@@ -441,6 +451,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         for (int u = 0; u < kFwdAhead; ++u) load(u, u);
         stash(0, 0);
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        GS_FWD_STAMP(1);
         // Every load and stash is unconditional (past the end: the last
         // chunk's slots re-read, zeros stored into a buffer no wave reads
         // again); only the MFMAs of a chunk past the end are skipped.  A
@@ -464,8 +475,13 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
                         av[g] = ta[4 * g + kq];
                         wv[g] = tw[4 * g + kq];
                     }
+#ifdef GS_FWD_LAB_NO_MFMA  // tools/lab/fwd_lab.hip: the K loop without its MFMAs
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) acc[g] += __uint_as_float(av[g].x ^ wv[g].y);
+#else
 #pragma unroll
                     for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
+#endif
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 stash(c + 1, (u + 1) % kFwdAhead);
@@ -474,12 +490,14 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
         return acc;
     };
     f32x4 acc = run_k();  // PEND: on the speculative W1 (sp.S)
+    GS_FWD_STAMP(2);
     if constexpr (PEND) {
         // the fold after the K loop (its loads long done): the coefficients,
         // the other parameters' update, and, when W1's coefficient is not 1,
         // the recomputed W1 in S's buffer and the whole product again
         if (pending_apply()) acc = run_k();
     }
+    GS_FWD_STAMP(3);
     const int col = c0 + 16 * wc + r;
     if (col < H && wr < nt) {
 #pragma unroll
@@ -491,6 +509,7 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
             }
         }
     }
+    GS_FWD_STAMP(4);
     kstamp_end(sp.stamp);
 }
 
@@ -508,10 +527,10 @@ constexpr int kDwMaxSlab = 2048;  // rows per slab (their self indices are stage
 constexpr int kDwCh = GS_DW_CHUNK;  // rows per LDS chunk (one barrier each); 16 or 32
 static_assert(kDwCh == 16 || kDwCh == 32, "dW chunk rows");
 constexpr int kDwRpt = kDwCh / 16;  // rows each thread loads per chunk
-#ifndef GS_DW_AHEAD
-#define GS_DW_AHEAD (64 / GS_DW_CHUNK)
+constexpr int kDwAhead = 2;  // row chunks whose global loads are in flight ahead of their stash
+#ifndef GS_DW_STAMP
+#define GS_DW_STAMP(i) ((void)0)  // stage stamps of tools/lab/dw_lab.hip
 #endif
-constexpr int kDwAhead = GS_DW_AHEAD;  // row chunks whose global loads are in flight ahead of the MFMAs
 
 // PH row phases (blockDim = 256·PH): the waves of phase ph run the chunks
 // ph, ph + PH, ... of the slab on their own LDS ring (one barrier per
@@ -520,14 +539,22 @@ constexpr int kDwAhead = GS_DW_AHEAD;  // row chunks whose global loads are in f
 // so deterministic) and stores the slab.  PH = 2 puts twice the rows in a slab
 // at the same chunk loop length: half the slabs (and half the split-K bytes
 // the slab sum re-reads) for the same per-workgroup latency.
+// The body's LDS, declared by the kernel (one object for every role of a
+// fused launch: two roles' own static arrays would add up per block).
+template <int PH>
+struct DwSmem {
+    float sbuf[PH][2][2][kDwCh * kDwPitch];  // [phase][dZ | inputs][ring buffer]
+    int sIdx[kDwMaxSlab];                    // the slab's self indices (HAS_SELF)
+};
+
 template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC, int PH = 1>
 __device__ __forceinline__ void linear_dw_body(
     int bx, int by, int bz, int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
     const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
-    const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
+    const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride, DwSmem<PH>& sm) {
     static_assert(PH == 1 || PH == 2, "one or two row phases");
-    __shared__ float sbuf[PH][2][2][kDwCh * kDwPitch];  // [phase][dZ | inputs][ring buffer]
-    __shared__ int sIdx[HAS_SELF ? kDwMaxSlab : 1];
+    auto& sbuf = sm.sbuf;
+    int* sIdx = sm.sIdx;
     const int ph = PH == 1 ? 0 : static_cast<int>(threadIdx.x >> 8);
     const int tid = threadIdx.x & (kThreads - 1), lane = tid & 63, wave = tid >> 6;
     float (&sZ)[2][kDwCh * kDwPitch] = sbuf[ph][0];
@@ -539,8 +566,10 @@ __device__ __forceinline__ void linear_dw_body(
     const int nC = (i_end - i_beg + kDwCh - 1) / kDwCh;
     const int nI = (nC + PH - 1) / PH;  // iterations: this phase's chunks (the last may be past the slab: zeros)
     const int lr = tid >> 4, lq = (tid & 15) * 4;
-    if (HAS_SELF)
-        for (int t = threadIdx.x; t < i_end - i_beg; t += kThreads * PH) sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
+    GS_DW_STAMP(0);
+    if (HAS_SELF)  // (PH = 1 indexes by tid: a 512-thread block may run two 256-thread bodies side by side)
+        for (int t = PH == 1 ? tid : static_cast<int>(threadIdx.x); t < i_end - i_beg; t += kThreads * PH)
+            sIdx[t] = sidx ? sidx[i_beg + t] : i_beg + t;
     __syncthreads();
 
     // Rows past the slab read a valid row and are zeroed at the LDS store
@@ -550,7 +579,11 @@ __device__ __forceinline__ void linear_dw_body(
         float4 z[kDwRpt], o[kDwRpt], x[kDwRpt];
     };
     auto load = [&](int it, Ld& L) {
+#ifdef GS_DW_LAB_HOT_LOADS  // tools/lab/dw_lab.hip: every chunk's loads re-read chunk 0 (cache hits)
+        const int c = ph;
+#else
         const int c = PH * it + ph;
+#endif
 #pragma unroll
         for (int q = 0; q < kDwRpt; ++q) {
             const int t = min(kDwCh * min(c, nC - 1) + lr + 16 * q, i_end - i_beg - 1);
@@ -578,60 +611,104 @@ __device__ __forceinline__ void linear_dw_body(
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // One chunk: its LDS operands are all read before its first MFMA (one
-    // wait instead of one per MFMA pair), then the MFMAs on 4 accumulators,
-    // rows in ascending groups of 4 (the same sequence for any chunk size).
-    auto compute = [&](int it) {
+    // A chunk's MFMA operands in registers: lane (r, kq) holds, for row group
+    // s, the input X[4s + kq][k0 + 16t + r] of each k tile t and the gradient
+    // dZ[4s + kq][h0 + 16·wave + r].  The MFMA takes the inputs as its A
+    // operand, so lane (r, kq) of tile t ends with dW[h0 + 16·wave + r][k0 +
+    // 16t + 4kq .. +3]: four consecutive k, one 16-byte store.  Rows in
+    // ascending groups of 4 (the same sequence for any chunk size).
+    constexpr int NS = kDwCh / 4;
+    struct Ops {
+        float z[NS], x[NS][4];
+    };
+    auto read_ops = [&](int it, Ops& o) {
         const float* tz = sZ[it & 1];
         const float* ti = sI[it & 1];
-        constexpr int NS = kDwCh / 4;
-        float a[NS], b[NS][4];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const int row = 4 * s + kq;
-            a[s] = tz[row * kDwPitch + wave * 16 + r];
+            o.z[s] = tz[row * kDwPitch + wave * 16 + r];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) b[s][t] = ti[row * kDwPitch + t * 16 + r];
+            for (int t = 0; t < 4; ++t) o.x[s][t] = ti[row * kDwPitch + t * 16 + r];
         }
-        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfma_ops = [&](const Ops& o) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][t], acc[t], 0, 0, 0);
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.x[s][t], o.z[s], acc[t], 0, 0, 0);
     };
-    // Global loads run kDwAhead iterations ahead of the MFMAs (a ring of
-    // register sets, loop unrolled by its length); LDS stays double-buffered.
-    // Slot u holds iteration i (stashed one iteration earlier) when i = u (mod
-    // kDwAhead) is computed, and is refilled with iteration i + kDwAhead then.
-    Ld ring[kDwAhead];
-#pragma unroll
-    for (int u = 0; u < kDwAhead; ++u) load(u, ring[u]);
+    // Software pipeline, one LDS barrier per iteration: iteration `it` reads
+    // chunk it + 1's operands from LDS into registers while the MFMAs of chunk
+    // it (read the iteration before) run, then stashes chunk it + 2 into the
+    // LDS buffer chunk it came from (every wave's reads of it completed before
+    // the barrier: it waits on them) and refills that register slot with
+    // chunk it + 4 from global memory (two chunks of loads in flight).  The
+    // MFMAs are unconditional within a pair of iterations (a phase's chunk
+    // past the slab: zero operands, zero products), so the compiler
+    // interleaves the stash, the address math and the loads between them.
+    // The loop runs whole pairs with the loads and stashes unconditional; an
+    // odd last iteration's MFMAs follow it (they need no stash or load): a
+    // break or a guarded stash inside the loop would let the compiler sink
+    // each load to its consumer, and the waits then drain the ring every
+    // iteration.
+    static_assert(kDwAhead == 2, "a pair of register slots (the loop unrolls by two)");
+    Ld ring[2];
+    load(0, ring[0]);
+    __builtin_amdgcn_sched_barrier(0);  // in chunk order (the loop's waits count on it)
+    load(1, ring[1]);
+    __builtin_amdgcn_sched_barrier(0);
     stash(0, ring[0]);
-    for (int i0 = 0; i0 < nI; i0 += kDwAhead) {
-#pragma unroll
-        for (int u = 0; u < kDwAhead; ++u) {
-            const int it = i0 + u;
-            if (it >= nI) break;
-            __syncthreads();
-            load(it + kDwAhead, ring[u]);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(it);
-            __builtin_amdgcn_sched_barrier(0);
-            const int un = (u + 1) % kDwAhead;
-            if (it + 1 < nI) stash(it + 1, ring[un]);
-        }
+    load(2, ring[0]);
+    stash(1, ring[1]);
+    load(3, ring[1]);
+    Ops ops[2];
+    __syncthreads();  // (no stores in flight: an LDS wait and the barrier, which the wait-count pass sees)
+    read_ops(0, ops[0]);
+    GS_DW_STAMP(1);
+    auto step = [&](int it, int u) {
+#ifdef GS_DW_LAB_MFMA_ONLY  // tools/lab/dw_lab.hip: the row loop's MFMAs alone
+        mfma_ops(ops[u]);
+        return;
+#endif
+#ifndef GS_DW_LAB_NO_BARRIER
+        __syncthreads();
+#endif
+#ifndef GS_DW_LAB_NO_READ
+        read_ops(it + 1, ops[u ^ 1]);
+#endif
+#ifndef GS_DW_LAB_NO_MFMA
+        mfma_ops(ops[u]);
+#endif
+#ifndef GS_DW_LAB_NO_STASH
+        stash(it + 2, ring[u]);
+        load(it + 4, ring[u]);
+#endif
+    };
+    int it = 0;
+    for (; it + 1 < nI; it += 2) {
+        step(it, 0);
+        step(it + 1, 1);
     }
+    if (it < nI) {  // odd nI: the last chunk, read into ops[0] by the last step
+#ifndef GS_DW_LAB_NO_MFMA
+        mfma_ops(ops[0]);
+#endif
+    }
+    GS_DW_STAMP(2);
     if constexpr (PH == 2) {
         // phase 1's sums to phase 0 through phase 1's ring (free: every
         // phase-1 wave is past its last compute once all reach the barrier)
+        // (LDS-only barriers: the loop's last prefetches, of chunks past the
+        // slab, may still be in flight, and a __syncthreads would wait for them)
         float* xch = &sbuf[1][0][0][0];
         static_assert(4 * kDwCh * kDwPitch >= kThreads * 16, "exchange area");
-        __syncthreads();
+        lds_barrier();
         if (ph == 1)
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 *reinterpret_cast<f32x4*>(&xch[(t * kThreads + tid) * 4]) = acc[t];
-        __syncthreads();
+        lds_barrier();
         if (ph == 1) return;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -640,16 +717,22 @@ __device__ __forceinline__ void linear_dw_body(
         }
     }
     float* slab = dst + static_cast<int64_t>(bz) * split_stride;
+    const int h = h0 + wave * 16 + r;
+    if (h < H) {
+        float* srow = slab + static_cast<int64_t>(h) * K;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const int k = k0 + t * 16 + r;
-        if (k >= K) continue;
+        for (int t = 0; t < 4; ++t) {
+            const int k = k0 + t * 16 + 4 * kq;
+            if (K % 4 == 0 && k < K) {
+                *reinterpret_cast<f32x4*>(srow + k) = acc[t];
+            } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int h = h0 + wave * 16 + 4 * kq + j;
-            if (h < H) slab[static_cast<int64_t>(h) * K + k] = acc[t][j];
+                for (int j = 0; j < 4; ++j)
+                    if (k + j < K) srow[k + j] = acc[t][j];
+            }
         }
     }
+    GS_DW_STAMP(3);
 }
 
 template <typename T, bool HAS_SELF, bool RELU, bool VLOAD, bool ZVEC>
@@ -657,8 +740,9 @@ __global__ __launch_bounds__(kThreads) void linear_dw_kernel(
     int n, int F, int H, int K, int rows_per_split, const T* __restrict__ Xs, int64_t ldxs,
     const int* __restrict__ sidx, const T* __restrict__ A, int64_t lda, const float* __restrict__ dout,
     const float* __restrict__ out, int64_t ldo, float* __restrict__ dst, int64_t split_stride) {
+    __shared__ DwSmem<1> sm;
     linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC>(blockIdx.x, blockIdx.y, blockIdx.z, n, F, H, K, rows_per_split,
-                                                   Xs, ldxs, sidx, A, lda, dout, out, ldo, dst, split_stride);
+                                                   Xs, ldxs, sidx, A, lda, dout, out, ldo, dst, split_stride, sm);
 }
 
 // The same tiles on a 1-D grid mapped XCD by XCD: workgroup w runs on XCD
@@ -680,8 +764,9 @@ __global__ __launch_bounds__(kThreads * PH) void linear_dw_xcd_kernel(
     const int z = w % kXcds + kXcds * (j / tiles);
     if (z >= S) return;
     const int t = j % tiles;
+    __shared__ DwSmem<PH> sm;
     linear_dw_body<T, HAS_SELF, RELU, VLOAD, ZVEC, PH>(t % gx, t / gx, z, n, F, H, K, rows_per_split, Xs, ldxs, sidx,
-                                                       A, lda, dout, out, ldo, dst, split_stride);
+                                                       A, lda, dout, out, ldo, dst, split_stride, sm);
     kstamp_end(ks);  // a timed launch's span (phase 1 of PH = 2 joins after handing its sums over)
 }
 

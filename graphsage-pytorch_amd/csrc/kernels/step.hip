@@ -20,14 +20,15 @@ struct gs_trainer {
     int64_t cls_w_off = 0, cls_b_off = 0, total = 0;
     // optional kernel-bound HIP-event timing (bench roofline): site 0 the
     // layer-1 gather-aggregate, 1 the layer-1 linear forward, 2 its weight
-    // gradient (the MFMA kernels), 3 the fused top layer + loss head (top.hip)
-    static constexpr int kSites = 4;
+    // gradient (the MFMA kernels), 3 the fused top layer + loss head (top.hip),
+    // 4 the step's slab-sum pair launch (sum_slabs_pair_launch)
+    static constexpr int kSites = 5;
     struct Timer {
         std::vector<hipEvent_t> ev0, ev1;
         int64_t n = 0;
         int64_t every = 1, calls = 0;  // time one launch of every `every`, the last of each run
         std::string kernel;  // demangled name of the kernel the site last timed
-        // sites 1 and 3: the kernel's own span (KStamp, kcommon.hpp) per entry,
+        // sites 1-4: the kernel's own span (KStamp, kcommon.hpp) per entry,
         // when the launch took it (else the entry's events timed it)
         unsigned long long* st0 = nullptr;  // device: per entry, kStampBlocks workgroup starts (100 MHz ticks)
         unsigned long long* st1 = nullptr;  // device: per entry, the workgroup ends
@@ -546,10 +547,12 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
                 // itself is left to the next forward
                 const bool spec = T.defer && !T.defer_comm && parts && np + sum_slabs_grid(H * K1) <= T.pstride &&
                                   n_cls <= T.pstride;
+                const bool armed = timed_arm(T, 4);
                 np += sum_slabs_pair_launch(SlabSum{s1_src, s1_n, H * K1, G + T.w_off[0], T.norm_part + np}, d2, st,
                                             spec ? T.w1_buf(T.w1_cur) : nullptr,
                                             spec ? T.w1_buf(T.w1_cur ^ 1) : nullptr, c.lr,
                                             spec && lowp ? T.lp_buf(T.w1_cur ^ 1) : nullptr);
+                timed_done(T, 4, armed);
                 T.pending = spec;
                 if (spec) {
                     T.pend_part = T.norm_part;
@@ -951,7 +954,7 @@ int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capa
         if (tm.st0) (void)hipFree(tm.st0);
         tm.st0 = tm.st1 = nullptr;
         tm.stamped.assign(cap, 0);
-        if (s >= 1 && s <= 3 && cap > 0) {  // span stamps (forward, dW, top)
+        if (s >= 1 && cap > 0) {  // span stamps (forward, dW, top, slab sum)
             const int64_t words = cap * gs::kStampBlocks;
             GS_REQUIRE(hipMalloc(&tm.st0, 2 * words * sizeof(unsigned long long)) == hipSuccess, GS_ENOMEM,
                        "hipMalloc(timer stamps)");
@@ -1002,6 +1005,18 @@ int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t 
             return -1;
     }
     return n;
+}
+
+int64_t gs_trainer_kernel_stamps(gs_trainer* t, int32_t site, int64_t launch, uint64_t* start, uint64_t* end) {
+    if (!t || !start || !end || site < 0 || site >= gs_trainer::kSites) return -1;
+    auto& tm = t->timer[site];
+    if (!tm.st0 || launch < 0 || launch >= tm.n) return 0;
+    const int64_t W = gs::kStampBlocks;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(start, tm.st0 + launch * W, W * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(end, tm.st1 + launch * W, W * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return W;
 }
 
 int64_t gs_trainer_kernel_block_stats(gs_trainer* t, int32_t site, float* us4, int64_t cap) {

@@ -67,6 +67,10 @@ struct TopArgs {
     KStamp stamp;        // a timed launch's span (g_kernel_stamp)
 };
 
+// The stages hand each other LDS only: lds_barrier() (kcommon.hpp), not
+// __syncthreads(), which would wait for the stage's global stores (E, dZ,
+// the slabs, the [self | agg] rows).  The W2 DMA is waited for explicitly.
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
@@ -95,6 +99,8 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 
     GS_TOP_STAMP(0);
     kstamp_begin(a.stamp);
+    // the fused layer-1 dW launch that follows waits on these (stream order
+    // makes the stores visible to it)
     // ---- W2 -> LDS by DMA (no registers), issued first so its latency hides
     // under the gather.  Row c is one wave instruction of 64 16-byte quads;
     // quad q of the row lands in slot q ^ (c & 15).  Waves 2..7 issue it (the
@@ -126,6 +132,12 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // neighbours added in list order) and the self row, one 32-lane group per
     // row.  With the padded records (a.tids) the root's self index and whole
     // list arrive in one load round (lane gl holds list entry gl).
+    // this thread's [self | agg] quads and MAX argmax, stored to global after
+    // the stage's barrier (a store in flight would hold the compiler's vmcnt(0)
+    // that follows the W2 DMA's barrier)
+    float4 st_xs{}, st_av{};
+    int4 st_am{};
+    const int st_g = tid / 32, st_f0 = (tid % 32) * 4;
     {
         constexpr int G = 32, NR = 32;
         const int g = tid / G, gl = tid % G;
@@ -200,19 +212,19 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             *reinterpret_cast<float4*>(&sX[g][f0]) = xs;
             const float4 av = make_float4(acc[0], acc[1], acc[2], acc[3]);
             *reinterpret_cast<float4*>(&sX[g][H + f0]) = av;
-            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * K + f0) = xs;
-            *reinterpret_cast<float4*>(a.agg + static_cast<int64_t>(r) * K + H + f0) = av;
-            if (OP == GS_AGG_MAX)
-                *reinterpret_cast<int4*>(a.argmax + static_cast<int64_t>(r) * H + f0) = make_int4(am[0], am[1], am[2],
-                                                                                                   am[3]);
+            st_xs = xs;
+            st_av = av;
+            if (OP == GS_AGG_MAX) st_am = make_int4(am[0], am[1], am[2], am[3]);
         } else if (g < kTopRows) {  // a ragged last block: zero rows (never stored)
             *reinterpret_cast<float4*>(&sX[g][gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
             *reinterpret_cast<float4*>(&sX[g][H + gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
     GS_TOP_STAMP(1);
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's W2 DMA has landed (vmcnt); the barrier covers the others'
-    __syncthreads();
+    // the W2 DMA has landed: waves 2..7 issued it (vmcnt); waves 0 and 1 ran
+    // the gather, whose row stores need not complete before the barrier
+    if (w >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
     GS_TOP_STAMP(2);
 
     // ---- stage 2: E = relu([self | agg] · W2ᵀ), 4x4x1 multi-block MFMAs.
@@ -231,6 +243,15 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             av[4 * m] = x4.x; av[4 * m + 1] = x4.y; av[4 * m + 2] = x4.z; av[4 * m + 3] = x4.w;
             bv[4 * m] = w4.x; bv[4 * m + 1] = w4.y; bv[4 * m + 2] = w4.z; bv[4 * m + 3] = w4.w;
         }
+        // stage 1's global stores, behind the first LDS reads (the compiler
+        // waits vmcnt(0) before those, for the DMA: stores issued before
+        // would be waited for there)
+        if (st_g < nr) {
+            const int64_t r = r0 + st_g;
+            *reinterpret_cast<float4*>(a.agg + r * K + st_f0) = st_xs;
+            *reinterpret_cast<float4*>(a.agg + r * K + H + st_f0) = st_av;
+            if (OP == GS_AGG_MAX) *reinterpret_cast<int4*>(a.argmax + r * H + st_f0) = st_am;
+        }
         f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
         for (int k = 0; k < 64; k += 2) {
@@ -241,7 +262,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 #pragma unroll
         for (int j = 0; j < kTopRows; ++j) pp[j * H + col] = c0[j] + c1[j];
     }
-    __syncthreads();
+    lds_barrier();
     GS_TOP_STAMP(3);
     // the quarters added in order, relu (NaN kept), E to LDS and global
     {
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         sE[row][col] = e;
         if (row < nr) a.E[static_cast<int64_t>(r0 + row) * H + col] = e;
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- stage 3: the loss head (models.py:8-27, utils.py:159-164).
     // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         z += __shfl_xor(z, 4, 64);
         if (part == 0 && rc < kTopRows * C) sdl[row * C + c] = z + sb[c];
     }
-    __syncthreads();
+    lds_barrier();
     // softmax / NLL / dlogits: wave w < rows, lane = class (C <= 32 <= 64)
     if (w < nr) {
         const int ii = w;
@@ -291,7 +312,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     } else if (w < kTopRows && lane < C) {
         sdl[w * C + lane] = 0.f;  // ragged block: no gradient from the missing rows
     }
-    __syncthreads();
+    lds_barrier();
     GS_TOP_STAMP(4);
     // dZ = (dlogits · Wc) ⊙ (E > 0): thread t = (row, d), classes in order
     // (eight classes' operands read ahead of their chain)
@@ -363,7 +384,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             if (tid == NT - 64) out[per] = sl;
         }
     }
-    __syncthreads();
+    lds_barrier();
     GS_TOP_STAMP(5);
 
     // ---- stage 4: dIn = dZ · W2 (4x4x1 multi-block).  Wave w: input columns
@@ -393,7 +414,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 #pragma unroll
         for (int j = 0; j < kTopRows; ++j) pp[j * K + kc] = c0[j] + c1[j];
     }
-    __syncthreads();
+    lds_barrier();
     // the two halves added in order, dIn to global: thread t = (row, 2 columns)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {

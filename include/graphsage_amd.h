@@ -547,7 +547,9 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 /* The same timers per site: 0 the layer-1 gather as above, 1 the layer-1
  * SageLayer forward GEMM (gs_sage_linear_fwd, unfused path), 2 the layer-1
  * weight-gradient GEMM of the fused backward (linear_dw slabs, before their
- * sum), 3 the fused top layer + loss head launch (2-layer models).
+ * sum), 3 the fused top layer + loss head launch (2-layer models), 4 the
+ * slab-sum pair launch (the layer-1 and layer-2 weight-gradient sums of the
+ * fused top path).
  * gs_trainer_time_kernels arms the sites in site_mask (bit s = site
  * s) for their next `capacity` launches and disarms the others;
  * gs_trainer_time_agg(t, n) == gs_trainer_time_kernels(t, 1, n).  Every
@@ -560,11 +562,15 @@ int64_t gs_trainer_agg_times(gs_trainer* t, float* ms, int64_t cap);
 int gs_trainer_time_kernels(gs_trainer* t, int32_t site_mask, int64_t capacity);
 int gs_trainer_time_kernels_every(gs_trainer* t, int32_t site_mask, int64_t capacity, int64_t every);
 int64_t gs_trainer_kernel_times(gs_trainer* t, int32_t site, float* ms, int64_t cap);
-/* For a stamped site (the forward GEMM, the top launch): per timed launch,
+/* For a stamped site (1-4): per timed launch,
  * four floats in us — span (first workgroup start .. last end), mean and max
  * workgroup duration, and the spread of workgroup starts; -1 for a launch
  * timed by events.  Returns the launches written, -1 on error. */
 int64_t gs_trainer_kernel_block_stats(gs_trainer* t, int32_t site, float* us4, int64_t cap);
+/* The raw per-workgroup stamps (100 MHz s_memrealtime ticks; 0 = none) of
+ * stamped launch `launch` of `site`: kStampBlocks (1024) entries each into
+ * start and end.  Returns the entries written, 0 for an unstamped launch. */
+int64_t gs_trainer_kernel_stamps(gs_trainer* t, int32_t site, int64_t launch, uint64_t* start, uint64_t* end);
 /* Demangled name of the kernel timer site `site` timed since it was last
  * armed ("" before its first timed launch) — the variant actually launched. */
 const char* gs_trainer_kernel_name(const gs_trainer* t, int32_t site);
