@@ -17,9 +17,13 @@
 #include <vector>
 
 __device__ unsigned long long* g_stamps;
-#define GS_FWD_STAMP(i)                                                                                       \
-    do {                                                                                                      \
-        if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+// (a global-address-space store: a flat store pending at the K loop would make
+// the wait-count pass drain every load in it)
+typedef __attribute__((address_space(1))) unsigned long long gstamp_t;
+#define GS_FWD_STAMP(i)                                                                                        \
+    do {                                                                                                       \
+        if (g_stamps && threadIdx.x == 0)                                                                      \
+            ((gstamp_t*)g_stamps)[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                   \
     } while (0)
 #include "../../graphsage-pytorch_amd/csrc/host/errors.cpp"
 #include "../../graphsage-pytorch_amd/csrc/kernels/linear_dev.hpp"
