@@ -265,7 +265,7 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
 #undef GS_BWDT
     check_launch("layer_bwd_top");
     *deferred = SlabSum{a.slabs, S, a.H * K, a.dW, nullptr};
-    return S > 1 ? sum_slabs_blocks(a.H * K) : 0;
+    return S > 1 ? sum_slabs_pair_parts2(a.H * K) : 0;
 }
 
 }  // namespace gs

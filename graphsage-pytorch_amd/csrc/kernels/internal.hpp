@@ -57,8 +57,10 @@ struct SlabSum {
     float* part;
 };
 // Both sums in one launch (s1 the split layer-1 sum, s2 a deferred layer-2
-// sum, S2 <= 1 = nothing to add); returns s1's partial count.
-bool sum_slabs_pair_ok(int64_t len1);
+// sum, S2 <= 1 = nothing to add); returns s1's partial count.  s2 writes
+// sum_slabs_pair_parts2(s2.len) partials.
+bool sum_slabs_pair_ok(int64_t len1, int64_t len2);
+int sum_slabs_pair_parts2(int64_t len2);
 // spec_S: also W1's speculative update spec_S = spec_P - lr·(layer-1 sum) (the
 // trainer's deferred update), and the launch takes the done flag (g_done_flag).
 int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P = nullptr,

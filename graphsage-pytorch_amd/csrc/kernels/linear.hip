@@ -96,10 +96,12 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_split_kernel(const 
 }
 
 // Two slab sums in one launch (the 2-layer step after the fused top layer):
-// blocks [nb2, nb2 + nb1) sum the layer-1 dW slabs as sum_slabs_split_kernel,
-// blocks [0, nb2) the layer-2 dW slabs as sum_slabs_body over nb2 blocks of
-// kThreads (the other threads of these wider blocks only join the partial's
-// reduction) -- each bitwise its standalone kernel, partials where those write.
+// blocks [0, nb2) sum the layer-2 dW slabs, blocks [nb2, nb2 + nb1) the
+// layer-1 ones, both as sum_slabs_split_kernel (64 quads per block, the slabs
+// split over its 8 waves: one memory round each; the layer-2 sum on 33 blocks
+// of one thread per quad took 3.4 us against 2.3 for the split blocks, the
+// launch's critical path) -- each bitwise its standalone kernel (the order of
+// sum_slabs_body), partials where those write.
 // With spec.S (the trainer's deferred update) the layer-1 sum also writes W1's
 // speculative update, and the launch stores the step's done flag (the
 // runner's completion signal, otherwise stored by the SGD launch).
@@ -109,8 +111,8 @@ __global__ __launch_bounds__(kSlabParts * 64) void sum_slabs_pair_kernel(SlabSum
     kstamp_begin(ks);
     signal_done(done, done_value);
     const int bx = blockIdx.x;
-    if (bx < nb2)  // the longer per-block chains first
-        sum_slabs_body(bx, nb2, s2.slabs, s2.S, s2.len, s2.out, s2.part, threadIdx.x < kThreads);
+    if (bx < nb2)
+        sum_slabs_split_body(bx, s2.slabs, s2.S, s2.len, s2.out, s2.part);
     else
         sum_slabs_split_body(bx - nb2, s1.slabs, s1.S, s1.len, s1.out, s1.part, spec);
     kstamp_end(ks);
@@ -315,13 +317,15 @@ int sum_slabs_launch(const float* slabs, int S, int64_t len, float* out, float* 
     return sum_slabs_blocks(len);
 }
 
-bool sum_slabs_pair_ok(int64_t len1) { return slab_split_on(len1); }
+bool sum_slabs_pair_ok(int64_t len1, int64_t len2) { return slab_split_on(len1) && slab_split_on(len2); }
+int sum_slabs_pair_parts2(int64_t len2) { return static_cast<int>(slab_split_blocks(len2)); }
 
 int sum_slabs_pair_launch(const SlabSum& s1, const SlabSum& s2, hipStream_t st, const float* spec_P, float* spec_S,
                           float lr, uint16_t* spec_S_lp) {
-    GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1, GS_EINVAL, "slab pair: layer-1 sum not split");
+    GS_REQUIRE(slab_split_on(s1.len) && s1.S > 1 && (s2.S <= 1 || slab_split_on(s2.len)), GS_EINVAL,
+               "slab pair: sums not split");
     const int nb1 = static_cast<int>(slab_split_blocks(s1.len));
-    const int nb2 = s2.S > 1 ? sum_slabs_blocks(s2.len) : 0;
+    const int nb2 = s2.S > 1 ? static_cast<int>(slab_split_blocks(s2.len)) : 0;
     SlabSpec spec;
     DoneFlag done;
     if (spec_S) {  // the step's last launch: it carries the done flag

@@ -493,7 +493,8 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             const int64_t K1 = T.w_cols[0];
             // top path, 2 layers, no bucketed all-reduce hook: one backward launch for
             // layer 2 and its slab sum beside layer 1's (same sums, partials, order)
-            const bool defer = top && lb.size() == 1 && !T.upper_hook && dw2_ws && sum_slabs_pair_ok(H * K1);
+            const bool defer = top && lb.size() == 1 && !T.upper_hook && dw2_ws &&
+                               sum_slabs_pair_ok(H * K1, H * T.w_cols[1]);
             int np = 0;
             bool parts = true;
             SlabSum d2{};
