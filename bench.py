@@ -276,7 +276,8 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 # and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
 # the kernel beside the live event-timed one
 # (newest round first: the first file present is used)
-ROCPROF_STATS = {("rmat2m", 512): ["profiles/r04f_kernel_stats_rmat2m_steps300.csv",
+ROCPROF_STATS = {("rmat2m", 512): ["profiles/r05_kernel_stats_rmat2m_steps300.csv",
+                                   "profiles/r04f_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04e_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04d_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04c_kernel_stats_rmat2m_steps300.csv",
@@ -286,7 +287,8 @@ ROCPROF_STATS = {("rmat2m", 512): ["profiles/r04f_kernel_stats_rmat2m_steps300.c
                                    "profiles/r03b_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r03_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r02_kernel_stats_rmat2m_steps300.csv"],
-                 ("rmat2m-max-bf16", 512): ["profiles/r04f_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                 ("rmat2m-max-bf16", 512): ["profiles/r05_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                                            "profiles/r04f_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04e_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04d_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04c_kernel_stats_rmat2m_max_bf16_steps300.csv",
