@@ -429,15 +429,9 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
     uint4 ar[kFwdAhead], wr_[kFwdAhead][WQ];
     auto load = [&](int c, int u) {
         const int kn = min(c, nC - 1) * BK;  // past the end: re-read the last chunk (never stored)
-#ifdef GS_FWD_LAB_NO_GLOBAL  // tools/lab/fwd_lab.hip: the K loop without its global loads
-        ar[u] = make_uint4(kn, ls, lr, 0x3f800000u);
-#pragma unroll
-        for (int q = 0; q < WQ; ++q) wr_[u][q] = make_uint4(kn, q, ls, 0x3f800000u);
-#else
         ar[u] = concat_slot_raw<T, HAS_SELF>(srow, arow, F, K, kn + ls * EPV);
 #pragma unroll
         for (int q = 0; q < WQ; ++q) wr_[u][q] = concat_slot_raw<T, false>(nullptr, wrow[q], K, K, kn + ls * EPV);
-#endif
     };
     auto stash = [&](int c, int u) {
         const int k = c * BK + ls * EPV;  // slots at and past K are zeros (both operands)
@@ -475,13 +469,8 @@ __global__ __launch_bounds__(ROWS * 16) void linear_fwd_wide_kernel(
                         av[g] = ta[4 * g + kq];
                         wv[g] = tw[4 * g + kq];
                     }
-#ifdef GS_FWD_LAB_NO_MFMA  // tools/lab/fwd_lab.hip: the K loop without its MFMAs
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) acc[g] += __uint_as_float(av[g].x ^ wv[g].y);
-#else
 #pragma unroll
                     for (int g = 0; g < 4; ++g) acc = mfma_slot<T>(av[g], wv[g], acc);
-#endif
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 stash(c + 1, (u + 1) % kFwdAhead);
@@ -579,11 +568,7 @@ __device__ __forceinline__ void linear_dw_body(
         float4 z[kDwRpt], o[kDwRpt], x[kDwRpt];
     };
     auto load = [&](int it, Ld& L) {
-#ifdef GS_DW_LAB_HOT_LOADS  // tools/lab/dw_lab.hip: every chunk's loads re-read chunk 0 (cache hits)
-        const int c = ph;
-#else
         const int c = PH * it + ph;
-#endif
 #pragma unroll
         for (int q = 0; q < kDwRpt; ++q) {
             const int t = min(kDwCh * min(c, nC - 1) + lr + 16 * q, i_end - i_beg - 1);
@@ -667,34 +652,18 @@ __device__ __forceinline__ void linear_dw_body(
     read_ops(0, ops[0]);
     GS_DW_STAMP(1);
     auto step = [&](int it, int u) {
-#ifdef GS_DW_LAB_MFMA_ONLY  // tools/lab/dw_lab.hip: the row loop's MFMAs alone
-        mfma_ops(ops[u]);
-        return;
-#endif
-#ifndef GS_DW_LAB_NO_BARRIER
         __syncthreads();
-#endif
-#ifndef GS_DW_LAB_NO_READ
         read_ops(it + 1, ops[u ^ 1]);
-#endif
-#ifndef GS_DW_LAB_NO_MFMA
         mfma_ops(ops[u]);
-#endif
-#ifndef GS_DW_LAB_NO_STASH
         stash(it + 2, ring[u]);
         load(it + 4, ring[u]);
-#endif
     };
     int it = 0;
     for (; it + 1 < nI; it += 2) {
         step(it, 0);
         step(it + 1, 1);
     }
-    if (it < nI) {  // odd nI: the last chunk, read into ops[0] by the last step
-#ifndef GS_DW_LAB_NO_MFMA
-        mfma_ops(ops[0]);
-#endif
-    }
+    if (it < nI) mfma_ops(ops[0]);  // odd nI: the last chunk, read into ops[0] by the last step
     GS_DW_STAMP(2);
     if constexpr (PH == 2) {
         // phase 1's sums to phase 0 through phase 1's ring (free: every

@@ -6,7 +6,10 @@
 // stamps (100 MHz): 0 start, 1 first chunk stashed, 2 row loop done, 3 stored.
 // Developer tool, not part of the library:
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include -I graphsage-pytorch_amd/csrc/kernels \
-//         [-DGS_DW_CHUNK=32] [-DGS_DW_LAB_NO_MFMA] tools/lab/dw_lab.hip -o tools/bin/dw_lab
+//         [-DGS_DW_CHUNK=32] tools/lab/dw_lab.hip -o tools/bin/dw_lab
+// (The round-5 ablations — no MFMA, MFMAs alone, no barrier, no operand reads,
+// no stash, cache-hot loads — compiled hooks into linear_dw_body that have since
+// been removed; their results are in DESIGN §14.)
 //   tools/bin/dw_lab [n] [rows per slab]
 #include <hip/hip_runtime.h>
 
