@@ -9,6 +9,7 @@ interleaved with other ``random`` users such as UnsupervisedLoss).
 (frontiers in CPython set order, sampled sets) and packs the int32 image the
 kernels read into one buffer for a single host->device copy.
 """
+import array as _array
 import ctypes
 import random as _pyrandom
 
@@ -61,13 +62,14 @@ class RNG:
         if ver != 3:
             raise ValueError("unsupported random state version")
         out = cls()
-        out.setstate(np.array(internal[:624], np.uint32), internal[624])
+        # array.array('I') takes the tuple's ints in one C loop (np.array: ~3x slower)
+        out.setstate(np.frombuffer(_array.array("I", internal[:624]), np.uint32), internal[624])
         return out
 
     def to_python(self, r=_pyrandom):
         ver, _old, gauss = r.getstate()
         mt, pos = self.getstate()
-        r.setstate((ver, tuple(int(x) for x in mt) + (pos,), gauss))
+        r.setstate((ver, tuple(mt.tolist()) + (pos,), gauss))
 
     # ----- known-answer helpers (tests / extend_nodes host code)
     def getrandbits(self, k, count=1):

@@ -145,6 +145,24 @@ class UnsupervisedLoss:
         self._plan = None
 
     # --------------------------------------------- reference attributes
+    # unique_nodes_batch (models.py:146) is the list the reference keeps; the
+    # last extend_nodes holds it as an int64 array and builds the list on first
+    # read (a 10k-id tolist is ~0.2 ms of a Pubmed step that never reads it).
+    @property
+    def unique_nodes_batch(self):
+        if self._uniq_list is None:
+            self._uniq_list = self._uniq_arr.tolist()
+        return self._uniq_list
+
+    @unique_nodes_batch.setter
+    def unique_nodes_batch(self, v):
+        self._uniq_list, self._uniq_arr = list(v), None
+
+    def _unique_array(self):
+        if self._uniq_arr is None:
+            self._uniq_arr = np.asarray(self._uniq_list, np.int64).reshape(-1)
+        return self._uniq_arr
+
     @property
     def positive_pairs(self):
         if self._pos_cache is None:
@@ -195,14 +213,23 @@ class UnsupervisedLoss:
     def extend_nodes(self, nodes, num_neg=6):
         """models.py:135-147: the batch extended by its walk positives and
         far negatives, as list(set(pos) | set(neg))."""
+        self._extend(nodes, num_neg)
+        return self.unique_nodes_batch
+
+    def extend_nodes_array(self, nodes, num_neg=6):
+        """extend_nodes with unique_nodes_batch returned as an int64 array (the
+        same ids in the same order, no Python list; utils.train_step's path)."""
+        self._extend(nodes, num_neg)
+        return self._uniq_arr
+
+    def _extend(self, nodes, num_neg):
         self._reset_pairs()
         self.target_nodes = nodes
         r = self._run(nodes, num_neg, PARTS_BOTH)
         self._pos_parts, self._neg_parts = [r], [r]
         self._last = r
-        self.unique_nodes_batch = r["unique"].tolist()
+        self._uniq_arr, self._uniq_list = r["unique"], None
         assert r["ok"], "set(target_nodes) < set(unique_nodes_batch) failed (models.py:147)"
-        return self.unique_nodes_batch
 
     def get_positive_nodes(self, nodes):
         return self._run_random_walks(nodes)
@@ -238,12 +265,12 @@ class UnsupervisedLoss:
         return self._plan
 
     def _loss(self, embeddings, nodes, kind):
-        uniq = self.unique_nodes_batch
+        uniq = self._unique_array()
         assert len(embeddings) == len(uniq)
         nodes = np.asarray(nodes).reshape(-1)
         if len(nodes) > len(uniq):  # the reference indexes unique_nodes_batch[i] for every i
             raise IndexError("list index out of range")
-        assert np.array_equal(nodes.astype(np.int64), np.asarray(uniq[:len(nodes)], np.int64))
+        assert np.array_equal(nodes.astype(np.int64), uniq[:len(nodes)])
         if not isinstance(embeddings, torch.Tensor) or not embeddings.is_cuda:
             raise RuntimeError("UnsupervisedLoss losses run on a HIP device (cuda embeddings)")
         plan, dims = self._device_plan(embeddings.device)

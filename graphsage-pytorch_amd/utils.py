@@ -73,7 +73,9 @@ def train_step(graphSage, classification, unsupervised_loss, optimizer, batch, l
     """The body of one apply_model batch (utils.py:146-191): extend, forward,
     losses, backward, clip per model, SGD.  Returns (loss, extended nodes);
     the loss stays on the device (no host sync)."""
-    nodes = np.asarray(list(unsupervised_loss.extend_nodes(batch, num_neg=num_neg)))
+    ext = getattr(unsupervised_loss, "extend_nodes_array", None)  # ours: the ids as an array
+    nodes = (ext(batch, num_neg=num_neg) if ext is not None
+             else np.asarray(list(unsupervised_loss.extend_nodes(batch, num_neg=num_neg))))
     embs = graphSage(nodes)
     parts = []
     if learn_method in ("sup", "plus_unsup"):
