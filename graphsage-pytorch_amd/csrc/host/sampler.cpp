@@ -171,8 +171,10 @@ struct HopScratch {
     std::unique_ptr<std::atomic<int>[]> chunk_done;  // sets_union: chunk c's sets are built
     int64_t n_chunk_cap = 0;
     std::atomic<int64_t> next_chunk{0};  // sets_union: the next chunk to build
-    int64_t n_items = 0;              // items of all sets of the hop (before gather_sets)
-    std::vector<int32_t> tmp, cur;    // lists()
+    int64_t n_items = 0;              // items of all sets of the hop
+    std::vector<int32_t> counts;      // sets_union: items per set
+    std::vector<int64_t> chunk_base;  // lists: chunk c's first item
+    std::vector<int32_t> cur;         // lists: transpose cursors
 };
 
 static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::vector<int64_t>& items,
@@ -235,13 +237,14 @@ static void sets_range(const Graph& g, const Hop& h, int64_t a, int64_t b, std::
 // unclaimed chunk itself whenever the one it needs is still in progress.
 // The union sees exactly the sequential merge order; only the set builds
 // overlap it.  Leaves each chunk's items in sc.part_items and per-set counts
-// in h.set_ptr[1 + r] (gather_sets makes set_ptr / set_items from them).
+// in sc.counts[r] (the lists job makes set_ptr / set_items from them).
 static constexpr int64_t kChunk = 32;
 
 static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     const int64_t n = static_cast<int64_t>(h.dst_ids.size());
     const int64_t nch = (n + kChunk - 1) / kChunk;
-    h.set_ptr.assign(n + 1, 0);
+    h.set_ptr.resize(n + 1);
+    sc.counts.resize(n);
     if (static_cast<int64_t>(sc.part_items.size()) < nch) sc.part_items.resize(nch);
     if (sc.n_chunk_cap < nch) {
         sc.chunk_done.reset(new std::atomic<int>[nch]);
@@ -249,7 +252,7 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     }
     for (int64_t c = 0; c < nch; ++c) sc.chunk_done[c].store(0, std::memory_order_relaxed);
     sc.next_chunk.store(0, std::memory_order_relaxed);
-    int32_t* counts = h.set_ptr.data() + 1;
+    int32_t* counts = sc.counts.data();
     // A chunk build that throws (bad_alloc in a set or an items vector) marks
     // its chunk failed (2) instead of done (1), so the merge loop stops
     // instead of spinning on it; the first exception is rethrown here once
@@ -313,21 +316,6 @@ static void sets_union(const Graph& g, Hop& h, HopScratch& sc, Team* team) {
     GS_PHASE(2);
 }
 
-// h.set_ptr (a scan of the per-set counts) and h.set_items (the chunks'
-// items concatenated) for lists() and the Sample view.
-static void gather_sets(Hop& h, HopScratch& sc) {
-    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    const int64_t nch = (n + kChunk - 1) / kChunk;
-    for (int64_t r = 0; r < n; ++r) h.set_ptr[r + 1] += h.set_ptr[r];
-    h.set_items.resize(static_cast<size_t>(sc.n_items));
-    size_t at = 0;
-    for (int64_t c = 0; c < nch; ++c) {
-        const auto& v = sc.part_items[c];
-        if (!v.empty()) std::memcpy(h.set_items.data() + at, v.data(), v.size() * sizeof(int64_t));
-        at += v.size();
-    }
-}
-
 static void union_map(Hop& h, HopScratch& sc) {
     PySet& u = sc.u;
     // The next frontier: the union's keys in slot order (a vector compaction
@@ -348,63 +336,168 @@ static void union_map(Hop& h, HopScratch& sc) {
         if (u.tab[sl] != PySet::EMPTY) *dst++ = u.tab[sl];
 }
 
-static void lists(Hop& h, HopScratch& sc, bool gcn) {
-    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
-    const PySet& u = sc.u;
-    // Union-local positions = rank of the key's slot in the union's table
-    // (its iteration order): a probe of that cache-resident table instead of
-    // a graph-sized node -> position array (random DRAM reads and writes).
-    sc.slot_local.resize(u.mask + 1);
-    int32_t rank = 0;
-    for (size_t sl = 0; sl <= u.mask; ++sl) {
-        sc.slot_local[sl] = rank;
-        rank += u.tab[sl] != PySet::EMPTY;
-    }
-    auto local_of = [&](int64_t key) -> int32_t {
-        return sc.slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(key)))];
+// part 0: the neighbour lists and self ids; part 1: the transposed lists
+static void copy_lists(const Hop& h, PackOut& po, int32_t j, int part) {
+    auto cpy = [&](int f, const std::vector<int32_t>& v) {
+        if (!v.empty()) std::memcpy(po.buf + po.off[j][f], v.data(), v.size() * sizeof(int32_t));
     };
-    // Neighbourhoods in union-local ids, ascending (= the dense mask's column
-    // order, :305-308); non-gcn removes self (:297-298).
-    h.nbr_ptr.assign(n + 1, 0);
-    h.nbr.clear();
-    h.self_local.resize(n);
-    std::vector<int32_t>& tmp = sc.tmp;
-    const int64_t n_items = static_cast<int64_t>(h.set_items.size());
-    for (int64_t r = 0; r < n; ++r) {
-        const int64_t v = h.dst_ids[r];
-        tmp.clear();
-        for (int32_t q = h.set_ptr[r]; q < h.set_ptr[r + 1]; ++q) {
-            if (q + 16 < n_items) __builtin_prefetch(u.tab + (static_cast<size_t>(h.set_items[q + 16]) & u.mask));
-            const int64_t key = h.set_items[q];
-            if (!gcn && key == v) continue;
-            tmp.push_back(local_of(key));
-        }
-        for (size_t a = 1; a < tmp.size(); ++a) {  // insertion sort: lists are <= k+1 long
-            const int32_t x = tmp[a];
-            size_t b = a;
-            for (; b > 0 && tmp[b - 1] > x; --b) tmp[b] = tmp[b - 1];
-            tmp[b] = x;
-        }
-        h.nbr.insert(h.nbr.end(), tmp.begin(), tmp.end());
-        h.nbr_ptr[r + 1] = static_cast<int32_t>(h.nbr.size());
-        h.self_local[r] = local_of(v);
+    if (part == 0) {
+        cpy(GS_PK_NBR_PTR, h.nbr_ptr);
+        cpy(GS_PK_NBR, h.nbr);
+        cpy(GS_PK_SELF, h.self_local);
+    } else {
+        cpy(GS_PK_TPTR, h.tptr);
+        cpy(GS_PK_TIDX, h.tidx);
     }
-    // Transposed lists over Fj: for source c, the destinations reading it
-    // (r >= 0) and the destinations whose self row it is (-(r+1)), r ascending.
+}
+
+// A hop's lists from its sets and the union (lists_task on up to
+// `workers` threads at once, each taking units of each stage in turn):
+//   stage 0  the union's slot -> rank map (one unit);
+//   stage 1  per sets_union chunk: h.set_items / h.set_ptr (the chunks'
+//            items concatenated and scanned, for the Sample view), each
+//            destination's neighbourhood in union-local ids, ascending (the
+//            dense mask's column order, :305-308; non-gcn drops self,
+//            :297-298), and its self id;
+//   stage 2  the transposed lists over the sources (for source c, the
+//            destinations reading it, r >= 0, and those whose self row it is,
+//            -(r+1), r ascending) and their pack copy; beside it (a second
+//            unit, with a pack) the pack copy of the stage-1 lists.
+// A worker claims units until its stage has none left, then waits for the
+// units other workers claimed (each is running: no wait depends on a task
+// that has not started), so one worker alone runs everything, in order, and
+// more workers give the same lists.  Every buffer is sized by lists_prepare
+// on the submitting thread: the tasks allocate nothing.
+struct ListsJob {
+    static constexpr int kStages = 3;
+    Hop* h = nullptr;
+    HopScratch* sc = nullptr;
+    PackOut* po = nullptr;
+    int32_t j = 0;
+    bool gcn = false;
+    int64_t units[kStages] = {1, 0, 1};
+    std::atomic<int64_t> claim[kStages], done[kStages];
+    std::atomic<bool> failed{false};
+};
+
+static void lists_prepare(ListsJob& L, Hop& h, HopScratch& sc, bool gcn, PackOut* po, int32_t j) {
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    const int64_t nch = (n + kChunk - 1) / kChunk;
     const int64_t ns = static_cast<int64_t>(h.src_ids.size());
-    h.tptr.assign(ns + 1, 0);
+    L.h = &h;
+    L.sc = &sc;
+    L.po = po;
+    L.j = j;
+    L.gcn = gcn;
+    L.units[1] = nch;
+    L.units[2] = po ? 2 : 1;
+    for (int s = 0; s < ListsJob::kStages; ++s) {
+        L.claim[s].store(0, std::memory_order_relaxed);
+        L.done[s].store(0, std::memory_order_relaxed);
+    }
+    L.failed.store(false, std::memory_order_relaxed);
+    // chunk c's first item (sc.chunk_base[c]); the per-set counts are in h.set_ptr[1 + r]
+    sc.chunk_base.resize(static_cast<size_t>(nch) + 1);
+    sc.chunk_base[0] = 0;
+    for (int64_t c = 0; c < nch; ++c)
+        sc.chunk_base[c + 1] = sc.chunk_base[c] + static_cast<int64_t>(sc.part_items[c].size());
+    h.set_items.resize(static_cast<size_t>(sc.n_items));
+    sc.slot_local.resize(sc.u.mask + 1);
+    h.nbr_ptr.resize(static_cast<size_t>(n) + 1);
+    h.nbr.resize(static_cast<size_t>(sc.n_items - (gcn ? 0 : n)));
+    h.self_local.resize(static_cast<size_t>(n));
+    h.tptr.assign(static_cast<size_t>(ns) + 1, 0);
+    h.tidx.resize(h.nbr.size() + static_cast<size_t>(n));
+    sc.cur.resize(static_cast<size_t>(ns));
+}
+
+static void lists_unit(ListsJob& L, int stage, int64_t unit) {
+    Hop& h = *L.h;
+    HopScratch& sc = *L.sc;
+    const PySet& u = sc.u;
+    const int64_t n = static_cast<int64_t>(h.dst_ids.size());
+    if (stage == 0) {
+        // union-local position = rank of the key's slot in the union's table
+        // (its iteration order): a probe of that cache-resident table instead
+        // of a graph-sized node -> position array
+        int32_t rank = 0;
+        for (size_t sl = 0; sl <= u.mask; ++sl) {
+            sc.slot_local[sl] = rank;
+            rank += u.tab[sl] != PySet::EMPTY;
+        }
+        return;
+    }
+    if (stage == 1) {
+        const int64_t c = unit, a = c * kChunk, b = std::min(n, a + kChunk);
+        const std::vector<int64_t>& items = sc.part_items[c];
+        const int64_t base = sc.chunk_base[c];
+        if (!items.empty()) std::memcpy(h.set_items.data() + base, items.data(), items.size() * sizeof(int64_t));
+        const int32_t* cnt = sc.counts.data() + a;
+        int64_t q = 0;  // item index within the chunk
+        const int64_t m = static_cast<int64_t>(items.size());
+        for (int64_t r = a; r < b; ++r) {
+            const int64_t v = h.dst_ids[r];
+            const int64_t beg = base + q;
+            h.set_ptr[r] = static_cast<int32_t>(beg);
+            int32_t* out = h.nbr.data() + (beg - (L.gcn ? 0 : r));
+            h.nbr_ptr[r] = static_cast<int32_t>(beg - (L.gcn ? 0 : r));
+            int32_t k = 0;
+            for (const int64_t qe = q + cnt[r - a]; q < qe; ++q) {
+                if (q + 16 < m) __builtin_prefetch(u.tab + (static_cast<size_t>(items[q + 16]) & u.mask));
+                const int64_t key = items[q];
+                if (!L.gcn && key == v) continue;
+                const int32_t x = sc.slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(key)))];
+                int32_t p = k++;  // insertion sort: lists are <= k+1 long
+                for (; p > 0 && out[p - 1] > x; --p) out[p] = out[p - 1];
+                out[p] = x;
+            }
+            h.self_local[r] = sc.slot_local[static_cast<size_t>(u.find_slot(static_cast<int32_t>(v)))];
+        }
+        if (b == n) {
+            h.set_ptr[n] = static_cast<int32_t>(base + m);
+            h.nbr_ptr[n] = static_cast<int32_t>(h.nbr.size());
+        }
+        return;
+    }
+    // stage 2
+    if (unit == 1) {
+        copy_lists(h, *L.po, L.j, 0);
+        return;
+    }
+    const int64_t ns = static_cast<int64_t>(h.src_ids.size());
     for (int32_t c : h.nbr) ++h.tptr[c + 1];
     for (int32_t c : h.self_local) ++h.tptr[c + 1];
     for (int64_t c = 0; c < ns; ++c) h.tptr[c + 1] += h.tptr[c];
-    h.tidx.resize(h.tptr[ns]);
     std::vector<int32_t>& cur = sc.cur;
-    cur.assign(h.tptr.begin(), h.tptr.end() - 1);
+    std::copy(h.tptr.begin(), h.tptr.end() - 1, cur.begin());
     for (int64_t r = 0; r < n; ++r) {
         h.tidx[cur[h.self_local[r]]++] = static_cast<int32_t>(-(r + 1));
-        for (int32_t e = h.nbr_ptr[r]; e < h.nbr_ptr[r + 1]; ++e)
-            h.tidx[cur[h.nbr[e]]++] = static_cast<int32_t>(r);
+        for (int32_t e = h.nbr_ptr[r]; e < h.nbr_ptr[r + 1]; ++e) h.tidx[cur[h.nbr[e]]++] = static_cast<int32_t>(r);
     }
     h.materialised = true;
+    if (L.po) copy_lists(h, *L.po, L.j, 1);
+}
+
+// A unit that throws marks the job failed (later units are skipped, their
+// stages still complete); the worker that caught it rethrows once every stage
+// is done, so the team's wait() (or the inline caller) sees it.
+static void lists_task(ListsJob& L) {
+    std::exception_ptr mine;
+    for (int s = 0; s < ListsJob::kStages; ++s) {
+        for (int64_t t; (t = L.claim[s].fetch_add(1, std::memory_order_relaxed)) < L.units[s];) {
+            if (!L.failed.load(std::memory_order_relaxed)) {
+                try {
+                    lists_unit(L, s, t);
+                } catch (...) {
+                    mine = std::current_exception();
+                    L.failed.store(true, std::memory_order_relaxed);
+                }
+            }
+            L.done[s].fetch_add(1, std::memory_order_acq_rel);
+        }
+        while (L.done[s].load(std::memory_order_acquire) < L.units[s]) _mm_pause();
+    }
+    if (mine) std::rethrow_exception(mine);
 }
 
 // Sampling state reused from batch to batch by one thread (the runner's
@@ -413,6 +506,7 @@ static void lists(Hop& h, HopScratch& sc, bool gcn) {
 struct SampleCtx {
     Sample s;
     HopScratch scratch[2];  // hop j's lists may still run on a helper while hop j+1 builds its sets
+    ListsJob lists[2];      // hop j's lists job (on scratch[j & 1])
     std::vector<int64_t> frontier;
 };
 
@@ -420,17 +514,6 @@ struct SampleCtx {
 // needs it only to fail MAX batches, GS_SAMPLE_FAIL_EMPTY — its scan re-reads
 // a row entry of every single-sample destination, ~2-3 % of a batch).
 // po: write the pack while sampling (PackOut; not with GS_SAMPLE_FULL).
-static void copy_lists(const Hop& h, PackOut& po, int32_t j) {
-    auto cpy = [&](int f, const std::vector<int32_t>& v) {
-        if (!v.empty()) std::memcpy(po.buf + po.off[j][f], v.data(), v.size() * sizeof(int32_t));
-    };
-    cpy(GS_PK_NBR_PTR, h.nbr_ptr);
-    cpy(GS_PK_NBR, h.nbr);
-    cpy(GS_PK_SELF, h.self_local);
-    cpy(GS_PK_TPTR, h.tptr);
-    cpy(GS_PK_TIDX, h.tidx);
-}
-
 static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const int64_t* roots, int64_t n_roots,
                             const int32_t* fanouts, int32_t n_hops, int32_t flags, Team* team,
                             bool count_empties = true, PackOut* po = nullptr) {
@@ -489,17 +572,14 @@ static void run_sample_into(SampleCtx& c, const Graph& g, MT19937& rng, const in
                 po->put(j, GS_PK_TPTR, static_cast<int64_t>(h.src_ids.size()) + 1);
                 po->put(j, GS_PK_TIDX, n_nbr + n);
             }
-            if (team) {  // lists + transpose (+ their pack copy) on a helper, under the next hop's draws
-                team->start(1, [&h, &sc, gcn, po, j](int) {
-                    gather_sets(h, sc);
-                    lists(h, sc, gcn);
-                    if (po) copy_lists(h, *po, j);
-                });
+            ListsJob& L = c.lists[j & 1];
+            lists_prepare(L, h, sc, gcn, po, j);
+            if (team) {  // lists + transpose (+ their pack copy) on the helpers, under the next hop's draws
+                const int64_t nw = std::min<int64_t>(team->helpers(), L.units[1]);
+                team->start(static_cast<int>(std::max<int64_t>(nw, 1)), [&L](int) { lists_task(L); });
                 pending = true;
             } else {
-                gather_sets(h, sc);
-                lists(h, sc, gcn);
-                if (po) copy_lists(h, *po, j);
+                lists_task(L);
             }
         }
     }

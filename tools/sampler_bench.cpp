@@ -5,7 +5,7 @@
 //   g++ -O3 -march=x86-64-v3 -std=c++17 -pthread -I include -I graphsage-pytorch_amd/csrc/host \
 //       tools/sampler_bench.cpp graphsage-pytorch_amd/csrc/host/graph.cpp \
 //       graphsage-pytorch_amd/csrc/host/errors.cpp -o /tmp/sampler_bench
-//   /tmp/sampler_bench [helpers=1] [batches=300] [streams=1] [shared=0]
+//   /tmp/sampler_bench [helpers=1] [batches=300] [streams=1] [shared=0] [pair file B fan0 fan1]
 // With streams > 1, that many independent streams run on their own threads
 // (each with its own team), as the runner's layout does; shared=1 gives them
 // one pool of helpers x streams threads (GS_SHARED_HELPERS=1 in the runner).
@@ -37,19 +37,35 @@ int main(int argc, char** argv) {
     const int batches = argc > 2 ? std::atoi(argv[2]) : 300;
     const int streams = argc > 3 ? std::atoi(argv[3]) : 1;
     const bool shared = argc > 4 && std::atoi(argv[4]) == 1;
+    // [graph file B fan0 fan1]: a pair file (int64 n, int64 count, count src ids,
+    // count dst ids; e.g. tools/lab/dump_pairs.py pubmed) instead of the R-MAT
+    const char* gfile = argc > 5 ? argv[5] : nullptr;
     const int scale = 21;
-    const int64_t pairs = 20000000, n = int64_t(1) << scale;
-    std::vector<int64_t> src(pairs), dst(pairs);
+    int64_t pairs = 20000000, n = int64_t(1) << scale;
+    std::vector<int64_t> src, dst;
     int64_t np = 0;
-    if (gs_rmat_pairs(scale, pairs, 0.57, 0.19, 0.19, 824, 1, 8, src.data(), dst.data(), &np) != GS_OK) return 1;
+    if (gfile) {
+        FILE* f = std::fopen(gfile, "rb");
+        if (!f || std::fread(&n, 8, 1, f) != 1 || std::fread(&pairs, 8, 1, f) != 1) return 1;
+        src.resize(pairs);
+        dst.resize(pairs);
+        if (std::fread(src.data(), 8, pairs, f) != size_t(pairs) || std::fread(dst.data(), 8, pairs, f) != size_t(pairs))
+            return 1;
+        std::fclose(f);
+        np = pairs;
+    } else {
+        src.resize(pairs);
+        dst.resize(pairs);
+        if (gs_rmat_pairs(scale, pairs, 0.57, 0.19, 0.19, 824, 1, 8, src.data(), dst.data(), &np) != GS_OK) return 1;
+    }
     gs_graph* gp = nullptr;
     if (gs_graph_build(src.data(), dst.data(), np, n, 8, &gp) != GS_OK) return 1;
     const auto& g = *reinterpret_cast<const gs::Graph*>(gp);
     std::vector<int64_t> cand;
     for (int64_t v = 0; v < n; ++v)
         if (g.degree(v) > 0) cand.push_back(v);
-    const int32_t fan[2] = {25, 10};
-    const int64_t B = 512;
+    const int32_t fan[2] = {gfile && argc > 7 ? std::atoi(argv[7]) : 25, gfile && argc > 8 ? std::atoi(argv[8]) : 10};
+    const int64_t B = gfile && argc > 6 ? std::atoll(argv[6]) : 512;
     std::vector<double> per(streams, 0.0);
     std::vector<uint64_t> check(streams, 0);
     gs_team* pool = nullptr;  // shared mode: the handle the streams' teams share threads with
