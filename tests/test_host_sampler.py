@@ -423,6 +423,50 @@ def test_team_pack_equals_single_thread(gs, helpers, fan, group):
         L.lib().gs_team_destroy(team)
 
 
+@pytest.mark.parametrize("gcn", [False, True])
+def test_team_lists_job_many_workers(gs, gcn):
+    """A hop's lists job split over seven helpers (slot ranks, then chunks of
+    32 destinations, then the transpose beside the pack copy): 2,000-root
+    batches (63 chunks) with and without gcn give the team-less pack bit for
+    bit, batch after batch."""
+    L = gs._lib
+    G_, _ = _graph(gs, "rmat")
+    fan = np.array((10, 10), np.int32)
+    nh = len(fan)
+    flags = L.GS_SAMPLE_GCN if gcn else 0
+    cand = np.nonzero(G_.degrees())[0]
+    rs = np.random.RandomState(11)
+    team = ctypes.c_void_p()
+    L.check(L.lib().gs_team_create(7, ctypes.byref(team)))
+    r1, r2 = gs.RNG(5), gs.RNG(5)
+
+    def run(rng, roots, t):
+        bound = int(L.lib().gs_sample_pack_bound(G_.handle, len(roots), fan.ctypes.data, nh))
+        buf = np.full(bound, -7, np.int32)
+        sizes = np.empty(4 * nh, np.int64)
+        offs = np.empty(L.GS_MAX_HOPS * L.GS_PK_NFIELDS, np.int64)
+        used = ctypes.c_int64()
+        if t is None:
+            L.check(L.lib().gs_sample_pack_run(G_.handle, rng._h, roots.ctypes.data, len(roots), fan.ctypes.data,
+                                               nh, flags, buf.ctypes.data, bound, sizes.ctypes.data,
+                                               offs.ctypes.data, ctypes.byref(used)))
+        else:
+            L.check(L.lib().gs_sample_pack_run_multi_team(G_.handle, rng._h, roots.ctypes.data, len(roots),
+                                                          len(roots), fan.ctypes.data, nh, flags, buf.ctypes.data,
+                                                          bound, sizes.ctypes.data, offs.ctypes.data,
+                                                          ctypes.byref(used), t))
+        return buf[:used.value].copy(), sizes.copy()
+
+    try:
+        for _ in range(3):
+            roots = rs.choice(cand, 2000).astype(np.int64)
+            want, got = run(r1, roots, None), run(r2, roots, team)
+            assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+            assert r1.getstate()[0].tolist() == r2.getstate()[0].tolist() and r1.getstate()[1] == r2.getstate()[1]
+    finally:
+        L.lib().gs_team_destroy(team)
+
+
 def test_shared_team_streams_equal_single_thread(gs):
     """Three sampling streams on three threads whose teams share one pool of
     helpers (gs_team_create_shared, the runner's GS_SHARED_HELPERS layout):
