@@ -276,7 +276,9 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 # and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
 # the kernel beside the live event-timed one
 # (newest round first: the first file present is used)
-ROCPROF_STATS = {("rmat2m", 512): ["profiles/r05_kernel_stats_rmat2m_steps300.csv",
+ROCPROF_TOL = 0.15  # live vs committed rocprofv3 average: `rocprof_agrees` within this fraction
+ROCPROF_STATS = {("rmat2m", 512): ["profiles/r06_kernel_stats_rmat2m_steps300.csv",
+                                   "profiles/r05_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04f_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04e_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r04d_kernel_stats_rmat2m_steps300.csv",
@@ -287,7 +289,8 @@ ROCPROF_STATS = {("rmat2m", 512): ["profiles/r05_kernel_stats_rmat2m_steps300.cs
                                    "profiles/r03b_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r03_kernel_stats_rmat2m_steps300.csv",
                                    "profiles/r02_kernel_stats_rmat2m_steps300.csv"],
-                 ("rmat2m-max-bf16", 512): ["profiles/r05_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                 ("rmat2m-max-bf16", 512): ["profiles/r06_kernel_stats_rmat2m_max_bf16_steps300.csv",
+                                            "profiles/r05_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04f_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04e_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r04d_kernel_stats_rmat2m_max_bf16_steps300.csv",
@@ -298,7 +301,8 @@ ROCPROF_STATS = {("rmat2m", 512): ["profiles/r05_kernel_stats_rmat2m_steps300.cs
                                             "profiles/r03b_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r03_kernel_stats_rmat2m_max_bf16_steps300.csv",
                                             "profiles/r02_kernel_stats_rmat2m_max_bf16_steps300.csv"],
-                 ("rmat16m", 512): ["profiles/r03c_kernel_stats_rmat16m_steps300.csv",
+                 ("rmat16m", 512): ["profiles/r06_kernel_stats_rmat16m_steps300.csv",
+                                    "profiles/r03c_kernel_stats_rmat16m_steps300.csv",
                                     "profiles/r03_kernel_stats_rmat16m_steps300.csv",
                                     "profiles/r02_kernel_stats_rmat16m_steps300.csv"]}
 
@@ -915,20 +919,24 @@ def main():
                 mb = load_mfma_busy(args.config, names[site])
                 work.update(mfma_busy=(mb["mfma_util"] if mb else None), mfma_busy_source=(mb["source"] if mb else None),
                             mfma_busy_dispatches=(mb["dispatches"] if mb else None))
-            achieved_live = scale / (us * 1e-6)
-            # `achieved` / `frac` on the committed rocprofv3 average of this kernel
-            # (the same command under --kernel-trace --stats, profiles/), so the
-            # line reproduces from profiles/; the live in-step timing beside it
+            # `achieved` / `frac` on this run's own in-step timing of the kernel;
+            # beside it the committed rocprofv3 average of the same kernel (the
+            # same command under --kernel-trace --stats, profiles/) and whether
+            # the two agree within ROCPROF_TOL (a stale profile or a slower
+            # build shows up as a disagreement, never in `frac`)
+            achieved = scale / (us * 1e-6)
             rp = prof_avg[site]
-            achieved = scale / (rp["avg_us"] * 1e-6) if rp else achieved_live
+            achieved_rp = scale / (rp["avg_us"] * 1e-6) if rp else None
             tr = load_traffic(args.config, cfg["batch"], names[site])
             rooflines[SITE_NAMES[site]] = dict(
                 bound=bound, achieved=round(achieved, 2), peak=peak, unit=unit, frac=round(achieved / peak, 4),
                 traffic=(tr["hbm_bytes"] if tr else None), traffic_source=(tr["source"] if tr else None),
                 traffic_dispatches=(tr["dispatches"] if tr else None),
-                achieved_from=("rocprofv3 average launch (rocprof.avg_us)" if rp else "live in-step timing"),
+                achieved_from="live in-step timing (avg_launch_us)",
                 rocprof=rp,
-                achieved_live=round(achieved_live, 2), frac_live=round(achieved_live / peak, 4),
+                achieved_rocprof=(round(achieved_rp, 2) if rp else None),
+                frac_rocprof=(round(achieved_rp / peak, 4) if rp else None),
+                rocprof_agrees=(abs(us - rp["avg_us"]) <= ROCPROF_TOL * rp["avg_us"] if rp else None),
                 kernel=names[site],
                 role=SITE_ROLES[site], avg_launch_us=round(us, 2),
                 timer=("kernel span (per-workgroup s_memrealtime stamps, min start .. max end)"

@@ -129,6 +129,7 @@ _SIGS = {
     "gs_trainer_forward_backward": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gs_trainer_update": (_i32, [_vp, _f32, _vp, _vp]),
     "gs_trainer_update_local": (_i32, [_vp, _vp]),
+    "gs_trainer_defer": (_i32, [_vp, _i32, _p(_i32), _vp]),
     "gs_trainer_gather_reserve": (_i32, [_vp, _i64, _i32]),
     "gs_trainer_gather": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),
     "gs_trainer_forward_backward_gathered": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),

@@ -396,7 +396,8 @@ static void lists_prepare(ListsJob& L, Hop& h, HopScratch& sc, bool gcn, PackOut
         L.done[s].store(0, std::memory_order_relaxed);
     }
     L.failed.store(false, std::memory_order_relaxed);
-    // chunk c's first item (sc.chunk_base[c]); the per-set counts are in h.set_ptr[1 + r]
+    // chunk c's first item (sc.chunk_base[c]); the per-set counts are in sc.counts
+    // (the lists job writes h.set_ptr itself)
     sc.chunk_base.resize(static_cast<size_t>(nch) + 1);
     sc.chunk_base[0] = 0;
     for (int64_t c = 0; c < nch; ++c)

@@ -66,7 +66,8 @@ struct gs_trainer {
     // clip-norm partials produced by the fused backward's reduce launches
     // (group 0: the sage weights' slab sums, group 1: the classifier reduce),
     // consumed by gs_trainer_update_local when no all-reduce came between
-    // gs_trainer_set_option switches (bitwise-equal alternatives the tests compare)
+    // gs_trainer_set_option switches (alternatives the tests compare with the
+    // default: bitwise, except top_launch, which matches within fp32 rounding)
     bool fuse_bwd = true;    // GS_TOPT_FUSED_BWD: layers >= 2 backward in fused launches
     bool use_top = true;     // GS_TOPT_TOP_LAUNCH: layer 2 + loss head + dIn2 in one launch
     bool want_self_rows = true;  // GS_TOPT_SELF_ROWS
@@ -1121,6 +1122,24 @@ int gs_trainer_update(gs_trainer* t, float grad_scale, float* ws, void* stream) 
     int rc = gs_clip_sgd(2, goff, t->cfg.params, t->cfg.grads, grad_scale, t->cfg.max_norm, t->cfg.lr, ws, stream);
     if (rc != GS_OK) return rc;
     arm.done();
+    GS_API_END
+}
+
+int gs_trainer_defer(gs_trainer* t, int32_t on, int32_t* active, void* stream) {
+    GS_API_BEGIN
+    GS_REQUIRE(t, GS_EINVAL, "NULL argument");
+    hipStream_t st = gs::as_stream(stream);
+    if (active) *active = 0;
+    if (on) {
+        GS_REQUIRE(!t->defer && !t->pending, GS_EINVAL, "gs_trainer_defer: already deferring");
+        gs::trainer_keep_lowp(t, true);  // the bf16 W1 follows every update, as in a runner loop
+        const bool ok = gs::trainer_defer_update(t, true, st, true);
+        if (!ok) gs::trainer_keep_lowp(t, false);
+        if (active) *active = ok ? 1 : 0;
+    } else {
+        if (t->defer) gs::trainer_defer_update(t, false, st);
+        gs::trainer_keep_lowp(t, false);
+    }
     GS_API_END
 }
 

@@ -132,8 +132,10 @@ class NativeTrainer:
                 "self_rows": _lib.GS_TOPT_SELF_ROWS, "defer_update": _lib.GS_TOPT_DEFER_UPDATE}
 
     def set_option(self, name, value):
-        """gs_trainer_set_option: switch a bitwise-equal alternative of the
-        step (fused_bwd, top_launch, self_rows, defer_update; default all on)."""
+        """gs_trainer_set_option: switch an alternative of the step (fused_bwd,
+        top_launch, self_rows, defer_update; default all on).  fused_bwd,
+        self_rows and defer_update are bitwise the default; top_launch matches
+        it within fp32 rounding of its split-K order."""
         check(lib().gs_trainer_set_option(self._h, self._OPTIONS[name], int(bool(value))))
         return self
 
@@ -156,6 +158,15 @@ class NativeTrainer:
         every rank runs after the gradient all-reduce (grad_scale = 1/world)."""
         check(lib().gs_trainer_update(self._h, float(grad_scale), self.clip_ws.data_ptr(),
                                       _lib.stream_ptr(self.device)))
+
+    def defer(self, on):
+        """gs_trainer_defer: from now on each update(1/W) after the gradient
+        all-reduce is left pending and applied by the next forward (the
+        runner's communicator path); defer(False) applies a pending update.
+        Returns whether deferring took effect for this step shape."""
+        active = ctypes.c_int32(0)
+        check(lib().gs_trainer_defer(self._h, int(bool(on)), ctypes.byref(active), _lib.stream_ptr(self.device)))
+        return bool(active.value)
 
     def apply_update(self, world_size=1, group=None):
         """All-reduce (sum) the flat gradients over ranks, then clip + SGD with 1/world."""

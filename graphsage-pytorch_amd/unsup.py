@@ -159,7 +159,9 @@ class UnsupervisedLoss:
         self._uniq_list, self._uniq_arr = list(v), None
 
     def _unique_array(self):
-        if self._uniq_arr is None:
+        # once the list has been handed out it is the reference's attribute and
+        # may have been edited in place: the losses read it, as models.py does
+        if self._uniq_list is not None:
             self._uniq_arr = np.asarray(self._uniq_list, np.int64).reshape(-1)
         return self._uniq_arr
 
@@ -218,9 +220,13 @@ class UnsupervisedLoss:
 
     def extend_nodes_array(self, nodes, num_neg=6):
         """extend_nodes with unique_nodes_batch returned as an int64 array (the
-        same ids in the same order, no Python list; utils.train_step's path)."""
+        same ids in the same order, no Python list; utils.train_step's path).
+        The array is a read-only view: the losses read the ids back through
+        the same buffer, so a caller cannot change them under the plan."""
         self._extend(nodes, num_neg)
-        return self._uniq_arr
+        view = self._uniq_arr.view()
+        view.flags.writeable = False
+        return view
 
     def _extend(self, nodes, num_neg):
         self._reset_pairs()

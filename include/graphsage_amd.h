@@ -585,9 +585,23 @@ float* gs_trainer_grads(const gs_trainer* t);
  * may be NULL; max_steps 0 disarms.  gs_trainer_captured: steps copied. */
 int gs_trainer_capture(gs_trainer* t, float* emb, int64_t emb_stride, float* grads, int64_t max_steps);
 int64_t gs_trainer_captured(const gs_trainer* t);
+/* Deferred clip + SGD for a caller's own data-parallel loop (utils.py:184-187
+ * per rank after the gradient sum), as gs_runner_run runs it with a
+ * communicator: with on = 1, each gs_trainer_update(t, 1/W, ...) after the
+ * all-reduce leaves the update pending — one launch computes the summed
+ * gradient's clip-norm partials and W1's speculative update S = W1 - lr*g/W —
+ * and the next forward applies the clip + SGD in its prologue (the fold of
+ * those partials with scale 1/W).  on = 0 applies a pending update and leaves
+ * deferred mode, so the flat parameters are current again.  *active (may be
+ * NULL): 1 when deferring took effect (the step's shape allows it: 2 layers,
+ * fused top launch and backward, 16-byte feature rows), else 0 and every
+ * update runs at once.  Not inside a runner loop. */
+int gs_trainer_defer(gs_trainer* t, int32_t on, int32_t* active, void* stream);
 /* Trainer options (gs_trainer_set_option, value 0 / 1; not inside a runner
- * loop).  Each alternative computes bitwise the default's results and exists
- * for the tests that prove it:
+ * loop).  Each alternative exists for the tests that compare it with the
+ * default.  fused_bwd, self_rows and defer_update compute bitwise the
+ * default's results; top_launch matches them within fp32 rounding of the
+ * k order (its split-K partial sums are added in a fixed, different order):
  *   GS_TOPT_FUSED_BWD     1: layers >= 2 backward in fused launches
  *   GS_TOPT_TOP_LAUNCH    1: a 2-layer step's layer 2 + loss head + dIn2 in one launch
  *   GS_TOPT_SELF_ROWS     1: gather slots hold [self | agg] rows (next gs_trainer_gather_reserve)

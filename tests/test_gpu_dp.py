@@ -47,12 +47,16 @@ def _setup(gs):
     return graph, adj, X, labels, cands
 
 
-def _oracle_dp(adj, X, labels, per_rank):
+def _oracle_dp(adj, X, labels, per_rank, max_norm=5.0, sums=None):
+    """The reference's step per rank on its own batch and stream, the rank
+    gradients summed (the all-reduce), then clip_grad_norm_(max_norm) per model
+    and SGD on the sum / W (utils.py:184-187).  sums: the summed flat gradient
+    [dW1 | dW2 | dWc | dbc] of each step is appended to it."""
     sage_w, cw, cb = train.reference_init(2, F, H, C, False, SEED)
     params = [w.clone().requires_grad_(True) for w in sage_w] + [cw.clone().requires_grad_(True),
                                                                 cb.clone().requires_grad_(True)]
     rngs = [random.Random(train.rank_seed(SEED, r)) for r in range(W)]
-    for i in range(STEPS):
+    for i in range(len(per_rank[0])):
         gsum = None
         for r in range(W):
             roots = per_rank[r][i]
@@ -64,11 +68,13 @@ def _oracle_dp(adj, X, labels, per_rank):
             for p in params:
                 p.grad = None
             gsum = g if gsum is None else [a + b for a, b in zip(gsum, g)]
+        if sums is not None:
+            sums.append(torch.cat([x.reshape(-1) for x in gsum]))
         with torch.no_grad():  # utils.py:185-187 on the averaged gradient
             scaled = [x / W for x in gsum]
             for group in ((0, 1), (2, 3)):
                 norm = torch.norm(torch.stack([torch.norm(scaled[j]) for j in group]))
-                coef = min(1.0, 5.0 / (float(norm) + 1e-6))
+                coef = min(1.0, max_norm / (float(norm) + 1e-6))
                 for j in group:
                     scaled[j] = scaled[j] * coef
             for p, x in zip(params, scaled):
@@ -97,6 +103,61 @@ def test_two_rank_step_arithmetic_on_one_gpu(gs):
     got = [sd["sage_layer1.weight"], sd["sage_layer2.weight"], sd["layer.0.weight"], sd["layer.0.bias"]]
     for a, b in zip(got, ref):
         torch.testing.assert_close(a.cpu(), b, atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("max_norm", [5.0, 1e-3])
+def test_two_rank_deferred_update_on_one_gpu(gs, max_norm):
+    """The N > 1 runner's update path at W = 2: two trainers
+    play ranks 0 and 1 in deferred-communicator mode (gs_trainer_defer, what
+    gs_runner_run enters with a communicator).  Per step each rank runs its
+    forward/backward on its own batch and stream; the two gradient buffers are
+    summed in place into both trainers (what the in-place RCCL sum leaves on
+    every rank); then each rank's gs_trainer_update(1/2) leaves the update
+    pending (group_sumsq_spec_kernel: the summed gradient's clip-norm partials
+    and W1's speculative update), and the next step's layer-1 forward applies
+    it with FwdSpec::scale = 1/2 (the pending-update kernel instance, checked by
+    name).  Four steps, so three forwards apply a pending update; max_norm 5
+    (the reference's) and 1e-3 (every step clipped: the forward's recompute
+    path).  Against the oracle's W = 2 step at 1e-5: each step's summed
+    gradient and the final weights; the ranks' weights bitwise equal."""
+    steps = 4
+    graph, adj, X, labels, cands = _setup(gs)
+    per_rank = [list(train.rank_batches(cands, B, r, W, SEED + 1000))[:steps] for r in range(W)]
+    trs = [train.NativeTrainer(graph, X.to(DEV), labels.to(DEV), C, hidden=H, fanouts=FAN, seed=SEED,
+                               max_norm=max_norm) for _ in range(W)]
+    assert all(t.defer(True) for t in trs)
+    rngs = [train.make_rng(SEED, r) for r in range(W)]
+    lib = gs._lib.lib()
+    sums = []
+    for i in range(steps):
+        if i == steps - 1:  # name the forward variant the last step launches (timer site 1)
+            for t in trs:
+                gs._lib.check(lib.gs_trainer_time_kernels(t._h, 0b10, 1))
+        for r in range(W):  # rank r: its own batch, stream and trainer
+            roots = per_rank[r][i]
+            ds = models.DeviceSample(gs.sample(graph, rngs[r], roots, FAN), DEV)
+            trs[r].forward_backward(ds, torch.from_numpy(roots.astype(np.int32)).to(DEV))
+        gsum = trs[0].p.grads + trs[1].p.grads
+        for t in trs:
+            t.p.grads.copy_(gsum)
+            t.update(grad_scale=1.0 / W)  # deferred: applied by the next forward
+        sums.append(gsum.cpu())
+    torch.cuda.synchronize()
+    for t in trs:
+        name = lib.gs_trainer_kernel_name(t._h, 1).decode()
+        assert "linear_fwd_wide_kernel" in name and name.split(">(")[0].endswith("true"), name
+    for t in trs:
+        t.defer(False)  # the last pending update
+    torch.cuda.synchronize()
+    ref_sums = []
+    ref = _oracle_dp(adj, X, labels, per_rank, max_norm=max_norm, sums=ref_sums)
+    for i, (a, b) in enumerate(zip(sums, ref_sums)):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5, msg=lambda m: f"step {i} summed grads: {m}")
+    assert torch.equal(trs[0].p.params, trs[1].p.params)
+    sd = trs[0].p.state_dict()
+    got = [sd["sage_layer1.weight"], sd["sage_layer2.weight"], sd["layer.0.weight"], sd["layer.0.bias"]]
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a.cpu(), b, atol=1e-5, rtol=1e-5)
 
 
 @pytest.mark.parametrize("agg,batch", [("MEAN", 48), ("MAX", 48), ("MEAN", 200)])

@@ -116,6 +116,14 @@ def test_fullsize_timed_step_embeddings_and_grads_vs_oracle(wl, adj):
     print("max |emb diff|, max |grad diff|, max |grad| per step:", worst)
 
 
+def test_fullsize_timed_step_fp32_max_vs_oracle(wl, adj):
+    """The headline graph with the MAX aggregator over the fp32 feature table
+    (models.py:316-326: per-row element-wise max, first-index argmax in the
+    backward): the bench's timed steps 1 and 2 against oracle autograd at 1e-5."""
+    worst = check_timed_steps_vs_oracle(train, wl, adj, wl["X"], wl["X"].cpu(), FAN, C, agg="MAX")
+    print("max |emb diff|, max |grad diff|, max |grad| per step:", worst)
+
+
 def test_fullsize_timed_step_bf16_max_vs_oracle(wl, adj):
     """configs[3]: the same over a bf16 feature table with MAX; the oracle
     rounds layer 1's W1 and aggregate to bf16 as the HIP GEMM reads them.
