@@ -273,7 +273,7 @@ def cpu_baseline(wl, cfg, seconds_budget=25.0, seed=824):
 
 
 # rocprofv3 --kernel-trace --stats summaries of the bench command, per config
-# and batch (tools/gpu_r02c.sh): the profiler's own per-launch average for
+# and batch (tools/gpu_pass.sh; earlier rounds: the pass scripts in git history): the profiler's own per-launch average for
 # the kernel beside the live event-timed one
 # (newest round first: the first file present is used)
 ROCPROF_TOL = 0.15  # live vs committed rocprofv3 average: `rocprof_agrees` within this fraction

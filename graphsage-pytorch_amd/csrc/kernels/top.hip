@@ -275,6 +275,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         if (row < nr) a.E[static_cast<int64_t>(r0 + row) * H + col] = e;
     }
     lds_barrier();
+    GS_TOP_STAMP(4);
 
     // ---- stage 3: the loss head (models.py:8-27, utils.py:159-164).
     // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
@@ -295,6 +296,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         if (part == 0 && rc < kTopRows * C) sdl[row * C + c] = z + sb[c];
     }
     lds_barrier();
+    GS_TOP_STAMP(5);
     // softmax / NLL / dlogits: wave w < rows, lane = class (C <= 32 <= 64)
     if (w < nr) {
         const int ii = w;
@@ -313,7 +315,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         sdl[w * C + lane] = 0.f;  // ragged block: no gradient from the missing rows
     }
     lds_barrier();
-    GS_TOP_STAMP(4);
+    GS_TOP_STAMP(6);
     // dZ = (dlogits · Wc) ⊙ (E > 0): thread t = (row, d), classes in order
     // (eight classes' operands read ahead of their chain)
     {
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         }
     }
     lds_barrier();
-    GS_TOP_STAMP(5);
+    GS_TOP_STAMP(7);
 
     // ---- stage 4: dIn = dZ · W2 (4x4x1 multi-block).  Wave w: input columns
     // 64 (w & 3) + lane, h half w >> 2 (64 h); W2[h][kc] read down a column of
@@ -415,6 +417,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         for (int j = 0; j < kTopRows; ++j) pp[j * K + kc] = c0[j] + c1[j];
     }
     lds_barrier();
+    GS_TOP_STAMP(8);
     // the two halves added in order, dIn to global: thread t = (row, 2 columns)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         const float v = sP[row * K + kc] + sP[kTopRows * K + row * K + kc];
         if (row < nr) a.dIn[static_cast<int64_t>(r0 + row) * K + kc] = v;
     }
-    GS_TOP_STAMP(6);
+    GS_TOP_STAMP(9);
     kstamp_end(a.stamp);
 }
 

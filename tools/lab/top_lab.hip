@@ -22,7 +22,7 @@
 __device__ unsigned long long* g_stamps;
 #define GS_TOP_STAMP(i)                                                                            \
     do {                                                                                           \
-        if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (g_stamps && threadIdx.x == 0) g_stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #include "../../graphsage-pytorch_amd/csrc/host/errors.cpp"
 #include "../../graphsage-pytorch_amd/csrc/kernels/top.hip"
@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dIn, B * K * 4)); CK(hipMalloc(&slab, (B / 4 + 1) * (C * (H + 1) + 1) * 4));
     unsigned long long* st;
     const int nb = (B + 3) / 4;
-    CK(hipMalloc(&st, nb * 8 * 8));
+    CK(hipMalloc(&st, nb * 16 * 8));
     if (!gs::top_supported(H, C, false)) { std::printf("top not supported (LDS)\n"); return 3; }
     hipStream_t s;
     CK(hipStreamCreate(&s));
@@ -167,25 +167,39 @@ int main(int argc, char** argv) {
     }
     // stamps of one launch
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
-    CK(hipMemset(st, 0, nb * 64));
-    launch();
-    CK(hipStreamSynchronize(s));
-    std::vector<unsigned long long> h(nb * 8);
-    CK(hipMemcpy(h.data(), st, nb * 64, hipMemcpyDeviceToHost));
-    unsigned long long t0 = ~0ull;
-    for (int b = 0; b < nb; ++b) t0 = std::min(t0, h[b * 8]);
-    double acc[8] = {0};
-    double last_end = 0, first_start = 1e18;
-    for (int b = 0; b < nb; ++b) {
-        for (int i = 1; i <= 6; ++i) acc[i] += (h[b * 8 + i] - h[b * 8 + i - 1]) * 0.01;
-        last_end = std::max(last_end, (h[b * 8 + 6] - t0) * 0.01);
-        first_start = std::min(first_start, (h[b * 8] - t0) * 0.01);
-    }
+    CK(hipMemset(st, 0, nb * 128));
+    const int NS = 10;
     const char* names[] = {"", "dma issue + Wc + gather", "wait W2 DMA + barrier", "E (4x4x1 split-K)",
-                           "E combine + loss head", "dZ + slab", "dIn (4x4x1 split-K) + store"};
-    for (int i = 1; i <= 6; ++i) std::printf("  stage %d %-32s mean %.2f us\n", i, names[i], acc[i] / nb);
-    double spread = 0;
-    for (int b = 0; b < nb; ++b) spread = std::max(spread, (h[b * 8] - t0) * 0.01);
-    std::printf("  block start spread %.2f us; first start -> last end %.2f us\n", spread, last_end - first_start);
+                           "E combine + barrier", "logits + barrier", "softmax + barrier", "dZ + slab + barrier",
+                           "dIn MFMA + barrier", "dIn combine + store"};
+    for (int rep = 0; rep < 3; ++rep) {  // three single launches (warm), stamped
+        for (int i = 0; i < 20; ++i) launch();
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
+        launch();
+        CK(hipStreamSynchronize(s));
+        unsigned long long* nul = nullptr;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &nul, sizeof(nul)));
+        std::vector<unsigned long long> h(nb * 16);
+        CK(hipMemcpy(h.data(), st, nb * 128, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull;
+        for (int b = 0; b < nb; ++b) t0 = std::min(t0, h[b * 16]);
+        double acc[16] = {0}, mx[16] = {0};
+        double last_end = 0, first_start = 1e18;
+        for (int b = 0; b < nb; ++b) {
+            for (int i = 1; i < NS; ++i) {
+                const double d = (h[b * 16 + i] - h[b * 16 + i - 1]) * 0.01;
+                acc[i] += d;
+                mx[i] = std::max(mx[i], d);
+            }
+            last_end = std::max(last_end, (h[b * 16 + NS - 1] - t0) * 0.01);
+            first_start = std::min(first_start, (h[b * 16] - t0) * 0.01);
+        }
+        std::printf("stamped launch %d\n", rep);
+        for (int i = 1; i < NS; ++i) std::printf("  stage %d %-32s mean %.2f us  max %.2f us\n", i, names[i], acc[i] / nb, mx[i]);
+        double spread = 0;
+        for (int b = 0; b < nb; ++b) spread = std::max(spread, (h[b * 16] - t0) * 0.01);
+        std::printf("  block start spread %.2f us; first start -> last end %.2f us\n", spread, last_end - first_start);
+    }
     return 0;
 }
