@@ -75,6 +75,29 @@ struct RowIO<bf16_t, 1> {
     static __device__ __forceinline__ void store(bf16_t* p, const float (&v)[1]) { *p = f2bf(v[0]); }
 };
 
+// Lane exchanges inside a row of 16 lanes by DPP (a VALU operand modifier,
+// no LDS round trip like __shfl's ds_bpermute): xor 1 and xor 2 as quad
+// permutes, then the half-row and row mirrors (lane i <-> 7 - i, 15 - i).
+// After dpp_sum8 every lane of an 8-lane group holds the group's sum, after
+// dpp_sum16 / dpp_max16 every lane of a 16-lane row the row's; each lane
+// adds the same two operands (a + b == b + a), so the lanes agree bitwise.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_sum8(float v) {
+    v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+    return v + dpp_f<0x141>(v);  // row_half_mirror
+}
+__device__ __forceinline__ float dpp_sum16(float v) { v = dpp_sum8(v); return v + dpp_f<0x140>(v); }  // row_mirror
+__device__ __forceinline__ float dpp_max16(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v));
+    v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v));
+    return fmaxf(v, dpp_f<0x140>(v));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -75,7 +75,7 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
-template <int OP>
+template <int OP, bool SMALLC>
 __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     constexpr int H = kTopH, K = kTopK, D = kTopH, NT = kTopThreads;
     // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, the
@@ -106,18 +106,27 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // quad q of the row lands in slot q ^ (c & 15).  Waves 2..7 issue it (the
     // gather's dependent load rounds run on waves 0 and 1; vmcnt retires in
     // order, so those would otherwise queue behind the DMA).
+#ifndef GS_TOP_LAB_NO_DMA  // lab probe only: W2 left unloaded (wrong results, timing insight)
     if (w >= 2)
+#else
+    if (w >= 2 && a.B < 0)
+#endif
         for (int c = w - 2; c < H; c += NT / 64 - 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
                                              0, 0);
 
-    // ---- loss-head operands (independent of the rest, issued before the
-    // gather so their dependent loads, label[root[r]], are long done)
-    if (tid < kTopRows) sy[tid] = tid < nr ? a.labels[a.roots[r0 + tid]] : 0;
-    else if (tid >= 64 && tid < 64 + C) sb[tid - 64] = a.bc[tid - 64];
-    {
+    // ---- loss-head operands (independent of the rest), on the DMA waves:
+    // their loads queue behind the DMA (vmcnt retires in order), and these
+    // waves wait for all of it before the first barrier anyway.  Waves 0 and 1
+    // go straight to the gather (its record -> rows chain is the stage's
+    // critical path; a labels[roots[]] chain or the Wc quads in front of it had
+    // put two dependent global round trips ahead of the record load).
+    if (w >= 2) {
+        const int t2 = tid - 128;  // 0 .. 383
+        if (t2 < kTopRows) sy[t2] = t2 < nr ? a.labels[a.roots[r0 + t2]] : 0;
+        else if (t2 >= 64 && t2 < 64 + C) sb[t2 - 64] = a.bc[t2 - 64];
         const int nW4 = C * D / 4;
-        for (int q = tid; q < nW4; q += NT) {
+        for (int q = t2; q < nW4; q += NT - 128) {
             const float4 v = reinterpret_cast<const float4*>(a.Wc)[q];
             const int t = 4 * q;
             float* d = sW + t + t / D;  // row pitch D + 1 (D % 4 == 0: a quad stays in one row)
@@ -278,41 +287,75 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     GS_TOP_STAMP(4);
 
     // ---- stage 3: the loss head (models.py:8-27, utils.py:159-164).
-    // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
-    // the eight parts are added by an xor butterfly.
     const float invB = 1.0f / static_cast<float>(a.B);
     const int wp = D + 1;
-    for (int base = 0; base < kTopRows * C; base += NT / 8) {
-        const int rc = base + (tid >> 3), part = tid & 7;
-        const int row = min(rc / C, kTopRows - 1), c = rc % C;
-        const float* e = sE[row] + 16 * part;
-        const float* wr = sW + static_cast<int64_t>(c) * wp + 16 * part;
-        float z = 0.f;
+    if constexpr (SMALLC) {
+        // C <= 16.  logits: thread t = (row t >> 7, class (t >> 3) & 15, 16 d
+        // of part t & 7), the eight parts added by DPP within their 8 lanes
+        {
+            const int row = tid >> 7, c = (tid >> 3) & 15, part = tid & 7;
+            const float* e = sE[row] + 16 * part;
+            const float* wr = sW + min(c, C - 1) * wp + 16 * part;
+            float z = 0.f;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) z = fmaf(e[t], wr[t], z);
-        z += __shfl_xor(z, 1, 64);
-        z += __shfl_xor(z, 2, 64);
-        z += __shfl_xor(z, 4, 64);
-        if (part == 0 && rc < kTopRows * C) sdl[row * C + c] = z + sb[c];
-    }
-    lds_barrier();
-    GS_TOP_STAMP(5);
-    // softmax / NLL / dlogits: wave w < rows, lane = class (C <= 32 <= 64)
-    if (w < nr) {
-        const int ii = w;
-        const int y = sy[ii];
-        const float z = lane < C ? sdl[ii * C + lane] : -INFINITY;
-        float mx = z;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        const float lse = logf(wave_sum(lane < C ? expf(z - mx) : 0.f));
-        if (lane < C) {
-            const float lp = z - mx - lse;
-            if (lane == y) sloss[ii] = -lp;
-            sdl[ii * C + lane] = (expf(lp) - (lane == y ? 1.f : 0.f)) * invB;
+            for (int t = 0; t < 16; ++t) z = fmaf(e[t], wr[t], z);
+            z = dpp_sum8(z);
+            if (part == 0 && c < C) sdl[row * C + c] = z + sb[c];
         }
-    } else if (w < kTopRows && lane < C) {
-        sdl[w * C + lane] = 0.f;  // ragged block: no gradient from the missing rows
+        lds_barrier();
+        GS_TOP_STAMP(5);
+        // softmax / NLL / dlogits: wave 0, lane = (row lane >> 4, class lane & 15);
+        // a row's classes are one 16-lane DPP row
+        if (w == 0) {
+            const int row = lane >> 4, c = lane & 15;
+            const bool cv = c < C;
+            const float z = cv ? sdl[row * C + c] : -INFINITY;
+            const float mx = dpp_max16(z);
+            const float lse = logf(dpp_sum16(cv ? expf(z - mx) : 0.f));
+            if (row < nr) {
+                const int y = sy[row];
+                const float lp = z - mx - lse;
+                if (c == y) sloss[row] = -lp;
+                if (cv) sdl[row * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+            } else if (cv) {
+                sdl[row * C + c] = 0.f;  // ragged block: no gradient from the missing rows
+            }
+        }
+    } else {
+        // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
+        // the eight parts are added by an xor butterfly.
+        for (int base = 0; base < kTopRows * C; base += NT / 8) {
+            const int rc = base + (tid >> 3), part = tid & 7;
+            const int row = min(rc / C, kTopRows - 1), c = rc % C;
+            const float* e = sE[row] + 16 * part;
+            const float* wr = sW + static_cast<int64_t>(c) * wp + 16 * part;
+            float z = 0.f;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) z = fmaf(e[t], wr[t], z);
+            z += __shfl_xor(z, 1, 64);
+            z += __shfl_xor(z, 2, 64);
+            z += __shfl_xor(z, 4, 64);
+            if (part == 0 && rc < kTopRows * C) sdl[row * C + c] = z + sb[c];
+        }
+        lds_barrier();
+        GS_TOP_STAMP(5);
+        // softmax / NLL / dlogits: wave w < rows, lane = class (C <= 32 <= 64)
+        if (w < nr) {
+            const int ii = w;
+            const int y = sy[ii];
+            const float z = lane < C ? sdl[ii * C + lane] : -INFINITY;
+            float mx = z;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            const float lse = logf(wave_sum(lane < C ? expf(z - mx) : 0.f));
+            if (lane < C) {
+                const float lp = z - mx - lse;
+                if (lane == y) sloss[ii] = -lp;
+                sdl[ii * C + lane] = (expf(lp) - (lane == y ? 1.f : 0.f)) * invB;
+            }
+        } else if (w < kTopRows && lane < C) {
+            sdl[w * C + lane] = 0.f;  // ragged block: no gradient from the missing rows
+        }
     }
     lds_barrier();
     GS_TOP_STAMP(6);
@@ -321,18 +364,30 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     {
         const int row = tid >> 7, d = tid & (D - 1);
         float s = 0.f;
-        int c = 0;
-        for (; c + 8 <= C; c += 8) {
-            float g[8], v[8];
+        if constexpr (SMALLC) {
+            float g[16], v[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                g[u] = sdl[row * C + c + u];
-                v[u] = sW[static_cast<int64_t>(c + u) * wp + d];
+            for (int u = 0; u < 16; ++u) {
+                g[u] = u < C ? sdl[row * C + u] : 0.f;
+                v[u] = u < C ? sW[u * wp + d] : 0.f;
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s = fmaf(g[u], v[u], s);
+            for (int u = 0; u < 16; ++u)
+                if (u < C) s = fmaf(g[u], v[u], s);
+        } else {
+            int c = 0;
+            for (; c + 8 <= C; c += 8) {
+                float g[8], v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    g[u] = sdl[row * C + c + u];
+                    v[u] = sW[static_cast<int64_t>(c + u) * wp + d];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s = fmaf(g[u], v[u], s);
+            }
+            for (; c < C; ++c) s = fmaf(sdl[row * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
         }
-        for (; c < C; ++c) s = fmaf(sdl[row * C + c], sW[static_cast<int64_t>(c) * wp + d], s);
         if (!(sE[row][d] > 0.f)) s = 0.f;
         sZ[row][d] = s;
         if (row < nr) a.dZ[static_cast<int64_t>(r0 + row) * D + d] = s;
@@ -360,7 +415,11 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                         if (ii < nr) sv[j] = fmaf(dl[ii], sE[ii][d], sv[j]);
                 }
 #pragma unroll
-                for (int j = 0; j < D / 16; ++j) out[c * (D + 1) + (tid & 15) + 16 * j] = sv[j];
+                for (int j = 0; j < D / 16; ++j)
+#ifdef GS_TOP_LAB_NO_SLAB  // lab probe only: the slab stores skipped
+                    if (a.B < 0)
+#endif
+                    out[c * (D + 1) + (tid & 15) + 16 * j] = sv[j];
                 if ((tid & 15) == 0) {
                     float sbias = 0.f;
 #pragma unroll
@@ -379,11 +438,10 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                 out[t] = sv;
             }
         }
-        if (tid >= NT - 64) {
+        if (tid == NT - 64) {  // the block's loss, rows in order
             float sl = 0.f;
-            for (int ii = tid - (NT - 64); ii < nr; ii += 64) sl += sloss[ii];
-            sl = wave_sum(sl);
-            if (tid == NT - 64) out[per] = sl;
+            for (int ii = 0; ii < nr; ++ii) sl += sloss[ii];
+            out[per] = sl;
         }
     }
     lds_barrier();
@@ -447,8 +505,10 @@ static bool top_lds_ready(int64_t C) {
             return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) ==
                    hipSuccess;
         };
-        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN>)) &&
-                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX>));
+        const bool a = raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, true>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, true>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MEAN, false>)) &&
+                       raise(reinterpret_cast<const void*>(sage_top_kernel<GS_AGG_MAX, false>));
         (void)hipGetLastError();
         ok_bytes = a ? static_cast<int>(want) : 0;
     }
@@ -472,8 +532,14 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
               aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()};
     const dim3 grid(static_cast<unsigned>((B + kTopRows - 1) / kTopRows));
     const size_t smem = top_smem_bytes(C);
-    if (agg == GS_AGG_MEAN) launch_k(sage_top_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, a);
-    else launch_k(sage_top_kernel<GS_AGG_MAX>, grid, dim3(kTopThreads), smem, st, a);
+    const bool small = C <= 16;
+    if (agg == GS_AGG_MEAN) {
+        if (small) launch_k(sage_top_kernel<GS_AGG_MEAN, true>, grid, dim3(kTopThreads), smem, st, a);
+        else launch_k(sage_top_kernel<GS_AGG_MEAN, false>, grid, dim3(kTopThreads), smem, st, a);
+    } else {
+        if (small) launch_k(sage_top_kernel<GS_AGG_MAX, true>, grid, dim3(kTopThreads), smem, st, a);
+        else launch_k(sage_top_kernel<GS_AGG_MAX, false>, grid, dim3(kTopThreads), smem, st, a);
+    }
     check_launch("sage_top");
     return static_cast<int>(grid.x);
 }

@@ -47,12 +47,12 @@ def _setup(gs):
     return graph, adj, X, labels, cands
 
 
-def _oracle_dp(adj, X, labels, per_rank, max_norm=5.0, sums=None):
+def _oracle_dp(adj, X, labels, per_rank, max_norm=5.0, sums=None, classes=C):
     """The reference's step per rank on its own batch and stream, the rank
     gradients summed (the all-reduce), then clip_grad_norm_(max_norm) per model
     and SGD on the sum / W (utils.py:184-187).  sums: the summed flat gradient
     [dW1 | dW2 | dWc | dbc] of each step is appended to it."""
-    sage_w, cw, cb = train.reference_init(2, F, H, C, False, SEED)
+    sage_w, cw, cb = train.reference_init(2, F, H, classes, False, SEED)
     params = [w.clone().requires_grad_(True) for w in sage_w] + [cw.clone().requires_grad_(True),
                                                                 cb.clone().requires_grad_(True)]
     rngs = [random.Random(train.rank_seed(SEED, r)) for r in range(W)]
@@ -120,10 +120,11 @@ def test_two_rank_deferred_update_on_one_gpu(gs, max_norm):
     (the reference's) and 1e-3 (every step clipped: the forward's recompute
     path).  Against the oracle's W = 2 step at 1e-5: each step's summed
     gradient and the final weights; the ranks' weights bitwise equal."""
-    steps = 4
-    graph, adj, X, labels, cands = _setup(gs)
+    steps, classes = 4, 16  # 16 classes: the flat buffer's groups stay float4-aligned (deferral needs it)
+    graph, adj, X, _, cands = _setup(gs)
+    labels = torch.from_numpy((np.arange(X.shape[0]) % classes).astype(np.int32))
     per_rank = [list(train.rank_batches(cands, B, r, W, SEED + 1000))[:steps] for r in range(W)]
-    trs = [train.NativeTrainer(graph, X.to(DEV), labels.to(DEV), C, hidden=H, fanouts=FAN, seed=SEED,
+    trs = [train.NativeTrainer(graph, X.to(DEV), labels.to(DEV), classes, hidden=H, fanouts=FAN, seed=SEED,
                                max_norm=max_norm) for _ in range(W)]
     assert all(t.defer(True) for t in trs)
     rngs = [train.make_rng(SEED, r) for r in range(W)]
@@ -150,7 +151,7 @@ def test_two_rank_deferred_update_on_one_gpu(gs, max_norm):
         t.defer(False)  # the last pending update
     torch.cuda.synchronize()
     ref_sums = []
-    ref = _oracle_dp(adj, X, labels, per_rank, max_norm=max_norm, sums=ref_sums)
+    ref = _oracle_dp(adj, X, labels, per_rank, max_norm=max_norm, sums=ref_sums, classes=classes)
     for i, (a, b) in enumerate(zip(sums, ref_sums)):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5, msg=lambda m: f"step {i} summed grads: {m}")
     assert torch.equal(trs[0].p.params, trs[1].p.params)
