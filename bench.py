@@ -599,7 +599,8 @@ def run_embed(args, cfg):
                                    f"fanout {tuple(cfg['fanouts'])}, MEAN, forward only + all-gather",
                        "global_batch": B * world, "parallelism": f"dp{world}",
                        "sampler_streams_per_gpu": args.sampler_streams,
-                       "sampler_helpers_per_stream": args.sampler_helpers, "batches_per_launch": emb.merge,
+                       "sampler_helpers_per_stream": args.sampler_helpers,
+                       "sampler_depth_per_stream": args.sampler_depth, "batches_per_launch": emb.merge,
                        "host_sampler_ms_per_batch": round(1e3 * st["sample_s"] / max(1, n_b), 3),
                        "host_ms_per_batch": {k: round(1e3 * st[k + "_s"] / max(1, n_b), 4)
                                              for k in ("wait", "wait_sample", "wait_ring", "wait_gather", "issue")},
@@ -678,6 +679,8 @@ def main():
     ap.add_argument("--sampler", default="host", choices=("host", "device"),
                     help="device: every stream samples on the GPU (gs_dsampler, SURVEY §8 f-4), no host sampler "
                          "threads; default 1 stream (the reference's single random stream)")
+    ap.add_argument("--sampler-depth", type=int, default=4,
+                    help="pinned pack slots per sampler stream (how far each stream may run ahead)")
     ap.add_argument("--sampler-helpers", type=int, default=None,
                     help="helper threads per sampler stream (same draws; lower per-batch latency); "
                          "default 1 with >= 8 host cores per GPU")
@@ -742,7 +745,8 @@ def main():
     # timed steps' batches are sampled inside the timed region (presampled_at_t0)
     runner = train.Runner(trainer, wl["graph"], batches, rngs, cfg["fanouts"], gcn=False,
                           fail_empty=cfg["agg"] == "MAX", comm=comm, hold=True, ar_buckets=args.ar_buckets,
-                          helpers=args.sampler_helpers, warm=not args.no_warm, sampler=args.sampler)
+                          helpers=args.sampler_helpers, warm=not args.no_warm, sampler=args.sampler,
+                          depth=args.sampler_depth)
     elem = 2 if cfg["dtype"] == "bf16" else 4
     L = len(cfg["fanouts"])
     lib = gs._lib.lib()
@@ -963,6 +967,7 @@ def main():
                        "sampler_kind": args.sampler,
                        "sampler_streams_per_gpu": args.sampler_streams,
                        "sampler_helpers_per_stream": args.sampler_helpers,
+                       "sampler_depth_per_stream": args.sampler_depth,
                        "sampler_contexts_warmed": not args.no_warm,
                        "sampled_nodes": {"per_step_mean": [round(float(x), 1) for x in fr.mean(0)],
                                          "fields": "B, |L1|, |L0| (unique frontiers, models.py:246-251)",

@@ -114,12 +114,70 @@ struct RawVec<bf16_t, 8> {
 // self_out[r] (its load in the same memory round as the neighbours'), so the
 // layer-1 GEMMs read [self | agg] as one dense block instead of gathering the
 // self rows through their index (GS_SELF_ROWS).
-template <int OP, typename T, int VEC, int G, bool SELF>
+// ONE (the launcher's choice when F == G·VEC, k <= kRows, no gcn and a grid
+// with a lane group per destination): each destination in two load rounds —
+// its k ids and its own id together, then the self row and every neighbour
+// row together — written straight-line, with no loop around the loads (the
+// general form's loops had the compiler drain the self row's load before the
+// id load and split the rows into two waits: five dependent rounds).  Same
+// rows, same order of adds: bitwise the general form.
+template <int OP, typename T, int VEC, int G, bool SELF, bool ONE>
 __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X, int64_t ldx, int F, int n_dst, int k,
                                                          const int* __restrict__ ids, const int* __restrict__ dst_ids,
                                                          int gcn, T* __restrict__ out, int64_t ldo,
                                                          T* __restrict__ self_out, int64_t ldso) {
     const int gl = threadIdx.x % G;
+    if constexpr (ONE) {
+        using Raw = typename RawVec<T, VEC>::type;
+        constexpr int NR = kRows;
+        const int r = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+        if (r >= n_dst) return;
+        const int f0 = gl * VEC;
+        const int node = SELF ? dst_ids[r] : 0;
+        const int nb = gl < k ? ids[static_cast<int64_t>(r) * k + gl] : -1;
+        int rows[NR];
+        bool ok[NR];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            rows[u] = __shfl(nb, u, G);
+            ok[u] = u < k && rows[u] >= 0;
+        }
+        const int fallback = SELF ? node : (rows[0] >= 0 ? rows[0] : 0);
+        Raw xself{};
+        if (SELF) xself = *reinterpret_cast<const Raw*>(X + static_cast<int64_t>(node) * ldx + f0);
+        Raw x[NR];
+#pragma unroll
+        for (int u = 0; u < NR; ++u)
+            x[u] = *reinterpret_cast<const Raw*>(X + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * ldx + f0);
+        __builtin_amdgcn_sched_barrier(0);  // every row load issued before the first add waits on one
+        float acc[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            cnt += ok[u];
+            float xv[VEC];
+            RawVec<T, VEC>::unpack(x[u], xv);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+                if (OP == GS_AGG_MEAN) {
+                    acc[v] += ok[u] ? xv[v] : 0.f;
+                } else {
+                    const bool take = ok[u] && xv[v] > acc[v];
+                    acc[v] = take ? xv[v] : acc[v];
+                }
+            }
+        }
+        if (SELF) *reinterpret_cast<Raw*>(self_out + static_cast<int64_t>(r) * ldso + f0) = xself;
+        if (OP == GS_AGG_MEAN) {
+            const float inv = 1.0f / static_cast<float>(cnt);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v] *= inv;
+        }
+        RowIO<T, VEC>::store(out + static_cast<int64_t>(r) * ldo + f0, acc);
+        return;
+    }
     // grid-stride over destinations (the launch caps the grid: agg_ids_block_cap)
     for (int r = blockIdx.x * (kBlock / G) + threadIdx.x / G; r < n_dst; r += gridDim.x * (kBlock / G)) {
     const int node = (gcn || SELF) ? dst_ids[r] : 0;
@@ -241,15 +299,26 @@ void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t 
                      (!self_out || (ldso % V == 0 && aligned16(self_out)));
     const int f = static_cast<int>(F), n = static_cast<int>(n_dst);
     static const int cap = agg_ids_block_cap();
-#define GS_IDS(OPV, TT, VV, GG)                                                                                  \
+#define GS_IDS1(OPV, TT, VV, GG, ONE)                                                                            \
     do {                                                                                                         \
         const dim3 grid_(std::min((n + (kBlock / GG) - 1) / (kBlock / GG), cap));                                \
         if (self_out)                                                                                            \
-            launch_k(agg_ids_kernel<OPV, TT, VV, GG, true>, grid_, dim3(kBlock), 0, st, static_cast<const TT*>(X), \
-                     ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo, static_cast<TT*>(self_out), ldso); \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, true, ONE>, grid_, dim3(kBlock), 0, st,                     \
+                     static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo,      \
+                     static_cast<TT*>(self_out), ldso);                                                          \
         else                                                                                                     \
-            launch_k(agg_ids_kernel<OPV, TT, VV, GG, false>, grid_, dim3(kBlock), 0, st, static_cast<const TT*>(X), \
-                     ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo, static_cast<TT*>(nullptr), ldso); \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, false, ONE>, grid_, dim3(kBlock), 0, st,                    \
+                     static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo,      \
+                     static_cast<TT*>(nullptr), ldso);                                                           \
+    } while (0)
+    // one lane group per destination (no grid cap), one vector per lane, at
+    // most kRows ids, no gcn: the two-round form
+    const bool one_ok = !gcn && k <= kRows && static_cast<int64_t>(n + 1) * 64 < (int64_t(1) << 31) &&
+                        cap >= (n + 3) / 4;
+#define GS_IDS(OPV, TT, VV, GG)                                      \
+    do {                                                             \
+        if (one_ok && f == (GG) * (VV)) GS_IDS1(OPV, TT, VV, GG, true); \
+        else GS_IDS1(OPV, TT, VV, GG, false);                        \
     } while (0)
 #define GS_IDS_T(OPV, TT)                                                     \
     do {                                                                      \
@@ -271,6 +340,7 @@ void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t 
     }
 #undef GS_IDS_T
 #undef GS_IDS
+#undef GS_IDS1
     check_launch("agg_ids");
 }
 

@@ -263,7 +263,7 @@ __device__ __forceinline__ void agg_bwd_rec_body(
 #pragma unroll
         for (int v = 0; v < VEC; ++v) g[v] = 0.f;
         float x[kTrec][VEC], w[kTrec];
-        int am[kTrec][VEC];
+        int am[kTrec][VEC], pa[kTrec], pb[kTrec];
 #pragma unroll
         for (int u = 0; u < kTrec; ++u) {
             const int eu = e[u];
@@ -273,11 +273,19 @@ __device__ __forceinline__ void agg_bwd_rec_body(
             RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
             if (OP == GS_AGG_MEAN) {
                 const int re = self_e ? 0 : eu;
-                w[u] = 1.0f / static_cast<float>(ptr[re + 1] - ptr[re]);
+                pa[u] = ptr[re];
+                pb[u] = ptr[re + 1];
             } else {
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) am[u][v] = argmax[static_cast<int64_t>(self_e ? 0 : eu) * F + f0c + v];
             }
+        }
+        // every load of the round issued before the first use waits on one
+        // (the counts' divisions had the compiler wait inside the load loop)
+        __builtin_amdgcn_sched_barrier(0);
+        if (OP == GS_AGG_MEAN) {
+#pragma unroll
+            for (int u = 0; u < kTrec; ++u) w[u] = 1.0f / static_cast<float>(pb[u] - pa[u]);
         }
         if (!act) continue;
 #pragma unroll

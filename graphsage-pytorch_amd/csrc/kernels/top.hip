@@ -74,10 +74,24 @@ struct TopArgs {
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
+// The same MFMA with block ABID's A operand broadcast to all 16 blocks
+// (CBSZ = 4): lanes 4·ABID .. 4·ABID + 3 supply the four rows' A values, the
+// other lanes' A registers are not read.  So one 16-byte LDS read per lane,
+// lane l = X[l & 3][k0 + 4 (l >> 2) .. + 3], holds the A operands of 64 k
+// steps (step k0 + 4 b + r: component r, ABID b) instead of one broadcast
+// read per 4 steps.
+template <int ABID>
+__device__ __forceinline__ f32x4 mfma4b(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 4, ABID, 0);
+}
 
 template <int OP, bool SMALLC>
 __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     constexpr int H = kTopH, K = kTopK, D = kTopH, NT = kTopThreads;
+    // Wc's LDS row pitch: D + 4 keeps its rows 16-byte aligned for the small-C
+    // logits' quad reads (class c's quads then start at bank 4c: conflict-free);
+    // D + 1 for the general path (its 8-part row reads)
+    constexpr int WP = SMALLC ? D + 4 : D + 1;
     // dynamic LDS: W2 (whole, quad-swizzled rows), [self | agg], E, dZ, the
     // GEMMs' partial sums, Wc, logits / dlogits, loss
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -87,11 +101,15 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     float (*sZ)[H] = reinterpret_cast<float (*)[H]>(sE[kTopRows]);
     // the GEMMs' partial sums: E [4 k quarters][rows][H], dIn [2 h halves][rows][K]
     float* sP = &sZ[kTopRows][0];
-    float* sW = sP + kTopPart;                                // [C][D + 1]
-    float* sdl = sW + a.C * (D + 1);                          // [rows][C]
+    float* sW = sP + kTopPart;                                // [C][WP]
+    float* sdl = sW + a.C * WP;                               // [rows][C]
     float* sloss = sdl + kTopRows * a.C;
     float* sb = sloss + kTopRows;                             // [C] classifier bias
     int* sy = reinterpret_cast<int*>(sb + a.C);               // [rows] labels
+    // C <= 16: dIn's four h-quarter partials [rows][K]: the E input rows (free
+    // after stage 2), the partial area, and one more area behind the labels
+    float* const dinq[4] = {&sX[0][0], sP, sP + kTopRows * K,
+                            smem + ((reinterpret_cast<float*>(sy) + kTopRows - smem + 3) & ~3)};
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int C = a.C;
     const int r0 = blockIdx.x * kTopRows;
@@ -106,11 +124,10 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // quad q of the row lands in slot q ^ (c & 15).  Waves 2..7 issue it (the
     // gather's dependent load rounds run on waves 0 and 1; vmcnt retires in
     // order, so those would otherwise queue behind the DMA).
-#ifndef GS_TOP_LAB_NO_DMA  // lab probe only: W2 left unloaded (wrong results, timing insight)
+    // (Measured and not kept: each block starting the DMA at its own row, so
+    // the blocks sharing an XCD's L2 request different lines at a time: the
+    // launch 11.15 -> 11.5 us in tools/lab/top_lab.hip.)
     if (w >= 2)
-#else
-    if (w >= 2 && a.B < 0)
-#endif
         for (int c = w - 2; c < H; c += NT / 64 - 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
                                              0, 0);
@@ -129,7 +146,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         for (int q = t2; q < nW4; q += NT - 128) {
             const float4 v = reinterpret_cast<const float4*>(a.Wc)[q];
             const int t = 4 * q;
-            float* d = sW + t + t / D;  // row pitch D + 1 (D % 4 == 0: a quad stays in one row)
+            float* d = sW + t + (WP - D) * (t / D);  // row pitch WP (D % 4 == 0: a quad stays in one row)
             d[0] = v.x;
             d[1] = v.y;
             d[2] = v.z;
@@ -153,23 +170,6 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         if (g < nr) {
             const int r = r0 + g;
             const int f0 = gl * 4;
-            int srow, beg, end, pre = -1;
-            if (a.tids) {
-                const int* rec = a.tids + static_cast<int64_t>(r) * (a.tk + 1);
-                const int v = gl <= a.tk ? rec[gl] : -1;
-                srow = __shfl(v, 0, G);
-                pre = __shfl(v, min(gl + 1, G - 1), G);  // lane gl: list entry gl
-                if (gl + 1 > a.tk) pre = -1;
-                const unsigned long long have = __ballot(pre >= 0);
-                const int sh = (tid & 63) & ~(G - 1);  // this group's lanes in the wave's ballot
-                beg = 0;
-                end = __popcll((have >> sh) & ((G == 64) ? ~0ull : ((1ull << G) - 1)));
-            } else {
-                srow = a.self[r];
-                beg = a.ptr[r];
-                end = a.ptr[r + 1];
-            }
-            const float4 xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
             float acc[4];
             int am[4];
 #pragma unroll
@@ -178,18 +178,67 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                 am[v] = -1;
             }
             int cnt = 0;
-            for (int base = beg; base < end; base += G) {
-                const int m = min(G, end - base);
-                const bool mine = gl < m;
-                const int e = a.tids ? pre : a.nbr[mine ? base + gl : base];
-                const int my = mine ? e : -1;
-                for (int j = 0; j < m; j += NR) {
+            // rows[u] in list order, ok[u] = a real neighbour: added in u order
+            auto add_rows = [&](const int (&rows)[NR], const bool (&ok)[NR], const float (&x)[NR][4]) {
+#pragma unroll
+                for (int u = 0; u < NR; ++u) {
+                    cnt += ok[u];
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        if (OP == GS_AGG_MEAN) {
+                            acc[v] += ok[u] ? x[u][v] : 0.f;
+                        } else {
+                            const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
+                            acc[v] = take ? x[u][v] : acc[v];
+                            am[v] = take ? rows[u] : am[v];
+                        }
+                    }
+                }
+            };
+            float4 xs;
+            if (a.tids) {
+                // one record load, then the self row and every neighbour row in
+                // ONE load round, straight-line (a loop here had the compiler wait
+                // for the self row before issuing the neighbour rows); the list
+                // reaches the group's lanes through LDS (sP, unused until stage 2:
+                // one 16-byte read per 4 entries instead of a ds_bpermute each)
+                const int* rec = a.tids + static_cast<int64_t>(r) * (a.tk + 1);
+                const int v = gl <= a.tk ? rec[gl] : -1;
+                int* srec = reinterpret_cast<int*>(sP) + g * G;
+                srec[gl == 0 ? G - 1 : gl - 1] = gl <= a.tk ? v : -1;  // list entry j at j, self at G - 1
+                const unsigned long long have = __ballot(gl >= 1 && gl <= a.tk && v >= 0);
+                const int sh = (tid & 63) & ~(G - 1);  // this group's lanes in the wave's ballot
+                const int m = __popcll((have >> sh) & ((1ull << G) - 1));  // <= tk <= 31
+                int rows[NR];
+                bool ok[NR];
+#pragma unroll
+                for (int q = 0; q < NR / 4; ++q) {
+                    const int4 r4 = reinterpret_cast<const int4*>(srec)[q];
+                    rows[4 * q] = r4.x; rows[4 * q + 1] = r4.y; rows[4 * q + 2] = r4.z; rows[4 * q + 3] = r4.w;
+                }
+                const int srow = rows[NR - 1];
+#pragma unroll
+                for (int u = 0; u < NR; ++u) ok[u] = u < m && rows[u] >= 0;
+                xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+                float x[NR][4];
+#pragma unroll
+                for (int u = 0; u < NR; ++u)  // past the list: the self row's line again
+                    RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : srow) * H + f0, x[u]);
+                add_rows(rows, ok, x);
+            } else {
+                const int srow = a.self[r];
+                const int beg = a.ptr[r], end = a.ptr[r + 1];
+                xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+                for (int base = beg; base < end; base += G) {
+                    const int m = min(G, end - base);
+                    const bool mine = gl < m;
+                    const int my = mine ? a.nbr[base + gl] : -1;
                     int rows[NR];
                     bool ok[NR];
 #pragma unroll
                     for (int u = 0; u < NR; ++u) {
-                        rows[u] = __shfl(my, j + u < m ? j + u : j, G);
-                        ok[u] = (j + u < m) && rows[u] >= 0;
+                        rows[u] = __shfl(my, u < m ? u : 0, G);
+                        ok[u] = u < m && rows[u] >= 0;
                     }
                     const int fallback = rows[0] >= 0 ? rows[0] : 0;
                     float x[NR][4];
@@ -197,20 +246,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                     for (int u = 0; u < NR; ++u)
                         RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * H + f0,
                                               x[u]);
-#pragma unroll
-                    for (int u = 0; u < NR; ++u) {
-                        cnt += ok[u];
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            if (OP == GS_AGG_MEAN) {
-                                acc[v] += ok[u] ? x[u][v] : 0.f;
-                            } else {
-                                const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
-                                acc[v] = take ? x[u][v] : acc[v];
-                                am[v] = take ? rows[u] : am[v];
-                            }
-                        }
-                    }
+                    add_rows(rows, ok, x);
                 }
             }
             if (OP == GS_AGG_MEAN) {
@@ -238,18 +274,17 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 
     // ---- stage 2: E = relu([self | agg] · W2ᵀ), 4x4x1 multi-block MFMAs.
     // Wave w: columns 64 (w & 1) + lane, k quarter w >> 1 (64 k).  Lane l
-    // supplies row l & 3 of A and column l of B; acc[j] = row j, column l.
+    // supplies column l of B; the A operand (row l & 3) comes by ABID
+    // broadcast from one 16-byte read per lane; acc[j] = row j, column l.
     {
         const int col = 64 * (w & 1) + lane, kb = 64 * (w >> 1);
-        const float* xr = sX[lane & 3] + kb;
+        const float4 xa = *reinterpret_cast<const float4*>(sX[lane & 3] + kb + 4 * (lane >> 2));
         const float* wrow = sW2 + col * K;
-        float av[64], bv[64];
+        float bv[64];
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            const float4 x4 = *reinterpret_cast<const float4*>(xr + 4 * m);
             const int q = (kb >> 2) + m;
             const float4 w4 = *reinterpret_cast<const float4*>(wrow + 4 * (q ^ (col & 15)));
-            av[4 * m] = x4.x; av[4 * m + 1] = x4.y; av[4 * m + 2] = x4.z; av[4 * m + 3] = x4.w;
             bv[4 * m] = w4.x; bv[4 * m + 1] = w4.y; bv[4 * m + 2] = w4.z; bv[4 * m + 3] = w4.w;
         }
         // stage 1's global stores, behind the first LDS reads (the compiler
@@ -261,12 +296,17 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             *reinterpret_cast<float4*>(a.agg + r * K + H + st_f0) = st_av;
             if (OP == GS_AGG_MAX) *reinterpret_cast<int4*>(a.argmax + r * H + st_f0) = st_am;
         }
+        // k = 4 b + r: even k on c0, odd on c1, each in k order (the order of
+        // the round-5 kernel's chains)
         f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-        for (int k = 0; k < 64; k += 2) {
-            c0 = mfma4(av[k], bv[k], c0);
-            c1 = mfma4(av[k + 1], bv[k + 1], c1);
-        }
+#define GS_E_STEP(b)                                     \
+        c0 = mfma4b<b>(xa.x, bv[4 * (b)], c0);           \
+        c1 = mfma4b<b>(xa.y, bv[4 * (b) + 1], c1);       \
+        c0 = mfma4b<b>(xa.z, bv[4 * (b) + 2], c0);       \
+        c1 = mfma4b<b>(xa.w, bv[4 * (b) + 3], c1);
+        GS_E_STEP(0) GS_E_STEP(1) GS_E_STEP(2) GS_E_STEP(3) GS_E_STEP(4) GS_E_STEP(5) GS_E_STEP(6) GS_E_STEP(7)
+        GS_E_STEP(8) GS_E_STEP(9) GS_E_STEP(10) GS_E_STEP(11) GS_E_STEP(12) GS_E_STEP(13) GS_E_STEP(14) GS_E_STEP(15)
+#undef GS_E_STEP
         float* pp = sP + (w >> 1) * (kTopRows * H);  // partial of quarter w >> 1: [row][col]
 #pragma unroll
         for (int j = 0; j < kTopRows; ++j) pp[j * H + col] = c0[j] + c1[j];
@@ -288,10 +328,12 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 
     // ---- stage 3: the loss head (models.py:8-27, utils.py:159-164).
     const float invB = 1.0f / static_cast<float>(a.B);
-    const int wp = D + 1;
+    const int wp = WP;
     if constexpr (SMALLC) {
         // C <= 16.  logits: thread t = (row t >> 7, class (t >> 3) & 15, 16 d
         // of part t & 7), the eight parts added by DPP within their 8 lanes
+        // (measured and not kept: the whole dot product per lane in wave 0,
+        // no barrier before the softmax: 1.36 -> 1.54 us for the two stages)
         {
             const int row = tid >> 7, c = (tid >> 3) & 15, part = tid & 7;
             const float* e = sE[row] + 16 * part;
@@ -365,15 +407,18 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         const int row = tid >> 7, d = tid & (D - 1);
         float s = 0.f;
         if constexpr (SMALLC) {
+            // every operand read unconditionally (clamped class), then the
+            // chain with selects: guarded reads became one branch and one LDS
+            // wait per class
             float g[16], v[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                g[u] = u < C ? sdl[row * C + u] : 0.f;
-                v[u] = u < C ? sW[u * wp + d] : 0.f;
+                const int uc = min(u, C - 1);
+                g[u] = sdl[row * C + uc];
+                v[u] = sW[uc * wp + d];
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (u < C) s = fmaf(g[u], v[u], s);
+            for (int u = 0; u < 16; ++u) s = u < C ? fmaf(g[u], v[u], s) : s;
         } else {
             int c = 0;
             for (; c + 8 <= C; c += 8) {
@@ -392,44 +437,47 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         sZ[row][d] = s;
         if (row < nr) a.dZ[static_cast<int64_t>(r0 + row) * D + d] = s;
     }
+    GS_TOP_STAMP(10);
     // ---- this block's classifier partial slab (cls_rows_kernel's sums):
     // out[c][d] = Σ_rows dlogits[row][c] · [E[row] | 1][d], rows in order.
     // Thread t owns class t / 16 (its 4 dlogits in registers) and columns
     // t % 16 + 16 j; the E reads are LDS broadcasts across the class groups.
-    {
+    // `t0`: the first thread of the role (C <= 16: waves 4..7, beside dIn).
+    auto slab_role = [&](int t0) {
+        const int tt = tid - t0;
         const int per = C * (D + 1);
         float* out = a.slab + static_cast<int64_t>(blockIdx.x) * (per + 1);
-        if (C * 16 <= NT) {
-            const int c = tid >> 4;
+        if (C * 16 <= NT - t0) {
+            const int c = tt >> 4;
             if (c < C) {
-                float dl[kTopRows];
+                // all operands read first, unconditionally (rows past nr are
+                // zeros in sE), then the chains with selects: guarded reads had
+                // the compiler branch and wait on LDS once per (row, column)
+                float dl[kTopRows], ev[kTopRows][D / 16];
 #pragma unroll
-                for (int ii = 0; ii < kTopRows; ++ii) dl[ii] = ii < nr ? sdl[ii * C + c] : 0.f;
+                for (int ii = 0; ii < kTopRows; ++ii) {
+                    dl[ii] = sdl[ii * C + c];
+#pragma unroll
+                    for (int j = 0; j < D / 16; ++j) ev[ii][j] = sE[ii][(tt & 15) + 16 * j];
+                }
                 float sv[D / 16];
 #pragma unroll
                 for (int j = 0; j < D / 16; ++j) {
-                    const int d = (tid & 15) + 16 * j;
                     sv[j] = 0.f;
 #pragma unroll
-                    for (int ii = 0; ii < kTopRows; ++ii)
-                        if (ii < nr) sv[j] = fmaf(dl[ii], sE[ii][d], sv[j]);
+                    for (int ii = 0; ii < kTopRows; ++ii) sv[j] = ii < nr ? fmaf(dl[ii], ev[ii][j], sv[j]) : sv[j];
                 }
 #pragma unroll
-                for (int j = 0; j < D / 16; ++j)
-#ifdef GS_TOP_LAB_NO_SLAB  // lab probe only: the slab stores skipped
-                    if (a.B < 0)
-#endif
-                    out[c * (D + 1) + (tid & 15) + 16 * j] = sv[j];
-                if ((tid & 15) == 0) {
+                for (int j = 0; j < D / 16; ++j) out[c * (D + 1) + (tt & 15) + 16 * j] = sv[j];
+                if ((tt & 15) == 0) {
                     float sbias = 0.f;
 #pragma unroll
-                    for (int ii = 0; ii < kTopRows; ++ii)
-                        if (ii < nr) sbias = fmaf(dl[ii], 1.f, sbias);
+                    for (int ii = 0; ii < kTopRows; ++ii) sbias = ii < nr ? fmaf(dl[ii], 1.f, sbias) : sbias;
                     out[c * (D + 1) + D] = sbias;
                 }
             }
         } else {
-            for (int t = tid; t < per; t += NT) {
+            for (int t = tt; t < per; t += NT - t0) {
                 const int c = t / (D + 1), d = t - c * (D + 1);
                 float sv = 0.f;
 #pragma unroll
@@ -443,14 +491,45 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             for (int ii = 0; ii < nr; ++ii) sl += sloss[ii];
             out[per] = sl;
         }
-    }
+    };
+    slab_role(0);
     lds_barrier();
     GS_TOP_STAMP(7);
 
-    // ---- stage 4: dIn = dZ · W2 (4x4x1 multi-block).  Wave w: input columns
-    // 64 (w & 3) + lane, h half w >> 2 (64 h); W2[h][kc] read down a column of
-    // the swizzled copy.
-    {
+    // ---- stage 4: dIn = dZ · W2 (4x4x1 multi-block)
+    if constexpr (SMALLC) {
+        // Wave w: input columns 128 (w & 1) + 2 lane and + 1 (one 8-byte read
+        // of the swizzled W2 row per h: both columns sit in one quad), h quarter
+        // w >> 1 (32 h); one MFMA chain per column; the dZ operand by ABID
+        // broadcast (blocks 0..7 of the read hold the quarter's 32 h)
+        const int k0 = 128 * (w & 1) + 2 * lane, hb = 32 * (w >> 1);
+        const float4 za = *reinterpret_cast<const float4*>(sZ[lane & 3] + min(hb + 4 * (lane >> 2), H - 4));
+        float2 wv[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+            const int h = hb + t;
+            wv[t] = *reinterpret_cast<const float2*>(sW2 + h * K + 4 * ((k0 >> 2) ^ (h & 15)) + (k0 & 3));
+        }
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#define GS_DIN_STEP(b)                                   \
+        c0 = mfma4b<b>(za.x, wv[4 * (b)].x, c0);         \
+        c1 = mfma4b<b>(za.x, wv[4 * (b)].y, c1);         \
+        c0 = mfma4b<b>(za.y, wv[4 * (b) + 1].x, c0);     \
+        c1 = mfma4b<b>(za.y, wv[4 * (b) + 1].y, c1);     \
+        c0 = mfma4b<b>(za.z, wv[4 * (b) + 2].x, c0);     \
+        c1 = mfma4b<b>(za.z, wv[4 * (b) + 2].y, c1);     \
+        c0 = mfma4b<b>(za.w, wv[4 * (b) + 3].x, c0);     \
+        c1 = mfma4b<b>(za.w, wv[4 * (b) + 3].y, c1);
+        GS_DIN_STEP(0) GS_DIN_STEP(1) GS_DIN_STEP(2) GS_DIN_STEP(3)
+        GS_DIN_STEP(4) GS_DIN_STEP(5) GS_DIN_STEP(6) GS_DIN_STEP(7)
+#undef GS_DIN_STEP
+        float* pp = dinq[w >> 1];
+#pragma unroll
+        for (int j = 0; j < kTopRows; ++j)
+            *reinterpret_cast<float2*>(pp + j * K + k0) = make_float2(c0[j], c1[j]);
+    } else {
+        // Wave w: input columns 64 (w & 3) + lane, h half w >> 2 (64 h); W2[h][kc]
+        // read down a column of the swizzled copy.
         const int kc = 64 * (w & 3) + lane, hb = 64 * (w >> 2);
         const float* zr = sZ[lane & 3] + hb;
         float zv[64], wv[64];
@@ -476,11 +555,15 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     }
     lds_barrier();
     GS_TOP_STAMP(8);
-    // the two halves added in order, dIn to global: thread t = (row, 2 columns)
+    // the h parts added in order, dIn to global: thread t = (row, 2 columns)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int o = tid + u * NT, row = o >> 8, kc = o & (K - 1);
-        const float v = sP[row * K + kc] + sP[kTopRows * K + row * K + kc];
+        float v;
+        if constexpr (SMALLC)
+            v = ((dinq[0][row * K + kc] + dinq[1][row * K + kc]) + dinq[2][row * K + kc]) + dinq[3][row * K + kc];
+        else
+            v = sP[row * K + kc] + sP[kTopRows * K + row * K + kc];
         if (row < nr) a.dIn[static_cast<int64_t>(r0 + row) * K + kc] = v;
     }
     GS_TOP_STAMP(9);
@@ -488,8 +571,10 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 }
 
 static size_t top_smem_bytes(int64_t C) {
+    const int64_t wp = C <= 16 ? kTopH + 4 : kTopH + 1;  // sage_top_kernel's WP
+    const int64_t q3 = C <= 16 ? kTopRows + 3 + kTopRows * kTopK : 0;  // its fourth dIn partial (16-B aligned)
     return sizeof(float) * (static_cast<size_t>(kTopH) * kTopK + kTopRows * (kTopK + 2 * kTopH) + kTopPart +
-                            C * (kTopH + 1) + kTopRows * C + kTopRows + C + kTopRows);
+                            C * wp + kTopRows * C + kTopRows + C + (q3 ? q3 : kTopRows));
 }
 
 // The kernel keeps W2 in LDS (~146 KiB at 16 classes): raise the launch limit

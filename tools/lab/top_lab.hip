@@ -197,6 +197,15 @@ int main(int argc, char** argv) {
         }
         std::printf("stamped launch %d\n", rep);
         for (int i = 1; i < NS; ++i) std::printf("  stage %d %-32s mean %.2f us  max %.2f us\n", i, names[i], acc[i] / nb, mx[i]);
+        {
+            double a10 = 0, a11 = 0, a7 = 0;
+            for (int b = 0; b < nb; ++b) {
+                a10 += (h[b * 16 + 10] - h[b * 16 + 6]) * 0.01;
+                a11 += (h[b * 16 + 11] - h[b * 16 + 10]) * 0.01;
+                a7 += (h[b * 16 + 7] - h[b * 16 + 11]) * 0.01;
+            }
+            std::printf("  stage 7 split: dZ %.2f  slab %.2f  loss + barrier %.2f us\n", a10 / nb, a11 / nb, a7 / nb);
+        }
         double spread = 0;
         for (int b = 0; b < nb; ++b) spread = std::max(spread, (h[b * 16] - t0) * 0.01);
         std::printf("  block start spread %.2f us; first start -> last end %.2f us\n", spread, last_end - first_start);
