@@ -98,10 +98,15 @@ __device__ __forceinline__ float dpp_max16(float v) {
     return fmaxf(v, dpp_f<0x140>(v));
 }
 
+// Sum over the 64 lanes of a wave, every lane active; every lane gets the
+// total.  DPP only (no ds_bpermute round trips): the 16-lane rows by
+// dpp_sum16, then row 1 += row 0 and row 3 += row 2 (row_bcast15), rows 2-3
+// += lane 31 (row_bcast31); lane 63 then holds (r2 + r3) + (r0 + r1).
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v = dpp_sum16(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));  // row_bcast15
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));  // row_bcast31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 // A workgroup barrier for a hand-off through LDS alone: the LDS ops done
