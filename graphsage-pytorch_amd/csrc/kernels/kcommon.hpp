@@ -109,6 +109,16 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Max over the 64 lanes of a wave (every lane active), the wave_sum scheme.
+__device__ __forceinline__ float wave_max(float v) {
+    v = dpp_max16(v);
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x142, 0xa,
+                                                            0xf, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), 0x143, 0xc,
+                                                            0xf, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // A workgroup barrier for a hand-off through LDS alone: the LDS ops done
 // (lgkmcnt), not the global stores in flight, which __syncthreads() waits for
 // (its fence drains vmcnt: a store round trip).  The memory clobber keeps the

@@ -330,39 +330,44 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     const float invB = 1.0f / static_cast<float>(a.B);
     const int wp = WP;
     if constexpr (SMALLC) {
-        // C <= 16.  logits: thread t = (row t >> 7, class (t >> 3) & 15, 16 d
-        // of part t & 7), the eight parts added by DPP within their 8 lanes
-        // (measured and not kept: the whole dot product per lane in wave 0,
-        // no barrier before the softmax: 1.36 -> 1.54 us for the two stages)
-        {
-            const int row = tid >> 7, c = (tid >> 3) & 15, part = tid & 7;
-            const float* e = sE[row] + 16 * part;
-            const float* wr = sW + min(c, C - 1) * wp + 16 * part;
+        // C <= 16: logits, softmax, NLL and dlogits of row w on wave w, in one
+        // stage: lane = (class lane >> 2, part lane & 3 of 32 d); the parts
+        // added by DPP within the quad, the row's max and exp-sum by DPP over
+        // the wave (each class counted once: the sum takes part 0 only).
+        // (Measured and not kept: the whole dot product per lane in wave 0
+        // after an 8-wave logits stage; 1.36 -> 1.54 us.)
+        if (w < kTopRows) {
+            const int row = w, c = lane >> 2, part = lane & 3;
+            const bool cv = c < C;
+            const float* e = sE[row] + 32 * part;
+            const float* wr = sW + min(c, C - 1) * wp + 32 * part;
             float z = 0.f;
 #pragma unroll
-            for (int t = 0; t < 16; ++t) z = fmaf(e[t], wr[t], z);
-            z = dpp_sum8(z);
-            if (part == 0 && c < C) sdl[row * C + c] = z + sb[c];
-        }
-        lds_barrier();
-        GS_TOP_STAMP(5);
-        // softmax / NLL / dlogits: wave 0, lane = (row lane >> 4, class lane & 15);
-        // a row's classes are one 16-lane DPP row
-        if (w == 0) {
-            const int row = lane >> 4, c = lane & 15;
-            const bool cv = c < C;
-            const float z = cv ? sdl[row * C + c] : -INFINITY;
-            const float mx = dpp_max16(z);
-            const float lse = logf(dpp_sum16(cv ? expf(z - mx) : 0.f));
-            if (row < nr) {
-                const int y = sy[row];
-                const float lp = z - mx - lse;
-                if (c == y) sloss[row] = -lp;
-                if (cv) sdl[row * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
-            } else if (cv) {
-                sdl[row * C + c] = 0.f;  // ragged block: no gradient from the missing rows
+            for (int t = 0; t < 32; t += 4) {
+                const float4 e4 = *reinterpret_cast<const float4*>(e + t);
+                const float4 w4 = *reinterpret_cast<const float4*>(wr + t);
+                z = fmaf(e4.x, w4.x, z);
+                z = fmaf(e4.y, w4.y, z);
+                z = fmaf(e4.z, w4.z, z);
+                z = fmaf(e4.w, w4.w, z);
+            }
+            z += dpp_f<0xB1>(z);  // quad_perm [1,0,3,2]
+            z += dpp_f<0x4E>(z);  // quad_perm [2,3,0,1]: (p0 + p1) + (p2 + p3) in every lane of the quad
+            const float zl = cv ? z + sb[min(c, C - 1)] : -INFINITY;
+            const float mx = wave_max(zl);
+            const float lse = logf(wave_sum(cv && part == 0 ? expf(zl - mx) : 0.f));
+            if (part == 0 && cv) {
+                if (row < nr) {
+                    const int y = sy[row];
+                    const float lp = zl - mx - lse;
+                    if (c == y) sloss[row] = -lp;
+                    sdl[row * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+                } else {
+                    sdl[row * C + c] = 0.f;  // ragged block: no gradient from the missing rows
+                }
             }
         }
+        GS_TOP_STAMP(5);
     } else {
         // logits: thread t owns (row, class) (t >> 3) and the 16 d of part t & 7;
         // the eight parts are added by an xor butterfly.
@@ -401,10 +406,8 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     }
     lds_barrier();
     GS_TOP_STAMP(6);
-    // dZ = (dlogits · Wc) ⊙ (E > 0): thread t = (row, d), classes in order
-    // (eight classes' operands read ahead of their chain)
-    {
-        const int row = tid >> 7, d = tid & (D - 1);
+    // dZ = (dlogits · Wc) ⊙ (E > 0) for one (row, d), classes in order
+    auto dz_one = [&](int row, int d) {
         float s = 0.f;
         if constexpr (SMALLC) {
             // every operand read unconditionally (clamped class), then the
@@ -436,8 +439,7 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
         if (!(sE[row][d] > 0.f)) s = 0.f;
         sZ[row][d] = s;
         if (row < nr) a.dZ[static_cast<int64_t>(r0 + row) * D + d] = s;
-    }
-    GS_TOP_STAMP(10);
+    };
     // ---- this block's classifier partial slab (cls_rows_kernel's sums):
     // out[c][d] = Σ_rows dlogits[row][c] · [E[row] | 1][d], rows in order.
     // Thread t owns class t / 16 (its 4 dlogits in registers) and columns
@@ -492,7 +494,19 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
             out[per] = sl;
         }
     };
-    slab_role(0);
+    if constexpr (SMALLC) {
+        // dZ on waves 0..3 (two outputs per thread), the classifier slab beside
+        // it on waves 4..7: the stage takes the longer of the two, not the sum
+        if (w < 4) {
+            dz_one(tid >> 6, tid & 63);
+            dz_one(tid >> 6, (tid & 63) + 64);
+        } else {
+            slab_role(256);
+        }
+    } else {
+        dz_one(tid >> 7, tid & (D - 1));
+        slab_role(0);
+    }
     lds_barrier();
     GS_TOP_STAMP(7);
 
