@@ -145,6 +145,8 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
         const int fallback = SELF ? node : (rows[0] >= 0 ? rows[0] : 0);
         Raw xself{};
         if (SELF) xself = *reinterpret_cast<const Raw*>(X + static_cast<int64_t>(node) * ldx + f0);
+        // every slot loaded (past k: the fallback row's line again), the adds in
+        // chunks of 4 up to k (uniform: slots past k add nothing)
         Raw x[NR];
 #pragma unroll
         for (int u = 0; u < NR; ++u)
@@ -154,21 +156,27 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
         int cnt = 0;
+        int ka = k;
+        asm volatile("" : "+s"(ka));  // (kept opaque: the adds stay behind the loads)
 #pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            cnt += ok[u];
-            float xv[VEC];
-            RawVec<T, VEC>::unpack(x[u], xv);
+        for (int q = 0; q < NR / 4; ++q)
+            if (4 * q < ka) {
 #pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                if (OP == GS_AGG_MEAN) {
-                    acc[v] += ok[u] ? xv[v] : 0.f;
-                } else {
-                    const bool take = ok[u] && xv[v] > acc[v];
-                    acc[v] = take ? xv[v] : acc[v];
+                for (int u = 4 * q; u < 4 * q + 4; ++u) {
+                    cnt += ok[u];
+                    float xv[VEC];
+                    RawVec<T, VEC>::unpack(x[u], xv);
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) {
+                        if (OP == GS_AGG_MEAN) {
+                            acc[v] += ok[u] ? xv[v] : 0.f;
+                        } else {
+                            const bool take = ok[u] && xv[v] > acc[v];
+                            acc[v] = take ? xv[v] : acc[v];
+                        }
+                    }
                 }
             }
-        }
         if (SELF) *reinterpret_cast<Raw*>(self_out + static_cast<int64_t>(r) * ldso + f0) = xself;
         if (OP == GS_AGG_MEAN) {
             const float inv = 1.0f / static_cast<float>(cnt);

@@ -178,22 +178,23 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
                 am[v] = -1;
             }
             int cnt = 0;
-            // rows[u] in list order, ok[u] = a real neighbour: added in u order
-            auto add_rows = [&](const int (&rows)[NR], const bool (&ok)[NR], const float (&x)[NR][4]) {
+            // one neighbour row (ok: a real one), added in list order
+            auto add_row = [&](int row, bool ok, const float (&x)[4]) {
+                cnt += ok;
 #pragma unroll
-                for (int u = 0; u < NR; ++u) {
-                    cnt += ok[u];
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        if (OP == GS_AGG_MEAN) {
-                            acc[v] += ok[u] ? x[u][v] : 0.f;
-                        } else {
-                            const bool take = ok[u] && x[u][v] > acc[v];  // strict: first index wins ties
-                            acc[v] = take ? x[u][v] : acc[v];
-                            am[v] = take ? rows[u] : am[v];
-                        }
+                for (int v = 0; v < 4; ++v) {
+                    if (OP == GS_AGG_MEAN) {
+                        acc[v] += ok ? x[v] : 0.f;
+                    } else {
+                        const bool take = ok && x[v] > acc[v];  // strict: first index wins ties
+                        acc[v] = take ? x[v] : acc[v];
+                        am[v] = take ? row : am[v];
                     }
                 }
+            };
+            auto add_rows = [&](const int (&rows)[NR], const bool (&ok)[NR], const float (&x)[NR][4]) {
+#pragma unroll
+                for (int u = 0; u < NR; ++u) add_row(rows[u], ok[u], x[u]);
             };
             float4 xs;
             if (a.tids) {
@@ -220,11 +221,32 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
 #pragma unroll
                 for (int u = 0; u < NR; ++u) ok[u] = u < m && rows[u] >= 0;
                 xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+                // rows in chunks of 8, a chunk only while the longer list of the
+                // wave's two groups reaches it (wave-uniform: the ballot): the
+                // lists average ~8 of the 25 slots, and rows past a list add
+                // nothing (+0 / never the max), so the sums are the same
+                const int mw = max(__popcll(have & 0xffffffffull), __popcll(have >> 32));
                 float x[NR][4];
 #pragma unroll
-                for (int u = 0; u < NR; ++u)  // past the list: the self row's line again
-                    RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : srow) * H + f0, x[u]);
-                add_rows(rows, ok, x);
+                for (int q = 0; q < NR / 8; ++q)
+                    if (8 * q < mw) {
+#pragma unroll
+                        for (int u = 8 * q; u < 8 * q + 8; ++u)  // past the list: the self row's line again
+                            RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : srow) * H + f0,
+                                                  x[u]);
+                    }
+                __builtin_amdgcn_sched_barrier(0);  // every row load issued before the first add waits
+                // the same bound through an opaque copy: with one condition the
+                // compiler merges each chunk's adds into its load block, and the
+                // next chunk's loads then wait for this one's data
+                int mwa = mw;
+                asm volatile("" : "+s"(mwa));
+#pragma unroll
+                for (int q = 0; q < NR / 8; ++q)
+                    if (8 * q < mwa) {
+#pragma unroll
+                        for (int u = 8 * q; u < 8 * q + 8; ++u) add_row(rows[u], ok[u], x[u]);
+                    }
             } else {
                 const int srow = a.self[r];
                 const int beg = a.ptr[r], end = a.ptr[r + 1];
