@@ -683,7 +683,7 @@ def main():
                     help="pinned pack slots per sampler stream (how far each stream may run ahead)")
     ap.add_argument("--sampler-helpers", type=int, default=None,
                     help="helper threads per sampler stream (same draws; lower per-batch latency); "
-                         "default 1 with >= 8 host cores per GPU")
+                         "default 0: more streams instead (profiles/r06_sampler_layout_ab.txt)")
     args = ap.parse_args()
     per_gpu = host_cores() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
     # as given on the command line, before the training runner's defaults below
@@ -694,10 +694,12 @@ def main():
         if args.sampler_streams is None:
             args.sampler_streams = 1
     if args.sampler_helpers is None:
-        # one helper per stream where the cores allow: a batch then samples in
-        # ~0.35-0.42 ms instead of ~0.5-0.57 (profiles/r02_ab_sampler_layouts.txt),
-        # which is what a cold pipeline waits for before its first step
-        args.sampler_helpers = 1 if per_gpu >= 8 and (args.sampler_streams or 2) > 1 else 0
+        # streams without helpers: a helper shortens one batch (0.31-0.33 against
+        # 0.45-0.48 ms in-bench) but halves the streams the cores hold, and at a
+        # ~50 us step the pipeline needs batches per second, not latency: 12 streams
+        # give 12.8-13.6 M roots/s of capacity against 10.8-11.7 M for 7 streams
+        # + 7 helpers, at the same step rate (profiles/r06_sampler_layout_ab.txt)
+        args.sampler_helpers = 0
     if args.sampler_streams is None:
         if args.sampler_helpers:  # two threads per stream, two cores for the issuing thread and the runtime
             args.sampler_streams = max(1, min(8, (per_gpu - 2) // (1 + args.sampler_helpers)))
