@@ -487,6 +487,75 @@ def test_top_launch_matches_separate_launches(gs, agg, name, B):
     assert done >= 1
 
 
+@pytest.mark.parametrize("classes,fan,agg,B", [(3, [25, 10], "MEAN", 97), (7, [15, 5], "MAX", 512),
+                                                (19, [25, 10], "MEAN", 130), (16, [31, 16], "MEAN", 64),
+                                                (5, [40, 20], "MAX", 96)])
+def test_top_launch_edge_shapes(gs, classes, fan, agg, B):
+    """The one-launch top layer away from the benchmark's shape, against the
+    separate launches: class counts below 16 (the small-C head's masked class
+    lanes), above 16 (the general head: 8-part logits, a softmax wave per row),
+    neighbour lists longer than one 32-row round of the launch's list gather
+    (fanout 40) and ragged last row blocks; within fp32 rounding of the k
+    order like the bench shape's test."""
+    graph, g, n = _graph(gs, "pubmed")
+    X = torch.from_numpy(uniform_features(9, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % classes).astype(np.int32)).to(DEV)
+    a = train.NativeTrainer(graph, X, labels, classes, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
+    b = train.NativeTrainer(graph, X, labels, classes, num_layers=2, fanouts=fan, agg_func=agg, seed=824)
+    b.set_option("top_launch", False)
+    rng = gs.RNG(7)
+    done = 0
+    for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 23):
+        if done == 2:
+            break
+        s = gs.sample(graph, rng, roots, fan)
+        if agg == "MAX" and any(s.n_empty(j) for j in range(1, 3)):
+            continue
+        ds = models.DeviceSample(s, DEV)
+        r = torch.from_numpy(roots.astype(np.int32)).to(DEV)
+        la = a.forward_backward(ds, r).clone()
+        lb = b.forward_backward(ds, r).clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(la).all()
+        torch.testing.assert_close(la, lb, atol=1e-6, rtol=1e-5)
+        torch.testing.assert_close(a.p.grads, b.p.grads, atol=1e-7, rtol=1e-5)
+        a.apply_update()
+        b.apply_update()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(a.p.params, b.p.params, atol=1e-7, rtol=1e-5)
+        b.p.params.copy_(a.p.params)
+        done += 1
+    assert done >= 1
+
+
+@pytest.mark.parametrize("classes,fan,agg", [(7, (15, 5), "MEAN"), (3, (31, 16), "MAX"), (5, (40, 20), "MEAN")])
+def test_native_runner_matches_python_loop_edge_shapes(gs, classes, fan, agg):
+    """The runner (resolved-id layer-1 gather, padded top records, deferred
+    update) at fanouts and class counts away from the benchmark's, against the
+    Python loop on the same sampler stream: bitwise equal parameters and loss,
+    including the one-round gather's largest fanout (16) and fanouts past what
+    the one-round gather and the top launch's records take (20, 40)."""
+    graph, g, n = _graph(gs, "rmat")
+    X = torch.from_numpy(uniform_features(5, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % classes).astype(np.int32)).to(DEV)
+    batches = list(train.rank_batches(np.nonzero(graph.degrees())[0], 48, 0, 1, 9))[:5]
+    a = train.NativeTrainer(graph, X, labels, classes, fanouts=fan, agg_func=agg, seed=824)
+    b = train.NativeTrainer(graph, X, labels, classes, fanouts=fan, agg_func=agg, seed=824)
+    pf = train.Prefetcher(graph, None, batches, list(fan), False, DEV, rngs=[train.make_rng(11, 0, 0)],
+                          fail_empty=agg == "MAX")
+    for _ in batches:
+        ds, roots_dev, _info = pf.next()
+        a.step(ds, roots_dev)
+    pf.close()
+    runner = train.Runner(b, graph, batches, [train.make_rng(11, 0, 0)], list(fan), gcn=False,
+                          fail_empty=agg == "MAX", depth=2)
+    runner.run(len(batches))
+    torch.cuda.synchronize()
+    assert torch.equal(a.p.params, b.p.params)
+    assert float(a.loss) == float(b.loss)
+    runner.close()
+
+
 def test_top_launch_is_deterministic(gs):
     """The top launch's split-K partial sums are added in a fixed order: two
     trainers on the same batches leave bitwise the same loss, gradients and
