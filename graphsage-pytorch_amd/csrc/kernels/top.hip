@@ -126,7 +126,9 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     // order, so those would otherwise queue behind the DMA).
     // (Measured and not kept: each block starting the DMA at its own row, so
     // the blocks sharing an XCD's L2 request different lines at a time: the
-    // launch 11.15 -> 11.5 us in tools/lab/top_lab.hip.)
+    // launch 11.15 -> 11.5 us in tools/lab/top_lab.hip; a quarter of the rows
+    // on the two gather waves, issued behind their row loads: 9.27 -> 9.6 us,
+    // their adds then start after those issues.)
     if (w >= 2)
         for (int c = w - 2; c < H; c += NT / 64 - 2)
             __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(c) * K + 4 * (lane ^ (c & 15)), sW2 + c * K, 16,
