@@ -27,7 +27,7 @@ GS_AGG_MEAN, GS_AGG_MAX = 0, 1
 GS_SAMPLE_GCN, GS_SAMPLE_FULL = 1, 2
 GS_DSAMPLER_NO_AUX = 8  # gs_dsampler_create: every kernel on the caller's stream
 GS_MAX_HOPS = 8
-GS_TOPT_FUSED_BWD, GS_TOPT_TOP_LAUNCH, GS_TOPT_SELF_ROWS, GS_TOPT_DEFER_UPDATE = range(4)
+GS_TOPT_FUSED_BWD, GS_TOPT_TOP_LAUNCH, GS_TOPT_SELF_ROWS, GS_TOPT_DEFER_UPDATE, GS_TOPT_TOP_PAIR = range(5)
 (GS_PK_POS_PTR, GS_PK_POS, GS_PK_DST_IDS, GS_PK_NBR_PTR, GS_PK_NBR, GS_PK_SELF,
  GS_PK_TPTR, GS_PK_TIDX, GS_PK_NFIELDS) = range(9)
 

@@ -144,7 +144,12 @@ __device__ __forceinline__ void agg_bwd_body(
     int bx, int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,
     const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
     int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
-    float* __restrict__ dH) {
+    float* __restrict__ dH, int64_t off2 = 0) {
+    // off2 != 0: the input gradient arrives as two partial sums (the top
+    // launch's pair form), the second off2 floats past the first; each row is
+    // their sum, first + second (the second load re-reads the first's row
+    // when off2 == 0 and is not used)
+    const bool pair = off2 != 0;
     const int gl = threadIdx.x % G;
     const int c = bx * (kBlock / G) + threadIdx.x / G;
     if (c >= n_src) return;
@@ -164,7 +169,7 @@ __device__ __forceinline__ void agg_bwd_body(
             int e[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) e[u] = tidx[min(t0 + u, end - 1)];
-            float x[8][VEC], w[8];
+            float x[8][VEC], y[8][VEC], w[8];
             int am[8][VEC];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -173,6 +178,7 @@ __device__ __forceinline__ void agg_bwd_body(
                 const int row = self_e ? -eu - 1 : eu;
                 const float* src = (self_e && dSelf) ? dSelf : dA;
                 RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
+                RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
                 if (OP == GS_AGG_MEAN) {
                     const int re = self_e ? 0 : eu;
                     w[u] = 1.0f / static_cast<float>(ptr[re + 1] - ptr[re]);
@@ -183,6 +189,10 @@ __device__ __forceinline__ void agg_bwd_body(
                 }
             }
             if (!act) continue;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) x[u][v] = pair ? x[u][v] + y[u][v] : x[u][v];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 if (t0 + u >= end) break;
@@ -205,21 +215,25 @@ __device__ __forceinline__ void agg_bwd_body(
             const int e = tidx[t];
             if (!act) continue;
             float x[VEC];
+            float x2[VEC];
             if (e < 0) {
                 if (!dSelf) continue;  // gcn: self rows feed no linear input
                 RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0, x);
+                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0 + off2, x2);
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += x[v];
+                for (int v = 0; v < VEC; ++v) g[v] += pair ? x[v] + x2[v] : x[v];
             } else if (OP == GS_AGG_MEAN) {
                 const float w = 1.0f / static_cast<float>(ptr[e + 1] - ptr[e]);
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += x[v] * w;
+                for (int v = 0; v < VEC; ++v) g[v] += (pair ? x[v] + x2[v] : x[v]) * w;
             } else {
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v)
-                    if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += x[v];
+                    if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += pair ? x[v] + x2[v] : x[v];
             }
         }
 #endif
@@ -247,7 +261,8 @@ __device__ __forceinline__ void agg_bwd_rec_body(
     int bx, int n_src, int F, const int4* __restrict__ rec, const int* __restrict__ tidx,
     const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
     int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
-    float* __restrict__ dH) {
+    float* __restrict__ dH, int64_t off2 = 0) {
+    const bool pair = off2 != 0;  // two partial input gradients (agg_bwd_body)
     const int gl = threadIdx.x % G;
     const int c = bx * (kBlock / G) + threadIdx.x / G;
     if (c >= n_src) return;
@@ -262,7 +277,7 @@ __device__ __forceinline__ void agg_bwd_rec_body(
         float g[VEC];
 #pragma unroll
         for (int v = 0; v < VEC; ++v) g[v] = 0.f;
-        float x[kTrec][VEC], w[kTrec];
+        float x[kTrec][VEC], y[kTrec][VEC], w[kTrec];
         int am[kTrec][VEC], pa[kTrec], pb[kTrec];
 #pragma unroll
         for (int u = 0; u < kTrec; ++u) {
@@ -271,6 +286,7 @@ __device__ __forceinline__ void agg_bwd_rec_body(
             const int row = self_e ? -eu - 1 : eu;
             const float* src = (self_e && dSelf) ? dSelf : dA;
             RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
+            RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
             if (OP == GS_AGG_MEAN) {
                 const int re = self_e ? 0 : eu;
                 pa[u] = ptr[re];
@@ -289,6 +305,10 @@ __device__ __forceinline__ void agg_bwd_rec_body(
         }
         if (!act) continue;
 #pragma unroll
+        for (int u = 0; u < kTrec; ++u)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) x[u][v] = pair ? x[u][v] + y[u][v] : x[u][v];
+#pragma unroll
         for (int u = 0; u < kTrec; ++u) {
             if (u >= n) break;
             if (e[u] < 0) {
@@ -306,22 +326,25 @@ __device__ __forceinline__ void agg_bwd_rec_body(
         }
         for (int t = beg + kTrec; t < beg + n; ++t) {  // hub rows: the rest of the list
             const int et = tidx[t];
-            float xt[VEC];
+            float xt[VEC], yt[VEC];
             if (et < 0) {
                 if (!dSelf) continue;
                 RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0, xt);
+                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0 + off2, yt);
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += xt[v];
+                for (int v = 0; v < VEC; ++v) g[v] += pair ? xt[v] + yt[v] : xt[v];
             } else if (OP == GS_AGG_MEAN) {
                 const float wt = 1.0f / static_cast<float>(ptr[et + 1] - ptr[et]);
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) g[v] += xt[v] * wt;
+                for (int v = 0; v < VEC; ++v) g[v] += (pair ? xt[v] + yt[v] : xt[v]) * wt;
             } else {
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
+                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v)
-                    if (argmax[static_cast<int64_t>(et) * F + f0 + v] == c) g[v] += xt[v];
+                    if (argmax[static_cast<int64_t>(et) * F + f0 + v] == c) g[v] += pair ? xt[v] + yt[v] : xt[v];
             }
         }
         if (Hprev) {

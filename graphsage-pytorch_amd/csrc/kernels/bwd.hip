@@ -61,6 +61,7 @@ struct BwdB {
     const float* Hprev;
     float* dH;
     const int4* rec = nullptr;  // agg_bwd_rec_body's records (layer_bwd_top only)
+    int64_t off2 = 0;           // dIn as two partials (the top launch's pair form), the second off2 floats on
 };
 
 template <int OP, int G>
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_b_kernel(BwdB b) {
         return;
     }
     agg_bwd_body<OP, 4, G>(bx - b.sum_nb, b.n_src, b.F, b.tptr, b.tidx, b.ptr, b.dA, b.dSelf, b.ldd, b.argmax,
-                           b.Hprev, b.F, b.dH);
+                           b.Hprev, b.F, b.dH, b.off2);
 }
 
 struct BwdT {
@@ -100,10 +101,10 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
     b -= t.cls_nb;
     if (t.b.rec)
         agg_bwd_rec_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.rec, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
-                                   t.b.argmax, t.b.Hprev, t.b.F, t.b.dH);
+                                   t.b.argmax, t.b.Hprev, t.b.F, t.b.dH, t.b.off2);
     else
         agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
-                               t.b.argmax, t.b.Hprev, t.b.F, t.b.dH);
+                               t.b.argmax, t.b.Hprev, t.b.F, t.b.dH, t.b.off2);
 }
 
 int cls_reduce_grid(int64_t C, int64_t D) { return cls_reduce_blocks(C, D); }
@@ -189,6 +190,7 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     Bq.argmax = a.argmax;
     Bq.Hprev = a.Hprev;
     Bq.dH = a.dH;
+    Bq.off2 = a.din_off2;
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
     const dim3 gb(static_cast<unsigned>(Bq.sum_nb + agg_nb));
@@ -250,6 +252,7 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     Bq.argmax = a.argmax;
     Bq.Hprev = a.Hprev;
     Bq.dH = a.dH;
+    Bq.off2 = a.din_off2;
     Bq.rec = a.trec;
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));

@@ -132,6 +132,7 @@ struct LayerBwd {
     const float* Hprev;                   // previous layer's output (relu mask), [n_src][H]
     float* dH;                            // [n_src][H] gradient of the previous layer's output (masked)
     bool din_ready = false;               // dIn already written (top.hip): launch A skips its dIn role
+    int64_t din_off2 = 0;                 // dIn as two partials, the second din_off2 floats on (the top pair form)
 };
 
 struct ClsReduce {
@@ -190,6 +191,20 @@ int top_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t
                 const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
                 const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* slab,
                 hipStream_t st, const int32_t* tids = nullptr, int tk = 0);
+// The pair form (C <= 16): two blocks per 4 roots, each with half of W2 and
+// E's columns, the partial logits exchanged between the pair as tagged
+// granules (xch: [8·ceil(quads / 8)][2][64] u64, zero at allocation; epoch:
+// the launch's tag, never 0 and never repeated on one buffer; fail: set if a
+// block gave up waiting, its outputs are then NaN).  dIn receives half 0's
+// partial of the input gradient, dIn2 half 1's: the consumer adds them,
+// dIn + dIn2 (LayerBwd::din_off2).  Returns the classifier slabs written.
+bool top_pair_supported(int64_t H, int64_t C, bool gcn);
+int top_pair_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
+                     const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
+                     const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* dIn2,
+                     float* slab, unsigned long long* xch, unsigned epoch, unsigned* fail, hipStream_t st,
+                     const int32_t* tids = nullptr, int tk = 0);
+inline int64_t top_pair_xch_words(int64_t B) { return 8 * ((((B + 3) / 4) + 7) / 8) * 2 * 64; }
 
 // dsample.hip: whether the last gs_dsampler_run has completed (no wait).
 bool dsampler_ready(gs_dsampler* ds);

@@ -72,6 +72,14 @@ struct gs_trainer {
     bool use_top = true;     // GS_TOPT_TOP_LAUNCH: layer 2 + loss head + dIn2 in one launch
     bool want_self_rows = true;  // GS_TOPT_SELF_ROWS
     bool opt_defer = true;   // GS_TOPT_DEFER_UPDATE: runner loops defer each clip + SGD
+    bool opt_top_pair = false;  // GS_TOPT_TOP_PAIR: the top launch on two blocks per 4 roots (C <= 16);
+                                // off: measured neutral in the step (DESIGN.md §4 top)
+    // the pair form's exchange: tagged granules ([quads][2][64], zeroed when
+    // allocated), this trainer's launch tag and the give-up flag
+    unsigned long long* xch = nullptr;
+    int64_t xch_quads = 0;  // (words of xch)
+    unsigned xch_epoch = 0;
+    unsigned* xch_fail = nullptr;
     float* norm_part = nullptr;
     int pstride = 0;
     int npart[2] = {0, 0};
@@ -124,6 +132,8 @@ struct gs_trainer {
         if (w1_alt) (void)hipFree(w1_alt);
         if (w1_lp_alt) (void)hipFree(w1_lp_alt);
         if (norm_part) (void)hipFree(norm_part);
+        if (xch) (void)hipFree(xch);
+        if (xch_fail) (void)hipFree(xch_fail);
         if (w1_lp) (void)hipFree(w1_lp);
         for (auto& tm : timer) {
             for (auto e : tm.ev0) (void)hipEventDestroy(e);
@@ -273,7 +283,9 @@ static void gather1_ids(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
 // embed_out the step is the forward alone (models.py:241-269 as called by
 // get_gnn_embeddings, utils.py:59-78): the last layer writes its [B, H]
 // embeddings straight into embed_out and nothing after the forward runs.
-static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
+static void top_pair_reserve(gs_trainer& t, int64_t B, hipStream_t st);
+
+int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_sizes, const int64_t* offsets,
                         const int32_t* roots, int64_t B, char* ws, int64_t ws_bytes, float* loss,
                         hipStream_t st, int a1_slot = -1, float* embed_out = nullptr) {
     const gs_trainer_config& c = T.cfg;
@@ -328,7 +340,11 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
     // the fused top path's dW_2 slabs outlive the layer-1 dW (their sum runs with layer 1's)
     const int64_t dw2_need = L == 2 ? gs_sage_linear_bwd_weight_ws(rows[1], T.w_cols[1], H) : 0;
     char* dw2_ws = dw2_need > 0 ? cv.take<char>(dw2_need) : nullptr;
-    float* dIn = cv.take<float>(dx_rows * (c.gcn ? H : 2 * H));
+    // the top launch's pair form writes dIn as two partials (dIn, then dIn + din2)
+    const bool pair = !embed_out && roots && T.fuse_bwd && T.use_top && T.opt_top_pair && L == 2 &&
+                      top_pair_supported(H, c.n_classes, c.gcn != 0);
+    const int64_t din2 = pair ? dx_rows * 2 * H : 0;
+    float* dIn = cv.take<float>(dx_rows * (c.gcn ? H : 2 * H) + din2);
     float* dbuf[2] = {cv.take<float>(dprev_rows * H), cv.take<float>(dprev_rows * H)};
     if (!ws) return cv.at + 256;
     GS_REQUIRE(cv.at <= ws_bytes, GS_EINVAL, "workspace too small");
@@ -479,10 +495,21 @@ static int64_t run_step(gs_trainer& T, const int32_t* pack, const int64_t* hop_s
             if (top) {
                 const bool armed = timed_arm(T, 3);
                 const bool tids = a1_slot >= 0 && T.top_ready[a1_slot];
-                cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
-                                       fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off, c.labels,
-                                       roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws, st,
-                                       tids ? T.top_slot[a1_slot] : nullptr, tids ? T.top_k : 0);
+                if (pair) {
+                    top_pair_reserve(T, B, st);
+                    cls_rows = top_pair_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
+                                                fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off,
+                                                c.labels, roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn,
+                                                dIn + din2, cls_ws, T.xch, ++T.xch_epoch == 0 ? ++T.xch_epoch : T.xch_epoch,
+                                                T.xch_fail, st, tids ? T.top_slot[a1_slot] : nullptr,
+                                                tids ? T.top_k : 0);
+                    lb[0].din_off2 = din2;
+                } else {
+                    cls_rows = top_fwd_bwd(c.agg, B, c.n_classes, h[0], fld(1, GS_PK_NBR_PTR), fld(1, GS_PK_NBR),
+                                           fld(1, GS_PK_SELF), P + T.w_off[1], P + T.cls_w_off, P + T.cls_b_off,
+                                           c.labels, roots, static_cast<float*>(agg[1]), am[1], h[1], demb, dIn, cls_ws,
+                                           st, tids ? T.top_slot[a1_slot] : nullptr, tids ? T.top_k : 0);
+                }
                 timed_done(T, 3, armed);
                 lb[0].din_ready = true;
             } else {
@@ -637,6 +664,23 @@ void trainer_set_upper_hook(gs_trainer* t, std::function<void(hipStream_t)> hook
 void trainer_set_w1_chunk_hook(gs_trainer* t, int chunks, std::function<void(hipStream_t, int64_t, int64_t)> hook) {
     t->w1_chunks = hook ? std::max(1, chunks) : 1;
     t->w1_chunk_hook = std::move(hook);
+}
+
+// the pair form's exchange buffer for batches of up to B roots (grown on
+// demand, zeroed on the stream when allocated) and its give-up flag
+void top_pair_reserve(gs_trainer& t, int64_t B, hipStream_t st) {
+    const int64_t words = top_pair_xch_words(B);
+    if (words > t.xch_quads) {
+        if (t.xch) GS_REQUIRE(hipFree(t.xch) == hipSuccess, GS_EHIP, "hipFree");
+        t.xch = nullptr;
+        GS_REQUIRE(hipMalloc(&t.xch, words * 8) == hipSuccess, GS_ENOMEM, "hipMalloc(top exchange)");
+        GS_REQUIRE(hipMemsetAsync(t.xch, 0, words * 8, st) == hipSuccess, GS_EHIP, "hipMemsetAsync");
+        t.xch_quads = words;
+    }
+    if (!t.xch_fail) {
+        GS_REQUIRE(hipMalloc(&t.xch_fail, 16) == hipSuccess, GS_ENOMEM, "hipMalloc(top exchange flag)");
+        GS_REQUIRE(hipMemsetAsync(t.xch_fail, 0, 16, st) == hipSuccess, GS_EHIP, "hipMemsetAsync");
+    }
 }
 
 void trainer_reserve_top(gs_trainer* t, int64_t B, int32_t tk) {
@@ -815,6 +859,7 @@ int gs_trainer_set_option(gs_trainer* t, int32_t opt, int32_t value) {
         case GS_TOPT_TOP_LAUNCH: t->use_top = on; break;
         case GS_TOPT_SELF_ROWS: t->want_self_rows = on; break;
         case GS_TOPT_DEFER_UPDATE: t->opt_defer = on; break;
+        case GS_TOPT_TOP_PAIR: t->opt_top_pair = on; break;
         default: GS_REQUIRE(false, GS_EINVAL, "unknown trainer option");
     }
     GS_API_END

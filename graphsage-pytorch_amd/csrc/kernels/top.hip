@@ -608,6 +608,408 @@ __global__ __launch_bounds__(kTopThreads) void sage_top_kernel(TopArgs a) {
     kstamp_end(a.stamp);
 }
 
+// ---------------------------------------------------------------- pair form
+// The same step on 2 blocks per 4 roots (lab form, C <= 16): block half hh
+// holds W2's rows 64·hh .. 64·hh + 63 (64 KB instead of 128), computes E's
+// columns of those rows, the logits' partial sums over them, dZ of those
+// columns and dIn's partial sum over those h; the two blocks of a pair (same
+// XCD: blocks b and b ^ 8) exchange the 4 x 16 partial logits as tagged
+// 8-byte granules (one write-through store each, relaxed agent-scope polls),
+// add them in a fixed order (half 0's + half 1's), and write dIn's two
+// partials to dIn (half 0) and dIn2 (half 1) for the consumer to add.
+struct TopPairArgs {
+    TopArgs a;
+    float* dIn2;                  // [B][2H]: half 1's dIn partial
+    unsigned long long* xch;      // granules [quads][2][64], zeroed once
+    unsigned epoch;               // this launch's tag (never 0, never repeated)
+    unsigned* fail;               // set when a poll gives up (the outputs are then wrong)
+};
+constexpr int kPairW = kTopH / 2;  // W2 rows / E columns per block
+
+template <int OP>
+__global__ __launch_bounds__(kTopThreads) void sage_top_pair_kernel(TopPairArgs pa) {
+    const TopArgs& a = pa.a;
+    constexpr int H = kTopH, K = kTopK, NT = kTopThreads, HW = kPairW, WP = kPairW + 4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sW2 = smem;                                               // [HW][K]
+    float (*sX)[K] = reinterpret_cast<float (*)[K]>(sW2 + HW * K);  // [rows][K]
+    float (*sE)[HW] = reinterpret_cast<float (*)[HW]>(sX[kTopRows]);
+    float (*sZ)[HW] = reinterpret_cast<float (*)[HW]>(sE[kTopRows]);
+    float* sP = &sZ[kTopRows][0];                                    // E: [8][rows][HW]; dIn: [4][rows][K]
+    float* sW = sP + 4 * kTopRows * K;                               // [C][WP] (this half's Wc columns)
+    float* sdl = sW + 16 * WP;                                       // [rows][C]
+    float* sloss = sdl + kTopRows * 16;
+    float* sb = sloss + kTopRows;
+    int* sy = reinterpret_cast<int*>(sb + 16);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int C = a.C;
+    const int bq = blockIdx.x, hh = (bq >> 3) & 1, q = (bq >> 4) * 8 + (bq & 7);
+    const int r0 = q * kTopRows;
+    if (r0 >= a.B) return;  // both halves of a quad past the batch leave together
+    const int nr = min(kTopRows, a.B - r0);
+    GS_TOP_STAMP(0);
+    kstamp_begin(a.stamp);
+    if (w >= 2)
+        for (int c = w - 2; c < HW; c += NT / 64 - 2)
+            __builtin_amdgcn_global_load_lds(a.W + static_cast<int64_t>(HW * hh + c) * K + 4 * (lane ^ (c & 15)),
+                                             sW2 + c * K, 16, 0, 0);
+    if (w >= 2) {
+        const int t2 = tid - 128;
+        if (t2 < kTopRows) sy[t2] = t2 < nr ? a.labels[a.roots[r0 + t2]] : 0;
+        else if (t2 >= 64 && t2 < 64 + C) sb[t2 - 64] = a.bc[t2 - 64];
+        for (int i = t2; i < C * (HW / 4); i += NT - 128) {  // this half's Wc quads
+            const int c = i / (HW / 4), j = 4 * (i % (HW / 4));
+            const float4 v = *reinterpret_cast<const float4*>(a.Wc + static_cast<int64_t>(c) * H + HW * hh + j);
+            *reinterpret_cast<float4*>(sW + c * WP + j) = v;
+        }
+    }
+    // ---- stage 1: sage_top_kernel's gather (padded records: one round)
+    float4 st_xs{}, st_av{};
+    int4 st_am{};
+    const int st_g = tid / 32, st_f0 = (tid % 32) * 4;
+    {
+        constexpr int G = 32, NR = 32;
+        const int g = tid / G, gl = tid % G;
+        if (g < nr) {
+            const int r = r0 + g;
+            const int f0 = gl * 4;
+            float acc[4];
+            int am[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                acc[v] = (OP == GS_AGG_MAX) ? -INFINITY : 0.f;
+                am[v] = -1;
+            }
+            int cnt = 0;
+            auto add_row = [&](int row, bool ok, const float (&x)[4]) {
+                cnt += ok;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    if (OP == GS_AGG_MEAN) {
+                        acc[v] += ok ? x[v] : 0.f;
+                    } else {
+                        const bool take = ok && x[v] > acc[v];
+                        acc[v] = take ? x[v] : acc[v];
+                        am[v] = take ? row : am[v];
+                    }
+                }
+            };
+            float4 xs;
+            if (a.tids) {
+                const int* rec = a.tids + static_cast<int64_t>(r) * (a.tk + 1);
+                const int v = gl <= a.tk ? rec[gl] : -1;
+                int* srec = reinterpret_cast<int*>(sP) + g * G;
+                srec[gl == 0 ? G - 1 : gl - 1] = gl <= a.tk ? v : -1;
+                const unsigned long long have = __ballot(gl >= 1 && gl <= a.tk && v >= 0);
+                const int sh = (tid & 63) & ~(G - 1);
+                const int m = __popcll((have >> sh) & ((1ull << G) - 1));
+                int rows[NR];
+                bool ok[NR];
+#pragma unroll
+                for (int qq = 0; qq < NR / 4; ++qq) {
+                    const int4 r4 = reinterpret_cast<const int4*>(srec)[qq];
+                    rows[4 * qq] = r4.x; rows[4 * qq + 1] = r4.y; rows[4 * qq + 2] = r4.z; rows[4 * qq + 3] = r4.w;
+                }
+                const int srow = rows[NR - 1];
+#pragma unroll
+                for (int u = 0; u < NR; ++u) ok[u] = u < m && rows[u] >= 0;
+                xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+                const int mw = max(__popcll(have & 0xffffffffull), __popcll(have >> 32));
+                float x[NR][4];
+#pragma unroll
+                for (int qq = 0; qq < NR / 8; ++qq)
+                    if (8 * qq < mw) {
+#pragma unroll
+                        for (int u = 8 * qq; u < 8 * qq + 8; ++u)
+                            RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : srow) * H + f0, x[u]);
+                    }
+                __builtin_amdgcn_sched_barrier(0);
+                int mwa = mw;
+                asm volatile("" : "+s"(mwa));
+#pragma unroll
+                for (int qq = 0; qq < NR / 8; ++qq)
+                    if (8 * qq < mwa) {
+#pragma unroll
+                        for (int u = 8 * qq; u < 8 * qq + 8; ++u) add_row(rows[u], ok[u], x[u]);
+                    }
+            } else {
+                const int srow = a.self[r];
+                const int beg = a.ptr[r], end = a.ptr[r + 1];
+                xs = *reinterpret_cast<const float4*>(a.Hprev + static_cast<int64_t>(srow) * H + f0);
+                for (int base = beg; base < end; base += G) {
+                    const int mm = min(G, end - base);
+                    const int my = gl < mm ? a.nbr[base + gl] : -1;
+                    int rows[NR];
+                    bool ok[NR];
+#pragma unroll
+                    for (int u = 0; u < NR; ++u) {
+                        rows[u] = __shfl(my, u < mm ? u : 0, G);
+                        ok[u] = u < mm && rows[u] >= 0;
+                    }
+                    const int fallback = rows[0] >= 0 ? rows[0] : 0;
+                    float x[NR][4];
+#pragma unroll
+                    for (int u = 0; u < NR; ++u)
+                        RowIO<float, 4>::load(a.Hprev + static_cast<int64_t>(ok[u] ? rows[u] : fallback) * H + f0, x[u]);
+#pragma unroll
+                    for (int u = 0; u < NR; ++u) add_row(rows[u], ok[u], x[u]);
+                }
+            }
+            if (OP == GS_AGG_MEAN) {
+                const float inv = 1.0f / static_cast<float>(cnt);
+#pragma unroll
+                for (int v = 0; v < 4; ++v) acc[v] *= inv;
+            }
+            *reinterpret_cast<float4*>(&sX[g][f0]) = xs;
+            const float4 av = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            *reinterpret_cast<float4*>(&sX[g][H + f0]) = av;
+            st_xs = xs;
+            st_av = av;
+            if (OP == GS_AGG_MAX) st_am = make_int4(am[0], am[1], am[2], am[3]);
+        } else if (g < kTopRows) {
+            *reinterpret_cast<float4*>(&sX[g][gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(&sX[g][H + gl * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    GS_TOP_STAMP(1);
+    if (w >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    GS_TOP_STAMP(2);
+    // ---- stage 2: E's 64 columns of this half; wave w: k eighth w (32 k)
+    {
+        const int kb = 32 * w;
+        const float4 xa = *reinterpret_cast<const float4*>(sX[lane & 3] + min(kb + 4 * (lane >> 2), K - 4));
+        const float* wrow = sW2 + lane * K;
+        float bv[32];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int qd = (kb >> 2) + m;
+            const float4 w4 = *reinterpret_cast<const float4*>(wrow + 4 * (qd ^ (lane & 15)));
+            bv[4 * m] = w4.x; bv[4 * m + 1] = w4.y; bv[4 * m + 2] = w4.z; bv[4 * m + 3] = w4.w;
+        }
+        if (hh == 0 && st_g < nr) {  // stage 1's global stores (half 0 owns them)
+            const int64_t r = r0 + st_g;
+            *reinterpret_cast<float4*>(a.agg + r * K + st_f0) = st_xs;
+            *reinterpret_cast<float4*>(a.agg + r * K + H + st_f0) = st_av;
+            if (OP == GS_AGG_MAX) *reinterpret_cast<int4*>(a.argmax + r * H + st_f0) = st_am;
+        }
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#define GS_PE_STEP(b)                                    \
+        c0 = mfma4b<b>(xa.x, bv[4 * (b)], c0);           \
+        c1 = mfma4b<b>(xa.y, bv[4 * (b) + 1], c1);       \
+        c0 = mfma4b<b>(xa.z, bv[4 * (b) + 2], c0);       \
+        c1 = mfma4b<b>(xa.w, bv[4 * (b) + 3], c1);
+        GS_PE_STEP(0) GS_PE_STEP(1) GS_PE_STEP(2) GS_PE_STEP(3) GS_PE_STEP(4) GS_PE_STEP(5) GS_PE_STEP(6) GS_PE_STEP(7)
+#undef GS_PE_STEP
+        float* pp = sP + w * (kTopRows * HW);
+#pragma unroll
+        for (int j = 0; j < kTopRows; ++j) pp[j * HW + lane] = c0[j] + c1[j];
+    }
+    lds_barrier();
+    GS_TOP_STAMP(3);
+    if (tid < kTopRows * HW) {
+        const int row = tid >> 6, col = tid & (HW - 1);
+        float e = sP[row * HW + col];
+#pragma unroll
+        for (int qq = 1; qq < 8; ++qq) e += sP[qq * (kTopRows * HW) + row * HW + col];
+        e = (!(e > 0.f) && e == e) ? 0.f : e;
+        sE[row][col] = e;
+        if (row < nr) a.E[static_cast<int64_t>(r0 + row) * H + HW * hh + col] = e;
+    }
+    lds_barrier();
+    GS_TOP_STAMP(4);
+    // ---- stage 3: partial logits over this half's 64 d, exchanged with the
+    // pair's other block, then the loss head on the sums (half 0's + half 1's)
+    const float invB = 1.0f / static_cast<float>(a.B);
+    if (w < kTopRows) {
+        const int row = w, c = lane >> 2, part = lane & 3;
+        const bool cv = c < C;
+        const float* e = sE[row] + 16 * part;
+        const float* wr = sW + min(c, C - 1) * WP + 16 * part;
+        float z = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; t += 4) {
+            const float4 e4 = *reinterpret_cast<const float4*>(e + t);
+            const float4 w4 = *reinterpret_cast<const float4*>(wr + t);
+            z = fmaf(e4.x, w4.x, z);
+            z = fmaf(e4.y, w4.y, z);
+            z = fmaf(e4.z, w4.z, z);
+            z = fmaf(e4.w, w4.w, z);
+        }
+        z += dpp_f<0xB1>(z);
+        z += dpp_f<0x4E>(z);
+        typedef __attribute__((address_space(1))) unsigned long long gu64;
+        gu64* mine = (gu64*)(pa.xch + (static_cast<int64_t>(q) * 2 + hh) * 64 + row * 16 + c);
+        gu64* theirs = (gu64*)(pa.xch + (static_cast<int64_t>(q) * 2 + (hh ^ 1)) * 64 + row * 16 + c);
+        if (part == 0)
+            __hip_atomic_store(mine, (static_cast<unsigned long long>(pa.epoch) << 32) | __float_as_uint(z),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long x = 0;
+        for (unsigned spins = 0;; ++spins) {
+            x = __hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(static_cast<unsigned>(x >> 32) == pa.epoch)) break;
+            if (spins > (1u << 18)) {  // the partner never came: flag it, poison the outputs (bounded wait)
+                if (lane == 0) atomicOr(pa.fail, 1u);
+                x = 0x7fc00000ull;  // NaN: the loss, dZ and dIn turn NaN
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const float zo = __uint_as_float(static_cast<unsigned>(x));
+        const float zs = hh == 0 ? z + zo : zo + z;  // half 0's partial first in both blocks
+        const float zl = cv ? zs + sb[min(c, C - 1)] : -INFINITY;
+        const float mx = wave_max(zl);
+        const float lse = logf(wave_sum(cv && part == 0 ? expf(zl - mx) : 0.f));
+        if (part == 0 && cv) {
+            if (row < nr) {
+                const int y = sy[row];
+                const float lp = zl - mx - lse;
+                if (c == y) sloss[row] = -lp;
+                sdl[row * C + c] = (expf(lp) - (c == y ? 1.f : 0.f)) * invB;
+            } else {
+                sdl[row * C + c] = 0.f;
+            }
+        }
+    }
+    lds_barrier();
+    GS_TOP_STAMP(6);
+    // ---- dZ of this half's 64 columns (waves 0..3) beside its slab columns (waves 4..7)
+    if (w < 4) {
+        const int row = w, d = lane;
+        float g[16], v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int uc = min(u, C - 1);
+            g[u] = sdl[row * C + uc];
+            v[u] = sW[uc * WP + d];
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s = u < C ? fmaf(g[u], v[u], s) : s;
+        if (!(sE[row][d] > 0.f)) s = 0.f;
+        sZ[row][d] = s;
+        if (row < nr) a.dZ[static_cast<int64_t>(r0 + row) * H + HW * hh + d] = s;
+    } else {
+        const int tt = tid - 256, c = tt >> 4;
+        const int per = C * (H + 1);
+        float* out = a.slab + static_cast<int64_t>(q) * (per + 1);
+        if (c < C) {
+            float dl[kTopRows], ev[kTopRows][HW / 16];
+#pragma unroll
+            for (int ii = 0; ii < kTopRows; ++ii) {
+                dl[ii] = sdl[ii * C + c];
+#pragma unroll
+                for (int j = 0; j < HW / 16; ++j) ev[ii][j] = sE[ii][(tt & 15) + 16 * j];
+            }
+#pragma unroll
+            for (int j = 0; j < HW / 16; ++j) {
+                float sv = 0.f;
+#pragma unroll
+                for (int ii = 0; ii < kTopRows; ++ii) sv = ii < nr ? fmaf(dl[ii], ev[ii][j], sv) : sv;
+                out[c * (H + 1) + HW * hh + (tt & 15) + 16 * j] = sv;
+            }
+            if (hh == 0 && (tt & 15) == 0) {
+                float sbias = 0.f;
+#pragma unroll
+                for (int ii = 0; ii < kTopRows; ++ii) sbias = ii < nr ? fmaf(dl[ii], 1.f, sbias) : sbias;
+                out[c * (H + 1) + H] = sbias;
+            }
+        }
+        if (hh == 0 && tid == NT - 64) {
+            float sl = 0.f;
+            for (int ii = 0; ii < nr; ++ii) sl += sloss[ii];
+            out[per] = sl;
+        }
+    }
+    lds_barrier();
+    GS_TOP_STAMP(7);
+    // ---- dIn's partial over this half's 64 h: wave w: input columns
+    // 128 (w & 1) + 2 lane, + 1; h quarter w >> 1 (16 h); dZ by ABID broadcast
+    {
+        const int k0 = 128 * (w & 1) + 2 * lane, hb = 16 * (w >> 1);
+        const float4 za = *reinterpret_cast<const float4*>(sZ[lane & 3] + min(hb + 4 * (lane >> 2), HW - 4));
+        float2 wv[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int h = hb + t;
+            wv[t] = *reinterpret_cast<const float2*>(sW2 + h * K + 4 * ((k0 >> 2) ^ (h & 15)) + (k0 & 3));
+        }
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#define GS_PD_STEP(b)                                    \
+        c0 = mfma4b<b>(za.x, wv[4 * (b)].x, c0);         \
+        c1 = mfma4b<b>(za.x, wv[4 * (b)].y, c1);         \
+        c0 = mfma4b<b>(za.y, wv[4 * (b) + 1].x, c0);     \
+        c1 = mfma4b<b>(za.y, wv[4 * (b) + 1].y, c1);     \
+        c0 = mfma4b<b>(za.z, wv[4 * (b) + 2].x, c0);     \
+        c1 = mfma4b<b>(za.z, wv[4 * (b) + 2].y, c1);     \
+        c0 = mfma4b<b>(za.w, wv[4 * (b) + 3].x, c0);     \
+        c1 = mfma4b<b>(za.w, wv[4 * (b) + 3].y, c1);
+        GS_PD_STEP(0) GS_PD_STEP(1) GS_PD_STEP(2) GS_PD_STEP(3)
+#undef GS_PD_STEP
+        float* pp = sP + (w >> 1) * (kTopRows * K);
+#pragma unroll
+        for (int j = 0; j < kTopRows; ++j) *reinterpret_cast<float2*>(pp + j * K + k0) = make_float2(c0[j], c1[j]);
+    }
+    lds_barrier();
+    GS_TOP_STAMP(8);
+    float* dst = hh == 0 ? a.dIn : pa.dIn2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int o = tid + u * NT, row = o >> 8, kc = o & (K - 1);
+        const float v = ((sP[row * K + kc] + sP[kTopRows * K + row * K + kc]) + sP[2 * kTopRows * K + row * K + kc]) +
+                        sP[3 * kTopRows * K + row * K + kc];
+        if (row < nr) dst[static_cast<int64_t>(r0 + row) * K + kc] = v;
+    }
+    GS_TOP_STAMP(9);
+    kstamp_end(a.stamp);
+}
+
+static size_t top_pair_smem_bytes() {
+    return sizeof(float) * (static_cast<size_t>(kPairW) * kTopK + kTopRows * kTopK + 2 * kTopRows * kPairW +
+                            4 * kTopRows * kTopK + 16 * (kPairW + 4) + kTopRows * 16 + kTopRows + 16 + kTopRows);
+}
+
+static bool top_pair_lds_ready() {
+    static int ok = -1;
+    if (ok < 0) {
+        const int smem = static_cast<int>(top_pair_smem_bytes());
+        ok = hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_pair_kernel<GS_AGG_MEAN>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess &&
+             hipFuncSetAttribute(reinterpret_cast<const void*>(sage_top_pair_kernel<GS_AGG_MAX>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, smem) == hipSuccess;
+        (void)hipGetLastError();
+    }
+    return ok == 1;
+}
+
+bool top_pair_supported(int64_t H, int64_t C, bool gcn) {
+    return H == kTopH && C >= 1 && C <= 16 && !gcn && top_pair_lds_ready();
+}
+
+int top_pair_fwd_bwd(int agg, int64_t B, int64_t C, const float* Hprev, const int32_t* ptr, const int32_t* nbr,
+                     const int32_t* self, const float* W, const float* Wc, const float* bc, const int32_t* labels,
+                     const int32_t* roots, float* aggo, int32_t* argmax, float* E, float* dZ, float* dIn, float* dIn2,
+                     float* slab, unsigned long long* xch, unsigned epoch, unsigned* fail, hipStream_t st,
+                     const int32_t* tids, int tk) {
+    GS_REQUIRE(B >= 1 && B < (int64_t(1) << 30) && C >= 1 && C <= 16 && epoch != 0 && xch && fail, GS_EINVAL,
+               "top pair: bad arguments");
+    GS_REQUIRE(!tids || (tk >= 1 && tk <= 31), GS_EINVAL, "top: padded lists need 1 <= tk <= 31");
+    GS_REQUIRE(aligned16(Hprev) && aligned16(W) && aligned16(Wc) && aligned16(aggo) && aligned16(E) && aligned16(dZ) &&
+                   aligned16(dIn) && aligned16(dIn2) && (agg == GS_AGG_MEAN || (argmax && aligned16(argmax))),
+               GS_EINVAL, "top pair: unaligned operand");
+    GS_REQUIRE(top_pair_lds_ready(), GS_EHIP, "top pair: LDS limit refused");
+    const size_t smem = top_pair_smem_bytes();
+    TopPairArgs pa{TopArgs{static_cast<int>(B), static_cast<int>(C), Hprev, ptr, nbr, self, W, Wc, bc, labels, roots,
+                           aggo, argmax, E, dZ, dIn, slab, tids, tids ? tk : 0, take_kernel_stamp()},
+                   dIn2, xch, epoch, fail};
+    const int64_t quads = (B + kTopRows - 1) / kTopRows;
+    const dim3 grid(static_cast<unsigned>(16 * ((quads + 7) / 8)));
+    if (agg == GS_AGG_MEAN) launch_k(sage_top_pair_kernel<GS_AGG_MEAN>, grid, dim3(kTopThreads), smem, st, pa);
+    else launch_k(sage_top_pair_kernel<GS_AGG_MAX>, grid, dim3(kTopThreads), smem, st, pa);
+    check_launch("sage_top_pair");
+    return static_cast<int>(quads);
+}
+
 static size_t top_smem_bytes(int64_t C) {
     const int64_t wp = C <= 16 ? kTopH + 4 : kTopH + 1;  // sage_top_kernel's WP
     const int64_t q3 = C <= 16 ? kTopRows + 3 + kTopRows * kTopK : 0;  // its fourth dIn partial (16-B aligned)

@@ -129,13 +129,16 @@ class NativeTrainer:
         return out
 
     _OPTIONS = {"fused_bwd": _lib.GS_TOPT_FUSED_BWD, "top_launch": _lib.GS_TOPT_TOP_LAUNCH,
-                "self_rows": _lib.GS_TOPT_SELF_ROWS, "defer_update": _lib.GS_TOPT_DEFER_UPDATE}
+                "self_rows": _lib.GS_TOPT_SELF_ROWS, "defer_update": _lib.GS_TOPT_DEFER_UPDATE,
+                "top_pair": _lib.GS_TOPT_TOP_PAIR}
 
     def set_option(self, name, value):
         """gs_trainer_set_option: switch an alternative of the step (fused_bwd,
-        top_launch, self_rows, defer_update; default all on).  fused_bwd,
-        self_rows and defer_update are bitwise the default; top_launch matches
-        it within fp32 rounding of its split-K order."""
+        top_launch, self_rows, defer_update, top_pair; default all on except
+        top_pair).
+        fused_bwd, self_rows and defer_update are bitwise the default;
+        top_launch and top_pair match it within fp32 rounding of their
+        split-K orders."""
         check(lib().gs_trainer_set_option(self._h, self._OPTIONS[name], int(bool(value))))
         return self
 

@@ -598,15 +598,20 @@ int64_t gs_trainer_captured(const gs_trainer* t);
  * update runs at once.  Not inside a runner loop. */
 int gs_trainer_defer(gs_trainer* t, int32_t on, int32_t* active, void* stream);
 /* Trainer options (gs_trainer_set_option, value 0 / 1; not inside a runner
- * loop).  Each alternative exists for the tests that compare it with the
- * default.  fused_bwd, self_rows and defer_update compute bitwise the
+ * loop; all default 1 except GS_TOPT_TOP_PAIR, default 0).  Each alternative
+ * exists for the tests that compare it with the default.  fused_bwd, self_rows and defer_update compute bitwise the
  * default's results; top_launch matches them within fp32 rounding of the
  * k order (its split-K partial sums are added in a fixed, different order):
  *   GS_TOPT_FUSED_BWD     1: layers >= 2 backward in fused launches
  *   GS_TOPT_TOP_LAUNCH    1: a 2-layer step's layer 2 + loss head + dIn2 in one launch
  *   GS_TOPT_SELF_ROWS     1: gather slots hold [self | agg] rows (next gs_trainer_gather_reserve)
- *   GS_TOPT_DEFER_UPDATE  1: runner loops defer each step's clip + SGD into the next step */
-enum { GS_TOPT_FUSED_BWD = 0, GS_TOPT_TOP_LAUNCH = 1, GS_TOPT_SELF_ROWS = 2, GS_TOPT_DEFER_UPDATE = 3 };
+ *   GS_TOPT_DEFER_UPDATE  1: runner loops defer each step's clip + SGD into the next step
+ *   GS_TOPT_TOP_PAIR      1: the top launch on two blocks per 4 roots (<= 16 classes), each with
+ *                         half of W2, the partial logits exchanged in the launch; within fp32
+ *                         rounding of the one-block form, deterministic; default 0 (the
+ *                         layer-2 backward then adds two dIn partials: neutral per step) */
+enum { GS_TOPT_FUSED_BWD = 0, GS_TOPT_TOP_LAUNCH = 1, GS_TOPT_SELF_ROWS = 2, GS_TOPT_DEFER_UPDATE = 3,
+       GS_TOPT_TOP_PAIR = 4 };
 int gs_trainer_set_option(gs_trainer* t, int32_t opt, int32_t value);
 
 /* ------------------------------------------------------- RCCL communicator

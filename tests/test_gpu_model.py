@@ -556,6 +556,45 @@ def test_native_runner_matches_python_loop_edge_shapes(gs, classes, fan, agg):
     runner.close()
 
 
+@pytest.mark.parametrize("agg,B,classes", [("MEAN", 512, 16), ("MAX", 97, 16), ("MEAN", 130, 7)])
+def test_top_pair_matches_one_block(gs, agg, B, classes):
+    """The top launch's pair form (two blocks per 4 roots, half of W2 each,
+    the partial logits exchanged inside the launch, dIn as two partials the
+    layer-2 backward adds) against the one-block form: loss, gradients and
+    updated parameters within fp32 rounding of the k order, ragged batches
+    and MAX included (a pair whose exchange gave up would turn them NaN)."""
+    graph, g, n = _graph(gs, "pubmed")
+    X = torch.from_numpy(uniform_features(3, n, 256)).to(DEV)
+    labels = torch.from_numpy((np.arange(n) % classes).astype(np.int32)).to(DEV)
+    a = train.NativeTrainer(graph, X, labels, classes, num_layers=2, fanouts=[25, 10], agg_func=agg, seed=824)
+    b = train.NativeTrainer(graph, X, labels, classes, num_layers=2, fanouts=[25, 10], agg_func=agg, seed=824)
+    a.set_option("top_pair", True)
+    b.set_option("top_pair", False)
+    rng = gs.RNG(11)
+    done = 0
+    for roots in train.rank_batches(np.nonzero(graph.degrees())[0], B, 0, 1, 29):
+        if done == 3:
+            break
+        s = gs.sample(graph, rng, roots, [25, 10])
+        if agg == "MAX" and any(s.n_empty(j) for j in range(1, 3)):
+            continue
+        ds = models.DeviceSample(s, DEV)
+        r = torch.from_numpy(roots.astype(np.int32)).to(DEV)
+        la = a.forward_backward(ds, r).clone()
+        lb = b.forward_backward(ds, r).clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(la).all() and torch.isfinite(a.p.grads).all()
+        torch.testing.assert_close(la, lb, atol=1e-6, rtol=1e-5)
+        torch.testing.assert_close(a.p.grads, b.p.grads, atol=1e-7, rtol=1e-5)
+        a.apply_update()
+        b.apply_update()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(a.p.params, b.p.params, atol=1e-7, rtol=1e-5)
+        b.p.params.copy_(a.p.params)
+        done += 1
+    assert done >= 1
+
+
 def test_top_launch_is_deterministic(gs):
     """The top launch's split-K partial sums are added in a fixed order: two
     trainers on the same batches leave bitwise the same loss, gradients and
