@@ -120,8 +120,10 @@ struct RawVec<bf16_t, 8> {
 // row together — written straight-line, with no loop around the loads (the
 // general form's loops had the compiler drain the self row's load before the
 // id load and split the rows into two waits: five dependent rounds).  Same
-// rows, same order of adds: bitwise the general form.
-template <int OP, typename T, int VEC, int G, bool SELF, bool ONE>
+// rows, same order of adds: bitwise the general form.  NR1: the row loads of
+// that form, k rounded up to a multiple of 4 (the adds run in chunks of 4 up
+// to k, so rows loaded past that chunk were never added).
+template <int OP, typename T, int VEC, int G, bool SELF, bool ONE, int NR1 = kRows>
 __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X, int64_t ldx, int F, int n_dst, int k,
                                                          const int* __restrict__ ids, const int* __restrict__ dst_ids,
                                                          int gcn, T* __restrict__ out, int64_t ldo,
@@ -129,7 +131,8 @@ __global__ __launch_bounds__(kBlock) void agg_ids_kernel(const T* __restrict__ X
     const int gl = threadIdx.x % G;
     if constexpr (ONE) {
         using Raw = typename RawVec<T, VEC>::type;
-        constexpr int NR = kRows;
+        constexpr int NR = NR1;
+        static_assert(NR % 4 == 0 && NR <= kRows, "row loads: whole chunks of 4");
         const int r = blockIdx.x * (kBlock / G) + threadIdx.x / G;
         if (r >= n_dst) return;
         const int f0 = gl * VEC;
@@ -307,17 +310,26 @@ void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t 
                      (!self_out || (ldso % V == 0 && aligned16(self_out)));
     const int f = static_cast<int>(F), n = static_cast<int>(n_dst);
     static const int cap = agg_ids_block_cap();
-#define GS_IDS1(OPV, TT, VV, GG, ONE)                                                                            \
+#define GS_IDS2(OPV, TT, VV, GG, ONE, NRV)                                                                       \
     do {                                                                                                         \
         const dim3 grid_(std::min((n + (kBlock / GG) - 1) / (kBlock / GG), cap));                                \
         if (self_out)                                                                                            \
-            launch_k(agg_ids_kernel<OPV, TT, VV, GG, true, ONE>, grid_, dim3(kBlock), 0, st,                     \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, true, ONE, NRV>, grid_, dim3(kBlock), 0, st,                \
                      static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo,      \
                      static_cast<TT*>(self_out), ldso);                                                          \
         else                                                                                                     \
-            launch_k(agg_ids_kernel<OPV, TT, VV, GG, false, ONE>, grid_, dim3(kBlock), 0, st,                    \
+            launch_k(agg_ids_kernel<OPV, TT, VV, GG, false, ONE, NRV>, grid_, dim3(kBlock), 0, st,               \
                      static_cast<const TT*>(X), ldx, f, n, k, ids, dst_ids, gcn, static_cast<TT*>(out), ldo,      \
                      static_cast<TT*>(nullptr), ldso);                                                           \
+    } while (0)
+    // the one-pass form loads k rounded up to 4 rows (a 10-neighbour hop: 12, not 16)
+#define GS_IDS1(OPV, TT, VV, GG, ONE)                                                                            \
+    do {                                                                                                         \
+        if (!(ONE)) GS_IDS2(OPV, TT, VV, GG, false, kRows);                                                      \
+        else if (k <= 4) GS_IDS2(OPV, TT, VV, GG, true, 4);                                                      \
+        else if (k <= 8) GS_IDS2(OPV, TT, VV, GG, true, 8);                                                      \
+        else if (k <= 12) GS_IDS2(OPV, TT, VV, GG, true, 12);                                                    \
+        else GS_IDS2(OPV, TT, VV, GG, true, kRows);                                                              \
     } while (0)
     // one lane group per destination (no grid cap), one vector per lane, at
     // most kRows ids, no gcn: the two-round form
@@ -349,6 +361,7 @@ void agg_ids_launch(gs_agg op, gs_dtype dt, const void* X, int64_t ldx, int64_t 
 #undef GS_IDS_T
 #undef GS_IDS
 #undef GS_IDS1
+#undef GS_IDS2
     check_launch("agg_ids");
 }
 

@@ -139,17 +139,16 @@ __global__ __launch_bounds__(kBlock) void agg_fwd_kernel(
 // Backward over source rows c (transposed neighbourhood lists, GS_PK_TIDX
 // encoding): self-row gradient + mean/max routing, then the relu mask of the
 // layer that produced these rows.  Fixed order, no atomics.
-template <int OP, int VEC, int G>
+template <int OP, int VEC, int G, bool PAIR = false>
 __device__ __forceinline__ void agg_bwd_body(
     int bx, int n_src, int F, const int* __restrict__ tptr, const int* __restrict__ tidx,
     const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
     int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
     float* __restrict__ dH, int64_t off2 = 0) {
-    // off2 != 0: the input gradient arrives as two partial sums (the top
-    // launch's pair form), the second off2 floats past the first; each row is
-    // their sum, first + second (the second load re-reads the first's row
-    // when off2 == 0 and is not used)
-    const bool pair = off2 != 0;
+    // PAIR: the input gradient arrives as two partial sums (the top launch's
+    // pair form), the second off2 floats past the first; each row is their
+    // sum, first + second (a separate instance: no second loads otherwise)
+    constexpr bool pair = PAIR;
     const int gl = threadIdx.x % G;
     const int c = bx * (kBlock / G) + threadIdx.x / G;
     if (c >= n_src) return;
@@ -178,7 +177,7 @@ __device__ __forceinline__ void agg_bwd_body(
                 const int row = self_e ? -eu - 1 : eu;
                 const float* src = (self_e && dSelf) ? dSelf : dA;
                 RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
-                RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
+                if constexpr (PAIR) RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
                 if (OP == GS_AGG_MEAN) {
                     const int re = self_e ? 0 : eu;
                     w[u] = 1.0f / static_cast<float>(ptr[re + 1] - ptr[re]);
@@ -219,18 +218,18 @@ __device__ __forceinline__ void agg_bwd_body(
             if (e < 0) {
                 if (!dSelf) continue;  // gcn: self rows feed no linear input
                 RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0, x);
-                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0 + off2, x2);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-e - 1) * ldd + f0 + off2, x2);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) g[v] += pair ? x[v] + x2[v] : x[v];
             } else if (OP == GS_AGG_MEAN) {
                 const float w = 1.0f / static_cast<float>(ptr[e + 1] - ptr[e]);
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) g[v] += (pair ? x[v] + x2[v] : x[v]) * w;
             } else {
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0, x);
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dA + static_cast<int64_t>(e) * ldd + f0 + off2, x2);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v)
                     if (argmax[static_cast<int64_t>(e) * F + f0 + v] == c) g[v] += pair ? x[v] + x2[v] : x[v];
@@ -256,13 +255,13 @@ __device__ __forceinline__ void agg_bwd_body(
 // (hub rows) follow one at a time from tidx.  Entries are added in list order
 // with agg_bwd_body's expressions: bitwise its result.
 constexpr int kTrec = 6;  // entries inline in a record
-template <int OP, int VEC, int G>
+template <int OP, int VEC, int G, bool PAIR = false>
 __device__ __forceinline__ void agg_bwd_rec_body(
     int bx, int n_src, int F, const int4* __restrict__ rec, const int* __restrict__ tidx,
     const int* __restrict__ ptr, const float* __restrict__ dA, const float* __restrict__ dSelf,
     int64_t ldd, const int* __restrict__ argmax, const float* __restrict__ Hprev, int64_t ldh,
     float* __restrict__ dH, int64_t off2 = 0) {
-    const bool pair = off2 != 0;  // two partial input gradients (agg_bwd_body)
+    constexpr bool pair = PAIR;  // two partial input gradients (agg_bwd_body)
     const int gl = threadIdx.x % G;
     const int c = bx * (kBlock / G) + threadIdx.x / G;
     if (c >= n_src) return;
@@ -286,7 +285,7 @@ __device__ __forceinline__ void agg_bwd_rec_body(
             const int row = self_e ? -eu - 1 : eu;
             const float* src = (self_e && dSelf) ? dSelf : dA;
             RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c, x[u]);
-            RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
+            if constexpr (PAIR) RowIO<float, VEC>::load(src + static_cast<int64_t>(row) * ldd + f0c + off2, y[u]);
             if (OP == GS_AGG_MEAN) {
                 const int re = self_e ? 0 : eu;
                 pa[u] = ptr[re];
@@ -330,18 +329,18 @@ __device__ __forceinline__ void agg_bwd_rec_body(
             if (et < 0) {
                 if (!dSelf) continue;
                 RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0, xt);
-                RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0 + off2, yt);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dSelf + static_cast<int64_t>(-et - 1) * ldd + f0 + off2, yt);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) g[v] += pair ? xt[v] + yt[v] : xt[v];
             } else if (OP == GS_AGG_MEAN) {
                 const float wt = 1.0f / static_cast<float>(ptr[et + 1] - ptr[et]);
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v) g[v] += (pair ? xt[v] + yt[v] : xt[v]) * wt;
             } else {
                 RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0, xt);
-                RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
+                if constexpr (PAIR) RowIO<float, VEC>::load(dA + static_cast<int64_t>(et) * ldd + f0 + off2, yt);
 #pragma unroll
                 for (int v = 0; v < VEC; ++v)
                     if (argmax[static_cast<int64_t>(et) * F + f0 + v] == c) g[v] += pair ? xt[v] + yt[v] : xt[v];

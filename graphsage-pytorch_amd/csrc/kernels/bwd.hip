@@ -64,14 +64,14 @@ struct BwdB {
     int64_t off2 = 0;           // dIn as two partials (the top launch's pair form), the second off2 floats on
 };
 
-template <int OP, int G>
+template <int OP, int G, bool PAIR>
 __global__ __launch_bounds__(kThreads) void layer_bwd_b_kernel(BwdB b) {
     const int bx = blockIdx.x;
     if (bx < b.sum_nb) {
         sum_slabs_body(bx, b.sum_nb, b.slabs, b.S, b.len, b.dW, b.part);
         return;
     }
-    agg_bwd_body<OP, 4, G>(bx - b.sum_nb, b.n_src, b.F, b.tptr, b.tidx, b.ptr, b.dA, b.dSelf, b.ldd, b.argmax,
+    agg_bwd_body<OP, 4, G, PAIR>(bx - b.sum_nb, b.n_src, b.F, b.tptr, b.tidx, b.ptr, b.dA, b.dSelf, b.ldd, b.argmax,
                            b.Hprev, b.F, b.dH, b.off2);
 }
 
@@ -81,7 +81,7 @@ struct BwdT {
     int cls_nb;
 };
 
-template <int OP, int G>
+template <int OP, int G, bool PAIR>
 __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
     int b = blockIdx.x;
     if (b < t.a.dw_nb) {
@@ -100,10 +100,10 @@ __global__ __launch_bounds__(kThreads) void layer_bwd_top_kernel(BwdT t) {
     }
     b -= t.cls_nb;
     if (t.b.rec)
-        agg_bwd_rec_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.rec, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
+        agg_bwd_rec_body<OP, 4, G, PAIR>(b, t.b.n_src, t.b.F, t.b.rec, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
                                    t.b.argmax, t.b.Hprev, t.b.F, t.b.dH, t.b.off2);
     else
-        agg_bwd_body<OP, 4, G>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
+        agg_bwd_body<OP, 4, G, PAIR>(b, t.b.n_src, t.b.F, t.b.tptr, t.b.tidx, t.b.ptr, t.b.dA, t.b.dSelf, t.b.ldd,
                                t.b.argmax, t.b.Hprev, t.b.F, t.b.dH, t.b.off2);
 }
 
@@ -194,15 +194,17 @@ int layer_bwd(const LayerBwd& a, const ClsReduce* cls, float* part, hipStream_t 
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
     const dim3 gb(static_cast<unsigned>(Bq.sum_nb + agg_nb));
-#define GS_BWDB(OP)                                                                         \
+#define GS_BWDB2(OP, PR)                                                                    \
     do {                                                                                    \
-        if (G == 16) layer_bwd_b_kernel<OP, 16><<<gb, kThreads, 0, st>>>(Bq);               \
-        else if (G == 32) layer_bwd_b_kernel<OP, 32><<<gb, kThreads, 0, st>>>(Bq);          \
-        else layer_bwd_b_kernel<OP, 64><<<gb, kThreads, 0, st>>>(Bq);                       \
+        if (G == 16) layer_bwd_b_kernel<OP, 16, PR><<<gb, kThreads, 0, st>>>(Bq);           \
+        else if (G == 32) layer_bwd_b_kernel<OP, 32, PR><<<gb, kThreads, 0, st>>>(Bq);      \
+        else layer_bwd_b_kernel<OP, 64, PR><<<gb, kThreads, 0, st>>>(Bq);                   \
     } while (0)
+#define GS_BWDB(OP) do { if (Bq.off2) GS_BWDB2(OP, true); else GS_BWDB2(OP, false); } while (0)
     if (a.agg == GS_AGG_MEAN) GS_BWDB(GS_AGG_MEAN);
     else GS_BWDB(GS_AGG_MAX);
 #undef GS_BWDB
+#undef GS_BWDB2
     check_launch("layer_bwd(B)");
     return Bq.sum_nb;
 }
@@ -257,15 +259,17 @@ int layer_bwd_top(const LayerBwd& a, const ClsReduce& cls, SlabSum* deferred, hi
     const int G = pick_group(static_cast<int>(a.H), 4);
     const int agg_nb = static_cast<int>((a.n_src + (kBlock / G) - 1) / (kBlock / G));
     const dim3 grid(static_cast<unsigned>(A.dw_nb + t.cls_nb + agg_nb));
-#define GS_BWDT(OP)                                                                     \
+#define GS_BWDT2(OP, PR)                                                                \
     do {                                                                                \
-        if (G == 16) layer_bwd_top_kernel<OP, 16><<<grid, kThreads, 0, st>>>(t);        \
-        else if (G == 32) layer_bwd_top_kernel<OP, 32><<<grid, kThreads, 0, st>>>(t);   \
-        else layer_bwd_top_kernel<OP, 64><<<grid, kThreads, 0, st>>>(t);                \
+        if (G == 16) layer_bwd_top_kernel<OP, 16, PR><<<grid, kThreads, 0, st>>>(t);    \
+        else if (G == 32) layer_bwd_top_kernel<OP, 32, PR><<<grid, kThreads, 0, st>>>(t); \
+        else layer_bwd_top_kernel<OP, 64, PR><<<grid, kThreads, 0, st>>>(t);            \
     } while (0)
+#define GS_BWDT(OP) do { if (t.b.off2) GS_BWDT2(OP, true); else GS_BWDT2(OP, false); } while (0)
     if (a.agg == GS_AGG_MEAN) GS_BWDT(GS_AGG_MEAN);
     else GS_BWDT(GS_AGG_MAX);
 #undef GS_BWDT
+#undef GS_BWDT2
     check_launch("layer_bwd_top");
     *deferred = SlabSum{a.slabs, S, a.H * K, a.dW, nullptr};
     return S > 1 ? sum_slabs_pair_parts2(a.H * K) : 0;
