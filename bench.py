@@ -12,8 +12,10 @@ timed steps (weak scaling: B roots per GPU per step).
 
 Prints ONE JSON line on rank 0.  `roofline` prices the dominant kernel (the
 largest average in the committed rocprofv3 summary of the config: the layer-1
-forward GEMM at fp32, the top launch at bf16) from its algorithmic flops or
-bytes and its launch duration inside the timed region: the kernel's own span
+forward GEMM at fp32, the dW GEMM at bf16) from its algorithmic flops or bytes
+against the peak of the MFMA it issues (the bf16 dW widens its operands to
+fp32: fp32 peak, the bf16 peak and fraction beside it) and its launch duration
+inside the timed region: the kernel's own span
 (per-workgroup s_memrealtime stamps, min start .. max end) for the forward
 and top launches, kernel-bound HIP events for the gather and dW;
 `cpu_baseline` times the oracle (the CPU restatement of the reference's
@@ -920,8 +922,17 @@ def main():
                 peak, unit, bound, scale = HBM_PEAK_GBS, "GB/s", "hbm", float(nb) / 1e9
                 work = {"algo_bytes_per_launch": int(nb)}
             else:
-                peak, unit, bound, scale = MFMA_PEAK_TFS[cfg["dtype"]], "TFLOP/s", "mfma", gemm_flops / 1e12
-                work = {"algo_flops_per_launch": int(gemm_flops)}
+                # the peak of the MFMA the kernel issues: the forward runs the config
+                # dtype's MFMA (bf16 16x16x32 for bf16 features); the dW GEMM widens
+                # bf16 operands to fp32 and runs the fp32 16x16x4 MFMA (exact
+                # products), so its ceiling is the fp32 peak -- the config dtype's
+                # peak and fraction are reported beside it
+                mfma_dt = "fp32" if site == 2 else cfg["dtype"]
+                peak, unit, bound, scale = MFMA_PEAK_TFS[mfma_dt], "TFLOP/s", "mfma", gemm_flops / 1e12
+                work = {"algo_flops_per_launch": int(gemm_flops), "mfma_dtype": mfma_dt}
+                if mfma_dt != cfg["dtype"]:
+                    work.update(peak_config_dtype=MFMA_PEAK_TFS[cfg["dtype"]],
+                                frac_config_dtype=round(scale / (us * 1e-6) / MFMA_PEAK_TFS[cfg["dtype"]], 4))
                 mb = load_mfma_busy(args.config, names[site])
                 work.update(mfma_busy=(mb["mfma_util"] if mb else None), mfma_busy_source=(mb["source"] if mb else None),
                             mfma_busy_dispatches=(mb["dispatches"] if mb else None))
